@@ -1,0 +1,268 @@
+#!/usr/bin/env python3
+"""Generate the golden parity fixtures by running the REFERENCE itself on CPU.
+
+Build-container tool only: it imports the read-only reference tree at /root/reference
+(which does not exist on the GPU box) and writes small .npz fixtures next to this file.
+Only inputs-by-seed and reference outputs are written; weights are regenerated from a seed
+by `skeletondiffusion_amd.synthetic` wherever the fixtures are consumed.
+
+Third-party gap: the reference's Denoiser imports
+`denoising_diffusion_pytorch.denoising_diffusion_pytorch_1d.{SinusoidalPosEmb,
+RandomOrLearnedSinusoidalPosEmb}` (pinned `denoising_diffusion_pytorch==1.9.4`,
+reference README.md:151), which is not installed here.  The module below is a restatement of
+that package's published sinusoidal embedding:
+    half = dim // 2; f_k = exp(-k * ln(theta) / (half - 1)), k < half
+    emb(t) = cat(sin(t * f), cos(t * f))
+It is injected into sys.modules for the duration of this script; nothing of the reference is
+copied into the repository.
+
+Usage:  PYTHONDONTWRITEBYTECODE=1 python tests/golden/gen_golden.py
+"""
+from __future__ import annotations
+
+import math
+import os
+import sys
+import types
+
+os.environ.setdefault("PYTHONDONTWRITEBYTECODE", "1")
+sys.dont_write_bytecode = True
+
+import numpy as np
+import torch
+from torch import nn
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+REF = os.environ.get("SKELDIFF_REFERENCE", "/root/reference")
+sys.path.insert(0, REPO)
+
+from skeletondiffusion_amd import synthetic  # noqa: E402
+
+
+def _install_ddp_shim() -> None:
+    class SinusoidalPosEmb(nn.Module):
+        def __init__(self, dim, theta=10000):
+            super().__init__()
+            self.dim = dim
+            self.theta = theta
+
+        def forward(self, x):
+            half = self.dim // 2
+            scale = math.log(self.theta) / (half - 1)
+            freqs = torch.exp(torch.arange(half, device=x.device) * -scale)
+            arg = x[:, None] * freqs[None, :]
+            return torch.cat((arg.sin(), arg.cos()), dim=-1)
+
+    class RandomOrLearnedSinusoidalPosEmb(nn.Module):
+        def __init__(self, dim, is_random=False):
+            super().__init__()
+            assert dim % 2 == 0
+            self.weights = nn.Parameter(torch.randn(dim // 2), requires_grad=not is_random)
+
+        def forward(self, x):
+            x = x[:, None]
+            freqs = x * self.weights[None, :] * 2 * math.pi
+            fouriered = torch.cat((freqs.sin(), freqs.cos()), dim=-1)
+            return torch.cat((x, fouriered), dim=-1)
+
+    pkg = types.ModuleType("denoising_diffusion_pytorch")
+    sub = types.ModuleType("denoising_diffusion_pytorch.denoising_diffusion_pytorch_1d")
+    sub.SinusoidalPosEmb = SinusoidalPosEmb
+    sub.RandomOrLearnedSinusoidalPosEmb = RandomOrLearnedSinusoidalPosEmb
+    pkg.denoising_diffusion_pytorch_1d = sub
+    pkg.__version__ = "1.9.4-restated"
+    sys.modules["denoising_diffusion_pytorch"] = pkg
+    sys.modules["denoising_diffusion_pytorch.denoising_diffusion_pytorch_1d"] = sub
+
+
+_install_ddp_shim()
+sys.path.insert(0, REF)
+from src.core.diffusion import (  # noqa: E402
+    IsotropicGaussianDiffusion, NonisotropicGaussianDiffusion, get_cov_from_corr)
+from src.core.network import Denoiser  # noqa: E402
+from src.data.skeleton.kinematic import (  # noqa: E402
+    AMASSKinematic, FreeManKinematic, H36MKinematic)
+
+torch.set_num_threads(8)
+torch.use_deterministic_algorithms(True)
+
+# -------------------------------------------------------------------------------------------
+# skeletons (hip excluded, as in eval: configs/config_eval/task/hmp.yaml:4)
+SKELETONS = {
+    "h36m16": lambda: H36MKinematic(num_joints=17, if_consider_hip=False),
+    "amass21": lambda: AMASSKinematic(num_joints=22, if_consider_hip=False),
+    "mano51": lambda: AMASSKinematic(num_joints=52, if_consider_hip=False),
+    "freeman17": lambda: FreeManKinematic(if_consider_hip=False),
+}
+
+RELEASE_ARCH = dict(use_attention=True, self_condition=False, norm_type="none", depth=4,
+                    attn_dim_head=32, attn_heads=8, learn_influence=True)
+
+WEIGHT_SEED = 1234
+
+
+def _save(name: str, **arrays) -> None:
+    path = os.path.join(HERE, name + ".npz")
+    clean = {}
+    for k, v in arrays.items():
+        if torch.is_tensor(v):
+            v = v.detach().cpu().numpy()
+        clean[k] = np.asarray(v)
+    np.savez_compressed(path, **clean)
+    print(f"wrote {path}: {os.path.getsize(path) / 1024:.1f} KiB")
+
+
+def diffusion_buffers(diff) -> dict:
+    return {f"buf_{k}": v for k, v in diff.state_dict().items() if not k.startswith("model.")}
+
+
+def build_release(skel_key, T, seed=WEIGHT_SEED, final_scale=1.0):
+    sk = SKELETONS[skel_key]()
+    J = sk.num_nodes
+    node_types = sk.nodes_type_id
+    corr = sk.adj_matrix
+    model = Denoiser(dim=96, cond_dim=96, out_dim=96, channels=J, num_nodes=J,
+                     node_types=node_types, **RELEASE_ARCH)
+    synthetic.fill_module_(model, seed)
+    if final_scale != 1.0:  # push x0 past +-1 so the clamp (base.py:318-319) is exercised
+        with torch.no_grad():
+            model.final_glin.weight.mul_(final_scale)
+            model.final_glin.bias.mul_(final_scale)
+    Sigma_N, Lambda_N, U = get_cov_from_corr(correlation_matrix=corr, if_sigma_n_scale=True,
+                                             sigma_n_scale="spectral", if_run_as_isotropic=False)
+    diff = NonisotropicGaussianDiffusion(Sigma_N=Sigma_N, Lambda_N=Lambda_N, U=U, model=model,
+                                         latent_size=96, diffusion_timesteps=T,
+                                         diffusion_objective="pred_x0",
+                                         diffusion_conditioning=True, beta_schedule="cosine",
+                                         diffusion_covariance_type="skeleton-diffusion",
+                                         gamma_scheduler="cosine", loss_reduction_type="l1")
+    diff.eval()
+    return sk, corr, node_types, diff
+
+
+def capture_forward(model, x, t, x_cond):
+    acts = {}
+    hooks = []
+
+    def hook(name):
+        def f(_m, _i, out):
+            acts[name] = out.detach().clone()
+        return f
+
+    hooks.append(model.init_lin.register_forward_hook(hook("init_lin")))
+    for i, (res, attn) in enumerate(model.layers):
+        hooks.append(res.register_forward_hook(hook(f"layer{i}_res")))
+        hooks.append(attn.register_forward_hook(hook(f"layer{i}_attn")))
+    hooks.append(model.final_res_block.register_forward_hook(hook("final_res")))
+    with torch.no_grad():
+        out = model(x, t, None, x_cond)
+    for h in hooks:
+        h.remove()
+    return out, acts
+
+
+def gen_covariances():
+    for key, ctor in SKELETONS.items():
+        sk = ctor()
+        corr = sk.adj_matrix
+        Sigma_N, Lambda_N, U = get_cov_from_corr(correlation_matrix=corr, if_sigma_n_scale=True,
+                                                 sigma_n_scale="spectral", if_run_as_isotropic=False)
+        arrays = dict(corr=corr, node_types=sk.nodes_type_id, Sigma_N=Sigma_N, Lambda_N=Lambda_N, U=U,
+                      node_names=np.array(list(sk.node_dict.values())))
+        J = corr.shape[0]
+        dummy = Denoiser(dim=96, cond_dim=0, out_dim=96, channels=J, num_nodes=J, depth=1)
+        for T in (10, 100):
+            d = NonisotropicGaussianDiffusion(Sigma_N=Sigma_N, Lambda_N=Lambda_N, U=U, model=dummy,
+                                              diffusion_timesteps=T)
+            for k, v in diffusion_buffers(d).items():
+                if v.dim() == 3 and T == 100:
+                    v = v[[0, 1, 50, 99]]  # keep the fixtures small at T=100
+                arrays[f"T{T}_{k}"] = v
+        _save(f"cov_{key}", **arrays)
+
+
+def gen_readme():
+    """Config 1: README plug-and-play Denoiser (J=16, D=96, T=10), `README.md:72-97`."""
+    J, B, T = 16, 4, 10
+    corr = torch.from_numpy(synthetic.readme_correlation(J, seed=7))
+    start = torch.from_numpy(synthetic.normal((B, J, 96), seed=11))
+    samp = torch.from_numpy(synthetic.normal((B, T - 1, J, 96), seed=12))
+    x_train = torch.from_numpy(synthetic.uniform((8, J, 96), seed=13, low=0.0, high=1.0))
+    train_noise = torch.from_numpy(synthetic.normal((8, J, 96), seed=14))
+    train_t = torch.tensor([0, 1, 2, 3, 5, 7, 8, 9])
+    out = dict(corr=corr, train_t=train_t)
+    for mode in ("noniso", "iso_as_noniso", "isotropic"):
+        model = Denoiser(dim=96, cond_dim=0, out_dim=96, channels=J, num_nodes=J)
+        synthetic.fill_module_(model, WEIGHT_SEED)
+        if mode == "isotropic":
+            diff = IsotropicGaussianDiffusion(model=model, diffusion_timesteps=T)
+        else:
+            Sigma_N, Lambda_N, U = get_cov_from_corr(correlation_matrix=corr, if_sigma_n_scale=True,
+                                                     sigma_n_scale="spectral",
+                                                     if_run_as_isotropic=(mode == "iso_as_noniso"))
+            diff = NonisotropicGaussianDiffusion(Sigma_N=Sigma_N, Lambda_N=Lambda_N, U=U, model=model,
+                                                 timesteps=10)
+        diff.eval()
+        with torch.no_grad():
+            img, (noise0, noise_t, mean_t) = diff.sample(batch_size=B, start_noise=start.clone(),
+                                                         sampling_noise=samp.clone(),
+                                                         return_sampling_noise=True)
+            loss, lw, mout = diff.p_losses(x_train.clone(), train_t, noise=train_noise.clone())
+        out.update({f"{mode}_img": img, f"{mode}_mean_t": mean_t, f"{mode}_loss": loss,
+                    f"{mode}_loss_weight": lw, f"{mode}_model_out": mout})
+        for k, v in diffusion_buffers(diff).items():
+            out[f"{mode}_{k}"] = v
+    _save("readme16_T10", **out)
+
+
+def gen_release(skel_key, T, B_seq, futures, with_acts, steps_to_keep=None, tag=None,
+                final_scale=1.0):
+    sk, corr, node_types, diff = build_release(skel_key, T, final_scale=final_scale)
+    J = corr.shape[0]
+    B = B_seq * futures
+    x_cond_seq = torch.from_numpy(synthetic.uniform((B_seq, J, 96), seed=21))
+    start = torch.from_numpy(synthetic.normal((B, J, 96), seed=22))
+    samp = torch.from_numpy(synthetic.normal((B, T - 1, J, 96), seed=23))
+    x_cond = x_cond_seq.repeat_interleave(futures, 0)
+    with torch.no_grad():
+        img, (noise0, noise_t, mean_t) = diff.sample(batch_size=B, x_cond=x_cond,
+                                                     start_noise=start.clone(),
+                                                     sampling_noise=samp.clone(),
+                                                     return_sampling_noise=True)
+    out = dict(img=img, node_types=node_types, corr=corr, B_seq=B_seq, futures=futures, T=T,
+               final_scale=final_scale, weight_seed=WEIGHT_SEED)
+    if steps_to_keep is None:
+        out["mean_t"] = mean_t
+    else:
+        out["mean_t_steps"] = np.array(steps_to_keep)
+        out["mean_t"] = mean_t[:, steps_to_keep]
+    if with_acts:
+        tt = torch.full((B,), T - 1, dtype=torch.long)
+        x0, acts = capture_forward(diff.model, start.clone(), tt, x_cond)
+        out["fwd_t"] = T - 1
+        out["fwd_x0"] = x0
+        for k, v in acts.items():
+            out[f"act_{k}"] = v
+        # training path: p_losses at fixed t / noise
+        t_train = torch.arange(B) % T
+        train_noise = torch.from_numpy(synthetic.normal((B, J, 96), seed=24))
+        x_start = torch.from_numpy(synthetic.uniform((B, J, 96), seed=25))
+        loss, lw, mout = diff.p_losses(x_start.clone(), t_train, noise=train_noise.clone(), x_cond=x_cond)
+        out.update(train_t=t_train, train_loss=loss.detach(), train_loss_weight=lw,
+                   train_model_out=mout.detach())
+    _save(tag or f"release_{skel_key}_T{T}", **out)
+
+
+def main():
+    gen_covariances()
+    gen_readme()
+    gen_release("h36m16", 10, B_seq=2, futures=4, with_acts=True)
+    gen_release("h36m16", 100, B_seq=2, futures=4, with_acts=False, steps_to_keep=[0, 9, 49, 98])
+    gen_release("amass21", 10, B_seq=1, futures=4, with_acts=True, final_scale=8.0)
+    gen_release("freeman17", 10, B_seq=1, futures=4, with_acts=False)
+    gen_release("mano51", 10, B_seq=1, futures=2, with_acts=False)
+
+
+if __name__ == "__main__":
+    main()
