@@ -1,0 +1,162 @@
+/*
+ * skeldiff.h — C ABI of libskeldiff.so, the MI355X (gfx950) sampling engine for the
+ * SkeletonDiffusion hot path: NonisotropicGaussianDiffusion.sample().
+ *
+ * Boundary rules: plain pointers and sizes, no torch types.  Tensors are row-major fp32,
+ * contiguous, in device memory (HBM) unless stated; `stream` is a hipStream_t passed as
+ * void* (NULL = default stream).  Every function returns 0 on success and a negative
+ * SD_E* code on error; sd_last_error() returns a thread-local message for the last failure.
+ * No C++ exception crosses the ABI.  A plan is immutable after sd_plan_finalize() and may be
+ * shared by several streams; a workspace belongs to one stream at a time.
+ *
+ * Which reference interface each entry point replaces (paths relative to the reference
+ * tree, tum-vision/skeletondiffusion):
+ *   sd_plan_create / sd_plan_set_tensor / sd_plan_finalize
+ *       -> module construction + strict load_state_dict of the diffusion and Denoiser
+ *          (src/core/diffusion_manager.py:16-27, src/eval_prepare_model.py:69-72,
+ *           src/core/diffusion/nonisotropic.py:72-127, src/core/network/nn/generator.py:8-84).
+ *          Tensors are handed over by their reference state_dict key.
+ *   sd_denoiser_forward
+ *       -> Denoiser.forward (src/core/network/nn/generator.py:86-107) as called by
+ *          LatentDiffusion.feed_model (src/core/diffusion/base.py:243-255).
+ *   sd_p_sample_update
+ *       -> q_posterior + p_combine_mean_var_noise of one reverse step
+ *          (src/core/diffusion/base.py:314-341, src/core/diffusion/nonisotropic.py:196-210;
+ *           isotropic.py:85-95 for IsotropicGaussianDiffusion), x0 clamp included.
+ *   sd_sample_loop
+ *       -> LatentDiffusion.p_sample_loop / sample (src/core/diffusion/base.py:343-390,
+ *          439-443).
+ *   sd_noise_fill
+ *       -> the white-noise draws get_noise/randn (src/core/diffusion/base.py:151-158,351),
+ *          replaced by counter-based Philox4x32-10 keyed by (seed, global row, step) so that
+ *          results do not depend on batch split or GPU count.
+ */
+#ifndef SKELDIFF_H
+#define SKELDIFF_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SD_ABI_VERSION 1
+
+enum {
+    SD_OK = 0,
+    SD_E_INVALID = -1,   /* bad argument / shape / unsupported configuration */
+    SD_E_STATE = -2,     /* plan not finalized, tensor missing, ... */
+    SD_E_HIP = -3,       /* HIP runtime error */
+    SD_E_NOMEM = -4,
+    SD_E_INTERNAL = -5
+};
+
+/* flags for sd_sample_loop */
+enum {
+    SD_FLAG_GRAPH = 1,          /* capture the whole T-step chain in a hipGraph, cache, replay */
+    SD_FLAG_DEVICE_START = 2,   /* x_T drawn on device (Philox, step index T) instead of x_T arg */
+    SD_FLAG_DEVICE_NOISE = 4    /* per-step noise drawn on device instead of eps_all */
+};
+
+typedef struct sd_plan sd_plan;
+
+typedef struct sd_plan_desc {
+    int32_t num_nodes;        /* J = channels = num_nodes (<= 64) */
+    int32_t latent_dim;       /* Denoiser `dim` = diffusion latent_size (seq_length) */
+    int32_t cond_dim;         /* 0, or latent_dim when diffusion_conditioning */
+    int32_t out_dim;          /* Denoiser out_dim (== latent_dim for sampling) */
+    int32_t depth;
+    int32_t attn_heads;
+    int32_t attn_dim_head;
+    int32_t use_attention;    /* 1: Attention blocks, 0: Residual(PreNorm(StaticGraphLinear)) */
+    int32_t self_condition;   /* must be 0 (no release config uses it) */
+    int32_t learn_influence;  /* 1: G-hat = row-L1-normalised G (graph_structural.py:31-32) */
+    int32_t num_node_types;   /* 0: shared weights (no node_types); else types in node_types */
+    const int64_t* node_types;/* host array[J] (ignored when num_node_types == 0) */
+    int32_t timesteps;        /* T */
+    int32_t isotropic;        /* 1: IsotropicGaussianDiffusion posterior (scalar coefficients) */
+    int32_t activation;       /* diffusion_activation: 0 identity, 1 tanh */
+    float sinusoidal_theta;   /* SinusoidalPosEmb theta (10000) */
+} sd_plan_desc;
+
+int32_t sd_abi_version(void);
+const char* sd_last_error(void);
+
+int sd_plan_create(sd_plan** out, const sd_plan_desc* desc);
+void sd_plan_destroy(sd_plan* plan);
+
+/* The tensors a plan requires, in reference state_dict key order ("model.init_lin.weight",
+ * ..., "posterior_mean_coef1_x0", ...). */
+int32_t sd_plan_num_tensors(const sd_plan* plan);
+const char* sd_plan_tensor_name(const sd_plan* plan, int32_t index);
+int64_t sd_plan_tensor_numel(const sd_plan* plan, int32_t index);
+
+/* Copy one tensor (fp32, contiguous, host or device pointer) into the plan. */
+int sd_plan_set_tensor(sd_plan* plan, const char* name, const float* data, int64_t numel,
+                       void* stream);
+/* Pack weights (G-hat, RMSNorm gain folding, time/FiLM tables, posterior tables). */
+int sd_plan_finalize(sd_plan* plan, void* stream);
+
+/* Bytes of device workspace needed for `rows` latent rows. */
+size_t sd_workspace_bytes(const sd_plan* plan, int64_t rows);
+
+/* x0_out(B,J,out_dim) = Denoiser(x_t(B,J,D), t, x_cond).  x_cond: (B / cond_repeat, J, cond_dim)
+ * with row b reading x_cond row b / cond_repeat (the repeat_interleave of base.py:246-248), or
+ * NULL when cond_dim == 0. */
+int sd_denoiser_forward(const sd_plan* plan, const float* x_t, const float* x_cond,
+                        int64_t cond_repeat, int32_t t, float* x0_out, int64_t rows,
+                        void* workspace, size_t workspace_bytes, void* stream);
+
+/* One reverse step for B rows at time t:
+ *   x0 = clamp(act(x0_raw), -1, 1); mean = C1[t] x0 + C2[t] x_t;
+ *   x_prev = mean + U (sigma_t * eps)   (nonisotropic)   |  c1 x0 + c2 x_t + sigma_t eps (iso)
+ * eps: (B, J, D) rows `eps_row_stride` floats apart, or NULL for device Philox noise
+ * (seed, global row row0 + b, step t).  t == 0 adds no noise.  mean_out / noise_out are
+ * optional (NULL) extra outputs with their own row strides (return_sampling_noise). */
+int sd_p_sample_update(const sd_plan* plan, const float* x0_raw, const float* x_t,
+                       const float* eps, int64_t eps_row_stride, uint64_t seed, int64_t row0,
+                       int32_t t, float* x_prev, float* mean_out, int64_t mean_row_stride,
+                       float* noise_out, int64_t noise_row_stride, int64_t rows, void* stream);
+
+/* The full reverse chain t = T-1 .. 0 (base.py:365-367).
+ *   x_T     : (B,J,D) start noise, or ignored with SD_FLAG_DEVICE_START
+ *   eps_all : (B, T-1, J, D) sampling noise in the reference layout (step t reads
+ *             eps_all[:, T-1-t]), or ignored with SD_FLAG_DEVICE_NOISE
+ *   out     : (B,J,D) final latents
+ *   means_out / noise_out / timages_out : optional (B, T-1, J, D) records of mean_t,
+ *             the noise used and x_t for t = T-1..1 (return_sampling_noise / return_timages)
+ *   start_out: optional (B,J,D) copy of the start noise used */
+int sd_sample_loop(const sd_plan* plan, const float* x_T, const float* x_cond,
+                   int64_t cond_repeat, const float* eps_all, uint64_t seed, int64_t row0,
+                   float* out, float* means_out, float* noise_out, float* timages_out,
+                   float* start_out, int64_t rows, void* workspace, size_t workspace_bytes,
+                   int32_t flags, void* stream);
+
+/* Fill out(B, n_per_row) with the device normals of (seed, rows row0.., step). n_per_row % 4 == 0. */
+int sd_noise_fill(float* out, int64_t rows, int64_t n_per_row, uint64_t seed, int64_t row0,
+                  int32_t step, void* stream);
+/* Raw Philox4x32-10 words for tests: out[4*i .. 4*i+3] = philox(ctr = (i % quads, step,
+ * row lo, row hi) with row = row0 + i / quads, key = seed). */
+int sd_philox_raw(uint32_t* out, int64_t rows, int64_t quads, uint64_t seed, int64_t row0,
+                  int32_t step, void* stream);
+
+/* Number of kernel launches one reverse step (denoiser + update) issues. */
+int32_t sd_plan_kernels_per_step(const sd_plan* plan);
+
+/* Algorithmic FLOPs of one reverse step over `rows` rows, from the plan's own layer list:
+ * flops_out[0] graph-linear GEMMs + G-hat mixing, [1] attention QK^T + PV, [2] posterior update. */
+int sd_plan_step_flops(const sd_plan* plan, int64_t rows, double* flops_out);
+
+/* Measurement hook: run one reverse step at time t `reps` times with HIP events recorded on
+ * `stream` around every kernel.  ms_out[4] = mean ms per step in graph-linear, attention and
+ * update kernels, and first-to-last event of the step; counts_out[3] (nullable) = launches per
+ * step per class.  Device noise is used for the update. */
+int sd_profile_step(const sd_plan* plan, const float* x_t, const float* x_cond, int64_t cond_repeat,
+                    int32_t t, int64_t rows, void* workspace, size_t workspace_bytes, int32_t reps,
+                    float* ms_out, int32_t* counts_out, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SKELDIFF_H */

@@ -1,0 +1,113 @@
+"""ctypes binding of libskeldiff.so (the C ABI declared in include/skeldiff.h).
+
+The library is built in-tree by `skeletondiffusion_amd.build.build_library()` (hipcc,
+--offload-arch=gfx950).  There is no fallback: if the library is missing or cannot be loaded,
+every sampling entry point raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+from typing import Optional
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libskeldiff.so")
+
+SD_FLAG_GRAPH = 1
+SD_FLAG_DEVICE_START = 2
+SD_FLAG_DEVICE_NOISE = 4
+
+# every symbol include/skeldiff.h declares (checked by tests/test_abi.py)
+EXPORTED = (
+    "sd_abi_version", "sd_last_error", "sd_plan_create", "sd_plan_destroy", "sd_plan_num_tensors",
+    "sd_plan_tensor_name", "sd_plan_tensor_numel", "sd_plan_set_tensor", "sd_plan_finalize",
+    "sd_workspace_bytes", "sd_denoiser_forward", "sd_p_sample_update", "sd_sample_loop",
+    "sd_noise_fill", "sd_philox_raw", "sd_plan_kernels_per_step", "sd_plan_step_flops", "sd_profile_step",
+)
+
+
+class SDPlanDesc(ctypes.Structure):
+    _fields_ = [
+        ("num_nodes", ctypes.c_int32),
+        ("latent_dim", ctypes.c_int32),
+        ("cond_dim", ctypes.c_int32),
+        ("out_dim", ctypes.c_int32),
+        ("depth", ctypes.c_int32),
+        ("attn_heads", ctypes.c_int32),
+        ("attn_dim_head", ctypes.c_int32),
+        ("use_attention", ctypes.c_int32),
+        ("self_condition", ctypes.c_int32),
+        ("learn_influence", ctypes.c_int32),
+        ("num_node_types", ctypes.c_int32),
+        ("node_types", ctypes.POINTER(ctypes.c_int64)),
+        ("timesteps", ctypes.c_int32),
+        ("isotropic", ctypes.c_int32),
+        ("activation", ctypes.c_int32),
+        ("sinusoidal_theta", ctypes.c_float),
+    ]
+
+
+class SkelDiffError(RuntimeError):
+    pass
+
+
+_lib: Optional[ctypes.CDLL] = None
+_lock = threading.Lock()
+
+
+def _declare(lib: ctypes.CDLL) -> None:
+    vp, i32, i64, u64, sz = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_uint64, ctypes.c_size_t
+    sig = {
+        "sd_abi_version": (i32, []),
+        "sd_last_error": (ctypes.c_char_p, []),
+        "sd_plan_create": (ctypes.c_int, [ctypes.POINTER(vp), ctypes.POINTER(SDPlanDesc)]),
+        "sd_plan_destroy": (None, [vp]),
+        "sd_plan_num_tensors": (i32, [vp]),
+        "sd_plan_tensor_name": (ctypes.c_char_p, [vp, i32]),
+        "sd_plan_tensor_numel": (i64, [vp, i32]),
+        "sd_plan_set_tensor": (ctypes.c_int, [vp, ctypes.c_char_p, vp, i64, vp]),
+        "sd_plan_finalize": (ctypes.c_int, [vp, vp]),
+        "sd_workspace_bytes": (sz, [vp, i64]),
+        "sd_denoiser_forward": (ctypes.c_int, [vp, vp, vp, i64, i32, vp, i64, vp, sz, vp]),
+        "sd_p_sample_update": (ctypes.c_int, [vp, vp, vp, vp, i64, u64, i64, i32, vp, vp, i64, vp, i64, i64, vp]),
+        "sd_sample_loop": (ctypes.c_int, [vp, vp, vp, i64, vp, u64, i64, vp, vp, vp, vp, vp, i64, vp, sz, i32, vp]),
+        "sd_noise_fill": (ctypes.c_int, [vp, i64, i64, u64, i64, i32, vp]),
+        "sd_philox_raw": (ctypes.c_int, [vp, i64, i64, u64, i64, i32, vp]),
+        "sd_plan_kernels_per_step": (i32, [vp]),
+        "sd_plan_step_flops": (ctypes.c_int, [vp, i64, ctypes.POINTER(ctypes.c_double)]),
+        "sd_profile_step": (ctypes.c_int, [vp, vp, vp, i64, i32, i64, vp, sz, i32, ctypes.POINTER(ctypes.c_float),
+                                           ctypes.POINTER(ctypes.c_int32), vp]),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+
+
+def lib() -> ctypes.CDLL:
+    """Load libskeldiff.so (once).  Raises SkelDiffError if it is missing."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is None:
+            if not os.path.exists(LIB_PATH):
+                raise SkelDiffError(
+                    f"{LIB_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'` "
+                    "(hipcc --offload-arch=gfx950).  There is no CPU fallback for sampling.")
+            handle = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
+            _declare(handle)
+            _lib = handle
+    return _lib
+
+
+def check(rc: int) -> None:
+    if rc != 0:
+        msg = lib().sd_last_error()
+        raise SkelDiffError(f"libskeldiff error {rc}: {msg.decode() if msg else '?'}")
+
+
+def ptr(t) -> Optional[int]:
+    """data_ptr of a torch tensor (None for None)."""
+    return None if t is None else t.data_ptr()

@@ -1,0 +1,71 @@
+// Internal interfaces between the host plan (sd_plan.hip) and the gfx950 kernels
+// (sd_kernels.hip).  Not part of the public ABI (see include/skeldiff.h).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace sd {
+
+constexpr int kMaxNodes = 64;
+
+// One StaticGraphLinear (graph_structural.py:30-43) with its fused epilogue:
+//   y_j   = s_j * (W_type(j) [x1_j | x2_j]) + bias_type(j)        (s_j = 1/max(|x1_j|,1e-12) if RMS)
+//   z_i   = sum_j Ghat[i][j] y_j
+//   z     = z * (film[n] + 1) + film[H + n]      (ResnetBlock FiLM, attention.py:71-73)
+//   z     = act(z)                               (tanh)
+//   z    += res                                  (residual, attention.py:16 / :102)
+struct GLArgs {
+    const float* x1; int64_t x1_rs; int K1; int x1_div;   // row b reads x1 row b / x1_div
+    const float* x2; int64_t x2_rs; int K2;               // optional second input (cat along K)
+    const float* W;                                       // (types, N, K1+K2), K contiguous
+    const float* bias;                                    // (types, N) or null
+    const float* G;                                       // (J, J) Ghat, row-major
+    const float* film;                                    // (2N): [scale | shift] or null
+    const float* res; int64_t res_rs;                     // (B, J, N) or null
+    float* out; int64_t out_rs;                           // (B, J, N)
+    int64_t B;
+    int N;
+    int J;
+    int act;                                              // 0 none, 1 tanh
+    int wrow[kMaxNodes];                                  // type(j) * N  (row offset into W)
+};
+
+// Multi-head attention over joints (attention.py:122-136) from a (B, J, 3*heads*dh) qkv buffer.
+struct AttnArgs {
+    const float* qkv; float* out; int64_t B; int J; int heads; int dh; float scale;
+};
+
+// Posterior mean + correlated noise step (nonisotropic.py:196-210 / isotropic.py:85-95).
+struct UpdArgs {
+    const float* x0; const float* xt;
+    const float* eps; int64_t eps_rs;      // given noise rows (noise_mode 1)
+    const float* C1; const float* C2; const float* U; const float* sig;   // step-t tables
+    float c1s, c2s, sigs;                  // isotropic scalars
+    int iso; int act; int noise_mode;      // noise_mode: 0 none (t == 0), 1 given, 2 Philox
+    uint64_t seed; int64_t row0; int step; const uint64_t* rng_dev;  // rng_dev: {seed,row0} or null
+    float* out; float* out2; int64_t out2_rs;
+    float* mean_out; int64_t mean_rs; float* noise_out; int64_t noise_rs;
+    int64_t B; int J; int D;
+};
+
+hipError_t launch_graph_linear(const GLArgs& a, bool rms, hipStream_t s);
+hipError_t launch_attention(const AttnArgs& a, hipStream_t s);
+hipError_t launch_update(const UpdArgs& a, hipStream_t s);
+hipError_t launch_noise_fill(float* out, int64_t rows, int64_t n_per_row, uint64_t seed,
+                             int64_t row0, int step, const uint64_t* rng_dev, hipStream_t s);
+hipError_t launch_philox_raw(uint32_t* out, int64_t rows, int64_t quads, uint64_t seed,
+                             int64_t row0, int step, hipStream_t s);
+hipError_t launch_set_rng(uint64_t* rng_dev, uint64_t seed, int64_t row0, hipStream_t s);
+hipError_t launch_copy_rows(float* dst, int64_t dst_rs, const float* src, int64_t src_rs,
+                            int64_t rows, int64_t n, hipStream_t s);
+
+// plan-finalize helpers (one-time)
+hipError_t launch_sinusoidal(float* emb, int T, int dim, float neg_scale, hipStream_t s);
+hipError_t launch_linear(const float* x, int M, int K, const float* W, const float* b, int N,
+                         float* y, int in_act, int out_act, hipStream_t s);
+hipError_t launch_ghat(const float* G, float* Ghat, int J, int normalize, hipStream_t s);
+hipError_t launch_fold_gain(const float* W, const float* g, float mult, float* out,
+                            int64_t rows, int K, hipStream_t s);
+hipError_t launch_sigma(const float* logvar, float* sig, int64_t n, hipStream_t s);
+
+}  // namespace sd

@@ -1,0 +1,631 @@
+// gfx950 (CDNA4, MI355X) kernels for the SkeletonDiffusion reverse-diffusion step.
+//
+//   k_graph_linear  StaticGraphLinear + fused epilogue        graph_structural.py:30-43,
+//                   (per-node-type GEMM on v_mfma_f32_16x16x4_f32, bias, G-hat node mixing,
+//                    RMSNorm scale, FiLM, tanh, residual)      attention.py:30-102
+//   k_attention     multi-head attention over joints, QK^T and PV on MFMA   attention.py:122-136
+//   k_update        x0 clamp + C1 x0 + C2 x_t + U (sigma . eps)   nonisotropic.py:196-210,
+//                   base.py:314-341, isotropic.py:85-95
+//   k_noise_fill    counter-based Philox4x32-10 + Box-Muller normals (replaces randn)
+//   plan helpers    sinusoidal embedding, small linears (time MLP / FiLM tables), G-hat,
+//                   RMSNorm gain folding, sigma table
+//
+// Layout in HBM: every activation is row-major (rows B, nodes J, features F), F contiguous.
+// All arithmetic is fp32; the GEMMs use the exact-f32 MFMA (a k-ordered fmaf chain).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "sd_internal.h"
+
+namespace sd {
+
+typedef float floatx4 __attribute__((ext_vector_type(4)));
+typedef float floatx2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ floatx4 ld4(const float* p) { return *reinterpret_cast<const floatx4*>(p); }
+__device__ __forceinline__ floatx2 ld2(const float* p) { return *reinterpret_cast<const floatx2*>(p); }
+__device__ __forceinline__ void st2(float* p, floatx2 v) { *reinterpret_cast<floatx2*>(p) = v; }
+
+__device__ __forceinline__ floatx4 mfma4(float a, float b, floatx4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
+// =============================================================================================
+// StaticGraphLinear
+//
+// Workgroup = 4 waves; a wave owns 16 rows x (16*NCB) output columns for ALL J nodes, so the
+// G-hat node mixing (which couples the J nodes of a row) happens in registers.
+// MFMA 16x16x4 f32 operand maps (cdna_hip_programming.md §3): lane l supplies
+// A[l&15][k=l>>4] and B[k=l>>4][l&15]; D[row=4*(l>>4)+r][col=l&15].  We permute k inside a
+// 16-wide chunk so each lane reads ONE float4 of x and ONE float4 of W per 4 MFMAs: in step s
+// of chunk kc, position p = l>>4 carries k = kc + 4p + s for both operands.
+// =============================================================================================
+
+template <int JM, bool EXACT, int NCB, bool RMS>
+__device__ __forceinline__ void gl_accumulate(floatx4 (&acc)[JM][NCB], float (&ss)[JM],
+                                              const float* __restrict__ xrow, bool row_ok,
+                                              int Kp, int koff, int K, int J,
+                                              const GLArgs& p, int c0, int lr, int lg) {
+    for (int kc = 0; kc < Kp; kc += 16) {
+#pragma unroll
+        for (int j = 0; j < JM; ++j) {
+            if (!EXACT && j >= J) continue;
+            floatx4 a = row_ok ? ld4(xrow + (int64_t)j * Kp + kc + 4 * lg) : floatx4{0.f, 0.f, 0.f, 0.f};
+            if (RMS) ss[j] += a.x * a.x + a.y * a.y + a.z * a.z + a.w * a.w;
+            const float* wb = p.W + (int64_t)p.wrow[j] * K + koff + kc + 4 * lg;
+#pragma unroll
+            for (int cb = 0; cb < NCB; ++cb) {
+                const int n = c0 + 16 * cb + lr;
+                floatx4 b = (n < p.N) ? ld4(wb + (int64_t)n * K) : floatx4{0.f, 0.f, 0.f, 0.f};
+                floatx4 c = acc[j][cb];
+                c = mfma4(a.x, b.x, c);
+                c = mfma4(a.y, b.y, c);
+                c = mfma4(a.z, b.z, c);
+                c = mfma4(a.w, b.w, c);
+                acc[j][cb] = c;
+            }
+        }
+    }
+}
+
+template <int JM, bool EXACT, int NCB, bool RMS>
+__global__ __launch_bounds__(256) void k_graph_linear(const GLArgs p) {
+    __shared__ float sG[JM * JM];
+    const int J = EXACT ? JM : p.J;
+    for (int i = threadIdx.x; i < J * J; i += 256) sG[i] = p.G[i];
+    __syncthreads();
+
+    const int lane = threadIdx.x & 63;
+    const int wave = threadIdx.x >> 6;
+    const int lr = lane & 15;
+    const int lg = lane >> 4;
+    const int ntile_c = (p.N + 16 * NCB - 1) / (16 * NCB);
+    const int ct = blockIdx.x % ntile_c;
+    const int64_t rt = blockIdx.x / ntile_c;
+    const int64_t row0 = rt * 64 + wave * 16;
+    if (row0 >= p.B) return;  // whole wave idle (no barrier follows)
+    const int c0 = ct * 16 * NCB;
+    const int K = p.K1 + p.K2;
+
+    floatx4 acc[JM][NCB];
+    float ss[JM];
+#pragma unroll
+    for (int j = 0; j < JM; ++j) {
+        ss[j] = 0.f;
+#pragma unroll
+        for (int cb = 0; cb < NCB; ++cb) acc[j][cb] = floatx4{0.f, 0.f, 0.f, 0.f};
+    }
+
+    const int64_t arow = row0 + lr;
+    const bool row_ok = arow < p.B;
+    const int64_t arow_c = row_ok ? arow : 0;
+    gl_accumulate<JM, EXACT, NCB, RMS>(acc, ss, p.x1 + (arow_c / p.x1_div) * p.x1_rs, row_ok,
+                                       p.K1, 0, K, J, p, c0, lr, lg);
+    if (p.K2 > 0) {
+        float dummy[JM];
+        gl_accumulate<JM, EXACT, NCB, false>(acc, dummy, p.x2 + arow_c * p.x2_rs, row_ok,
+                                             p.K2, p.K1, K, J, p, c0, lr, lg);
+    }
+
+    if (RMS) {  // F.normalize(x, dim=-1): scale row (b, j) by 1 / max(||x_bj||, 1e-12)
+#pragma unroll
+        for (int j = 0; j < JM; ++j) {
+            if (!EXACT && j >= J) continue;
+            float t = ss[j];
+            t += __shfl_xor(t, 16);
+            t += __shfl_xor(t, 32);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const float n2 = __shfl(t, 4 * lg + r);
+                const float s = 1.0f / fmaxf(sqrtf(n2), 1e-12f);
+#pragma unroll
+                for (int cb = 0; cb < NCB; ++cb) acc[j][cb][r] *= s;
+            }
+        }
+    }
+    if (p.bias) {  // bias added per source node BEFORE the mixing (graph_structural.py:38-41)
+#pragma unroll
+        for (int j = 0; j < JM; ++j) {
+            if (!EXACT && j >= J) continue;
+#pragma unroll
+            for (int cb = 0; cb < NCB; ++cb) {
+                const int n = c0 + 16 * cb + lr;
+                const float bv = (n < p.N) ? p.bias[p.wrow[j] + n] : 0.f;
+                acc[j][cb] += bv;
+            }
+        }
+    }
+
+    float fa[NCB], fb[NCB];
+#pragma unroll
+    for (int cb = 0; cb < NCB; ++cb) {
+        const int n = c0 + 16 * cb + lr;
+        fa[cb] = 1.f;
+        fb[cb] = 0.f;
+        if (p.film && n < p.N) {
+            fa[cb] = p.film[n] + 1.0f;
+            fb[cb] = p.film[p.N + n];
+        }
+    }
+
+    for (int i = 0; i < J; ++i) {
+        floatx4 z[NCB];
+#pragma unroll
+        for (int cb = 0; cb < NCB; ++cb) z[cb] = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int j = 0; j < JM; ++j) {
+            if (!EXACT && j >= J) continue;
+            const float g = sG[i * J + j];
+#pragma unroll
+            for (int cb = 0; cb < NCB; ++cb) z[cb] += g * acc[j][cb];
+        }
+#pragma unroll
+        for (int cb = 0; cb < NCB; ++cb) {
+            const int n = c0 + 16 * cb + lr;
+            if (n >= p.N) continue;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int64_t row = row0 + 4 * lg + r;
+                if (row >= p.B) continue;
+                float v = z[cb][r];
+                if (p.film) v = v * fa[cb] + fb[cb];
+                if (p.act == 1) v = tanhf(v);
+                if (p.res) v += p.res[row * p.res_rs + (int64_t)i * p.N + n];
+                p.out[row * p.out_rs + (int64_t)i * p.N + n] = v;
+            }
+        }
+    }
+}
+
+template <int JM, bool EXACT, int NCB>
+static hipError_t gl_dispatch_rms(const GLArgs& a, bool rms, hipStream_t s) {
+    const int ntile_c = (a.N + 16 * NCB - 1) / (16 * NCB);
+    const int64_t ntile_r = (a.B + 63) / 64;
+    const dim3 grid((unsigned)(ntile_c * ntile_r));
+    if (rms)
+        hipLaunchKernelGGL((k_graph_linear<JM, EXACT, NCB, true>), grid, dim3(256), 0, s, a);
+    else
+        hipLaunchKernelGGL((k_graph_linear<JM, EXACT, NCB, false>), grid, dim3(256), 0, s, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_graph_linear(const GLArgs& a, bool rms, hipStream_t s) {
+    if (a.B <= 0) return hipSuccess;
+    switch (a.J) {
+        case 16: return gl_dispatch_rms<16, true, 2>(a, rms, s);
+        case 17: return gl_dispatch_rms<17, true, 2>(a, rms, s);
+        case 21: return gl_dispatch_rms<21, true, 2>(a, rms, s);
+        case 51: return gl_dispatch_rms<51, true, 1>(a, rms, s);
+        default: break;
+    }
+    if (a.J <= 8) return gl_dispatch_rms<8, false, 2>(a, rms, s);
+    if (a.J <= 16) return gl_dispatch_rms<16, false, 2>(a, rms, s);
+    if (a.J <= 32) return gl_dispatch_rms<32, false, 1>(a, rms, s);
+    return gl_dispatch_rms<64, false, 1>(a, rms, s);
+}
+
+// =============================================================================================
+// Attention over joints.  One wave per (row b, head h).  S^T = K Q^T (scaled q, as
+// attention.py:128) on 16x16x4 MFMA tiles, softmax over j in registers + 2 lane swaps, then
+// O^T = V^T P^T with the S^T accumulator used directly as the B operand (no LDS round trip).
+// J <= 16*JT, padded rows/cols masked.
+// =============================================================================================
+
+template <int JT>
+__global__ __launch_bounds__(256) void k_attention(const AttnArgs p) {
+    const int lane = threadIdx.x & 63;
+    const int lr = lane & 15, lg = lane >> 4;
+    const int64_t pair = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (pair >= p.B * p.heads) return;
+    const int64_t b = pair / p.heads;
+    const int h = (int)(pair % p.heads);
+    const int J = p.J, dh = p.dh, hid = p.heads * p.dh;
+    const int64_t rs = 3 * (int64_t)hid;
+    const float* base = p.qkv + b * J * rs;
+    const float* qb = base + h * dh;
+    const float* kb = base + hid + h * dh;
+    const float* vb = base + 2 * hid + h * dh;
+
+    floatx4 S[JT][JT];
+#pragma unroll
+    for (int a = 0; a < JT; ++a)
+#pragma unroll
+        for (int c = 0; c < JT; ++c) S[a][c] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+    for (int cc = 0; cc < dh; cc += 16) {
+        floatx4 ka[JT], qv[JT];
+#pragma unroll
+        for (int t = 0; t < JT; ++t) {
+            const int j = t * 16 + lr;
+            ka[t] = (j < J) ? ld4(kb + j * rs + cc + 4 * lg) : floatx4{0.f, 0.f, 0.f, 0.f};
+            qv[t] = (j < J) ? ld4(qb + j * rs + cc + 4 * lg) * p.scale : floatx4{0.f, 0.f, 0.f, 0.f};
+        }
+#pragma unroll
+        for (int jt = 0; jt < JT; ++jt)
+#pragma unroll
+            for (int nt = 0; nt < JT; ++nt) {
+                floatx4 c = S[jt][nt];
+                c = mfma4(ka[jt].x, qv[nt].x, c);
+                c = mfma4(ka[jt].y, qv[nt].y, c);
+                c = mfma4(ka[jt].z, qv[nt].z, c);
+                c = mfma4(ka[jt].w, qv[nt].w, c);
+                S[jt][nt] = c;
+            }
+    }
+
+    // softmax over j (rows of S^T) for every query column n = nt*16 + lr
+#pragma unroll
+    for (int nt = 0; nt < JT; ++nt) {
+        float m = -INFINITY;
+#pragma unroll
+        for (int jt = 0; jt < JT; ++jt)
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+                if (jt * 16 + 4 * lg + r < J) m = fmaxf(m, S[jt][nt][r]);
+        m = fmaxf(m, __shfl_xor(m, 16));
+        m = fmaxf(m, __shfl_xor(m, 32));
+        float sum = 0.f;
+#pragma unroll
+        for (int jt = 0; jt < JT; ++jt)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const float e = (jt * 16 + 4 * lg + r < J) ? expf(S[jt][nt][r] - m) : 0.f;
+                S[jt][nt][r] = e;
+                sum += e;
+            }
+        sum += __shfl_xor(sum, 16);
+        sum += __shfl_xor(sum, 32);
+        const float inv = 1.0f / sum;
+#pragma unroll
+        for (int jt = 0; jt < JT; ++jt) S[jt][nt] *= inv;
+    }
+
+    // O^T[d][n] = sum_j V[j][d] P^T[j][n]
+    for (int dc = 0; dc < dh; dc += 16) {
+        floatx4 vv[JT];
+#pragma unroll
+        for (int jt = 0; jt < JT; ++jt)
+#pragma unroll
+            for (int s4 = 0; s4 < 4; ++s4) {
+                const int j = jt * 16 + 4 * lg + s4;
+                vv[jt][s4] = (j < J) ? vb[j * rs + dc + lr] : 0.f;
+            }
+#pragma unroll
+        for (int nt = 0; nt < JT; ++nt) {
+            floatx4 o = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int jt = 0; jt < JT; ++jt) {
+                o = mfma4(vv[jt].x, S[jt][nt].x, o);
+                o = mfma4(vv[jt].y, S[jt][nt].y, o);
+                o = mfma4(vv[jt].z, S[jt][nt].z, o);
+                o = mfma4(vv[jt].w, S[jt][nt].w, o);
+            }
+            const int n = nt * 16 + lr;
+            if (n < J) {
+                float* ob = p.out + (b * J + n) * hid + h * dh + dc + 4 * lg;
+                *reinterpret_cast<floatx4*>(ob) = o;
+            }
+        }
+    }
+}
+
+hipError_t launch_attention(const AttnArgs& a, hipStream_t s) {
+    if (a.B <= 0) return hipSuccess;
+    const int64_t waves = a.B * a.heads;
+    const dim3 grid((unsigned)((waves + 3) / 4));
+    if (a.J <= 16) hipLaunchKernelGGL((k_attention<1>), grid, dim3(256), 0, s, a);
+    else if (a.J <= 32) hipLaunchKernelGGL((k_attention<2>), grid, dim3(256), 0, s, a);
+    else if (a.J <= 48) hipLaunchKernelGGL((k_attention<3>), grid, dim3(256), 0, s, a);
+    else hipLaunchKernelGGL((k_attention<4>), grid, dim3(256), 0, s, a);
+    return hipGetLastError();
+}
+
+// =============================================================================================
+// Counter-based noise: Philox4x32-10 (Salmon et al. SC'11) + Box-Muller.
+// ctr = (quad q within the row, step, row lo, row hi), key = (seed lo, seed hi);
+// u = ((x >> 8) + 0.5) * 2^-24; z = sqrt(-2 ln u0) * (cos, sin)(2 pi u1), (u2, u3) likewise.
+// Identical stream in oracle/skeldiff_oracle.py:philox_normal.
+// =============================================================================================
+
+__device__ __forceinline__ uint4 philox(uint4 c, uint32_t k0, uint32_t k1) {
+#pragma unroll
+    for (int r = 0; r < 10; ++r) {
+        const uint32_t hi0 = __umulhi(0xD2511F53u, c.x), lo0 = 0xD2511F53u * c.x;
+        const uint32_t hi1 = __umulhi(0xCD9E8D57u, c.z), lo1 = 0xCD9E8D57u * c.z;
+        c = make_uint4(hi1 ^ c.y ^ k0, lo1, hi0 ^ c.w ^ k1, lo0);
+        k0 += 0x9E3779B9u;
+        k1 += 0xBB67AE85u;
+    }
+    return c;
+}
+
+__device__ __forceinline__ float u01(uint32_t x) { return ((float)(x >> 8) + 0.5f) * 5.9604644775390625e-8f; }
+
+__device__ __forceinline__ floatx2 box_muller(uint32_t a, uint32_t b) {
+    const float rad = sqrtf(-2.0f * logf(u01(a)));
+    float sn, cs;
+    sincospif(2.0f * u01(b), &sn, &cs);
+    return floatx2{rad * cs, rad * sn};
+}
+
+__device__ __forceinline__ uint4 philox_at(uint64_t seed, uint64_t row, int step, uint32_t quad) {
+    return philox(make_uint4(quad, (uint32_t)step, (uint32_t)row, (uint32_t)(row >> 32)),
+                  (uint32_t)seed, (uint32_t)(seed >> 32));
+}
+
+// normals e and e+1 (e even) of the row
+__device__ __forceinline__ floatx2 noise_pair(uint64_t seed, uint64_t row, int step, uint32_t e) {
+    const uint4 x = philox_at(seed, row, step, e >> 2);
+    return ((e >> 1) & 1) ? box_muller(x.z, x.w) : box_muller(x.x, x.y);
+}
+
+__global__ __launch_bounds__(256) void k_noise_fill(float* out, int64_t rows, int64_t quads,
+                                                    uint64_t seed, int64_t row0, int step,
+                                                    const uint64_t* rng_dev) {
+    const int64_t g = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (g >= rows * quads) return;
+    if (rng_dev) {
+        seed = rng_dev[0];
+        row0 = (int64_t)rng_dev[1];
+    }
+    const int64_t r = g / quads;
+    const uint32_t q = (uint32_t)(g % quads);
+    const uint4 x = philox_at(seed, (uint64_t)(row0 + r), step, q);
+    const floatx2 z0 = box_muller(x.x, x.y), z1 = box_muller(x.z, x.w);
+    *reinterpret_cast<floatx4*>(out + 4 * g) = floatx4{z0.x, z0.y, z1.x, z1.y};
+}
+
+hipError_t launch_noise_fill(float* out, int64_t rows, int64_t n_per_row, uint64_t seed,
+                             int64_t row0, int step, const uint64_t* rng_dev, hipStream_t s) {
+    const int64_t quads = n_per_row / 4;
+    const int64_t n = rows * quads;
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_noise_fill, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, out, rows,
+                       quads, seed, row0, step, rng_dev);
+    return hipGetLastError();
+}
+
+__global__ void k_philox_raw(uint32_t* out, int64_t rows, int64_t quads, uint64_t seed,
+                             int64_t row0, int step) {
+    const int64_t g = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (g >= rows * quads) return;
+    const uint4 x = philox_at(seed, (uint64_t)(row0 + g / quads), step, (uint32_t)(g % quads));
+    reinterpret_cast<uint4*>(out)[g] = x;
+}
+
+hipError_t launch_philox_raw(uint32_t* out, int64_t rows, int64_t quads, uint64_t seed,
+                             int64_t row0, int step, hipStream_t s) {
+    const int64_t n = rows * quads;
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_philox_raw, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, out, rows,
+                       quads, seed, row0, step);
+    return hipGetLastError();
+}
+
+__global__ void k_set_rng(uint64_t* rng, uint64_t seed, int64_t row0) {
+    if (threadIdx.x == 0) {
+        rng[0] = seed;
+        rng[1] = (uint64_t)row0;
+    }
+}
+
+hipError_t launch_set_rng(uint64_t* rng_dev, uint64_t seed, int64_t row0, hipStream_t s) {
+    hipLaunchKernelGGL(k_set_rng, dim3(1), dim3(64), 0, s, rng_dev, seed, row0);
+    return hipGetLastError();
+}
+
+__global__ __launch_bounds__(256) void k_copy_rows(float* dst, int64_t dst_rs, const float* src,
+                                                   int64_t src_rs, int64_t rows, int64_t n) {
+    const int64_t g = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    const int64_t n4 = n / 4;
+    if (g >= rows * n4) return;
+    const int64_t r = g / n4, c = g % n4;
+    *reinterpret_cast<floatx4*>(dst + r * dst_rs + 4 * c) = ld4(src + r * src_rs + 4 * c);
+}
+
+hipError_t launch_copy_rows(float* dst, int64_t dst_rs, const float* src, int64_t src_rs,
+                            int64_t rows, int64_t n, hipStream_t s) {
+    const int64_t tot = rows * (n / 4);
+    if (tot <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_copy_rows, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, s, dst,
+                       dst_rs, src, src_rs, rows, n);
+    return hipGetLastError();
+}
+
+// =============================================================================================
+// Reverse-step update.  One thread per (row, feature pair): the J values of x0, x_t, eps of
+// its two features stay in registers; C1[t], C2[t], U and sigma_t come from LDS as
+// wave-uniform broadcasts.  HBM-bound: 4 * J * D * 4 B per row (x0, x_t, eps in; x_{t-1} out).
+// =============================================================================================
+
+template <int JM, bool EXACT>
+__global__ __launch_bounds__(256) void k_update(const UpdArgs p) {
+    __shared__ float sC1[JM * JM], sC2[JM * JM], sU[JM * JM], sS[JM];
+    const int J = EXACT ? JM : p.J;
+    if (!p.iso) {
+        for (int i = threadIdx.x; i < J * J; i += 256) {
+            sC1[i] = p.C1[i];
+            sC2[i] = p.C2[i];
+            sU[i] = p.U[i];
+        }
+        for (int i = threadIdx.x; i < J; i += 256) sS[i] = p.sig[i];
+    }
+    __syncthreads();
+    const int D = p.D;
+    const int DP = D >> 1;
+    const int64_t g = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    const int64_t row = g / DP;
+    if (row >= p.B) return;
+    const int d = 2 * (int)(g % DP);
+    const int64_t rb = row * (int64_t)J * D;
+
+    uint64_t seed = p.seed;
+    int64_t row0 = p.row0;
+    if (p.noise_mode == 2 && p.rng_dev) {
+        seed = p.rng_dev[0];
+        row0 = (int64_t)p.rng_dev[1];
+    }
+
+    floatx2 x0v[JM], xtv[JM], ev[JM];
+#pragma unroll
+    for (int j = 0; j < JM; ++j) {
+        if (!EXACT && j >= J) continue;
+        floatx2 a = ld2(p.x0 + rb + j * D + d);
+        if (p.act == 1) {
+            a.x = tanhf(a.x);
+            a.y = tanhf(a.y);
+        }
+        x0v[j] = floatx2{fminf(fmaxf(a.x, -1.f), 1.f), fminf(fmaxf(a.y, -1.f), 1.f)};
+        xtv[j] = ld2(p.xt + rb + j * D + d);
+        if (p.noise_mode == 1)
+            ev[j] = ld2(p.eps + row * p.eps_rs + j * D + d);
+        else if (p.noise_mode == 2)
+            ev[j] = noise_pair(seed, (uint64_t)(row0 + row), p.step, (uint32_t)(j * D + d));
+        else
+            ev[j] = floatx2{0.f, 0.f};
+        if (p.noise_out) st2(p.noise_out + row * p.noise_rs + j * D + d, ev[j]);
+    }
+
+    if (p.iso) {
+#pragma unroll
+        for (int j = 0; j < JM; ++j) {
+            if (!EXACT && j >= J) continue;
+            const floatx2 mean = p.c1s * x0v[j] + p.c2s * xtv[j];
+            const floatx2 v = (p.noise_mode != 0) ? mean + p.sigs * ev[j] : mean;
+            st2(p.out + rb + j * D + d, v);
+            if (p.out2) st2(p.out2 + row * p.out2_rs + j * D + d, v);
+            if (p.mean_out) st2(p.mean_out + row * p.mean_rs + j * D + d, mean);
+        }
+        return;
+    }
+    if (p.noise_mode != 0) {
+#pragma unroll
+        for (int j = 0; j < JM; ++j) {
+            if (!EXACT && j >= J) continue;
+            ev[j] *= sS[j];
+        }
+    }
+    for (int i = 0; i < J; ++i) {
+        floatx2 m1 = {0.f, 0.f}, m2 = {0.f, 0.f}, nz = {0.f, 0.f};
+#pragma unroll
+        for (int j = 0; j < JM; ++j) {
+            if (!EXACT && j >= J) continue;
+            m1 += sC1[i * J + j] * x0v[j];
+            m2 += sC2[i * J + j] * xtv[j];
+            nz += sU[i * J + j] * ev[j];
+        }
+        const floatx2 mean = m1 + m2;
+        const floatx2 v = (p.noise_mode != 0) ? mean + nz : mean;
+        st2(p.out + rb + i * D + d, v);
+        if (p.out2) st2(p.out2 + row * p.out2_rs + i * D + d, v);
+        if (p.mean_out) st2(p.mean_out + row * p.mean_rs + i * D + d, mean);
+    }
+}
+
+hipError_t launch_update(const UpdArgs& a, hipStream_t s) {
+    if (a.B <= 0) return hipSuccess;
+    const int64_t n = a.B * (a.D / 2);
+    const dim3 grid((unsigned)((n + 255) / 256));
+    switch (a.J) {
+        case 16: hipLaunchKernelGGL((k_update<16, true>), grid, dim3(256), 0, s, a); break;
+        case 17: hipLaunchKernelGGL((k_update<17, true>), grid, dim3(256), 0, s, a); break;
+        case 21: hipLaunchKernelGGL((k_update<21, true>), grid, dim3(256), 0, s, a); break;
+        case 51: hipLaunchKernelGGL((k_update<51, true>), grid, dim3(256), 0, s, a); break;
+        default:
+            if (a.J <= 16) hipLaunchKernelGGL((k_update<16, false>), grid, dim3(256), 0, s, a);
+            else if (a.J <= 32) hipLaunchKernelGGL((k_update<32, false>), grid, dim3(256), 0, s, a);
+            else hipLaunchKernelGGL((k_update<64, false>), grid, dim3(256), 0, s, a);
+    }
+    return hipGetLastError();
+}
+
+// =============================================================================================
+// One-time plan helpers
+// =============================================================================================
+
+// SinusoidalPosEmb (denoising_diffusion_pytorch 1.9.4, restated): emb[t] = [sin(t f), cos(t f)],
+// f_k = exp(k * neg_scale), neg_scale = -ln(theta)/(half-1) rounded to fp32 as torch does.
+__global__ void k_sinusoidal(float* emb, int T, int dim, float neg_scale) {
+    const int half = dim / 2;
+    const int g = blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= T * half) return;
+    const int t = g / half, k = g % half;
+    const float f = expf((float)k * neg_scale);
+    const float a = (float)t * f;
+    emb[t * dim + k] = sinf(a);
+    emb[t * dim + half + k] = cosf(a);
+}
+
+hipError_t launch_sinusoidal(float* emb, int T, int dim, float neg_scale, hipStream_t s) {
+    const int n = T * (dim / 2);
+    hipLaunchKernelGGL(k_sinusoidal, dim3((n + 255) / 256), dim3(256), 0, s, emb, T, dim, neg_scale);
+    return hipGetLastError();
+}
+
+// y[m][n] = out_act( sum_k in_act(x[m][k]) W[n][k] + b[n] ); in_act 1 = tanh, out_act 1 = GELU(erf)
+__global__ void k_linear(const float* x, int M, int K, const float* W, const float* b, int N,
+                         float* y, int in_act, int out_act) {
+    const int g = blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= M * N) return;
+    const int m = g / N, n = g % N;
+    float acc = 0.f;
+    for (int k = 0; k < K; ++k) {
+        float v = x[m * K + k];
+        if (in_act == 1) v = tanhf(v);
+        acc = fmaf(v, W[(int64_t)n * K + k], acc);
+    }
+    if (b) acc += b[n];
+    if (out_act == 1) acc = 0.5f * acc * (1.0f + erff(acc * 0.70710678118654752f));
+    y[g] = acc;
+}
+
+hipError_t launch_linear(const float* x, int M, int K, const float* W, const float* b, int N,
+                         float* y, int in_act, int out_act, hipStream_t s) {
+    const int n = M * N;
+    hipLaunchKernelGGL(k_linear, dim3((n + 255) / 256), dim3(256), 0, s, x, M, K, W, b, N, y,
+                       in_act, out_act);
+    return hipGetLastError();
+}
+
+// G-hat = F.normalize(G, p=1, dim=1) (row-L1, graph_structural.py:31-32) or G unchanged.
+__global__ void k_ghat(const float* G, float* Gh, int J, int normalize) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= J) return;
+    float s = 0.f;
+    for (int j = 0; j < J; ++j) s += fabsf(G[i * J + j]);
+    const float den = fmaxf(s, 1e-12f);
+    for (int j = 0; j < J; ++j) Gh[i * J + j] = normalize ? G[i * J + j] / den : G[i * J + j];
+}
+
+hipError_t launch_ghat(const float* G, float* Ghat, int J, int normalize, hipStream_t s) {
+    hipLaunchKernelGGL(k_ghat, dim3(1), dim3(64), 0, s, G, Ghat, J, normalize);
+    return hipGetLastError();
+}
+
+// RMSNorm gain folded into the following projection: W'[r][k] = W[r][k] * (g[k] * mult)
+__global__ void k_fold_gain(const float* W, const float* g, float mult, float* out, int64_t rows, int K) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= rows * K) return;
+    out[i] = W[i] * (g[i % K] * mult);
+}
+
+hipError_t launch_fold_gain(const float* W, const float* g, float mult, float* out, int64_t rows,
+                            int K, hipStream_t s) {
+    const int64_t n = rows * K;
+    hipLaunchKernelGGL(k_fold_gain, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, W, g, mult,
+                       out, rows, K);
+    return hipGetLastError();
+}
+
+// sigma_t = exp(0.5 * log_variance_clipped)   (nonisotropic.py:210)
+__global__ void k_sigma(const float* lv, float* sig, int64_t n) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) sig[i] = expf(0.5f * lv[i]);
+}
+
+hipError_t launch_sigma(const float* logvar, float* sig, int64_t n, hipStream_t s) {
+    hipLaunchKernelGGL(k_sigma, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, logvar, sig, n);
+    return hipGetLastError();
+}
+
+}  // namespace sd

@@ -1,0 +1,752 @@
+// Host side of libskeldiff: plan construction (state_dict-keyed tensor registry), one-time
+// packing, the per-step launch sequence of the Denoiser + posterior update, and the hipGraph
+// capture of the whole T-step chain.  Implements include/skeldiff.h.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/skeldiff.h"
+#include "sd_internal.h"
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+    g_err = msg;
+    return code;
+}
+
+#define SD_HIP(x)                                                                              \
+    do {                                                                                       \
+        hipError_t e_ = (x);                                                                   \
+        if (e_ != hipSuccess) return fail(SD_E_HIP, std::string(#x) + ": " + hipGetErrorString(e_)); \
+    } while (0)
+
+struct Slot {
+    std::string name;
+    int64_t numel = 0;
+    float* dev = nullptr;
+    bool set = false;
+};
+
+// One StaticGraphLinear of the plan.
+struct GL {
+    int w = -1, g = -1, b = -1;  // slot indices (b = -1: no bias)
+    int K1 = 0, K2 = 0, N = 0;
+    float* ghat = nullptr;       // packed (J, J)
+    const float* wuse = nullptr; // weights used by the kernel (folded copy for RMS layers)
+    bool rms = false;
+    int gain = -1;               // RMSNorm gain slot folded into this layer
+};
+
+struct GraphKey {
+    int64_t rows;
+    const void* ptrs[10];
+    int64_t cond_repeat;
+    int32_t flags;
+    void* stream;
+    bool operator<(const GraphKey& o) const { return std::memcmp(this, &o, sizeof(GraphKey)) < 0; }
+};
+
+}  // namespace
+
+struct sd_plan {
+    sd_plan_desc d{};
+    int J = 0, D = 0, C = 0, H = 0, O = 0, hid = 0, T = 0, depth = 0, nres = 0, ntypes = 1;
+    std::vector<int> types;
+    std::vector<Slot> slots;
+    std::map<std::string, int> index;
+    bool finalized = false;
+    std::vector<void*> allocs;
+
+    GL init_lin;
+    std::vector<GL> r1, r2;        // ResnetBlock block1/block2 for layers.{L}.0, L < 2*depth, then final
+    std::vector<int> mlp_w, mlp_b; // ResnetBlock mlp.1 weight/bias slots (FiLM)
+    std::vector<GL> qkv, outp;     // attention (or single GL when use_attention == 0)
+    std::vector<bool> has_attn;
+    GL fres_res, fglin;
+    int t1w = -1, t1b = -1, t3w = -1, t3b = -1;
+    int s_c1 = -1, s_c2 = -1, s_lv = -1, s_u = -1;
+
+    float* film = nullptr;  // (nres, T, 2H) raw Linear(tanh(temb)) outputs
+    float* sig = nullptr;   // (T, J) or (T)
+    std::vector<float> iso_c1, iso_c2, iso_sig;  // host copies of the scalar tables (isotropic)
+
+    std::mutex gmu;
+    std::map<GraphKey, hipGraphExec_t> graphs;
+
+    ~sd_plan() {
+        for (auto& kv : graphs) (void)hipGraphExecDestroy(kv.second);
+        for (auto& s : slots)
+            if (s.dev) (void)hipFree(s.dev);
+        for (void* p : allocs) (void)hipFree(p);
+    }
+
+    int add(const std::string& name, int64_t numel) {
+        const int id = (int)slots.size();
+        slots.push_back(Slot{name, numel, nullptr, false});
+        index[name] = id;
+        return id;
+    }
+    GL add_gl(const std::string& name, int K1, int K2, int N, bool bias) {
+        GL g;
+        const int64_t K = K1 + K2;
+        g.g = add(name + ".G", (int64_t)J * J);
+        g.w = add(name + ".weight", (int64_t)ntypes * N * K);
+        g.b = bias ? add(name + ".bias", (int64_t)ntypes * N) : -1;
+        g.K1 = K1;
+        g.K2 = K2;
+        g.N = N;
+        return g;
+    }
+    const float* ptr(int slot) const { return slot < 0 ? nullptr : slots[slot].dev; }
+};
+
+namespace {
+
+int check_dims(const sd_plan_desc* d) {
+    if (!d) return fail(SD_E_INVALID, "null desc");
+    if (d->num_nodes < 1 || d->num_nodes > sd::kMaxNodes)
+        return fail(SD_E_INVALID, "num_nodes must be in [1, 64]");
+    if (d->latent_dim <= 0 || d->latent_dim % 16) return fail(SD_E_INVALID, "latent_dim must be a positive multiple of 16");
+    if (d->cond_dim != 0 && d->cond_dim % 16) return fail(SD_E_INVALID, "cond_dim must be 0 or a multiple of 16");
+    if (d->out_dim != d->latent_dim) return fail(SD_E_INVALID, "out_dim must equal latent_dim for sampling");
+    if (d->depth < 1) return fail(SD_E_INVALID, "depth must be >= 1");
+    if (d->self_condition) return fail(SD_E_INVALID, "self_condition=True is not supported by the sampling engine");
+    if (d->use_attention && (d->attn_heads < 1 || d->attn_dim_head <= 0 || d->attn_dim_head % 16))
+        return fail(SD_E_INVALID, "attn_dim_head must be a positive multiple of 16");
+    if (d->timesteps < 1) return fail(SD_E_INVALID, "timesteps must be >= 1");
+    if (d->activation != 0 && d->activation != 1) return fail(SD_E_INVALID, "activation must be 0 (identity) or 1 (tanh)");
+    return SD_OK;
+}
+
+template <typename T>
+int dalloc(sd_plan* p, T** out, size_t n) {
+    void* q = nullptr;
+    if (hipMalloc(&q, n * sizeof(T) + 16) != hipSuccess) return fail(SD_E_NOMEM, "hipMalloc failed");
+    p->allocs.push_back(q);
+    *out = (T*)q;
+    return SD_OK;
+}
+
+// workspace carve (all offsets 256-B aligned)
+struct WS {
+    uint64_t* rng;
+    float *x, *r, *h, *qkv, *o, *res, *x0, *img0, *img1;
+};
+
+size_t align256(size_t v) { return (v + 255) & ~(size_t)255; }
+
+size_t carve(const sd_plan* p, int64_t rows, char* base, WS* w) {
+    const size_t f = sizeof(float);
+    const size_t nH = (size_t)rows * p->J * p->H * f;
+    const size_t nQ = (size_t)rows * p->J * (p->d.use_attention ? 3 * p->hid : p->H) * f;
+    const size_t nO = (size_t)rows * p->J * (p->d.use_attention ? p->hid : 1) * f;
+    const size_t nD = (size_t)rows * p->J * p->D * f;
+    size_t off = 0;
+    auto take = [&](size_t n) {
+        char* q = base ? base + off : nullptr;
+        off += align256(n);
+        return q;
+    };
+    WS tmp;
+    WS& W = w ? *w : tmp;
+    W.rng = (uint64_t*)take(64);
+    W.x = (float*)take(nH);
+    W.r = (float*)take(nH);
+    W.h = (float*)take(nH);
+    W.qkv = (float*)take(nQ);
+    W.o = (float*)take(nO);
+    W.res = (float*)take(nH);
+    W.x0 = (float*)take(nD);
+    W.img0 = (float*)take(nD);
+    W.img1 = (float*)take(nD);
+    return off;
+}
+
+sd::GLArgs gl_args(const sd_plan* p, const GL& g, const float* x1, int x1_div, const float* x2,
+                   const float* film, const float* res, float* out, int64_t rows) {
+    sd::GLArgs a{};
+    a.x1 = x1;
+    a.K1 = g.K1;
+    a.x1_rs = (int64_t)p->J * g.K1;
+    a.x1_div = x1_div;
+    a.x2 = x2;
+    a.K2 = g.K2;
+    a.x2_rs = (int64_t)p->J * g.K2;
+    a.W = g.wuse;
+    a.bias = p->ptr(g.b);
+    a.G = g.ghat;
+    a.film = film;
+    a.res = res;
+    a.res_rs = (int64_t)p->J * g.N;
+    a.out = out;
+    a.out_rs = (int64_t)p->J * g.N;
+    a.B = rows;
+    a.N = g.N;
+    a.J = p->J;
+    a.act = 0;
+    for (int j = 0; j < p->J; ++j) a.wrow[j] = p->types[j] * g.N;
+    return a;
+}
+
+// Optional per-launch event timing (sd_profile_step): classes 0 graph-linear, 1 attention,
+// 2 update.  Events are recorded on the launch stream around each kernel.
+struct Prof {
+    std::vector<int> cls;
+    std::vector<hipEvent_t> ev;  // pairs
+    int pre(int c, hipStream_t s) {
+        hipEvent_t a, b;
+        if (hipEventCreate(&a) != hipSuccess || hipEventCreate(&b) != hipSuccess) return -1;
+        cls.push_back(c);
+        ev.push_back(a);
+        ev.push_back(b);
+        return hipEventRecord(a, s) == hipSuccess ? 0 : -1;
+    }
+    int post(hipStream_t s) { return hipEventRecord(ev.back(), s) == hipSuccess ? 0 : -1; }
+    ~Prof() {
+        for (auto e : ev) (void)hipEventDestroy(e);
+    }
+};
+
+#define SD_LAUNCH(prof, c, expr)                                                               \
+    do {                                                                                       \
+        if (prof && prof->pre(c, s)) return fail(SD_E_HIP, "hipEventRecord failed");          \
+        SD_HIP(expr);                                                                          \
+        if (prof && prof->post(s)) return fail(SD_E_HIP, "hipEventRecord failed");            \
+    } while (0)
+
+// Denoiser.forward (generator.py:86-107) for `rows` rows at time t.
+int run_denoiser(const sd_plan* p, const float* x_t, const float* x_cond, int64_t cond_repeat,
+                 int t, float* x0_out, int64_t rows, const WS& w, hipStream_t s, Prof* prof = nullptr) {
+    const int H = p->H;
+    // init_lin on cat([x_cond, x]) (generator.py:91-94)
+    sd::GLArgs a;
+    // The init_lin output is `r` (generator.py:95, r = x.clone()); it is written to w.r and the
+    // first ResnetBlock reads it from there and writes its result to w.x, so no copy is needed.
+    if (p->C > 0)
+        a = gl_args(p, p->init_lin, x_cond, (int)cond_repeat, x_t, nullptr, nullptr, w.r, rows);
+    else
+        a = gl_args(p, p->init_lin, x_t, 1, nullptr, nullptr, nullptr, w.r, rows);
+    SD_LAUNCH(prof, 0, sd::launch_graph_linear(a, false, s));
+
+    const int L = 2 * p->depth;
+    for (int l = 0; l < L; ++l) {
+        const float* film = p->film + ((size_t)l * p->T + t) * 2 * H;
+        const float* xin = (l == 0) ? w.r : w.x;
+        // ResnetBlock: h = tanh(FiLM(GL1 x)); x = tanh(GL2 h) + x     (attention.py:96-102)
+        a = gl_args(p, p->r1[l], xin, 1, nullptr, film, nullptr, w.h, rows);
+        a.act = 1;
+        SD_LAUNCH(prof, 0, sd::launch_graph_linear(a, false, s));
+        a = gl_args(p, p->r2[l], w.h, 1, nullptr, nullptr, xin, w.x, rows);
+        a.act = 1;
+        SD_LAUNCH(prof, 0, sd::launch_graph_linear(a, false, s));
+        if (!p->has_attn[l]) continue;
+        if (p->d.use_attention) {
+            // Residual(PreNorm(Attention)): x = to_out(attn(to_qkv(rmsnorm(x)))) + x
+            a = gl_args(p, p->qkv[l], w.x, 1, nullptr, nullptr, nullptr, w.qkv, rows);
+            SD_LAUNCH(prof, 0, sd::launch_graph_linear(a, true, s));
+            // q * dim_head ** -0.5 (attention.py:114,128): Python double scalar cast to fp32
+            sd::AttnArgs aa{w.qkv, w.o, rows, p->J, p->d.attn_heads, p->d.attn_dim_head,
+                            (float)std::pow((double)p->d.attn_dim_head, -0.5)};
+            SD_LAUNCH(prof, 1, sd::launch_attention(aa, s));
+            a = gl_args(p, p->outp[l], w.o, 1, nullptr, nullptr, w.x, w.x, rows);
+            SD_LAUNCH(prof, 0, sd::launch_graph_linear(a, false, s));
+        } else {
+            // Residual(PreNorm(StaticGraphLinear)): x = GL(rmsnorm(x)) + x
+            a = gl_args(p, p->qkv[l], w.x, 1, nullptr, nullptr, w.x, w.x, rows);
+            SD_LAUNCH(prof, 0, sd::launch_graph_linear(a, true, s));
+        }
+    }
+    // final_res_block on cat(x, r) (generator.py:104-106)
+    const float* film = p->film + ((size_t)L * p->T + t) * 2 * H;
+    a = gl_args(p, p->fres_res, w.x, 1, w.r, nullptr, nullptr, w.res, rows);
+    SD_LAUNCH(prof, 0, sd::launch_graph_linear(a, false, s));
+    a = gl_args(p, p->r1[L], w.x, 1, w.r, film, nullptr, w.h, rows);
+    a.act = 1;
+    SD_LAUNCH(prof, 0, sd::launch_graph_linear(a, false, s));
+    a = gl_args(p, p->r2[L], w.h, 1, nullptr, nullptr, w.res, w.res, rows);
+    a.act = 1;
+    SD_LAUNCH(prof, 0, sd::launch_graph_linear(a, false, s));
+    // final_glin (generator.py:107)
+    a = gl_args(p, p->fglin, w.res, 1, nullptr, nullptr, nullptr, x0_out, rows);
+    SD_LAUNCH(prof, 0, sd::launch_graph_linear(a, false, s));
+    return SD_OK;
+}
+
+int run_update(const sd_plan* p, const float* x0, const float* xt, const float* eps,
+               int64_t eps_rs, int noise_mode, uint64_t seed, int64_t row0,
+               const uint64_t* rng_dev, int t, float* out, float* out2, int64_t out2_rs,
+               float* mean_out, int64_t mean_rs, float* noise_out, int64_t noise_rs, int64_t rows,
+               hipStream_t s, Prof* prof = nullptr) {
+    sd::UpdArgs u{};
+    u.x0 = x0;
+    u.xt = xt;
+    u.eps = eps;
+    u.eps_rs = eps_rs;
+    u.iso = p->d.isotropic;
+    u.act = p->d.activation;
+    u.noise_mode = (t > 0) ? noise_mode : 0;
+    u.seed = seed;
+    u.row0 = row0;
+    u.step = t;
+    u.rng_dev = rng_dev;
+    u.out = out;
+    u.out2 = out2;
+    u.out2_rs = out2_rs;
+    u.mean_out = mean_out;
+    u.mean_rs = mean_rs;
+    u.noise_out = noise_out;
+    u.noise_rs = noise_rs;
+    u.B = rows;
+    u.J = p->J;
+    u.D = p->D;
+    if (p->d.isotropic) {
+        u.c1s = p->iso_c1[t];
+        u.c2s = p->iso_c2[t];
+        u.sigs = p->iso_sig[t];
+    } else {
+        const size_t JJ = (size_t)p->J * p->J;
+        u.C1 = p->ptr(p->s_c1) + t * JJ;
+        u.C2 = p->ptr(p->s_c2) + t * JJ;
+        u.U = p->ptr(p->s_u);
+        u.sig = p->sig + (size_t)t * p->J;
+    }
+    SD_LAUNCH(prof, 2, sd::launch_update(u, s));
+    return SD_OK;
+}
+
+// algorithmic FLOPs of one reverse step for `rows` rows: [graph-linear, attention, update]
+void step_flops(const sd_plan* p, int64_t rows, double* f) {
+    const double J = p->J, R = (double)rows;
+    auto gl = [&](const GL& g) { return 2.0 * R * J * g.N * (g.K1 + g.K2) + 2.0 * R * J * J * g.N; };
+    f[0] = gl(p->init_lin) + gl(p->fres_res) + gl(p->fglin);
+    for (auto& g : p->r1) f[0] += gl(g);
+    for (auto& g : p->r2) f[0] += gl(g);
+    f[1] = 0.0;
+    for (size_t l = 0; l < p->has_attn.size(); ++l) {
+        if (!p->has_attn[l]) continue;
+        f[0] += gl(p->qkv[l]);
+        if (p->d.use_attention) {
+            f[0] += gl(p->outp[l]);
+            f[1] += 4.0 * R * J * J * p->d.attn_dim_head * p->d.attn_heads;  // QK^T and PV
+        }
+    }
+    // C1 x0 + C2 x_t + U (sigma eps): three J x J products per latent column
+    f[2] = p->d.isotropic ? 6.0 * R * J * p->D : 6.0 * R * J * J * p->D;
+}
+
+}  // namespace
+
+extern "C" {
+
+int32_t sd_abi_version(void) { return SD_ABI_VERSION; }
+
+const char* sd_last_error(void) { return g_err.c_str(); }
+
+int sd_plan_create(sd_plan** out, const sd_plan_desc* desc) {
+    if (!out) return fail(SD_E_INVALID, "null out");
+    *out = nullptr;
+    int rc = check_dims(desc);
+    if (rc) return rc;
+    std::unique_ptr<sd_plan> p(new sd_plan());
+    p->d = *desc;
+    p->J = desc->num_nodes;
+    p->D = desc->latent_dim;
+    p->C = desc->cond_dim;
+    p->H = desc->latent_dim + desc->cond_dim;
+    p->O = desc->out_dim;
+    p->hid = desc->use_attention ? desc->attn_heads * desc->attn_dim_head : 0;
+    p->T = desc->timesteps;
+    p->depth = desc->depth;
+    p->types.assign(p->J, 0);
+    if (desc->num_node_types > 0) {
+        if (!desc->node_types) return fail(SD_E_INVALID, "node_types is null");
+        for (int j = 0; j < p->J; ++j) {
+            const int64_t v = desc->node_types[j];
+            if (v < 0 || v >= desc->num_node_types) return fail(SD_E_INVALID, "node_types out of range");
+            p->types[j] = (int)v;
+        }
+        p->ntypes = desc->num_node_types;
+    }
+    const int J = p->J, H = p->H, hid = p->hid;
+    p->ntypes = desc->num_node_types > 0 ? desc->num_node_types : 1;
+
+    // tensor registry in the reference layout (generator.py:30-84)
+    const std::string m = "model.";
+    p->init_lin = p->add_gl(m + "init_lin", p->C > 0 ? p->C : p->D, p->C > 0 ? p->D : 0, H, true);
+    p->t1w = p->add(m + "time_mlp.1.weight", (int64_t)4 * H * H);
+    p->t1b = p->add(m + "time_mlp.1.bias", 4 * H);
+    p->t3w = p->add(m + "time_mlp.3.weight", (int64_t)16 * H * H);
+    p->t3b = p->add(m + "time_mlp.3.bias", 4 * H);
+    const int L = 2 * p->depth;
+    p->qkv.resize(L);
+    p->outp.resize(L);
+    p->has_attn.assign(L, false);
+    for (int l = 0; l < L; ++l) {
+        const std::string r = m + "layers." + std::to_string(l) + ".0.";
+        p->mlp_w.push_back(p->add(r + "mlp.1.weight", (int64_t)2 * H * 4 * H));
+        p->mlp_b.push_back(p->add(r + "mlp.1.bias", 2 * H));
+        p->r1.push_back(p->add_gl(r + "block1.proj", H, 0, H, true));
+        p->r2.push_back(p->add_gl(r + "block2.proj", H, 0, H, true));
+        const bool attn = (l != L - 1);  // generator.py:71-76: last layer gets nn.Identity
+        p->has_attn[l] = attn;
+        if (!attn) continue;
+        const std::string a = m + "layers." + std::to_string(l) + ".1.fn.";
+        const int gain = p->add(a + "norm.g", H);
+        if (desc->use_attention) {
+            p->qkv[l] = p->add_gl(a + "fn.to_qkv", H, 0, 3 * hid, false);
+            p->outp[l] = p->add_gl(a + "fn.to_out", hid, 0, H, false);
+        } else {
+            p->qkv[l] = p->add_gl(a + "fn", H, 0, H, false);
+        }
+        p->qkv[l].rms = true;
+        p->qkv[l].gain = gain;
+    }
+    {
+        const std::string r = m + "final_res_block.";
+        p->mlp_w.push_back(p->add(r + "mlp.1.weight", (int64_t)2 * H * 4 * H));
+        p->mlp_b.push_back(p->add(r + "mlp.1.bias", 2 * H));
+        p->r1.push_back(p->add_gl(r + "block1.proj", H, H, H, true));
+        p->r2.push_back(p->add_gl(r + "block2.proj", H, 0, H, true));
+        p->fres_res = p->add_gl(r + "res_linear", H, H, H, false);
+    }
+    p->fglin = p->add_gl(m + "final_glin", H, 0, p->O, true);
+    p->nres = L + 1;
+    if (desc->isotropic) {
+        p->s_c1 = p->add("posterior_mean_coef1", p->T);
+        p->s_c2 = p->add("posterior_mean_coef2", p->T);
+        p->s_lv = p->add("posterior_log_variance_clipped", p->T);
+    } else {
+        p->s_c1 = p->add("posterior_mean_coef1_x0", (int64_t)p->T * J * J);
+        p->s_c2 = p->add("posterior_mean_coef2_xt", (int64_t)p->T * J * J);
+        p->s_lv = p->add("Lambda_posterior_log_variance_clipped", (int64_t)p->T * J);
+        p->s_u = p->add("U", (int64_t)J * J);
+    }
+    *out = p.release();
+    return SD_OK;
+}
+
+void sd_plan_destroy(sd_plan* plan) { delete plan; }
+
+int32_t sd_plan_num_tensors(const sd_plan* plan) { return plan ? (int32_t)plan->slots.size() : 0; }
+
+const char* sd_plan_tensor_name(const sd_plan* plan, int32_t i) {
+    if (!plan || i < 0 || i >= (int32_t)plan->slots.size()) return nullptr;
+    return plan->slots[i].name.c_str();
+}
+
+int64_t sd_plan_tensor_numel(const sd_plan* plan, int32_t i) {
+    if (!plan || i < 0 || i >= (int32_t)plan->slots.size()) return -1;
+    return plan->slots[i].numel;
+}
+
+int sd_plan_set_tensor(sd_plan* plan, const char* name, const float* data, int64_t numel, void* stream) {
+    if (!plan || !name || !data) return fail(SD_E_INVALID, "null argument");
+    if (plan->finalized) return fail(SD_E_STATE, "plan already finalized");
+    auto it = plan->index.find(name);
+    if (it == plan->index.end()) return fail(SD_E_INVALID, std::string("unexpected tensor: ") + name);
+    Slot& s = plan->slots[it->second];
+    if (numel != s.numel)
+        return fail(SD_E_INVALID, std::string("size mismatch for ") + name + ": got " +
+                                      std::to_string(numel) + ", expected " + std::to_string(s.numel));
+    if (!s.dev) SD_HIP(hipMalloc(&s.dev, (size_t)numel * sizeof(float) + 16));
+    SD_HIP(hipMemcpyAsync(s.dev, data, (size_t)numel * sizeof(float), hipMemcpyDefault, (hipStream_t)stream));
+    // the source may be pageable host memory the caller frees right after: complete the copy
+    SD_HIP(hipStreamSynchronize((hipStream_t)stream));
+    s.set = true;
+    return SD_OK;
+}
+
+int sd_plan_finalize(sd_plan* p, void* stream_) {
+    if (!p) return fail(SD_E_INVALID, "null plan");
+    if (p->finalized) return SD_OK;
+    for (auto& s : p->slots)
+        if (!s.set) return fail(SD_E_STATE, "missing tensor: " + s.name);
+    hipStream_t s = (hipStream_t)stream_;
+    const int J = p->J, H = p->H, T = p->T;
+    int rc;
+
+    auto pack_gl = [&](GL& g) -> int {
+        int r = dalloc(p, &g.ghat, (size_t)J * J);
+        if (r) return r;
+        SD_HIP(sd::launch_ghat(p->ptr(g.g), g.ghat, J, p->d.learn_influence, s));
+        g.wuse = p->ptr(g.w);
+        if (g.rms) {  // fold RMSNorm gain * sqrt(dim) (attention.py:36) into the projection
+            float* wf = nullptr;
+            const int64_t K = g.K1 + g.K2;
+            const int64_t rows = (int64_t)p->ntypes * g.N;
+            r = dalloc(p, &wf, (size_t)(rows * K));
+            if (r) return r;
+            SD_HIP(sd::launch_fold_gain(p->ptr(g.w), p->ptr(g.gain), std::sqrt((float)H), wf, rows, (int)K, s));
+            g.wuse = wf;
+        }
+        return SD_OK;
+    };
+    if ((rc = pack_gl(p->init_lin))) return rc;
+    for (auto& g : p->r1)
+        if ((rc = pack_gl(g))) return rc;
+    for (auto& g : p->r2)
+        if ((rc = pack_gl(g))) return rc;
+    for (size_t l = 0; l < p->qkv.size(); ++l) {
+        if (!p->has_attn[l]) continue;
+        if ((rc = pack_gl(p->qkv[l]))) return rc;
+        if (p->d.use_attention && (rc = pack_gl(p->outp[l]))) return rc;
+    }
+    if ((rc = pack_gl(p->fres_res))) return rc;
+    if ((rc = pack_gl(p->fglin))) return rc;
+
+    // time MLP (generator.py:50-55, 97) and per-block FiLM tables (attention.py:81-84, 96-100)
+    float *emb = nullptr, *t1 = nullptr, *temb = nullptr;
+    if ((rc = dalloc(p, &emb, (size_t)T * H))) return rc;
+    if ((rc = dalloc(p, &t1, (size_t)T * 4 * H))) return rc;
+    if ((rc = dalloc(p, &temb, (size_t)T * 4 * H))) return rc;
+    const int half = H / 2;
+    if (half < 2) return fail(SD_E_INVALID, "model dim too small for the sinusoidal embedding");
+    const float neg_scale = (float)(-(std::log((double)p->d.sinusoidal_theta) / (double)(half - 1)));
+    SD_HIP(sd::launch_sinusoidal(emb, T, H, neg_scale, s));
+    SD_HIP(sd::launch_linear(emb, T, H, p->ptr(p->t1w), p->ptr(p->t1b), 4 * H, t1, 0, 1, s));
+    SD_HIP(sd::launch_linear(t1, T, 4 * H, p->ptr(p->t3w), p->ptr(p->t3b), 4 * H, temb, 0, 0, s));
+    if ((rc = dalloc(p, &p->film, (size_t)p->nres * T * 2 * H))) return rc;
+    for (int r = 0; r < p->nres; ++r)
+        SD_HIP(sd::launch_linear(temb, T, 4 * H, p->ptr(p->mlp_w[r]), p->ptr(p->mlp_b[r]), 2 * H,
+                                 p->film + (size_t)r * T * 2 * H, 1, 0, s));
+
+    // posterior tables
+    if (p->d.isotropic) {
+        std::vector<float> lv(T);
+        p->iso_c1.resize(T);
+        p->iso_c2.resize(T);
+        p->iso_sig.resize(T);
+        SD_HIP(hipMemcpyAsync(p->iso_c1.data(), p->ptr(p->s_c1), T * sizeof(float), hipMemcpyDeviceToHost, s));
+        SD_HIP(hipMemcpyAsync(p->iso_c2.data(), p->ptr(p->s_c2), T * sizeof(float), hipMemcpyDeviceToHost, s));
+        SD_HIP(hipMemcpyAsync(lv.data(), p->ptr(p->s_lv), T * sizeof(float), hipMemcpyDeviceToHost, s));
+        SD_HIP(hipStreamSynchronize(s));
+        for (int t = 0; t < T; ++t) p->iso_sig[t] = std::exp(0.5f * lv[t]);
+    } else {
+        if ((rc = dalloc(p, &p->sig, (size_t)T * J))) return rc;
+        SD_HIP(sd::launch_sigma(p->ptr(p->s_lv), p->sig, (int64_t)T * J, s));
+    }
+    SD_HIP(hipStreamSynchronize(s));
+    SD_HIP(hipFree(emb));
+    SD_HIP(hipFree(t1));
+    SD_HIP(hipFree(temb));
+    for (auto it = p->allocs.begin(); it != p->allocs.end();) {
+        if (*it == emb || *it == t1 || *it == temb) it = p->allocs.erase(it);
+        else ++it;
+    }
+    p->finalized = true;
+    return SD_OK;
+}
+
+size_t sd_workspace_bytes(const sd_plan* plan, int64_t rows) {
+    if (!plan || rows < 0) return 0;
+    return carve(plan, rows, nullptr, nullptr) + 256;
+}
+
+int32_t sd_plan_kernels_per_step(const sd_plan* p) {
+    if (!p) return 0;
+    int n = 1;  // init_lin
+    for (size_t l = 0; l < p->has_attn.size(); ++l) n += 2 + (p->has_attn[l] ? (p->d.use_attention ? 3 : 1) : 0);
+    n += 4 + 1;     // final res block (3) + final_glin + update
+    return n;
+}
+
+static int ws_setup(const sd_plan* p, int64_t rows, void* ws, size_t bytes, WS* w) {
+    if (!p || !p->finalized) return fail(SD_E_STATE, "plan is not finalized");
+    if (rows < 0) return fail(SD_E_INVALID, "rows < 0");
+    const size_t need = carve(p, rows, nullptr, nullptr);
+    if (!ws || bytes < need) return fail(SD_E_INVALID, "workspace too small: need " + std::to_string(need));
+    char* base = (char*)(((uintptr_t)ws + 255) & ~(uintptr_t)255);
+    if ((size_t)(base - (char*)ws) + need > bytes) return fail(SD_E_INVALID, "workspace too small after alignment");
+    carve(p, rows, base, w);
+    return SD_OK;
+}
+
+int sd_denoiser_forward(const sd_plan* p, const float* x_t, const float* x_cond, int64_t cond_repeat,
+                        int32_t t, float* x0_out, int64_t rows, void* workspace, size_t ws_bytes,
+                        void* stream) {
+    WS w;
+    int rc = ws_setup(p, rows, workspace, ws_bytes, &w);
+    if (rc) return rc;
+    if (t < 0 || t >= p->T) return fail(SD_E_INVALID, "t out of range");
+    if (!x_t || !x0_out) return fail(SD_E_INVALID, "null tensor");
+    if (p->C > 0 && !x_cond) return fail(SD_E_INVALID, "x_cond is required (diffusion_conditioning)");
+    if (cond_repeat < 1) return fail(SD_E_INVALID, "cond_repeat must be >= 1");
+    return run_denoiser(p, x_t, x_cond, cond_repeat, t, x0_out, rows, w, (hipStream_t)stream);
+}
+
+int sd_p_sample_update(const sd_plan* p, const float* x0_raw, const float* x_t, const float* eps,
+                       int64_t eps_rs, uint64_t seed, int64_t row0, int32_t t, float* x_prev,
+                       float* mean_out, int64_t mean_rs, float* noise_out, int64_t noise_rs,
+                       int64_t rows, void* stream) {
+    if (!p || !p->finalized) return fail(SD_E_STATE, "plan is not finalized");
+    if (t < 0 || t >= p->T) return fail(SD_E_INVALID, "t out of range");
+    if (!x0_raw || !x_t || !x_prev) return fail(SD_E_INVALID, "null tensor");
+    if (!eps && p->D % 4) return fail(SD_E_INVALID, "device noise needs latent_dim % 4 == 0");
+    const int64_t JD = (int64_t)p->J * p->D;
+    return run_update(p, x0_raw, x_t, eps, eps ? eps_rs : JD, eps ? 1 : 2, seed, row0, nullptr, t,
+                      x_prev, nullptr, 0, mean_out, mean_out ? mean_rs : JD, noise_out,
+                      noise_out ? noise_rs : JD, rows, (hipStream_t)stream);
+}
+
+static int record_loop(const sd_plan* p, const float* x_T, const float* x_cond, int64_t cond_repeat,
+                       const float* eps_all, uint64_t seed, int64_t row0, float* out, float* means,
+                       float* noise_out, float* timages, float* start_out, int64_t rows, const WS& w,
+                       int32_t flags, bool use_rng_dev, hipStream_t s) {
+    const int T = p->T;
+    const int64_t JD = (int64_t)p->J * p->D;
+    const int64_t step_rs = (int64_t)(T > 1 ? T - 1 : 1) * JD;  // row stride of (B, T-1, J, D)
+    const uint64_t* rng = use_rng_dev ? w.rng : nullptr;
+    const float* cur = x_T;
+    if (flags & SD_FLAG_DEVICE_START) {
+        SD_HIP(sd::launch_noise_fill(w.img1, rows, JD, seed, row0, T, rng, s));
+        cur = w.img1;
+    }
+    if (start_out) SD_HIP(sd::launch_copy_rows(start_out, JD, cur, JD, rows, JD, s));
+    const bool dev_noise = (flags & SD_FLAG_DEVICE_NOISE) != 0;
+    for (int t = T - 1; t >= 0; --t) {
+        int rc = run_denoiser(p, cur, x_cond, cond_repeat, t, w.x0, rows, w, s);
+        if (rc) return rc;
+        float* nxt = (t == 0) ? out : (((T - 1 - t) & 1) ? w.img1 : w.img0);
+        const int64_t k = T - 1 - t;  // index into the (B, T-1, ...) records
+        const float* eps = (!dev_noise && t > 0) ? eps_all + k * JD : nullptr;
+        const bool rec = t > 0;
+        rc = run_update(p, w.x0, cur, eps, step_rs, dev_noise ? 2 : 1, seed, row0, rng, t, nxt,
+                        (rec && timages) ? timages + k * JD : nullptr, step_rs,
+                        (rec && means) ? means + k * JD : nullptr, step_rs,
+                        (rec && noise_out) ? noise_out + k * JD : nullptr, step_rs, rows, s);
+        if (rc) return rc;
+        cur = nxt;
+    }
+    return SD_OK;
+}
+
+int sd_sample_loop(const sd_plan* p, const float* x_T, const float* x_cond, int64_t cond_repeat,
+                   const float* eps_all, uint64_t seed, int64_t row0, float* out, float* means_out,
+                   float* noise_out, float* timages_out, float* start_out, int64_t rows,
+                   void* workspace, size_t ws_bytes, int32_t flags, void* stream) {
+    WS w;
+    int rc = ws_setup(p, rows, workspace, ws_bytes, &w);
+    if (rc) return rc;
+    if (!out) return fail(SD_E_INVALID, "null out");
+    if (!(flags & SD_FLAG_DEVICE_START) && !x_T) return fail(SD_E_INVALID, "x_T is null (pass SD_FLAG_DEVICE_START)");
+    if (!(flags & SD_FLAG_DEVICE_NOISE) && p->T > 1 && !eps_all)
+        return fail(SD_E_INVALID, "eps_all is null (pass SD_FLAG_DEVICE_NOISE)");
+    if ((flags & (SD_FLAG_DEVICE_START | SD_FLAG_DEVICE_NOISE)) && p->D % 4)
+        return fail(SD_E_INVALID, "device noise needs latent_dim % 4 == 0");
+    if (p->C > 0 && !x_cond) return fail(SD_E_INVALID, "x_cond is required (diffusion_conditioning)");
+    if (cond_repeat < 1) return fail(SD_E_INVALID, "cond_repeat must be >= 1");
+    if (rows == 0) return SD_OK;
+    hipStream_t s = (hipStream_t)stream;
+    if (!(flags & SD_FLAG_GRAPH))
+        return record_loop(p, x_T, x_cond, cond_repeat, eps_all, seed, row0, out, means_out, noise_out,
+                           timages_out, start_out, rows, w, flags, false, s);
+
+    // Graph mode: the chain is captured once per (rows, pointers, flags, stream) and replayed;
+    // seed / row0 live in the workspace so a replay can draw fresh noise.
+    GraphKey key;
+    std::memset(&key, 0, sizeof(key));
+    key.rows = rows;
+    const void* ptrs[10] = {x_T, x_cond, eps_all, out, means_out, noise_out, timages_out, start_out, workspace, nullptr};
+    std::memcpy(key.ptrs, ptrs, sizeof(ptrs));
+    key.cond_repeat = cond_repeat;
+    key.flags = flags;
+    key.stream = stream;
+    SD_HIP(sd::launch_set_rng(w.rng, seed, row0, s));
+    hipGraphExec_t exec = nullptr;
+    {
+        std::lock_guard<std::mutex> lk(const_cast<sd_plan*>(p)->gmu);
+        auto it = p->graphs.find(key);
+        if (it != p->graphs.end()) exec = it->second;
+    }
+    if (!exec) {
+        hipGraph_t graph = nullptr;
+        SD_HIP(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
+        rc = record_loop(p, x_T, x_cond, cond_repeat, eps_all, seed, row0, out, means_out, noise_out,
+                         timages_out, start_out, rows, w, flags, true, s);
+        hipError_t e = hipStreamEndCapture(s, &graph);
+        if (rc) {
+            if (graph) (void)hipGraphDestroy(graph);
+            return rc;
+        }
+        if (e != hipSuccess) return fail(SD_E_HIP, std::string("hipStreamEndCapture: ") + hipGetErrorString(e));
+        e = hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0);
+        (void)hipGraphDestroy(graph);
+        if (e != hipSuccess) return fail(SD_E_HIP, std::string("hipGraphInstantiate: ") + hipGetErrorString(e));
+        std::lock_guard<std::mutex> lk(const_cast<sd_plan*>(p)->gmu);
+        auto& cache = const_cast<sd_plan*>(p)->graphs;
+        if (cache.size() >= 8) {  // bounded cache: callers that reuse buffers hit it every call
+            for (auto& kv : cache) (void)hipGraphExecDestroy(kv.second);
+            cache.clear();
+        }
+        cache[key] = exec;
+    }
+    SD_HIP(hipGraphLaunch(exec, s));
+    return SD_OK;
+}
+
+int sd_plan_step_flops(const sd_plan* p, int64_t rows, double* flops_out) {
+    if (!p || !flops_out || rows < 0) return fail(SD_E_INVALID, "bad arguments");
+    step_flops(p, rows, flops_out);
+    return SD_OK;
+}
+
+int sd_profile_step(const sd_plan* p, const float* x_t, const float* x_cond, int64_t cond_repeat, int32_t t,
+                    int64_t rows, void* workspace, size_t ws_bytes, int32_t reps, float* ms_out,
+                    int32_t* counts_out, void* stream) {
+    WS w;
+    int rc = ws_setup(p, rows, workspace, ws_bytes, &w);
+    if (rc) return rc;
+    if (!x_t || !ms_out || reps < 1) return fail(SD_E_INVALID, "bad arguments");
+    if (t < 0 || t >= p->T) return fail(SD_E_INVALID, "t out of range");
+    if (p->C > 0 && !x_cond) return fail(SD_E_INVALID, "x_cond is required (diffusion_conditioning)");
+    hipStream_t s = (hipStream_t)stream;
+    double acc[4] = {0, 0, 0, 0};
+    int32_t counts[3] = {0, 0, 0};
+    for (int r = 0; r < reps; ++r) {
+        Prof prof;
+        rc = run_denoiser(p, x_t, x_cond, cond_repeat, t, w.x0, rows, w, s, &prof);
+        if (rc) return rc;
+        rc = run_update(p, w.x0, x_t, nullptr, 0, 2, 1234 + r, 0, nullptr, t, w.img0, nullptr, 0, nullptr, 0,
+                        nullptr, 0, rows, s, &prof);
+        if (rc) return rc;
+        SD_HIP(hipStreamSynchronize(s));
+        for (size_t i = 0; i < prof.cls.size(); ++i) {
+            float ms = 0.f;
+            SD_HIP(hipEventElapsedTime(&ms, prof.ev[2 * i], prof.ev[2 * i + 1]));
+            acc[prof.cls[i]] += ms;
+            if (r == 0) counts[prof.cls[i]]++;
+        }
+        float tot = 0.f;
+        SD_HIP(hipEventElapsedTime(&tot, prof.ev.front(), prof.ev.back()));
+        acc[3] += tot;
+    }
+    for (int i = 0; i < 4; ++i) ms_out[i] = (float)(acc[i] / reps);
+    if (counts_out)
+        for (int i = 0; i < 3; ++i) counts_out[i] = counts[i];
+    return SD_OK;
+}
+
+int sd_noise_fill(float* out, int64_t rows, int64_t n_per_row, uint64_t seed, int64_t row0, int32_t step,
+                  void* stream) {
+    if (!out || rows < 0 || n_per_row % 4) return fail(SD_E_INVALID, "bad arguments (n_per_row % 4 != 0?)");
+    SD_HIP(sd::launch_noise_fill(out, rows, n_per_row, seed, row0, step, nullptr, (hipStream_t)stream));
+    return SD_OK;
+}
+
+int sd_philox_raw(uint32_t* out, int64_t rows, int64_t quads, uint64_t seed, int64_t row0, int32_t step,
+                  void* stream) {
+    if (!out || rows < 0 || quads < 0) return fail(SD_E_INVALID, "bad arguments");
+    SD_HIP(sd::launch_philox_raw(out, rows, quads, seed, row0, step, (hipStream_t)stream));
+    return SD_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,244 @@
+"""SamplingEngine: binds a (Nonisotropic|Isotropic)GaussianDiffusion module to a libskeldiff plan.
+
+* The plan is built from the module's own state_dict (the reference key names), so a checkpoint
+  loaded with `load_state_dict` (reference src/utils/load.py:11-17) is what runs.
+* The plan is rebuilt automatically when any parameter/buffer changes (tracked through torch's
+  per-tensor version counters and storage pointers), e.g. after an optimizer step.
+* Workspaces are cached per (device, rows).  All launches go to torch's current HIP stream.
+* There is no CPU path: a module on the CPU, or a missing library, raises SkelDiffError.
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Optional, Tuple
+
+import torch
+
+from . import _lib
+from ._lib import SkelDiffError, check, ptr
+
+
+def _stream(dev: torch.device) -> int:
+    return torch.cuda.current_stream(dev).cuda_stream
+
+
+class SamplingEngine:
+    def __init__(self, diffusion):
+        self.diff = diffusion
+        self._plan = None
+        self._key = None
+        self._device = None
+        self._ws = {}
+        self._graph = False
+
+    # ---------------------------------------------------------------------------------------
+    def __del__(self):
+        try:
+            if self._plan is not None:
+                _lib.lib().sd_plan_destroy(self._plan)
+        except Exception:
+            pass
+
+    def _device_of_module(self) -> torch.device:
+        dev = self.diff.betas.device
+        if dev.type != "cuda":
+            raise SkelDiffError(
+                "skeletondiffusion_amd samples on the MI355X HIP engine only: move the diffusion module to "
+                "a ROCm device first (e.g. diffusion.to('cuda')); there is no CPU sampling path")
+        return dev
+
+    def _fingerprint(self):
+        return tuple((t.data_ptr(), t._version) for t in self.diff.state_dict(keep_vars=True).values()
+                     if torch.is_tensor(t))
+
+    def _desc(self):
+        m = self.diff.model
+        d = _lib.SDPlanDesc()
+        unsupported = []
+        if getattr(m, "learned_time_embedding", False):
+            unsupported.append("learned/random sinusoidal time embedding")
+        if getattr(m, "learned_variance", False):
+            unsupported.append("learned_variance")
+        if m.self_condition:
+            unsupported.append("self_condition")
+        if m.graph_kwargs.get("norm_type", "none") != "none":
+            unsupported.append("norm_type != 'none'")
+        if self.diff.objective != "pred_x0":
+            unsupported.append(f"objective {self.diff.objective!r} (the reference samples pred_x0)")
+        if unsupported:
+            raise SkelDiffError("sampling engine does not support: " + ", ".join(unsupported))
+        d.num_nodes = m.channels
+        d.latent_dim = self.diff.seq_length
+        d.cond_dim = m.cond_dim
+        d.out_dim = m.out_dim
+        d.depth = m.depth
+        d.attn_heads = m.attn_heads
+        d.attn_dim_head = m.attn_dim_head
+        d.use_attention = int(bool(m.use_attention))
+        d.self_condition = 0
+        d.learn_influence = int(bool(m.learn_influence))
+        nt = m.node_types
+        self._node_types = None
+        if nt is not None:
+            arr = (ctypes.c_int64 * m.channels)(*[int(v) for v in torch.as_tensor(nt).tolist()])
+            self._node_types = arr
+            d.num_node_types = int(torch.as_tensor(nt).max()) + 1
+            d.node_types = ctypes.cast(arr, ctypes.POINTER(ctypes.c_int64))
+        else:
+            d.num_node_types = 0
+        d.timesteps = self.diff.num_timesteps
+        d.isotropic = int(not hasattr(self.diff, "posterior_mean_coef1_x0"))
+        d.activation = 1 if self.diff.diffusion_activation == "tanh" else 0
+        d.sinusoidal_theta = float(m.sinusoidal_pos_emb_theta)
+        return d
+
+    def plan(self):
+        dev = self._device_of_module()
+        key = (dev, self._fingerprint())
+        if self._plan is not None and key == self._key:
+            return self._plan
+        L = _lib.lib()
+        if self._plan is not None:
+            torch.cuda.synchronize(dev)
+            L.sd_plan_destroy(self._plan)
+            self._plan = None
+        desc = self._desc()
+        handle = ctypes.c_void_p()
+        with torch.cuda.device(dev):
+            check(L.sd_plan_create(ctypes.byref(handle), ctypes.byref(desc)))
+            sd = self.diff.state_dict()
+            stream = _stream(dev)
+            keep = []
+            try:
+                for i in range(L.sd_plan_num_tensors(handle)):
+                    name = L.sd_plan_tensor_name(handle, i).decode()
+                    if name not in sd:
+                        raise SkelDiffError(f"state_dict has no tensor {name!r} required by the sampling engine")
+                    t = sd[name].detach().to(device=dev, dtype=torch.float32).contiguous()
+                    keep.append(t)
+                    check(L.sd_plan_set_tensor(handle, name.encode(), ptr(t), t.numel(), stream))
+                check(L.sd_plan_finalize(handle, stream))
+            except Exception:
+                L.sd_plan_destroy(handle)
+                raise
+        self._plan, self._key, self._device = handle, key, dev
+        return handle
+
+    def workspace(self, rows: int) -> Tuple[torch.Tensor, int]:
+        plan = self.plan()
+        nbytes = int(_lib.lib().sd_workspace_bytes(plan, rows))
+        k = (self._device, rows)
+        ws = self._ws.get(k)
+        if ws is None or ws.numel() < nbytes:
+            self._ws.clear()
+            ws = torch.empty(nbytes, dtype=torch.uint8, device=self._device)
+            self._ws[k] = ws
+        return ws, nbytes
+
+    # ---------------------------------------------------------------------------------------
+    def _f32(self, t: Optional[torch.Tensor], shape=None) -> Optional[torch.Tensor]:
+        if t is None:
+            return None
+        t = t.to(device=self._device, dtype=torch.float32).contiguous()
+        if shape is not None and tuple(t.shape) != tuple(shape):
+            raise SkelDiffError(f"expected shape {tuple(shape)}, got {tuple(t.shape)}")
+        return t
+
+    def _cond(self, x_cond, rows):
+        m = self.diff.model
+        if m.cond_dim == 0 or not self.diff.condition:
+            return None, 1
+        if x_cond is None:
+            raise SkelDiffError("x_cond is required (diffusion_conditioning=True)")
+        x_cond = self._f32(x_cond)
+        bc = x_cond.shape[0]
+        if bc == 0 or rows % bc:
+            raise SkelDiffError(f"x_cond rows ({bc}) must divide the batch ({rows}) (base.py:246-248)")
+        return x_cond, rows // bc
+
+    def denoiser_forward(self, x: torch.Tensor, t: int, x_cond=None) -> torch.Tensor:
+        plan = self.plan()
+        J, D = self.diff.channels, self.diff.seq_length
+        x = self._f32(x)
+        rows = x.shape[0]
+        if tuple(x.shape[1:]) != (J, D):
+            raise SkelDiffError(f"x must be (B, {J}, {D})")
+        xc, rep = self._cond(x_cond, rows)
+        out = torch.empty((rows, J, self.diff.model.out_dim), device=self._device, dtype=torch.float32)
+        ws, nb = self.workspace(rows)
+        check(_lib.lib().sd_denoiser_forward(plan, ptr(x), ptr(xc), rep, int(t), ptr(out), rows, ptr(ws), nb,
+                                             _stream(self._device)))
+        return out
+
+    def p_sample(self, x, t: int, x_cond=None, eps=None):
+        plan = self.plan()
+        x = self._f32(x)
+        rows = x.shape[0]
+        x0_raw = self.denoiser_forward(x, t, x_cond)
+        out = torch.empty_like(x)
+        mean = torch.empty_like(x)
+        eps = self._f32(eps, x.shape) if (eps is not None and t > 0) else None
+        noise_used = torch.empty_like(x) if t > 0 else None
+        L = _lib.lib()
+        JD = x.shape[1] * x.shape[2]
+        if eps is None and t > 0:
+            seed = int(torch.randint(0, 2 ** 62, (1,)).item())
+        else:
+            seed = 0
+        check(L.sd_p_sample_update(plan, ptr(x0_raw), ptr(x), ptr(eps), JD, seed, 0, int(t), ptr(out),
+                                   ptr(mean), JD, ptr(noise_used), JD, rows, _stream(self._device)))
+        x0 = torch.tanh(x0_raw) if self.diff.diffusion_activation == "tanh" else x0_raw
+        return out, x0.clamp_(-1.0, 1.0), (noise_used if t > 0 else 0.0), mean
+
+    def sample_loop(self, rows: int, x_cond=None, start_noise=None, sampling_noise=None,
+                    record=(False, False), seed: Optional[int] = None, row0: int = 0,
+                    graph: Optional[bool] = None, out: Optional[torch.Tensor] = None,
+                    keep_start: bool = True):
+        """-> (img, start_noise, noise_t, mean_t, imgs).  Unrequested records are None.
+        `out` (rows, J, D) fp32 may be passed to reuse an output buffer (keeps a captured
+        hipGraph valid across calls)."""
+        plan = self.plan()
+        J, D, T = self.diff.channels, self.diff.seq_length, self.diff.num_timesteps
+        dev = self._device
+        flags = 0
+        start = self._f32(start_noise, (rows, J, D))
+        samp = self._f32(sampling_noise, (rows, T - 1, J, D)) if sampling_noise is not None else None
+        if start is None:
+            flags |= _lib.SD_FLAG_DEVICE_START
+        if samp is None:
+            flags |= _lib.SD_FLAG_DEVICE_NOISE
+        if graph if graph is not None else self._graph:
+            flags |= _lib.SD_FLAG_GRAPH
+        if seed is None:
+            seed = int(torch.randint(0, 2 ** 62, (1,)).item()) if (flags & 6) else 0
+        xc, rep = self._cond(x_cond, rows)
+        rec_noise, rec_img = record
+        if out is None:
+            out = torch.empty((rows, J, D), device=dev, dtype=torch.float32)
+        elif out.shape != (rows, J, D) or out.dtype != torch.float32 or not out.is_contiguous() or out.device != dev:
+            raise SkelDiffError("out must be a contiguous fp32 (rows, J, D) tensor on the module's device")
+        tm1 = max(T - 1, 0)
+        mean_t = torch.empty((rows, tm1, J, D), device=dev) if rec_noise and not rec_img else None
+        noise_t = torch.empty((rows, tm1, J, D), device=dev) if rec_noise else None
+        imgs = torch.empty((rows, tm1, J, D), device=dev) if rec_img else None
+        start_out = torch.empty((rows, J, D), device=dev) if (start is None and keep_start) else None
+        ws, nb = self.workspace(rows)
+        args = (plan, ptr(start), ptr(xc), rep, ptr(samp), seed, int(row0), ptr(out), ptr(mean_t), ptr(noise_t),
+                ptr(imgs), ptr(start_out), rows, ptr(ws), nb, flags)
+        cur = torch.cuda.current_stream(dev)
+        if (flags & _lib.SD_FLAG_GRAPH) and cur.cuda_stream == 0:
+            # stream capture is not possible on the legacy default stream: run on a side stream
+            if getattr(self, "_side", None) is None:
+                self._side = torch.cuda.Stream(dev)
+            self._side.wait_stream(cur)
+            with torch.cuda.stream(self._side):
+                check(_lib.lib().sd_sample_loop(*args, self._side.cuda_stream))
+            cur.wait_stream(self._side)
+        else:
+            check(_lib.lib().sd_sample_loop(*args, cur.cuda_stream))
+        start_ret = start.clone() if start is not None else start_out
+        return out, start_ret, noise_t, mean_t, imgs
+
+    def enable_graph(self, on: bool = True):
+        """Capture whole sample() chains in hipGraphs (cached per shape/pointer set)."""
+        self._graph = on

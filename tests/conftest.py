@@ -1,0 +1,94 @@
+import os
+import sys
+
+import numpy as np
+import pytest
+import torch
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if REPO not in sys.path:
+    sys.path.insert(0, REPO)
+GOLDEN = os.path.join(REPO, "tests", "golden")
+WEIGHT_SEED = 1234  # tests/golden/gen_golden.py
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (gfx950) HIP device; run with -m gpu")
+
+
+def pytest_collection_modifyitems(config, items):
+    if torch.cuda.is_available():
+        return
+    skip = pytest.mark.skip(reason="no HIP device in this container (GPU tests run on the MI355X box)")
+    for it in items:
+        if "gpu" in it.keywords:
+            it.add_marker(skip)
+
+
+def golden(name):
+    return np.load(os.path.join(GOLDEN, name + ".npz"))
+
+
+RELEASE_FIXTURES = ["release_h36m16_T10", "release_h36m16_T100", "release_amass21_T10",
+                    "release_freeman17_T10", "release_mano51_T10"]
+
+
+def build_release_diffusion(z, device="cpu", T=None):
+    """Product NonisotropicGaussianDiffusion + Denoiser (release architecture) with the fixture's
+    synthetic weights (gen_golden.py:build_release)."""
+    from skeletondiffusion_amd import synthetic
+    from skeletondiffusion_amd.core.diffusion import NonisotropicGaussianDiffusion, get_cov_from_corr
+    from skeletondiffusion_amd.core.network import Denoiser
+
+    J = z["corr"].shape[0]
+    T = int(z["T"]) if T is None else T
+    m = Denoiser(dim=96, cond_dim=96, out_dim=96, channels=J, num_nodes=J,
+                 node_types=torch.from_numpy(z["node_types"]), use_attention=True, self_condition=False,
+                 norm_type="none", depth=4, attn_dim_head=32, attn_heads=8, learn_influence=True)
+    synthetic.fill_module_(m, WEIGHT_SEED)
+    fs = float(z["final_scale"]) if "final_scale" in z else 1.0
+    if fs != 1.0:
+        with torch.no_grad():
+            m.final_glin.weight.mul_(fs)
+            m.final_glin.bias.mul_(fs)
+    S, L, U = get_cov_from_corr(torch.from_numpy(z["corr"]))
+    d = NonisotropicGaussianDiffusion(Sigma_N=S, Lambda_N=L, U=U, model=m, latent_size=96,
+                                      diffusion_timesteps=T, diffusion_objective="pred_x0",
+                                      diffusion_conditioning=True, beta_schedule="cosine")
+    return d.to(device).eval()
+
+
+def release_inputs(z, T=None):
+    from skeletondiffusion_amd import synthetic
+
+    J = z["corr"].shape[0]
+    T = int(z["T"]) if T is None else T
+    bs, fu = int(z["B_seq"]), int(z["futures"])
+    B = bs * fu
+    x_cond_seq = torch.from_numpy(synthetic.uniform((bs, J, 96), 21))
+    start = torch.from_numpy(synthetic.normal((B, J, 96), 22))
+    samp = torch.from_numpy(synthetic.normal((B, T - 1, J, 96), 23))
+    return x_cond_seq, fu, start, samp
+
+
+def build_readme_diffusion(mode, device="cpu"):
+    """README plug-and-play config (README.md:72-97) in the three fixture modes."""
+    from skeletondiffusion_amd import synthetic
+    from skeletondiffusion_amd.core.diffusion import (IsotropicGaussianDiffusion, NonisotropicGaussianDiffusion,
+                                                      get_cov_from_corr)
+    from skeletondiffusion_amd.core.network import Denoiser
+
+    z = golden("readme16_T10")
+    m = Denoiser(dim=96, cond_dim=0, out_dim=96, channels=16, num_nodes=16)
+    synthetic.fill_module_(m, WEIGHT_SEED)
+    if mode == "isotropic":
+        d = IsotropicGaussianDiffusion(model=m, diffusion_timesteps=10)
+    else:
+        S, L, U = get_cov_from_corr(torch.from_numpy(z["corr"]), if_run_as_isotropic=(mode == "iso_as_noniso"))
+        d = NonisotropicGaussianDiffusion(Sigma_N=S, Lambda_N=L, U=U, model=m, timesteps=10)
+    return d.to(device).eval()
+
+
+@pytest.fixture(scope="session")
+def cuda():
+    return torch.device("cuda:0")

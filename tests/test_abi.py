@@ -1,0 +1,72 @@
+"""The C-ABI library loads and exports every symbol include/skeldiff.h declares (no GPU work),
+and its host-side argument validation behaves (no device call happens on these paths)."""
+import ctypes
+import os
+import re
+
+from conftest import REPO
+from skeletondiffusion_amd import _lib
+
+HEADER = os.path.join(REPO, "include", "skeldiff.h")
+
+
+def declared_symbols():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(sd_[a-z_0-9]+)\s*\(", src)))
+
+
+def test_header_and_binding_agree():
+    assert declared_symbols() == sorted(_lib.EXPORTED)
+
+
+def test_library_exports_every_declared_symbol():
+    lib = _lib.lib()
+    for name in declared_symbols():
+        assert hasattr(lib, name), name
+    assert lib.sd_abi_version() == 1
+
+
+def test_invalid_desc_is_rejected_on_host():
+    lib = _lib.lib()
+    d = _lib.SDPlanDesc()
+    d.num_nodes = 65  # > 64
+    d.latent_dim = 96
+    d.out_dim = 96
+    d.depth = 1
+    d.timesteps = 10
+    h = ctypes.c_void_p()
+    rc = lib.sd_plan_create(ctypes.byref(h), ctypes.byref(d))
+    assert rc == -1 and b"num_nodes" in lib.sd_last_error()
+    d.num_nodes = 16
+    d.self_condition = 1
+    assert lib.sd_plan_create(ctypes.byref(h), ctypes.byref(d)) == -1
+    assert b"self_condition" in lib.sd_last_error()
+
+
+def test_plan_registry_uses_reference_state_dict_keys():
+    """The plan's tensor registry (host-only, no device memory yet) lists exactly the
+    reference's Denoiser keys plus the posterior buffers the sampler needs."""
+    import torch
+
+    import oracle as O
+
+    lib = _lib.lib()
+    nt = torch.tensor([0, 1, 2, 0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 7, 8, 9])
+    d = _lib.SDPlanDesc(num_nodes=16, latent_dim=96, cond_dim=96, out_dim=96, depth=4, attn_heads=8,
+                        attn_dim_head=32, use_attention=1, self_condition=0, learn_influence=1,
+                        num_node_types=10, timesteps=100, isotropic=0, activation=0, sinusoidal_theta=10000.0)
+    arr = (ctypes.c_int64 * 16)(*nt.tolist())
+    d.node_types = ctypes.cast(arr, ctypes.POINTER(ctypes.c_int64))
+    h = ctypes.c_void_p()
+    assert lib.sd_plan_create(ctypes.byref(h), ctypes.byref(d)) == 0
+    try:
+        names = {lib.sd_plan_tensor_name(h, i).decode(): lib.sd_plan_tensor_numel(h, i)
+                 for i in range(lib.sd_plan_num_tensors(h))}
+        expect = {k: int(torch.Size(s).numel()) for k, s, _ in O.denoiser_param_shapes(O.release_config(16, nt))}
+        expect.update({"posterior_mean_coef1_x0": 100 * 256, "posterior_mean_coef2_xt": 100 * 256,
+                       "Lambda_posterior_log_variance_clipped": 100 * 16, "U": 256})
+        assert names == expect
+        assert lib.sd_plan_kernels_per_step(h) == 1 + 8 * 2 + 7 * 3 + 3 + 1 + 1
+    finally:
+        lib.sd_plan_destroy(h)
