@@ -82,6 +82,13 @@ def build_config(name, device, T=None, batch=None, futures=None, seed=1234, seq0
     return d, torch.from_numpy(xc).to(device), batch * futures
 
 
+def shard(rank: int, batch: int, futures: int):
+    """Weak-scaling shard of rank `rank`: sequences [rank*batch, (rank+1)*batch), all futures of a
+    sequence on one rank (eval_prepare_model.py:96 repeat_interleave order).
+    Returns (seq0, row0, rows); row0 keys the device noise so outputs are GPU-count invariant."""
+    return rank * batch, rank * batch * futures, batch * futures
+
+
 def profile_kernels(d, x_cond, rows, reps=5):
     eng = d.engine
     plan = eng.plan()
@@ -151,10 +158,10 @@ def main():
 
     c = CONFIGS[args.config]
     batch = args.batch or c["batch"]
-    d, x_cond, rows = build_config(args.config, dev, T=args.T, batch=batch, futures=args.futures,
-                                   seq0=rank * batch)
+    futures = args.futures or c["futures"]
+    seq0, row0, rows = shard(rank, batch, futures)
+    d, x_cond, rows = build_config(args.config, dev, T=args.T, batch=batch, futures=futures, seq0=seq0)
     J, D, T = d.channels, d.seq_length, d.num_timesteps
-    row0 = rank * rows                      # global row index of this shard (device-noise key)
     eng = d.engine
     eng.plan()
     graph = not args.no_graph

@@ -156,6 +156,18 @@ int sd_profile_step(const sd_plan* plan, const float* x_t, const float* x_cond, 
                     int32_t t, int64_t rows, void* workspace, size_t workspace_bytes, int32_t reps,
                     float* ms_out, int32_t* counts_out, void* stream);
 
+/* Test hooks: one kernel on caller buffers, for the per-kernel numerics tests.
+ * sd_test_graph_linear: out(B,J,N) = act(FiLM(ghat @ (s_j W[type j] [x1_j | x2_j] + bias[type j]))) + res,
+ *   W (types,N,K1+K2), bias (types,N) or NULL, ghat (J,J), film (2N) or NULL, res (B,J,N) or NULL,
+ *   x1 row b read at b / x1_div, s_j = 1/max(||x1_j||,1e-12) when rms (else 1), act 0/1 = none/tanh.
+ * sd_test_attention: out(B,J,heads*dh) = softmax(q k^T / sqrt(dh)) v per head, qkv (B,J,3*heads*dh). */
+int sd_test_graph_linear(const float* x1, int32_t K1, int64_t x1_div, const float* x2, int32_t K2,
+                         const float* W, const float* bias, const int64_t* node_types, const float* ghat,
+                         const float* film, int32_t act, const float* res, float* out, int64_t rows,
+                         int32_t J, int32_t N, int32_t rms, void* stream);
+int sd_test_attention(const float* qkv, float* out, int64_t rows, int32_t J, int32_t heads,
+                      int32_t dim_head, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

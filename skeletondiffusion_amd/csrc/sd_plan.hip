@@ -735,6 +735,47 @@ int sd_profile_step(const sd_plan* p, const float* x_t, const float* x_cond, int
     return SD_OK;
 }
 
+int sd_test_graph_linear(const float* x1, int32_t K1, int64_t x1_div, const float* x2, int32_t K2,
+                         const float* W, const float* bias, const int64_t* node_types, const float* ghat,
+                         const float* film, int32_t act, const float* res, float* out, int64_t rows,
+                         int32_t J, int32_t N, int32_t rms, void* stream) {
+    if (!x1 || !W || !ghat || !out || !node_types || J < 1 || J > sd::kMaxNodes || N < 1 || K1 % 16 ||
+        K2 % 16 || x1_div < 1 || rows < 0)
+        return fail(SD_E_INVALID, "bad arguments");
+    sd::GLArgs a{};
+    a.x1 = x1;
+    a.K1 = K1;
+    a.x1_rs = (int64_t)J * K1;
+    a.x1_div = (int)x1_div;
+    a.x2 = x2;
+    a.K2 = x2 ? K2 : 0;
+    a.x2_rs = (int64_t)J * K2;
+    a.W = W;
+    a.bias = bias;
+    a.G = ghat;
+    a.film = film;
+    a.res = res;
+    a.res_rs = (int64_t)J * N;
+    a.out = out;
+    a.out_rs = (int64_t)J * N;
+    a.B = rows;
+    a.N = N;
+    a.J = J;
+    a.act = act;
+    for (int j = 0; j < J; ++j) a.wrow[j] = (int)node_types[j] * N;
+    SD_HIP(sd::launch_graph_linear(a, rms != 0, (hipStream_t)stream));
+    return SD_OK;
+}
+
+int sd_test_attention(const float* qkv, float* out, int64_t rows, int32_t J, int32_t heads, int32_t dim_head,
+                      void* stream) {
+    if (!qkv || !out || J < 1 || J > sd::kMaxNodes || heads < 1 || dim_head % 16 || rows < 0)
+        return fail(SD_E_INVALID, "bad arguments");
+    sd::AttnArgs aa{qkv, out, rows, J, heads, dim_head, (float)std::pow((double)dim_head, -0.5)};
+    SD_HIP(sd::launch_attention(aa, (hipStream_t)stream));
+    return SD_OK;
+}
+
 int sd_noise_fill(float* out, int64_t rows, int64_t n_per_row, uint64_t seed, int64_t row0, int32_t step,
                   void* stream) {
     if (!out || rows < 0 || n_per_row % 4) return fail(SD_E_INVALID, "bad arguments (n_per_row % 4 != 0?)");

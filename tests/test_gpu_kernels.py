@@ -1,0 +1,110 @@
+"""Per-kernel numerics on the GPU: each HIP kernel (through the ABI test hooks) against a plain
+PyTorch fp32 CPU computation of the same op, on random inputs, across the J / N / K shapes the
+configs use (and odd ones that take the generic paths)."""
+import ctypes
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+from skeletondiffusion_amd import _lib
+
+pytestmark = pytest.mark.gpu
+
+
+def _gl_reference(x1, x2, W, bias, types, ghat, film, act, res, rms, div):
+    B = x1.shape[0] * div
+    x1r = x1.repeat_interleave(div, 0)
+    x = torch.cat([x1r, x2], -1) if x2 is not None else x1r
+    w = W[types]                                              # (J, N, K)
+    y = torch.einsum("jnk,bjk->bjn", w.double(), x.double())
+    if rms:
+        y = y / x1r.double().norm(dim=-1, keepdim=True).clamp_min(1e-12)
+    if bias is not None:
+        y = y + bias[types].double()
+    z = ghat.double() @ y
+    if film is not None:
+        N = W.shape[1]
+        z = z * (film[:N].double() + 1) + film[N:].double()
+    if act:
+        z = torch.tanh(z)
+    if res is not None:
+        z = z + res.double()
+    assert z.shape[0] == B
+    return z.float()
+
+
+def _run_gl(dev, x1, x2, W, bias, types, ghat, film, act, res, rms, div):
+    B = x1.shape[0] * div
+    J, N = x1.shape[1], W.shape[1]
+    t = lambda a: None if a is None else a.to(dev).contiguous()  # noqa: E731
+    g = {k: t(v) for k, v in dict(x1=x1, x2=x2, W=W, bias=bias, ghat=ghat, film=film, res=res).items()}
+    out = torch.full((B, J, N), float("nan"), device=dev)
+    nt = (ctypes.c_int64 * J)(*types.tolist())
+    p = lambda a: None if a is None else a.data_ptr()  # noqa: E731
+    _lib.check(_lib.lib().sd_test_graph_linear(p(g["x1"]), x1.shape[2], div, p(g["x2"]),
+                                               0 if x2 is None else x2.shape[2], p(g["W"]), p(g["bias"]), nt,
+                                               p(g["ghat"]), p(g["film"]), act, p(g["res"]), out.data_ptr(), B, J,
+                                               N, int(rms), 0))
+    torch.cuda.synchronize()
+    return out.cpu()
+
+
+CASES = [  # (J, n_types, K1, K2, N, div, bias, film, act, res, rms)
+    (16, 1, 96, 0, 96, 1, True, False, 0, False, False),      # README shared weights
+    (16, 10, 96, 96, 192, 4, True, False, 0, False, False),    # init_lin with x_cond broadcast
+    (16, 10, 192, 0, 192, 1, True, True, 1, False, False),    # ResnetBlock block1 (FiLM + tanh)
+    (16, 10, 192, 0, 192, 1, True, False, 1, True, False),    # block2 (tanh + residual)
+    (16, 10, 192, 0, 768, 1, False, False, 0, False, True),   # to_qkv with RMSNorm scale
+    (16, 10, 256, 0, 192, 1, False, False, 0, True, False),   # to_out + residual
+    (16, 10, 192, 192, 192, 1, False, False, 0, False, False),  # final res_linear on cat(x, r)
+    (16, 10, 192, 0, 96, 1, True, False, 0, False, False),    # final_glin
+    (17, 9, 192, 0, 192, 1, True, True, 1, False, False),
+    (21, 13, 96, 96, 192, 50, True, False, 0, False, False),
+    (21, 13, 192, 0, 768, 1, False, False, 0, False, True),
+    (51, 43, 192, 0, 192, 1, True, True, 1, True, False),
+    (51, 43, 192, 0, 768, 1, False, False, 0, False, True),
+    (5, 3, 96, 0, 96, 1, True, False, 0, False, False),       # generic JM=8 path
+    (12, 4, 192, 0, 192, 1, True, True, 1, True, True),       # generic JM=16 path, everything on
+    (33, 7, 96, 0, 192, 1, True, False, 1, False, False),     # generic JM=64 path
+]
+
+
+@pytest.mark.parametrize("J,nty,K1,K2,N,div,has_bias,has_film,act,has_res,rms", CASES)
+@pytest.mark.parametrize("Bseq", [64, 67])
+def test_graph_linear_kernel(J, nty, K1, K2, N, div, has_bias, has_film, act, has_res, rms, Bseq, cuda):
+    g = torch.Generator().manual_seed(J * 1000 + N + K1 + K2 + Bseq)
+    B = Bseq if div == 1 else max(1, Bseq // div) * div
+    r = lambda *s: torch.rand(*s, generator=g) * 2 - 1  # noqa: E731
+    x1 = r(B // div, J, K1)
+    x2 = r(B, J, K2) if K2 else None
+    W = r(nty, N, K1 + K2) / (K1 + K2) ** 0.5
+    types = torch.randint(0, nty, (J,), generator=g)
+    types[:nty] = torch.randperm(nty, generator=g)[: min(nty, J)] if nty <= J else types[:nty]
+    bias = r(nty, N) * 0.1 if has_bias else None
+    G = torch.eye(J) + torch.rand(J, J, generator=g) * 0.1
+    ghat = F.normalize(G, p=1.0, dim=1)
+    film = r(2 * N) * 0.5 if has_film else None
+    res = r(B, J, N) if has_res else None
+    got = _run_gl(cuda, x1, x2, W, bias, types, ghat, film, act, res, rms, div)
+    ref = _gl_reference(x1, x2, W, bias, types, ghat, film, act, res, rms, div)
+    assert torch.isfinite(got).all()
+    assert (got - ref).abs().max().item() < 2e-5
+
+
+@pytest.mark.parametrize("J", [16, 17, 21, 51, 7, 33])
+@pytest.mark.parametrize("heads,dh", [(8, 32), (4, 32), (2, 64)])
+def test_attention_kernel(J, heads, dh, cuda):
+    g = torch.Generator().manual_seed(J + heads)
+    B = 37
+    hid = heads * dh
+    qkv = torch.randn(B, J, 3 * hid, generator=g)
+    q, k, v = (c.reshape(B, J, heads, dh).permute(0, 2, 3, 1) for c in qkv.chunk(3, dim=-1))
+    sim = torch.einsum("bhcn,bhcj->bhnj", q.double() * dh ** -0.5, k.double())
+    ref = torch.einsum("bhnj,bhdj->bhnd", sim.softmax(-1), v.double()).permute(0, 2, 1, 3).reshape(B, J, hid)
+    out = torch.full((B, J, hid), float("nan"), device=cuda)
+    qd = qkv.to(cuda)
+    _lib.check(_lib.lib().sd_test_attention(qd.data_ptr(), out.data_ptr(), B, J, heads, dh, 0))
+    torch.cuda.synchronize()
+    assert torch.isfinite(out).all()
+    assert (out.cpu().double() - ref).abs().max().item() < 2e-5

@@ -1,0 +1,26 @@
+#!/bin/bash
+# rocprofv3 profile of the default bench command (run on the GPU box via gpurun):
+#   1. --kernel-trace --stats            -> per-kernel average durations
+#   2. --pmc FETCH_SIZE  (separate pass)  -> HBM read bytes  (x2 on gfx950 for wide streams)
+#   3. --pmc WRITE_SIZE  (separate pass)  -> HBM write bytes
+# Counters are collected in their own runs, never combined with sys/runtime traces.
+# Output: gpurun_out/prof_<tag>/...
+set -u
+TAG=${1:-r01}
+ARGS=${BENCH_ARGS:-"--steps 2 --warmup 1 --no-cpu-baseline --no-graph"}
+cd /tmp && export TMPDIR=/tmp
+cd "$GRAFT_REPO_ROOT"
+OUT=gpurun_out/prof_$TAG
+mkdir -p $OUT
+timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o run -- \
+    python3 bench.py $ARGS > $OUT/trace.log 2>&1
+rc=$?; echo "trace_rc=$rc"; [ $rc -eq 0 ] || exit $rc
+if [ "${PMC:-1}" = "1" ]; then
+  timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/pmc_fetch -o run -- \
+      python3 bench.py $ARGS > $OUT/pmc_fetch.log 2>&1
+  rc=$?; echo "pmc_fetch_rc=$rc"; [ $rc -eq 0 ] || exit $rc
+  timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/pmc_write -o run -- \
+      python3 bench.py $ARGS > $OUT/pmc_write.log 2>&1
+  rc=$?; echo "pmc_write_rc=$rc"; [ $rc -eq 0 ] || exit $rc
+fi
+exit 0
