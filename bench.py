@@ -61,6 +61,18 @@ RELEASE_ARCH = dict(use_attention=True, self_condition=False, norm_type="none", 
                     attn_heads=8, learn_influence=True)
 
 
+def skeleton_covariance(skel, adj):
+    """(Sigma_N, Lambda_N, U) for a skeleton.  In deployment these are checkpoint buffers; here the
+    values the reference computed in the build container (tests/golden/cov_<skel>.npz) are used,
+    because eigh on another LAPACK build may pick other eigenvector signs / degenerate-eigenspace
+    bases (and for MANO the reference's own PD assert fails on the GPU box's LAPACK)."""
+    path = os.path.join(HERE, "tests", "golden", f"cov_{skel}.npz")
+    if os.path.exists(path):
+        z = np.load(path)
+        return tuple(torch.from_numpy(z[k]) for k in ("Sigma_N", "Lambda_N", "U"))
+    return get_cov_from_corr(torch.from_numpy(adj), if_sigma_n_scale=True, sigma_n_scale="spectral")
+
+
 def build_config(name, device, T=None, batch=None, futures=None, seed=1234, seq0=0):
     """Release-architecture diffusion with synthetic weights + per-sequence conditioning latents.
     Returns (diffusion on `device`, x_cond (batch, J, 96) on `device`, rows = batch * futures)."""
@@ -73,7 +85,7 @@ def build_config(name, device, T=None, batch=None, futures=None, seed=1234, seq0
     m = Denoiser(dim=96, cond_dim=96, out_dim=96, channels=J, num_nodes=J, node_types=torch.from_numpy(types),
                  **RELEASE_ARCH)
     synthetic.fill_module_(m, seed)
-    S, L, U = get_cov_from_corr(torch.from_numpy(adj), if_sigma_n_scale=True, sigma_n_scale="spectral")
+    S, L, U = skeleton_covariance(c["skel"], adj)
     d = NonisotropicGaussianDiffusion(Sigma_N=S, Lambda_N=L, U=U, model=m, latent_size=96, diffusion_timesteps=T,
                                       diffusion_objective="pred_x0", diffusion_conditioning=True,
                                       beta_schedule="cosine").to(device).eval()

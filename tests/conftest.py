@@ -33,11 +33,26 @@ RELEASE_FIXTURES = ["release_h36m16_T10", "release_h36m16_T100", "release_amass2
                     "release_freeman17_T10", "release_mano51_T10"]
 
 
+_SKEL_BY_J = {16: "h36m16", 21: "amass21", 17: "freeman17", 51: "mano51"}
+
+
+def pinned_cov(J):
+    """(Sigma_N, Lambda_N, U) as the reference computed them in the build container.
+
+    U is NOT recomputed on the test machine: LAPACK builds differ in eigenvector signs and in the
+    basis chosen inside degenerate eigenspaces (measured on the GPU box: 4-8 columns differ for
+    the skeletons here, and for MANO the reference's own `is_positive_def` assert fires there).
+    The noise term U (sigma * eps) depends on that choice, so - exactly like a release checkpoint,
+    where U is a state_dict buffer - the fixtures pin it."""
+    z = golden("cov_" + _SKEL_BY_J[J])
+    return tuple(torch.from_numpy(z[k]) for k in ("Sigma_N", "Lambda_N", "U"))
+
+
 def build_release_diffusion(z, device="cpu", T=None):
     """Product NonisotropicGaussianDiffusion + Denoiser (release architecture) with the fixture's
     synthetic weights (gen_golden.py:build_release)."""
     from skeletondiffusion_amd import synthetic
-    from skeletondiffusion_amd.core.diffusion import NonisotropicGaussianDiffusion, get_cov_from_corr
+    from skeletondiffusion_amd.core.diffusion import NonisotropicGaussianDiffusion
     from skeletondiffusion_amd.core.network import Denoiser
 
     J = z["corr"].shape[0]
@@ -51,7 +66,7 @@ def build_release_diffusion(z, device="cpu", T=None):
         with torch.no_grad():
             m.final_glin.weight.mul_(fs)
             m.final_glin.bias.mul_(fs)
-    S, L, U = get_cov_from_corr(torch.from_numpy(z["corr"]))
+    S, L, U = pinned_cov(J)
     d = NonisotropicGaussianDiffusion(Sigma_N=S, Lambda_N=L, U=U, model=m, latent_size=96,
                                       diffusion_timesteps=T, diffusion_objective="pred_x0",
                                       diffusion_conditioning=True, beta_schedule="cosine")
@@ -74,8 +89,7 @@ def release_inputs(z, T=None):
 def build_readme_diffusion(mode, device="cpu"):
     """README plug-and-play config (README.md:72-97) in the three fixture modes."""
     from skeletondiffusion_amd import synthetic
-    from skeletondiffusion_amd.core.diffusion import (IsotropicGaussianDiffusion, NonisotropicGaussianDiffusion,
-                                                      get_cov_from_corr)
+    from skeletondiffusion_amd.core.diffusion import IsotropicGaussianDiffusion, NonisotropicGaussianDiffusion
     from skeletondiffusion_amd.core.network import Denoiser
 
     z = golden("readme16_T10")
@@ -84,7 +98,7 @@ def build_readme_diffusion(mode, device="cpu"):
     if mode == "isotropic":
         d = IsotropicGaussianDiffusion(model=m, diffusion_timesteps=10)
     else:
-        S, L, U = get_cov_from_corr(torch.from_numpy(z["corr"]), if_run_as_isotropic=(mode == "iso_as_noniso"))
+        S, L, U = (torch.from_numpy(z[f"{mode}_buf_{k}"]) for k in ("Sigma_N", "Lambda_N", "U"))
         d = NonisotropicGaussianDiffusion(Sigma_N=S, Lambda_N=L, U=U, model=m, timesteps=10)
     return d.to(device).eval()
 

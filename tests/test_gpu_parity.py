@@ -11,7 +11,7 @@ import torch
 
 import oracle as O
 from conftest import (RELEASE_FIXTURES, WEIGHT_SEED, build_readme_diffusion, build_release_diffusion, golden,
-                      release_inputs)
+                      pinned_cov, release_inputs)
 from skeletondiffusion_amd import _lib
 
 pytestmark = pytest.mark.gpu
@@ -103,7 +103,7 @@ def test_device_noise_chain_matches_oracle(cuda):
     assert _max_err(start, st) < 2e-5 and _max_err(noise_t, sn) < 2e-5
     cfg = O.release_config(J, z["node_types"])
     sd = O.synthetic_state_dict(cfg, WEIGHT_SEED)
-    S, L, U = O.get_cov_from_corr(torch.from_numpy(z["corr"]))
+    S, L, U = pinned_cov(J)
     bufs = O.nonisotropic_buffers(S, L, U, O.beta_schedule("cosine", T))
     ref, _ = O.p_sample_loop(sd, cfg, bufs, st, sn, x_cond=xcs)
     assert _max_err(img, ref) < TOL
@@ -115,9 +115,10 @@ def test_graph_replay_equals_eager_bitwise(cuda):
     xc = release_inputs(z)[0].to(cuda)
     a = d.engine.sample_loop(8, x_cond=xc, seed=77, graph=False)[0]
     out = torch.empty_like(a)
-    b = d.engine.sample_loop(8, x_cond=xc, seed=77, graph=True, out=out)[0]
-    c = d.engine.sample_loop(8, x_cond=xc, seed=77, graph=True, out=out)[0].clone()  # replay
-    e = d.engine.sample_loop(8, x_cond=xc, seed=78, graph=True, out=out)[0]          # new seed, same graph
+    # `out` is reused so the captured graph is replayed: clone each result before the next call
+    b = d.engine.sample_loop(8, x_cond=xc, seed=77, graph=True, out=out, keep_start=False)[0].clone()
+    c = d.engine.sample_loop(8, x_cond=xc, seed=77, graph=True, out=out, keep_start=False)[0].clone()
+    e = d.engine.sample_loop(8, x_cond=xc, seed=78, graph=True, out=out, keep_start=False)[0].clone()
     torch.cuda.synchronize()
     assert torch.equal(a, b) and torch.equal(a, c)
     assert not torch.equal(a, e)
@@ -147,7 +148,7 @@ def test_ragged_batches(B, cuda):
     img = d.sample(batch_size=B, x_cond=xc.to(cuda), start_noise=start.to(cuda), sampling_noise=samp.to(cuda))[0]
     cfg = O.release_config(J, z["node_types"])
     sd = O.synthetic_state_dict(cfg, WEIGHT_SEED)
-    S, L, U = O.get_cov_from_corr(torch.from_numpy(z["corr"]))
+    S, L, U = pinned_cov(J)
     bufs = O.nonisotropic_buffers(S, L, U, O.beta_schedule("cosine", 10))
     ref, _ = O.p_sample_loop(sd, cfg, bufs, start, samp, x_cond=xc)
     assert _max_err(img, ref) < TOL
@@ -175,7 +176,7 @@ def test_single_step_p_sample(cuda):
     J = 21
     cfg = O.release_config(J, z["node_types"])
     sd = O.synthetic_state_dict(cfg, WEIGHT_SEED, float(z["final_scale"]))
-    S, L, U = O.get_cov_from_corr(torch.from_numpy(z["corr"]))
+    S, L, U = pinned_cov(J)
     bufs = O.nonisotropic_buffers(S, L, U, O.beta_schedule("cosine", 10))
     xc = xcs.repeat_interleave(fu, 0)
     out = O.denoiser_forward(sd, cfg, start, torch.full((4,), t), xc).clamp(-1, 1)
