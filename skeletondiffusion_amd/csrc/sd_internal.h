@@ -27,7 +27,9 @@ struct GLArgs {
     int N;
     int J;
     int act;                                              // 0 none, 1 tanh
+    int ntypes;                                           // number of node types (rows of W / N)
     int wrow[kMaxNodes];                                  // type(j) * N  (row offset into W)
+    int ntype[kMaxNodes];                                 // type(j)
 };
 
 // Multi-head attention over joints (attention.py:122-136) from a (B, J, 3*heads*dh) qkv buffer.
@@ -48,7 +50,10 @@ struct UpdArgs {
     int64_t B; int J; int D;
 };
 
-hipError_t launch_graph_linear(const GLArgs& a, bool rms, hipStream_t s);
+hipError_t launch_graph_linear(const GLArgs& a, bool rms, hipStream_t s);     // dispatches v1 / v2
+hipError_t launch_graph_linear_v1(const GLArgs& a, bool rms, hipStream_t s);
+hipError_t launch_graph_linear_v2(const GLArgs& a, bool rms, hipStream_t s);
+int graph_linear_variant();  // SKELDIFF_GL_VARIANT (default 2), read once
 hipError_t launch_attention(const AttnArgs& a, hipStream_t s);
 hipError_t launch_update(const UpdArgs& a, hipStream_t s);
 hipError_t launch_noise_fill(float* out, int64_t rows, int64_t n_per_row, uint64_t seed,

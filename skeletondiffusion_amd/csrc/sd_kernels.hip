@@ -14,6 +14,7 @@
 // All arithmetic is fp32; the GEMMs use the exact-f32 MFMA (a k-ordered fmaf chain).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "sd_internal.h"
 
@@ -189,7 +190,19 @@ static hipError_t gl_dispatch_rms(const GLArgs& a, bool rms, hipStream_t s) {
     return hipGetLastError();
 }
 
+int graph_linear_variant() {
+    static const int v = [] {
+        const char* e = getenv("SKELDIFF_GL_VARIANT");
+        return (e && atoi(e) == 1) ? 1 : 2;
+    }();
+    return v;
+}
+
 hipError_t launch_graph_linear(const GLArgs& a, bool rms, hipStream_t s) {
+    return graph_linear_variant() == 1 ? launch_graph_linear_v1(a, rms, s) : launch_graph_linear_v2(a, rms, s);
+}
+
+hipError_t launch_graph_linear_v1(const GLArgs& a, bool rms, hipStream_t s) {
     if (a.B <= 0) return hipSuccess;
     switch (a.J) {
         case 16: return gl_dispatch_rms<16, true, 2>(a, rms, s);

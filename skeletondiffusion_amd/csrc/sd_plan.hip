@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cmath>
+#include <algorithm>
 #include <cstring>
 #include <map>
 #include <memory>
@@ -193,7 +194,11 @@ sd::GLArgs gl_args(const sd_plan* p, const GL& g, const float* x1, int x1_div, c
     a.N = g.N;
     a.J = p->J;
     a.act = 0;
-    for (int j = 0; j < p->J; ++j) a.wrow[j] = p->types[j] * g.N;
+    a.ntypes = p->ntypes;
+    for (int j = 0; j < p->J; ++j) {
+        a.wrow[j] = p->types[j] * g.N;
+        a.ntype[j] = p->types[j];
+    }
     return a;
 }
 
@@ -762,7 +767,13 @@ int sd_test_graph_linear(const float* x1, int32_t K1, int64_t x1_div, const floa
     a.N = N;
     a.J = J;
     a.act = act;
-    for (int j = 0; j < J; ++j) a.wrow[j] = (int)node_types[j] * N;
+    a.ntypes = 1;
+    for (int j = 0; j < J; ++j) {
+        if (node_types[j] < 0) return fail(SD_E_INVALID, "negative node type");
+        a.wrow[j] = (int)node_types[j] * N;
+        a.ntype[j] = (int)node_types[j];
+        a.ntypes = std::max(a.ntypes, (int)node_types[j] + 1);
+    }
     SD_HIP(sd::launch_graph_linear(a, rms != 0, (hipStream_t)stream));
     return SD_OK;
 }
