@@ -61,9 +61,14 @@ __global__ __launch_bounds__(256, MINW) void k_gl2(const GLArgs p) {
     float* sW1 = smem + stage;
     float* sG = smem + 2 * stage;
 
+    // XCD-aware tile order (cdna_hip_programming.md §5.5 T1): blocks b and b+8 share an XCD, so
+    // logical tile L = (blocks of this XCD, in order) keeps the column tiles of one row tile -
+    // which re-read the same x rows - inside one XCD's L2.  Bijective for any grid size.
     const int ntile_c = (p.N + NT - 1) / NT;
-    const int ct = blockIdx.x % ntile_c;
-    const int64_t rt = blockIdx.x / ntile_c;
+    const int nwg = gridDim.x, xcd = blockIdx.x & 7, q8 = nwg >> 3, r8 = nwg & 7;
+    const int L = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (blockIdx.x >> 3);
+    const int ct = L % ntile_c;
+    const int64_t rt = L / ntile_c;
     const int64_t row0 = rt * 64 + wave * 16;
     const int c0 = ct * NT;
     const int K = p.K1 + p.K2;
