@@ -16,6 +16,7 @@
 // next fill overwrites (WAR).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "sd_internal.h"
 
@@ -32,6 +33,14 @@ __device__ __forceinline__ floatx4 mfma4(float a, float b, floatx4 c) {
 }
 
 typedef __attribute__((address_space(3))) void lds_void;
+
+// s_waitcnt immediate for "vmcnt <= n" with lgkmcnt / expcnt untouched (gfx9 encoding:
+// vmcnt[3:0] | expcnt[6:4] | lgkmcnt[11:8] | vmcnt_hi[15:14])
+template <int N>
+struct VmCnt {
+    static_assert(N >= 0 && N < 64, "vmcnt range");
+    static constexpr int imm = (N & 0xF) | (0x7 << 4) | (0xF << 8) | ((N >> 4) << 14);
+};
 
 template <int NT>
 __device__ __forceinline__ void fill_w_stage(const GLArgs& p, int c0, int k0, int K, float* dst, int wave,
@@ -79,10 +88,12 @@ __global__ __launch_bounds__(256, MINW) void k_gl2(const GLArgs p) {
     const int64_t arow_c = rok ? arow : 0;
     const float* x1r = p.x1 + (arow_c / p.x1_div) * p.x1_rs + 4 * lg;
     const float* x2r = p.K2 ? p.x2 + arow_c * p.x2_rs + 4 * lg : nullptr;
+    // Tail rows read row 0 (valid memory) and are never stored, so every wave issues exactly J
+    // x loads per chunk - the counted vmcnt below relies on that count.
     auto load_a = [&](int c, int j) -> floatx4 {
         const int k0 = c << 4;
         const float* src = (k0 < p.K1) ? x1r + (int64_t)j * p.K1 + k0 : x2r + (int64_t)j * p.K2 + (k0 - p.K1);
-        return rok ? gld4(src) : floatx4{0.f, 0.f, 0.f, 0.f};
+        return gld4(src);
     };
 
     floatx4 acc[JM][NCB];
@@ -109,21 +120,35 @@ __global__ __launch_bounds__(256, MINW) void k_gl2(const GLArgs p) {
         const float* cur = (c & 1) ? sW1 : sW0;
         if (c + 1 < nchunk) fill_w_stage<NT>(p, c0, (c + 1) << 4, K, (c & 1) ? sW0 : sW1, wave, lane);
         const bool rms_chunk = RMS && (c << 4) < p.K1;
+        const int cn = min(c + 1, nchunk - 1);  // branch-free prefetch (last chunk re-reads itself)
+        // B fragments are read one node ahead so the ds_read latency hides under the MFMAs
+        floatx4 bnext[NCB];
+#pragma unroll
+        for (int cb = 0; cb < NCB; ++cb)
+            bnext[cb] = *reinterpret_cast<const floatx4*>(cur + ((p.ntype[0] * 4 + lg) * NT + lr) * 4 + cb * 64);
 #pragma unroll
         for (int j = 0; j < JM; ++j) {
             if (!EXACT && j >= J) continue;
+            floatx4 bj[NCB];
+#pragma unroll
+            for (int cb = 0; cb < NCB; ++cb) bj[cb] = bnext[cb];
+            if (j + 1 < JM && (EXACT || j + 1 < J)) {
+#pragma unroll
+                for (int cb = 0; cb < NCB; ++cb)
+                    bnext[cb] = *reinterpret_cast<const floatx4*>(
+                        cur + ((p.ntype[j + 1] * 4 + lg) * NT + lr) * 4 + cb * 64);
+            }
             floatx4 aj;
             if (PREF) {
                 aj = a[j];
-                if (c + 1 < nchunk) a[j] = load_a(c + 1, j);
+                a[j] = load_a(cn, j);
             } else {
                 aj = load_a(c, j);
             }
             if (rms_chunk) ss[j] += aj.x * aj.x + aj.y * aj.y + aj.z * aj.z + aj.w * aj.w;
-            const float* wl = cur + ((p.ntype[j] * 4 + lg) * NT + lr) * 4;
 #pragma unroll
             for (int cb = 0; cb < NCB; ++cb) {
-                const floatx4 b = *reinterpret_cast<const floatx4*>(wl + cb * 64);
+                const floatx4 b = bj[cb];
                 floatx4 cc = acc[j][cb];
                 cc = mfma4(aj.x, b.x, cc);
                 cc = mfma4(aj.y, b.y, cc);
@@ -132,8 +157,21 @@ __global__ __launch_bounds__(256, MINW) void k_gl2(const GLArgs p) {
                 acc[j][cb] = cc;
             }
         }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
+        bool counted = false;
+        if constexpr (PREF && EXACT) {
+            if (c + 1 < nchunk) {
+                // Issue order in this chunk: weight DMA for c+1 first, then the J x prefetches
+                // for c+1.  vmcnt(J) retires the DMA while leaving the x loads in flight across
+                // the barrier (a __syncthreads() would emit vmcnt(0) and drain them).
+                __builtin_amdgcn_s_waitcnt(VmCnt<JM>::imm);
+                __builtin_amdgcn_s_barrier();
+                counted = true;
+            }
+        }
+        if (!counted) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();
+        }
     }
 
     if (row0 >= p.B) return;  // no barrier below
@@ -220,13 +258,26 @@ static hipError_t gl2_launch(const GLArgs& a, bool rms, hipStream_t s) {
     return hipGetLastError();
 }
 
+// Column-tile width: 32 (NCB=2) halves the x re-reads, 16 (NCB=1) doubles the number of
+// workgroups; at small B*N the 32-wide grid cannot give every CU two workgroups, so go narrow.
+// SKELDIFF_GL_NCB=1|2 forces a width (tuning / A-B runs).
+static int ncb_choice(const GLArgs& a) {
+    static const int forced = [] {
+        const char* e = getenv("SKELDIFF_GL_NCB");
+        return e ? atoi(e) : 0;
+    }();
+    if (forced == 1 || forced == 2) return forced;
+    const int64_t wgs32 = (int64_t)((a.N + 31) / 32) * ((a.B + 63) / 64);
+    return wgs32 >= 2 * 256 ? 2 : 1;
+}
+
 hipError_t launch_graph_linear_v2(const GLArgs& a, bool rms, hipStream_t s) {
     if (a.B <= 0) return hipSuccess;
-    // NCB=2 keeps the 32-column tile when the plan's weights fit two LDS stages comfortably
-    const bool wide = a.ntypes * 32 * 16 * 4 * 2 <= 96 * 1024;
+    // two 32-column weight stages must fit comfortably in LDS
+    const bool wide = ncb_choice(a) == 2 && a.ntypes * 32 * 16 * 4 * 2 <= 96 * 1024;
     switch (a.J) {
-        case 16: return wide ? gl2_launch<16, true, 2, true, 2>(a, rms, s) : gl2_launch<16, true, 1, true, 2>(a, rms, s);
-        case 17: return wide ? gl2_launch<17, true, 2, true, 2>(a, rms, s) : gl2_launch<17, true, 1, true, 2>(a, rms, s);
+        case 16: return wide ? gl2_launch<16, true, 2, true, 2>(a, rms, s) : gl2_launch<16, true, 1, true, 3>(a, rms, s);
+        case 17: return wide ? gl2_launch<17, true, 2, true, 2>(a, rms, s) : gl2_launch<17, true, 1, true, 3>(a, rms, s);
         case 21: return gl2_launch<21, true, 1, true, 2>(a, rms, s);
         case 51: return gl2_launch<51, true, 1, false, 1>(a, rms, s);
         default: break;
