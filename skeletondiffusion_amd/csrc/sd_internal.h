@@ -53,7 +53,8 @@ struct UpdArgs {
 hipError_t launch_graph_linear(const GLArgs& a, bool rms, hipStream_t s);     // dispatches v1 / v2
 hipError_t launch_graph_linear_v1(const GLArgs& a, bool rms, hipStream_t s);
 hipError_t launch_graph_linear_v2(const GLArgs& a, bool rms, hipStream_t s);
-int graph_linear_variant();  // SKELDIFF_GL_VARIANT (default 2), read once
+hipError_t launch_graph_linear_v3(const GLArgs& a, bool rms, hipStream_t s);  // J in {16,17,21}
+int graph_linear_variant();  // SKELDIFF_GL_VARIANT (1, 2, 3), read once
 hipError_t launch_attention(const AttnArgs& a, hipStream_t s);
 hipError_t launch_update(const UpdArgs& a, hipStream_t s);
 hipError_t launch_noise_fill(float* out, int64_t rows, int64_t n_per_row, uint64_t seed,

@@ -193,13 +193,22 @@ static hipError_t gl_dispatch_rms(const GLArgs& a, bool rms, hipStream_t s) {
 int graph_linear_variant() {
     static const int v = [] {
         const char* e = getenv("SKELDIFF_GL_VARIANT");
-        return (e && atoi(e) == 1) ? 1 : 2;
+        const int x = e ? atoi(e) : 0;
+        return (x >= 0 && x <= 3) ? x : 0;
     }();
     return v;
 }
 
+// 0 (default) = per shape: v3 (node-split waves, 32x32 MFMA) for N < 512, where it measured
+// 1.15-1.25x faster than v2; v2 with 32-column tiles for the wide to_qkv layer (N = 768).
 hipError_t launch_graph_linear(const GLArgs& a, bool rms, hipStream_t s) {
-    return graph_linear_variant() == 1 ? launch_graph_linear_v1(a, rms, s) : launch_graph_linear_v2(a, rms, s);
+    const int v = graph_linear_variant();
+    if (v == 1) return launch_graph_linear_v1(a, rms, s);
+    if (v == 3 || (v == 0 && a.N < 512)) {
+        const hipError_t e = launch_graph_linear_v3(a, rms, s);
+        if (e != hipErrorNotSupported) return e;
+    }
+    return launch_graph_linear_v2(a, rms, s);
 }
 
 hipError_t launch_graph_linear_v1(const GLArgs& a, bool rms, hipStream_t s) {

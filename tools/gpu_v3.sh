@@ -1,0 +1,11 @@
+#!/bin/bash
+mkdir -p gpurun_out
+SKELDIFF_GL_VARIANT=3 timeout -k 10 600 python -m pytest tests/test_gpu_kernels.py tests/test_gpu_parity.py -m gpu -q -x > gpurun_out/pytest_v3.log 2>&1
+rc=$?; echo "pytest_rc=$rc"; [ $rc -le 1 ] || exit $rc
+: > gpurun_out/bench_gl.log
+for v in "SKELDIFF_GL_VARIANT=2" "SKELDIFF_GL_VARIANT=3"; do
+  env $v timeout -k 10 120 python tools/bench_gl.py >> gpurun_out/bench_gl.log 2>&1
+  rc=$?; [ $rc -eq 0 ] || { echo "bench_gl $v rc=$rc"; exit $rc; }
+done
+SKELDIFF_GL_VARIANT=3 timeout -k 10 300 python bench.py --steps 3 --warmup 1 --no-cpu-baseline > gpurun_out/bench_v3.log 2>&1
+echo "bench_rc=$?"

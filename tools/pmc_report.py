@@ -1,0 +1,24 @@
+"""Summarise tools/pmc_gl.sh output: MFMA utilisation, stall split, instruction mix."""
+import collections
+import csv
+import glob
+import sys
+
+for tag in sys.argv[1:]:
+    vals = collections.defaultdict(list)
+    for f in sorted(glob.glob(f"gpurun_out/pmc_gl_{tag}/p*/run_counter_collection.csv")):
+        for r in csv.DictReader(open(f)):
+            if "k_gl" not in r["Kernel_Name"] and "k_graph_linear" not in r["Kernel_Name"]:
+                continue
+            vals[r["Counter_Name"]].append(float(r["Counter_Value"]))
+    a = {k: sum(v) / len(v) for k, v in vals.items()}
+    w = a.get("SQ_WAVE_CYCLES", 1)
+    gui = a.get("GRBM_GUI_ACTIVE", 8) / 8          # summed over the 8 XCDs
+    print(f"===== {tag}: kernel {gui / 2.4e3:.1f} us (at 2.4 GHz)  MFMA util "
+          f"{a.get('SQ_VALU_MFMA_BUSY_CYCLES', 0) / (gui * 1024) * 100:.1f}%  waves/SIMD {w * 4 / (gui * 1024):.2f}")
+    print(f"  wait_any {a.get('SQ_WAIT_ANY', 0) / w * 100:.1f}%  wait_inst {a.get('SQ_WAIT_INST_ANY', 0) / w * 100:.1f}%"
+          f"  active {a.get('SQ_ACTIVE_INST_ANY', 0) / w * 100:.1f}%")
+    hit = a.get("TCC_HIT_sum", 0) / max(a.get("TCC_HIT_sum", 0) + a.get("TCC_MISS_sum", 0), 1)
+    print(f"  insts VALU {a.get('SQ_INSTS_VALU', 0):,.0f} LDS {a.get('SQ_INSTS_LDS', 0):,.0f} VMEM "
+          f"{a.get('SQ_INSTS_VMEM', 0):,.0f} SALU {a.get('SQ_INSTS_SALU', 0):,.0f}  LDS bank conflicts "
+          f"{a.get('SQ_LDS_BANK_CONFLICT', 0):,.0f}  L2 hit {hit * 100:.1f}%")
