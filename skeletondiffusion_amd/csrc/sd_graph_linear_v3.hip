@@ -39,6 +39,13 @@ struct VmCnt3 {
     static constexpr int imm = (N & 0xF) | (0x7 << 4) | (0xF << 8) | ((N >> 4) << 14);
 };
 
+// tanh(x) = 1 - 2 / (exp(2x) + 1): v_exp_f32 + v_rcp_f32; saturates cleanly at +-1 and is
+// within ~2e-7 absolute of tanhf (the layer outputs feed a 1e-4 end-to-end bar)
+__device__ __forceinline__ float fast_tanh(float x) {
+    const float e = __expf(2.0f * x);
+    return 1.0f - 2.0f * __frcp_rn(e + 1.0f);
+}
+
 constexpr int YSTRIDE = 528;  // floats per node in the Y half-tile (16 x 32 + 16 pad: lg rows -> other banks)
 
 // weight chunk -> LDS stage, piece q = ((type*2 + h)*2 + kq)*32 + col  (16 B each)
@@ -115,17 +122,22 @@ __global__ __launch_bounds__(256, 2) void k_gl3(const GLArgs p) {
         if (c + 1 < nchunk) fill_w3(p, c0, (c + 1) << 4, K, (c & 1) ? sW0 : sW1, wave, lane);
         const int cn = min(c + 1, nchunk - 1);
         const bool rms_chunk = RMS && (c << 4) < p.K1;
+        auto wfrag = [&](int m) { return cur + (((p.ntype[min(node_of(m), J - 1)] * 2 + h) * 2) * 32 + l32) * 4; };
+        floatx4 wa_n = l4(wfrag(0)), wb_n = l4(wfrag(0) + 128);  // weight fragments read one node ahead
 #pragma unroll
         for (int m = 0; m < NPW; ++m) {
             const int j = node_of(m);
             const floatx4 xa = a0[m], xb = a1[m];
+            const floatx4 wa = wa_n, wb = wb_n;
+            if (m + 1 < NPW) {
+                wa_n = l4(wfrag(m + 1));
+                wb_n = l4(wfrag(m + 1) + 128);
+            }
             load_x(cn, m, a0[m], a1[m]);  // every wave issues exactly 2*NPW loads (vmcnt below)
             if (j >= J) continue;         // wave-uniform: only the MFMAs are skipped
             if (rms_chunk)
                 ss[m] += xa.x * xa.x + xa.y * xa.y + xa.z * xa.z + xa.w * xa.w + xb.x * xb.x + xb.y * xb.y +
                          xb.z * xb.z + xb.w * xb.w;
-            const float* wl = cur + (((p.ntype[j] * 2 + h) * 2) * 32 + l32) * 4;
-            const floatx4 wa = l4(wl), wb = l4(wl + 128);
             floatx16 cc = acc[m];
             cc = __builtin_amdgcn_mfma_f32_32x32x2f32(xa.x, wa.x, cc, 0, 0, 0);
             cc = __builtin_amdgcn_mfma_f32_32x32x2f32(xa.y, wa.y, cc, 0, 0, 0);
@@ -208,30 +220,40 @@ __global__ __launch_bounds__(256, 2) void k_gl3(const GLArgs p) {
 #pragma unroll 2
         for (int b = 0; b < 8; ++b) {
             const int rc = (wave * 8 + b) * 16 + lr;
+            const int r = rc >> 5, cc = rc & 31;
+            const int64_t row = row0 + 16 * hf + r;
+            const int n = c0 + cc;
+            const int hb = cc >> 4;
+            const bool ok = row < p.B && n < p.N;
+            // residual loads first: their latency hides under the LDS reads + mixing MFMAs
+            float rv[IB][4];
+#pragma unroll
+            for (int ib = 0; ib < IB; ++ib)
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const int i = ib * 16 + 4 * lg + e;
+                    rv[ib][e] = (p.res && ok && i < J) ? p.res[row * p.res_rs + (int64_t)i * p.N + n] : 0.f;
+                }
             float yb[KS];
 #pragma unroll
             for (int s = 0; s < KS; ++s) {
                 const int jj = 4 * s + lg;
                 yb[s] = jj < J ? sY[jj * YSTRIDE + rc] : 0.f;
             }
-            const int r = rc >> 5, cc = rc & 31;
-            const int64_t row = row0 + 16 * hf + r;
-            const int n = c0 + cc;
-            const int hb = cc >> 4;
 #pragma unroll
             for (int ib = 0; ib < IB; ++ib) {
                 floatx4 z = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
                 for (int s = 0; s < KS; ++s) z = __builtin_amdgcn_mfma_f32_16x16x4f32(ga[ib][s], yb[s], z, 0, 0, 0);
-                if (row >= p.B || n >= p.N) continue;
+                if (!ok) continue;
 #pragma unroll
                 for (int e = 0; e < 4; ++e) {
                     const int i = ib * 16 + 4 * lg + e;
                     if (i >= J) continue;
                     float v = z[e];
                     if (p.film) v = v * fa[hb] + fb[hb];
-                    if (p.act == 1) v = tanhf(v);
-                    if (p.res) v += p.res[row * p.res_rs + (int64_t)i * p.N + n];
+                    if (p.act == 1) v = fast_tanh(v);
+                    v += rv[ib][e];
                     p.out[row * p.out_rs + (int64_t)i * p.N + n] = v;
                 }
             }
