@@ -31,11 +31,14 @@ ntile_r = (rows_b + 63) // 64
 by_shape = defaultdict(list)
 for r in trace:
     n = r["Kernel_Name"]
-    if "k_gl2" not in n and "k_graph_linear" not in n:
+    if "k_gl2" not in n and "k_graph_linear" not in n and "k_gl3" not in n:
         continue
     wgs = int(r.get("Grid_Size") or r["Grid_Size_X"]) // 256
-    nt = wgs // ntile_r
-    NT = 32 if ", 2, " in n.split("<")[1] else 16
+    if "k_gl3" in n:
+        nt, NT = wgs // ((rows_b + 31) // 32), 32
+    else:
+        nt = wgs // ntile_r
+        NT = 32 if ", 2, " in n.split("<")[1] else 16
     by_shape[(short(n), nt * NT)].append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
 
 # per layer (K1+K2, N) of the release Denoiser at this J
@@ -67,7 +70,7 @@ if traffic:
         f = traffic["fetch"].get(k, 0.0)
         w = traffic.get("write", {}).get(k, 0.0)
         lines.append(f"| `{k[:60]}` | {f:.0f} | {w:.0f} | {(2 * f + w) * 1024 / 1e6:.1f} |")
-    gl = [k for k in traffic.get("fetch", {}) if "k_gl2" in k or "k_graph_linear" in k]
+    gl = [k for k in traffic.get("fetch", {}) if "k_gl" in k or "k_graph_linear" in k]
     if gl:
         calls = {short(s["Name"]): int(s["Calls"]) for s in stats}
         tot_calls = sum(calls.get(k, 0) for k in gl)
