@@ -167,6 +167,11 @@ int sd_test_graph_linear(const float* x1, int32_t K1, int64_t x1_div, const floa
                          int32_t J, int32_t N, int32_t rms, void* stream);
 int sd_test_attention(const float* qkv, float* out, int64_t rows, int32_t J, int32_t heads,
                       int32_t dim_head, void* stream);
+/* Kernel-generation selector (tests / tuning; process-wide, affects launches recorded after it):
+ * gl_variant 0 = auto (v4 split-f16 where available, else exact-f32 v3/v2), 1..3 = exact-f32
+ * generations, 4 = v4; gl4_tile = <waves><row tiles><col tiles> (e.g. 822) or 0 = auto,
+ * -1 leaves it.  Returns the previous gl_variant, or -1 for an invalid one (nothing changed). */
+int sd_set_kernel_variant(int32_t gl_variant, int32_t gl4_tile);
 
 #ifdef __cplusplus
 }

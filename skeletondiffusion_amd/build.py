@@ -9,7 +9,8 @@ import subprocess
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 OUT = os.path.join(HERE, "libskeldiff.so")
-SOURCES = ["sd_kernels.hip", "sd_graph_linear.hip", "sd_graph_linear_v3.hip", "sd_plan.hip"]
+SOURCES = ["sd_kernels.hip", "sd_graph_linear.hip", "sd_graph_linear_v3.hip", "sd_graph_linear_v4.hip",
+           "sd_plan.hip"]
 HEADERS = ["sd_internal.h", os.path.join("..", "..", "include", "skeldiff.h")]
 
 
@@ -30,15 +31,18 @@ def _stale() -> bool:
 def build_library(force: bool = False, verbose: bool = False) -> str:
     if not force and not _stale():
         return OUT
-    objs = []
-    for src in SOURCES:
+    objs, procs = [], []
+    for src in SOURCES:  # one hipcc per translation unit, in parallel
         obj = os.path.join(CSRC, src.replace(".hip", ".o"))
         cmd = [_hipcc(), "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-c",
                "-Wno-pass-failed", os.path.join(CSRC, src), "-o", obj]
         if verbose:
             print(" ".join(cmd))
-        subprocess.run(cmd, check=True)
+        procs.append((src, subprocess.Popen(cmd)))
         objs.append(obj)
+    failed = [src for src, pr in procs if pr.wait() != 0]
+    if failed:
+        raise RuntimeError("hipcc failed: " + ", ".join(failed))
     tmp = OUT + ".tmp"
     subprocess.run([_hipcc(), "--offload-arch=gfx950", "-shared", "-fPIC", "-o", tmp] + objs, check=True)
     os.replace(tmp, OUT)

@@ -1,0 +1,531 @@
+// k_gl4: StaticGraphLinear (graph_structural.py:30-43) + fused epilogue on f16 MFMA with
+// f32-accurate split products.
+//
+// gfx950 runs f32-input MFMA at 1/16 of the f16 rate (MI355X_MICROARCH.md: 157 vs 2,500 TF/s).
+// v4 keeps f32 accuracy by splitting both operands into two f16 terms and summing three
+// products in the f32 accumulator:
+//     W' = W * 2^sW  (sW per layer: max|W'| < 2^15),  W'_hi = f16(W'),  W'_lo = f16(W' - W'_hi)
+//     x_hi = f16(x),  x_lo = f16(x - x_hi)
+//     y = 2^-sW * (x_hi W'_hi + x_hi W'_lo + x_lo W'_hi)          (all products exact in f32)
+// Each operand keeps ~22 significant bits; the dropped x_lo W'_lo term is ~2^-22 relative and an
+// f16-subnormal x_lo costs at most 2^-25 absolute per element.  tools/sim_split_f16.py measures
+// the end-to-end effect on T=100 chains: within the f32-vs-f64 drift of the exact path
+// (|split - f64| <= |f32 - f64|, ~1e-7, against the 1e-4 parity bar).
+//
+// Schedule (one workgroup = RT*32 rows x CT*32 output columns x all J nodes):
+//   * NW waves; wave w owns nodes w, w+NW, ...; per node an RT x CT grid of 32x32 f32
+//     accumulators on v_mfma_f32_32x32x16_f16 (3 MFMAs per 16-deep k step and tile);
+//   * weights: pre-split at plan finalize into the exact B-fragment order
+//     [type][k16 chunk][32-col tile][hi|lo][lane][8], so a chunk's slice for the workgroup's
+//     columns is one contiguous span per type, streamed into LDS by LDS-DMA (16 B per lane,
+//     double-buffered) and read back with conflict-free ds_read_b128 (lane l -> l*16 B);
+//   * x: each lane streams 8 contiguous k of one row per node (2 float4) a chunk ahead and
+//     splits them in registers (the activations stay f32 in HBM);
+//   * epilogue as v3: scale/RMS/bias in the accumulator layout, Y through LDS in 16-row slabs,
+//     G-hat mixing on 16x16x4 f32 MFMA, FiLM / tanh / residual / store.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdlib.h>
+
+#include <algorithm>
+#include <cmath>
+
+#include "sd_internal.h"
+
+namespace sd {
+
+typedef float floatx4 __attribute__((ext_vector_type(4)));
+typedef float floatx8 __attribute__((ext_vector_type(8)));
+typedef float floatx16 __attribute__((ext_vector_type(16)));
+typedef _Float16 halfx8 __attribute__((ext_vector_type(8)));
+
+namespace {
+
+typedef __attribute__((address_space(3))) void lds_void;
+
+template <int N>
+struct VmCnt4 {
+    static_assert(N >= 0 && N < 64, "vmcnt range");
+    static constexpr int imm = (N & 0xF) | (0x7 << 4) | (0xF << 8) | ((N >> 4) << 14);
+};
+
+__device__ __forceinline__ floatx4 g4(const float* p) { return *reinterpret_cast<const floatx4*>(p); }
+
+// tanh(x) = 1 - 2 / (exp(2x) + 1) on v_exp_f32 + v_rcp_f32 (no IEEE division sequence):
+// saturates cleanly at +-1, within ~3e-7 absolute of tanhf
+__device__ __forceinline__ float tanh4(float x) {
+    const float e = __builtin_amdgcn_exp2f(2.0f * 1.44269504088896341f * x);
+    return 1.0f - 2.0f * __builtin_amdgcn_rcpf(e + 1.0f);
+}
+
+// ---- one-time weight preparation ------------------------------------------------------------
+
+__global__ void k_absmax(const float* __restrict__ w, int64_t n, unsigned* __restrict__ out) {
+    unsigned m = 0;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+        m = max(m, __float_as_uint(fabsf(w[i])));
+    for (int o = 32; o > 0; o >>= 1) m = max(m, (unsigned)__shfl_xor((int)m, o));
+    if ((threadIdx.x & 63) == 0) atomicMax(out, m);
+}
+
+// out[type][c][ct][hl][lane][e] = split(W[type][32ct + (lane&31)][16c + 8(lane>>5) + e] * scale)
+__global__ void k_split_w(const float* __restrict__ W, int ntypes, int N, int K, int nct, float scale,
+                          _Float16* __restrict__ out) {
+    const int nchunk = K >> 4;
+    const int64_t total = (int64_t)ntypes * nchunk * nct * 64;
+    for (int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; g < total; g += (int64_t)gridDim.x * blockDim.x) {
+        const int lane = (int)(g & 63);
+        int64_t r = g >> 6;
+        const int ct = (int)(r % nct);
+        r /= nct;
+        const int c = (int)(r % nchunk);
+        const int t = (int)(r / nchunk);
+        const int n = 32 * ct + (lane & 31);
+        const int k0 = 16 * c + 8 * (lane >> 5);
+        _Float16* hi = out + ((((int64_t)t * nchunk + c) * nct + ct) * 2) * 512 + lane * 8;
+        _Float16* lo = hi + 512;
+        for (int e = 0; e < 8; ++e) {
+            const float v = n < N ? W[((int64_t)t * N + n) * K + k0 + e] * scale : 0.f;
+            const _Float16 h = (_Float16)v;
+            hi[e] = h;
+            lo[e] = (_Float16)(v - (float)h);
+        }
+    }
+}
+
+}  // namespace
+
+hipError_t make_split_weights(const float* W, int ntypes, int N, int K, SplitW* out, hipStream_t s) {
+    out->nct = ((N + 31) / 32 + 1) & ~1;  // 32-col tiles, padded to a multiple of 2 (CT <= 2)
+    const int64_t n = (int64_t)ntypes * N * K;
+    unsigned* dmax = nullptr;
+    unsigned hmax = 0;
+    hipError_t e = hipMalloc(&dmax, sizeof(unsigned));
+    if (e != hipSuccess) return e;
+    if ((e = hipMemsetAsync(dmax, 0, sizeof(unsigned), s)) != hipSuccess) return e;
+    hipLaunchKernelGGL(k_absmax, dim3(256), dim3(256), 0, s, W, n, dmax);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    if ((e = hipMemcpyAsync(&hmax, dmax, sizeof(unsigned), hipMemcpyDeviceToHost, s)) != hipSuccess) return e;
+    if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;
+    (void)hipFree(dmax);
+    const float amax = __builtin_bit_cast(float, hmax);
+    int ex = 0;
+    if (amax > 0.f && amax == amax && amax < 3.0e38f) (void)frexpf(amax, &ex);  // amax < 2^ex
+    // W * 2^(15 - ex) < 2^15: inside f16 range, and the lo term of every weight within 2^-18
+    // of the largest stays a normal f16
+    out->scale = ldexpf(1.0f, 15 - ex);
+    out->unscale = ldexpf(1.0f, ex - 15);
+    const size_t halves = (size_t)ntypes * (K / 16) * out->nct * 1024;
+    if ((e = hipMalloc(&out->w, halves * sizeof(_Float16))) != hipSuccess) return e;
+    const int64_t total = (int64_t)ntypes * (K / 16) * out->nct * 64;
+    const int blocks = (int)std::min<int64_t>((total + 255) / 256, 4096);
+    hipLaunchKernelGGL(k_split_w, dim3(blocks), dim3(256), 0, s, W, ntypes, N, K, out->nct, out->scale, out->w);
+    return hipGetLastError();
+}
+
+template <int J, int NW, int RT, int CT, bool RMS, int DBG = 0>
+__global__ __launch_bounds__(NW * 64, 1) void k_gl4(const GLArgs p) {
+    constexpr int NPW = (J + NW - 1) / NW;  // nodes per wave
+    constexpr int KS = (J + 3) / 4;         // 4-deep k steps of the mixing GEMM (K = J padded)
+    constexpr int IB = (J + 15) / 16;       // 16-row i blocks of the mixing GEMM
+    constexpr int COLS = 32 * CT;
+    constexpr int YS = 16 * COLS + 16;      // floats per node in a 16-row Y slab (+16: bank shift)
+    constexpr int NTH = NW * 64;
+    constexpr int BPW = (COLS + NW - 1) / NW;  // 16-wide mixing blocks per wave per slab
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int l32 = lane & 31, h = lane >> 5, lr = lane & 15, lg = lane >> 4;
+    const int stage_h = p.ntypes * CT * 1024;  // halves per weight stage
+    const int wfl = stage_h;                   // two stages of halves = stage_h floats
+    const int yfl = J * YS;
+    _Float16* sW0 = reinterpret_cast<_Float16*>(smem);
+    _Float16* sW1 = sW0 + stage_h;
+    float* sY = smem;  // aliases the weight stages after the K loop
+    float* sG = smem + (wfl > yfl ? wfl : yfl);
+    float* sF = sG + J * J;  // FiLM (scale + 1 | shift) for this workgroup's columns
+
+    const int ntile_c = (p.N + COLS - 1) / COLS;
+    const int nwg = gridDim.x, xcd = blockIdx.x & 7, q8 = nwg >> 3, r8 = nwg & 7;
+    const int L = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (blockIdx.x >> 3);
+    const int ctile = L % ntile_c;
+    const int64_t row0 = (int64_t)(L / ntile_c) * (32 * RT);
+    const int c0 = ctile * COLS;
+    const int K = p.K1 + p.K2;
+    const int nchunk = K >> 4;  // even (checked at launch)
+
+    const float* x1r[RT];
+    const float* x2r[RT];
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt) {
+        const int64_t arow = row0 + 32 * rt + l32;
+        const int64_t ac = arow < p.B ? arow : 0;  // tail rows read row 0, never stored
+        x1r[rt] = p.x1 + ((DBG == 4 ? row0 : ac) / p.x1_div) * p.x1_rs + 8 * h;  // DBG 4: one row per wave
+        x2r[rt] = p.K2 ? p.x2 + (DBG == 4 ? row0 : ac) * p.x2_rs + 8 * h : nullptr;
+    }
+    int jn[NPW], toff[NPW];  // wave-uniform (SGPR): clamped node, its type's stage offset
+#pragma unroll
+    for (int m = 0; m < NPW; ++m) {
+        jn[m] = min(wave + NW * m, J - 1);
+        toff[m] = p.ntype[jn[m]] * (CT * 1024);
+    }
+
+    floatx16 acc[NPW][RT][CT];
+    float ss[NPW][RT];
+#pragma unroll
+    for (int m = 0; m < NPW; ++m)
+#pragma unroll
+        for (int rt = 0; rt < RT; ++rt) {
+            ss[m][rt] = 0.f;
+#pragma unroll
+            for (int ct = 0; ct < CT; ++ct)
+#pragma unroll
+                for (int e = 0; e < 16; ++e) acc[m][rt][ct][e] = 0.f;
+        }
+
+    struct XBuf {
+        floatx4 a[NPW][RT], b[NPW][RT];
+    };
+    XBuf X0, X1;
+    auto load_x = [&](int c, XBuf& xb) {
+        const int k0 = c << 4;
+        if (DBG == 8) {  // timing experiment: x as if stored chunk-blocked (1 KiB per instruction)
+#pragma unroll
+            for (int m = 0; m < NPW; ++m)
+#pragma unroll
+                for (int rt = 0; rt < RT; ++rt) {
+                    const int64_t nblk = max((int64_t)1, (p.B / p.x1_div / 32) * J * (p.K1 / 16));  // stays inside x1
+                    const float* src = p.x1 + (((((L / ntile_c) * RT + rt) * (int64_t)J + jn[m]) * nchunk + c) % nblk) * 512;
+                    xb.a[m][rt] = g4(src + lane * 4);
+                    xb.b[m][rt] = g4(src + 256 + lane * 4);
+                }
+            return;
+        }
+#pragma unroll
+        for (int m = 0; m < NPW; ++m)
+#pragma unroll
+            for (int rt = 0; rt < RT; ++rt) {
+                const float* src = (k0 < p.K1) ? x1r[rt] + (int64_t)jn[m] * p.K1 + k0
+                                               : x2r[rt] + (int64_t)jn[m] * p.K2 + (k0 - p.K1);
+                xb.a[m][rt] = g4(src);
+                xb.b[m][rt] = g4(src + 4);
+            }
+    };
+    // LDS-DMA of chunk c's weight slice for this workgroup's columns: per type one contiguous
+    // span of CT * 2 KiB starting at tile (c0 / 32)
+    auto fill_w = [&](int c, _Float16* dst) {
+        const int per_type = CT * 128;  // 16-B pieces
+        const int npieces = p.ntypes * per_type;
+        for (int q0 = wave * 64; q0 < npieces; q0 += NTH) {
+            const int q = min(q0 + lane, npieces - 1);
+            const int t = q / per_type, rem = q - t * per_type;
+            const _Float16* src = p.wsp + (((int64_t)t * nchunk + c) * p.wsp_nct + (c0 >> 5)) * 1024 + rem * 8;
+            __builtin_amdgcn_global_load_lds((const void*)src, (lds_void*)(dst + (size_t)q0 * 8), 16, 0, 0);
+        }
+    };
+    auto compute = [&](int c, const XBuf& xb) {
+        const _Float16* cur = (c & 1) ? sW1 : sW0;
+        const bool rms_chunk = RMS && (c << 4) < p.K1;
+#pragma unroll
+        for (int m = 0; m < NPW; ++m) {
+            if (wave + NW * m >= J || DBG == 1) continue;  // wave-uniform (DBG 1: loads only)
+            const _Float16* wt = cur + toff[m] + lane * 8;
+            halfx8 xh[RT], xl[RT];
+#pragma unroll
+            for (int rt = 0; rt < RT; ++rt) {
+                const floatx8 f = {xb.a[m][rt].x, xb.a[m][rt].y, xb.a[m][rt].z, xb.a[m][rt].w,
+                                   xb.b[m][rt].x, xb.b[m][rt].y, xb.b[m][rt].z, xb.b[m][rt].w};
+                if (rms_chunk) {
+                    const floatx8 q = f * f;
+                    ss[m][rt] += ((q[0] + q[1]) + (q[2] + q[3])) + ((q[4] + q[5]) + (q[6] + q[7]));
+                }
+                if (DBG == 3) {  // timing experiment: no split VALU (operands are garbage)
+                    xh[rt] = __builtin_bit_cast(halfx8, xb.a[m][rt]);
+                    xl[rt] = __builtin_bit_cast(halfx8, xb.b[m][rt]);
+                } else {
+                    xh[rt] = __builtin_convertvector(f, halfx8);
+                    xl[rt] = __builtin_convertvector(f - __builtin_convertvector(xh[rt], floatx8), halfx8);
+                }
+            }
+#pragma unroll
+            for (int ct = 0; ct < CT; ++ct) {
+                const halfx8 wh = *reinterpret_cast<const halfx8*>(wt + ct * 1024);
+                const halfx8 wl = *reinterpret_cast<const halfx8*>(wt + ct * 1024 + 512);
+#pragma unroll
+                for (int rt = 0; rt < RT; ++rt) {
+                    floatx16 a = acc[m][rt][ct];
+                    a = __builtin_amdgcn_mfma_f32_32x32x16_f16(xh[rt], wh, a, 0, 0, 0);
+                    a = __builtin_amdgcn_mfma_f32_32x32x16_f16(xh[rt], wl, a, 0, 0, 0);
+                    a = __builtin_amdgcn_mfma_f32_32x32x16_f16(xl[rt], wh, a, 0, 0, 0);
+                    acc[m][rt][ct] = a;
+                }
+            }
+        }
+    };
+    // One k chunk: everything issued for chunk c (weight DMA + x loads) has landed -> barrier
+    // (stage c visible to all waves; every wave is past chunk c-1, so its stage is free) ->
+    // issue chunk c+1 into the other stage / register buffer -> MFMAs on chunk c.  The waitcnt
+    // is a builtin (not inline asm) so the compiler knows x(c) is complete and inserts no
+    // further vmcnt waits before the MFMAs.
+    auto step = [&](int c, const XBuf& cur, XBuf& nxt) {
+        __builtin_amdgcn_s_waitcnt(VmCnt4<0>::imm);
+        __builtin_amdgcn_s_barrier();
+        if (c + 1 < nchunk) {
+            if (DBG != 5) fill_w(c + 1, (c & 1) ? sW0 : sW1);  // DBG 5: no weight DMA
+            load_x(c + 1, nxt);
+        }
+        compute(c, cur);
+    };
+
+    uint64_t ts[6];  // DBG 6: phase stamps (s_memrealtime, 100 MHz)
+    if (DBG == 6) ts[0] = wall_clock64();
+    // G-hat and FiLM (scale + 1 | shift) for this workgroup's columns -> LDS, bias -> registers:
+    // all read by the epilogue only, after the K loop's barriers
+    for (int i = tid; i < J * J; i += NTH) sG[i] = p.G[i];
+    for (int i = tid; i < COLS; i += NTH) {
+        const int n = c0 + i;
+        sF[i] = (p.film && n < p.N) ? p.film[n] + 1.0f : 1.0f;
+        sF[COLS + i] = (p.film && n < p.N) ? p.film[p.N + n] : 0.0f;
+    }
+    float bv[NPW][CT];
+#pragma unroll
+    for (int m = 0; m < NPW; ++m)
+#pragma unroll
+        for (int ct = 0; ct < CT; ++ct) {
+            const int ncol = c0 + 32 * ct + l32;
+            bv[m][ct] = (p.bias && ncol < p.N) ? p.bias[p.wrow[jn[m]] + ncol] : 0.f;
+        }
+    fill_w(0, sW0);
+    load_x(0, X0);
+    for (int c = 0; c < nchunk; c += 2) {
+        step(c, X0, X1);
+        if (DBG == 6 && c == 0) ts[1] = wall_clock64();
+        step(c + 1, X1, X0);
+    }
+    if (DBG == 6) ts[2] = wall_clock64();
+
+    // ---- unscale, RMS, bias in the accumulator layout:
+    //      D[row = (r&3) + 8(r>>2) + 4h][col = l32] for register r of a 32x32 tile
+#pragma unroll
+    for (int m = 0; m < NPW; ++m) {
+        const int j = wave + NW * m;
+        if (j >= J) continue;
+#pragma unroll
+        for (int rt = 0; rt < RT; ++rt) {
+            float sc[16];
+#pragma unroll
+            for (int r = 0; r < 16; ++r) sc[r] = p.wsp_unscale;
+            if (RMS) {
+                const float t = ss[m][rt] + __shfl_xor(ss[m][rt], 32);  // full row l32 sum of squares
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const float n2 = __shfl(t, (r & 3) + 8 * (r >> 2) + 4 * h);
+                    sc[r] *= 1.0f / fmaxf(sqrtf(n2), 1e-12f);
+                }
+            }
+#pragma unroll
+            for (int ct = 0; ct < CT; ++ct)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) acc[m][rt][ct][r] = acc[m][rt][ct][r] * sc[r] + bv[m][ct];
+        }
+    }
+    if (DBG == 2) {  // timing experiment: K loop only, one store per lane
+        float t = 0.f;
+#pragma unroll
+        for (int m = 0; m < NPW; ++m)
+#pragma unroll
+            for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+                for (int ct = 0; ct < CT; ++ct) t += acc[m][rt][ct][0];
+        p.out[(int64_t)blockIdx.x * NTH + tid] = t;
+        return;
+    }
+
+    if (DBG == 6) ts[3] = wall_clock64();
+    // ---- mixing + epilogue, one 16-row slab at a time.  Z^T = Y^T G-hat^T on 16x16x4 f32 MFMA
+    // with Y^T as the A operand: lane (lr, lg) ends up holding D[rc = 4lg + e][i = lr], i.e. four
+    // consecutive columns of one row for node i, so residual loads and output stores are 16 B
+    // per lane.  Mixing block b covers rc = 16b .. 16b+15 (one row, 16 consecutive columns).
+    float ga[IB][KS];  // B operand: G-hat^T[k = j = 4s + lg][col = i = 16ib + lr]
+#pragma unroll
+    for (int ib = 0; ib < IB; ++ib)
+#pragma unroll
+        for (int s = 0; s < KS; ++s) {
+            const int i = ib * 16 + lr, jj = 4 * s + lg;
+            ga[ib][s] = (i < J && jj < J) ? sG[i * J + jj] : 0.f;
+        }
+    floatx4 rv[BPW][IB];
+    auto load_res = [&](int hc) {
+#pragma unroll
+        for (int k = 0; k < BPW; ++k) {
+            const int b = wave + NW * k;
+            const int rc = b * 16 + 4 * lg;
+            const int r = rc / COLS, cc = rc - r * COLS;
+            const int64_t row = row0 + 16 * hc + r;
+            const int n = c0 + cc;
+            const bool ok = b < COLS && row < p.B && n < p.N;  // N % 4 == 0 (checked at launch)
+#pragma unroll
+            for (int ib = 0; ib < IB; ++ib) {
+                const int i = ib * 16 + lr;
+                rv[k][ib] = (ok && i < J) ? g4(p.res + row * p.res_rs + (int64_t)i * p.N + n)
+                                          : floatx4{0.f, 0.f, 0.f, 0.f};
+            }
+        }
+    };
+
+#pragma unroll
+    for (int hc = 0; hc < 2 * RT; ++hc) {
+        const int rt = hc >> 1, hf = hc & 1;
+        if (p.res) load_res(hc);  // latency hides under the Y exchange below
+        __syncthreads();          // K loop / previous slab done with the LDS that sY aliases
+#pragma unroll
+        for (int m = 0; m < NPW; ++m) {
+            const int j = wave + NW * m;
+            if (j >= J) continue;
+#pragma unroll
+            for (int ct = 0; ct < CT; ++ct)
+#pragma unroll
+                for (int q = 0; q < 8; ++q) {
+                    const int r = (q & 3) + 8 * (q >> 2) + 4 * h;
+                    sY[j * YS + r * COLS + 32 * ct + l32] = acc[m][rt][ct][8 * hf + q];
+                }
+        }
+        __syncthreads();
+        // per group of PG blocks: phase 1 every LDS read, phase 2 the mixing MFMAs, phase 3
+        // FiLM / tanh / residual / 16-B stores -- no dependent chain per block
+        constexpr int PG = (IB == 1 && BPW <= 8) ? BPW : (BPW < 4 ? BPW : 4);
+#pragma unroll
+        for (int k0 = 0; k0 < BPW; k0 += PG) {
+            float ya[PG][KS];  // A operand: Y^T[row = rc = 16b + lr][k = j = 4s + lg]
+#pragma unroll
+            for (int kk = 0; kk < PG; ++kk) {
+                const int b = min(wave + NW * (k0 + kk), COLS - 1);
+#pragma unroll
+                for (int s = 0; s < KS; ++s) {
+                    const int jj = 4 * s + lg;
+                    ya[kk][s] = (k0 + kk < BPW && jj < J) ? sY[jj * YS + b * 16 + lr] : 0.f;
+                }
+            }
+            floatx4 z[PG][IB];
+#pragma unroll
+            for (int kk = 0; kk < PG; ++kk)
+#pragma unroll
+                for (int ib = 0; ib < IB; ++ib) {
+                    floatx4 t = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                    for (int s = 0; s < KS; ++s)
+                        t = __builtin_amdgcn_mfma_f32_16x16x4f32(ya[kk][s], ga[ib][s], t, 0, 0, 0);
+                    z[kk][ib] = t;
+                }
+#pragma unroll
+            for (int kk = 0; kk < PG; ++kk) {
+                const int k = k0 + kk;
+                if (k >= BPW) continue;
+                const int b = wave + NW * k;
+                const int rc = b * 16 + 4 * lg;
+                const int r = rc / COLS, cc = rc - r * COLS;
+                const int64_t row = row0 + 16 * hc + r;
+                const int n = c0 + cc;
+                const bool ok = b < COLS && row < p.B && n < p.N;
+                const floatx4 fa = *reinterpret_cast<const floatx4*>(sF + cc);
+                const floatx4 fb = *reinterpret_cast<const floatx4*>(sF + COLS + cc);
+#pragma unroll
+                for (int ib = 0; ib < IB; ++ib) {
+                    const int i = ib * 16 + lr;
+                    floatx4 v = z[kk][ib] * fa + fb;
+                    if (p.act == 1) {
+                        v.x = tanh4(v.x);
+                        v.y = tanh4(v.y);
+                        v.z = tanh4(v.z);
+                        v.w = tanh4(v.w);
+                    }
+                    if (p.res) v += rv[k][ib];
+                    if (DBG == 9) {  // timing experiment: no output stores (keep the values live)
+                        if (v.x == 12345.f) p.out[0] = v.y;
+                    } else if (DBG == 7) {  // timing experiment: each store instruction 1 KiB contiguous
+                        const int64_t nblk = max((int64_t)1, p.B * J * p.N / (NTH * 4));  // stays inside out
+                        const int64_t o = (((((int64_t)blockIdx.x * (2 * RT) + hc) * BPW + k) * IB + ib) % nblk) * NTH * 4;
+                        *reinterpret_cast<floatx4*>(p.out + o + (int64_t)tid * 4) = v;
+                    } else if (ok && i < J) {
+                        *reinterpret_cast<floatx4*>(p.out + row * p.out_rs + (int64_t)i * p.N + n) = v;
+                    }
+                }
+            }
+        }
+    }
+    if (DBG == 6) {  // stamps of wave 0 lane 0 -> out[blockIdx * 8 ..] (timing experiment only)
+        ts[4] = wall_clock64();
+        __syncthreads();
+        ts[5] = wall_clock64();
+        if (tid == 0) {
+            unsigned* o = reinterpret_cast<unsigned*>(p.out) + (size_t)blockIdx.x * 8;
+            for (int i = 0; i < 6; ++i) o[i] = (unsigned)ts[i];
+            o[6] = __smid();
+            o[7] = L;
+        }
+    }
+}
+
+template <int J, int NW, int RT, int CT, int DBG = 0>
+static hipError_t gl4_launch(const GLArgs& a, bool rms, hipStream_t s) {
+    constexpr int COLS = 32 * CT;
+    const int ntile_c = (a.N + COLS - 1) / COLS;
+    const int64_t ntile_r = (a.B + 32 * RT - 1) / (32 * RT);
+    const dim3 grid((unsigned)(ntile_c * ntile_r));
+    const size_t wfl = (size_t)a.ntypes * CT * 1024;  // two stages of halves, in floats
+    const size_t yfl = (size_t)J * (16 * COLS + 16);
+    const size_t lds = ((wfl > yfl ? wfl : yfl) + (size_t)J * J + 2 * COLS) * sizeof(float);
+    if (lds > 160 * 1024) return hipErrorNotSupported;
+    auto kt = rms ? k_gl4<J, NW, RT, CT, true, DBG> : k_gl4<J, NW, RT, CT, false, DBG>;
+    if (lds > 64 * 1024) {
+        hipError_t e = hipFuncSetAttribute((const void*)kt, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        if (e != hipSuccess) return e;
+    }
+    hipLaunchKernelGGL(kt, grid, dim3(NW * 64), lds, s, a);
+    return hipGetLastError();
+}
+
+// SKELDIFF_GL4_CFG = <NW><RT><CT> (e.g. 822) forces a tile for tuning; 0/unset = per shape.
+static int g_gl4_cfg = [] {
+    const char* e = getenv("SKELDIFF_GL4_CFG");
+    return e ? atoi(e) : 0;
+}();
+static int gl4_cfg() { return g_gl4_cfg; }
+int set_gl4_tile(int cfg) {
+    const int old = g_gl4_cfg;
+    g_gl4_cfg = cfg;
+    return old;
+}
+
+hipError_t launch_graph_linear_v4(const GLArgs& a, bool rms, hipStream_t s) {
+    if (a.B <= 0) return hipSuccess;
+    // K1, K2 multiples of 16 and an even number of 16-deep chunks (the K loop is unrolled by 2)
+    // 16-B row segments in the epilogue: N, row strides and buffers 16-B aligned
+    if ((a.N & 3) || ((uintptr_t)a.out & 15) || ((uintptr_t)a.res & 15) || (a.res && (a.res_rs & 3)) || (a.out_rs & 3))
+        return hipErrorNotSupported;
+    if (!a.wsp || (a.K1 + a.K2) % 32 || a.K1 % 16) return hipErrorNotSupported;
+    const int cfg = gl4_cfg();
+    switch (a.J) {
+        case 16:
+            if (cfg == 422) return gl4_launch<16, 4, 2, 2>(a, rms, s);
+            if (cfg == 412) return gl4_launch<16, 4, 1, 2>(a, rms, s);
+            if (cfg == 421) return gl4_launch<16, 4, 2, 1>(a, rms, s);
+            if (cfg == 821) return gl4_launch<16, 8, 2, 1>(a, rms, s);
+            if (cfg == 812) return gl4_launch<16, 8, 1, 2>(a, rms, s);
+            if (cfg == 1) return gl4_launch<16, 8, 2, 2, 1>(a, rms, s);  // timing experiments
+            if (cfg == 2) return gl4_launch<16, 8, 2, 2, 2>(a, rms, s);
+            if (cfg == 3) return gl4_launch<16, 8, 2, 2, 3>(a, rms, s);
+            if (cfg == 4) return gl4_launch<16, 8, 2, 2, 4>(a, rms, s);
+            if (cfg == 5) return gl4_launch<16, 8, 2, 2, 5>(a, rms, s);
+            if (cfg == 6) return gl4_launch<16, 8, 2, 2, 6>(a, rms, s);
+            if (cfg == 7) return gl4_launch<16, 8, 2, 2, 7>(a, rms, s);
+            if (cfg == 8) return gl4_launch<16, 8, 2, 2, 8>(a, rms, s);
+            if (cfg == 9) return gl4_launch<16, 8, 2, 2, 9>(a, rms, s);
+            return gl4_launch<16, 8, 2, 2>(a, rms, s);
+        case 17: return gl4_launch<17, 8, 2, 1>(a, rms, s);
+        case 21: return gl4_launch<21, 8, 1, 2>(a, rms, s);
+        default: return hipErrorNotSupported;
+    }
+}
+
+}  // namespace sd

@@ -30,7 +30,18 @@ struct GLArgs {
     int ntypes;                                           // number of node types (rows of W / N)
     int wrow[kMaxNodes];                                  // type(j) * N  (row offset into W)
     int ntype[kMaxNodes];                                 // type(j)
+    // v4 only: W pre-split into f16 hi/lo B fragments (make_split_weights); null -> v4 unusable
+    const _Float16* wsp; int wsp_nct; float wsp_unscale;
 };
+
+// f16 hi/lo split of a (types, N, K) f32 weight in MFMA B-fragment order (sd_graph_linear_v4.hip)
+struct SplitW {
+    _Float16* w = nullptr;  // device, owned by the caller (hipFree)
+    int nct = 0;            // 32-column tiles in the layout (padded to even)
+    float scale = 1.f;      // W' = W * scale (a power of two)
+    float unscale = 1.f;    // 1 / scale
+};
+hipError_t make_split_weights(const float* W, int ntypes, int N, int K, SplitW* out, hipStream_t s);
 
 // Multi-head attention over joints (attention.py:122-136) from a (B, J, 3*heads*dh) qkv buffer.
 struct AttnArgs {
@@ -54,7 +65,10 @@ hipError_t launch_graph_linear(const GLArgs& a, bool rms, hipStream_t s);     //
 hipError_t launch_graph_linear_v1(const GLArgs& a, bool rms, hipStream_t s);
 hipError_t launch_graph_linear_v2(const GLArgs& a, bool rms, hipStream_t s);
 hipError_t launch_graph_linear_v3(const GLArgs& a, bool rms, hipStream_t s);  // J in {16,17,21}
-int graph_linear_variant();  // SKELDIFF_GL_VARIANT (1, 2, 3), read once
+hipError_t launch_graph_linear_v4(const GLArgs& a, bool rms, hipStream_t s);  // needs a.wsp
+int graph_linear_variant();  // SKELDIFF_GL_VARIANT (0 auto, 1, 2, 3, 4), read at load
+int set_graph_linear_variant(int v);  // returns the previous value, -1 if v is out of range
+int set_gl4_tile(int cfg);            // SKELDIFF_GL4_CFG (<NW><RT><CT>, 0 = auto); returns previous
 hipError_t launch_attention(const AttnArgs& a, hipStream_t s);
 hipError_t launch_update(const UpdArgs& a, hipStream_t s);
 hipError_t launch_noise_fill(float* out, int64_t rows, int64_t n_per_row, uint64_t seed,

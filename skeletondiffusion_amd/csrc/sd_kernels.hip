@@ -190,20 +190,32 @@ static hipError_t gl_dispatch_rms(const GLArgs& a, bool rms, hipStream_t s) {
     return hipGetLastError();
 }
 
-int graph_linear_variant() {
-    static const int v = [] {
-        const char* e = getenv("SKELDIFF_GL_VARIANT");
-        const int x = e ? atoi(e) : 0;
-        return (x >= 0 && x <= 3) ? x : 0;
-    }();
-    return v;
+static int g_gl_variant = [] {
+    const char* e = getenv("SKELDIFF_GL_VARIANT");
+    const int x = e ? atoi(e) : 0;
+    return (x >= 0 && x <= 4) ? x : 0;
+}();
+
+int graph_linear_variant() { return g_gl_variant; }
+
+int set_graph_linear_variant(int v) {
+    if (v < 0 || v > 4) return -1;
+    const int old = g_gl_variant;
+    g_gl_variant = v;
+    return old;
 }
 
-// 0 (default) = per shape: v3 (node-split waves, 32x32 MFMA) for N < 512, where it measured
-// 1.15-1.25x faster than v2; v2 with 32-column tiles for the wide to_qkv layer (N = 768).
+// 0 (default): v4 (f32-accurate split-f16 MFMA) where the plan prepared split weights and the
+// skeleton has an instantiation; otherwise the exact-f32 kernels per shape: v3 (node-split
+// waves, 32x32 f32 MFMA) for N < 512, where it measured 1.15-1.25x faster than v2; v2 with
+// 32-column tiles for the wide to_qkv layer (N = 768).  1/2/3/4 force one generation.
 hipError_t launch_graph_linear(const GLArgs& a, bool rms, hipStream_t s) {
     const int v = graph_linear_variant();
     if (v == 1) return launch_graph_linear_v1(a, rms, s);
+    if (v == 4 || v == 0) {
+        const hipError_t e = launch_graph_linear_v4(a, rms, s);
+        if (e != hipErrorNotSupported) return e;
+    }
     if (v == 3 || (v == 0 && a.N < 512)) {
         const hipError_t e = launch_graph_linear_v3(a, rms, s);
         if (e != hipErrorNotSupported) return e;

@@ -10,6 +10,7 @@
 #include <memory>
 #include <mutex>
 #include <string>
+#include <tuple>
 #include <vector>
 
 #include "../../include/skeldiff.h"
@@ -45,6 +46,7 @@ struct GL {
     const float* wuse = nullptr; // weights used by the kernel (folded copy for RMS layers)
     bool rms = false;
     int gain = -1;               // RMSNorm gain slot folded into this layer
+    sd::SplitW split;            // f16 hi/lo B fragments of wuse for the v4 kernel
 };
 
 struct GraphKey {
@@ -199,6 +201,9 @@ sd::GLArgs gl_args(const sd_plan* p, const GL& g, const float* x1, int x1_div, c
         a.wrow[j] = p->types[j] * g.N;
         a.ntype[j] = p->types[j];
     }
+    a.wsp = g.split.w;
+    a.wsp_nct = g.split.nct;
+    a.wsp_unscale = g.split.unscale;
     return a;
 }
 
@@ -493,6 +498,10 @@ int sd_plan_finalize(sd_plan* p, void* stream_) {
             SD_HIP(sd::launch_fold_gain(p->ptr(g.w), p->ptr(g.gain), std::sqrt((float)H), wf, rows, (int)K, s));
             g.wuse = wf;
         }
+        if ((g.K1 + g.K2) % 16 == 0 && g.K1 % 16 == 0) {
+            SD_HIP(sd::make_split_weights(g.wuse, p->ntypes, g.N, g.K1 + g.K2, &g.split, s));
+            p->allocs.push_back(g.split.w);
+        }
         return SD_OK;
     };
     if ((rc = pack_gl(p->init_lin))) return rc;
@@ -740,6 +749,13 @@ int sd_profile_step(const sd_plan* p, const float* x_t, const float* x_cond, int
     return SD_OK;
 }
 
+int sd_set_kernel_variant(int32_t gl_variant, int32_t gl4_tile) {
+    const int old = sd::set_graph_linear_variant(gl_variant);
+    if (old < 0) return fail(SD_E_INVALID, "gl_variant out of range");
+    if (gl4_tile >= 0) (void)sd::set_gl4_tile(gl4_tile);
+    return old;
+}
+
 int sd_test_graph_linear(const float* x1, int32_t K1, int64_t x1_div, const float* x2, int32_t K2,
                          const float* W, const float* bias, const int64_t* node_types, const float* ghat,
                          const float* film, int32_t act, const float* res, float* out, int64_t rows,
@@ -774,7 +790,33 @@ int sd_test_graph_linear(const float* x1, int32_t K1, int64_t x1_div, const floa
         a.ntype[j] = (int)node_types[j];
         a.ntypes = std::max(a.ntypes, (int)node_types[j] + 1);
     }
-    SD_HIP(sd::launch_graph_linear(a, rms != 0, (hipStream_t)stream));
+    // split weights for v4: made per call (tests), or cached by W pointer when
+    // SKELDIFF_GL_CACHE_SPLIT=1 (tools/bench_gl.py: weights fixed across timed calls)
+    static const bool cache = [] {
+        const char* e = getenv("SKELDIFF_GL_CACHE_SPLIT");
+        return e && atoi(e) == 1;
+    }();
+    static std::map<std::tuple<const float*, int, int, int>, sd::SplitW> cached;
+    sd::SplitW sw;
+    if (sd::graph_linear_variant() == 0 || sd::graph_linear_variant() == 4) {
+        const auto key = std::make_tuple(W, a.ntypes, N, K1 + a.K2);
+        auto it = cache ? cached.find(key) : cached.end();
+        if (it != cached.end()) {
+            sw = it->second;
+        } else {
+            SD_HIP(sd::make_split_weights(W, a.ntypes, N, K1 + a.K2, &sw, (hipStream_t)stream));
+            if (cache) cached[key] = sw;
+        }
+        a.wsp = sw.w;
+        a.wsp_nct = sw.nct;
+        a.wsp_unscale = sw.unscale;
+    }
+    const hipError_t e = sd::launch_graph_linear(a, rms != 0, (hipStream_t)stream);
+    if (sw.w && !cache) {
+        (void)hipStreamSynchronize((hipStream_t)stream);
+        (void)hipFree(sw.w);
+    }
+    SD_HIP(e);
     return SD_OK;
 }
 

@@ -73,6 +73,39 @@ CASES = [  # (J, n_types, K1, K2, N, div, bias, film, act, res, rms)
 @pytest.mark.parametrize("J,nty,K1,K2,N,div,has_bias,has_film,act,has_res,rms", CASES)
 @pytest.mark.parametrize("Bseq", [64, 67])
 def test_graph_linear_kernel(J, nty, K1, K2, N, div, has_bias, has_film, act, has_res, rms, Bseq, cuda):
+    _check_gl(J, nty, K1, K2, N, div, has_bias, has_film, act, has_res, rms, Bseq, cuda)
+
+
+@pytest.fixture
+def kernel_variant():
+    """Select a graph-linear generation / v4 tile for one test, restoring auto afterwards."""
+    L = _lib.lib()
+
+    def set_(v, tile=0):
+        assert L.sd_set_kernel_variant(v, tile) >= 0
+
+    yield set_
+    L.sd_set_kernel_variant(0, 0)
+
+
+# every v4 tile instantiation for J=16 and the exact-f32 generations on the release shapes
+V4_TILES = [0, 412, 421, 821, 812]
+
+
+@pytest.mark.parametrize("case", [c for c in CASES if c[0] == 16])
+@pytest.mark.parametrize("variant,tile", [(4, t) for t in V4_TILES] + [(3, 0), (2, 0), (1, 0)])
+def test_graph_linear_generations(case, variant, tile, kernel_variant, cuda):
+    kernel_variant(variant, tile)
+    _check_gl(*case, 67, cuda)
+
+
+def test_kernel_variant_rejects_bad_value():
+    L = _lib.lib()
+    assert L.sd_set_kernel_variant(9, -1) < 0
+    assert L.sd_set_kernel_variant(0, -1) == 0
+
+
+def _check_gl(J, nty, K1, K2, N, div, has_bias, has_film, act, has_res, rms, Bseq, cuda):
     g = torch.Generator().manual_seed(J * 1000 + N + K1 + K2 + Bseq)
     B = Bseq if div == 1 else max(1, Bseq // div) * div
     r = lambda *s: torch.rand(*s, generator=g) * 2 - 1  # noqa: E731

@@ -5,7 +5,8 @@ import ctypes
 import os
 import sys
 
-import torch
+os.environ.setdefault("SKELDIFF_GL_CACHE_SPLIT", "1")  # split weights once, not per timed call
+import torch  # noqa: E402
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from skeletondiffusion_amd import _lib  # noqa: E402
@@ -20,7 +21,7 @@ SHAPES = [  # name, K1, K2, N, bias, film, act, res, rms, per-step count
     ("res_block2", 192, 0, 192, 1, 0, 1, 1, 0, 8), ("to_qkv", 192, 0, 768, 0, 0, 0, 0, 1, 7),
     ("to_out", 256, 0, 192, 0, 0, 0, 1, 0, 7), ("final_b1/res", 192, 192, 192, 1, 1, 1, 0, 0, 2),
     ("final_b2", 192, 0, 192, 1, 0, 1, 1, 0, 1), ("final_glin", 192, 0, 96, 1, 0, 0, 0, 0, 1)]
-tag = f"v{os.environ.get('SKELDIFF_GL_VARIANT', '2')}/ncb{os.environ.get('SKELDIFF_GL_NCB', 'auto')}"
+tag = f"v{os.environ.get('SKELDIFF_GL_VARIANT', '0')}/t{os.environ.get('SKELDIFF_GL4_CFG', 'auto')}"
 tot_f = tot_t = 0.0
 only = os.environ.get("SHAPE")
 for name, K1, K2, N, bias, film, act, res, rms, cnt in SHAPES:

@@ -22,3 +22,6 @@ for tag in sys.argv[1:]:
     print(f"  insts VALU {a.get('SQ_INSTS_VALU', 0):,.0f} LDS {a.get('SQ_INSTS_LDS', 0):,.0f} VMEM "
           f"{a.get('SQ_INSTS_VMEM', 0):,.0f} SALU {a.get('SQ_INSTS_SALU', 0):,.0f}  LDS bank conflicts "
           f"{a.get('SQ_LDS_BANK_CONFLICT', 0):,.0f}  L2 hit {hit * 100:.1f}%")
+    if "FETCH_SIZE" in a:
+        print(f"  HBM/MALL bytes per launch: fetch {2 * a['FETCH_SIZE'] * 1024 / 1e6:.1f} MB (2x FETCH_SIZE, gfx950)"
+              f"  write {a.get('WRITE_SIZE', 0) * 1024 / 1e6:.1f} MB")
