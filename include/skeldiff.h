@@ -167,6 +167,12 @@ int sd_test_graph_linear(const float* x1, int32_t K1, int64_t x1_div, const floa
                          int32_t J, int32_t N, int32_t rms, void* stream);
 int sd_test_attention(const float* qkv, float* out, int64_t rows, int32_t J, int32_t heads,
                       int32_t dim_head, void* stream);
+/* sd_test_qkv_attention: the fused to_qkv + Attention kernel on caller buffers: qkv = G-hat-mixed
+ *   StaticGraphLinear (s_j W[type j] x_j, s_j = RMS scale when rms, no bias) with W (types, 3*heads*32, K),
+ *   then out(B,J,heads*32) = softmax(q k^T / sqrt(32)) v per head.  SD_E_INVALID where the fused
+ *   kernel does not apply (J > 16).  Replaces to_qkv + Attention, attention.py:105-136. */
+int sd_test_qkv_attention(const float* x, int32_t K, const float* W, const int64_t* node_types, const float* ghat,
+                          float* out, int64_t rows, int32_t J, int32_t heads, int32_t rms, void* stream);
 /* Kernel-generation selector (tests / tuning; process-wide, affects launches recorded after it):
  * gl_variant 0 = auto (v4 split-f16 where available, else exact-f32 v3/v2), 1..3 = exact-f32
  * generations, 4 = v4; gl4_tile = <waves><row tiles><col tiles> (e.g. 822) or 0 = auto,

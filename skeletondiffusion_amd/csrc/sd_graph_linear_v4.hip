@@ -96,7 +96,7 @@ __global__ void k_split_w(const float* __restrict__ W, int ntypes, int N, int K,
 }  // namespace
 
 hipError_t make_split_weights(const float* W, int ntypes, int N, int K, SplitW* out, hipStream_t s) {
-    out->nct = ((N + 31) / 32 + 1) & ~1;  // 32-col tiles, padded to a multiple of 2 (CT <= 2)
+    out->nct = ((N + 31) / 32 + 5) / 6 * 6;  // 32-col tiles, padded to a multiple of 6 (CT in 1, 2, 3)
     const int64_t n = (int64_t)ntypes * N * K;
     unsigned* dmax = nullptr;
     unsigned hmax = 0;
@@ -123,8 +123,117 @@ hipError_t make_split_weights(const float* W, int ntypes, int N, int K, SplitW* 
     return hipGetLastError();
 }
 
-template <int J, int NW, int RT, int CT, bool RMS, int DBG = 0>
+// Epilogue of the fused to_qkv + Attention kernel (MODE 1), J <= 16, dh = 32, 8 waves, a
+// 32-row tile.  Per 8-row slab: the mixed-in q|k|v (Z = G-hat Y) goes to LDS as [row][node][96],
+// then wave w runs the attention of row 8*slab + w exactly as k_attention does (same f32 MFMA
+// order, expf softmax), writing out[row][n][head*32 + d].
+template <int J, int NW, int NPW>
+__device__ __forceinline__ void attention_epilogue(const GLArgs& p, floatx16 (&acc)[NPW][1][3], float* smem,
+                                                   const float* sG, int64_t row0, int head, int wave, int lane) {
+    constexpr int COLS = 96;
+    constexpr int YS8 = 8 * COLS + 16;  // floats per node in an 8-row Y slab (+16: bank shift)
+    constexpr int ZN = 100;             // floats per node in a Z row (+4: bank shift)
+    constexpr int ZR = 16 * ZN;         // floats per Z row
+    const int l32 = lane & 31, h = lane >> 5, lr = lane & 15, lg = lane >> 4;
+    const int hid = p.attn_heads * 32;
+    float* sY = smem;
+    float* sZ = smem + J * YS8;
+    float ga[4];  // G-hat^T[k = j = 4s + lg][col = i = lr]
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+        const int jj = 4 * s + lg;
+        ga[s] = (lr < J && jj < J) ? sG[lr * J + jj] : 0.f;
+    }
+#pragma unroll
+    for (int q8 = 0; q8 < 4; ++q8) {  // rows 8 q8 .. 8 q8 + 7 = accumulator registers 4 q8 .. 4 q8 + 3
+        __syncthreads();              // K loop / previous slab done with this LDS
+#pragma unroll
+        for (int m = 0; m < NPW; ++m) {
+            const int j = wave + NW * m;
+            if (j >= J) continue;
+#pragma unroll
+            for (int ct = 0; ct < 3; ++ct)
+#pragma unroll
+                for (int e = 0; e < 4; ++e) sY[j * YS8 + (e + 4 * h) * COLS + 32 * ct + l32] = acc[m][0][ct][4 * q8 + e];
+        }
+        __syncthreads();
+        // node mixing: 48 blocks of 16 (row, column) positions, 6 per wave
+#pragma unroll
+        for (int k = 0; k < 48 / NW; ++k) {
+            const int rc0 = (wave + NW * k) * 16;
+            float ya[4];
+#pragma unroll
+            for (int s = 0; s < 4; ++s) {
+                const int jj = 4 * s + lg;
+                ya[s] = jj < J ? sY[jj * YS8 + rc0 + lr] : 0.f;
+            }
+            floatx4 z = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int s = 0; s < 4; ++s) z = __builtin_amdgcn_mfma_f32_16x16x4f32(ya[s], ga[s], z, 0, 0, 0);
+            const int rc = rc0 + 4 * lg, r = rc / COLS, c = rc - r * COLS;
+            if (lr < J) *reinterpret_cast<floatx4*>(sZ + r * ZR + lr * ZN + c) = z;
+        }
+        __syncthreads();
+        // attention of one row per wave (k_attention's math, one 16-node tile)
+        const int64_t row = row0 + 8 * q8 + wave;
+        const float* zr = sZ + wave * ZR;
+        floatx4 S = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int cc = 0; cc < 32; cc += 16) {
+            const floatx4 ka = lr < J ? *reinterpret_cast<const floatx4*>(zr + lr * ZN + 32 + cc + 4 * lg)
+                                      : floatx4{0.f, 0.f, 0.f, 0.f};
+            const floatx4 qv = lr < J ? *reinterpret_cast<const floatx4*>(zr + lr * ZN + cc + 4 * lg) * p.attn_scale
+                                      : floatx4{0.f, 0.f, 0.f, 0.f};
+            S = __builtin_amdgcn_mfma_f32_16x16x4f32(ka.x, qv.x, S, 0, 0, 0);
+            S = __builtin_amdgcn_mfma_f32_16x16x4f32(ka.y, qv.y, S, 0, 0, 0);
+            S = __builtin_amdgcn_mfma_f32_16x16x4f32(ka.z, qv.z, S, 0, 0, 0);
+            S = __builtin_amdgcn_mfma_f32_16x16x4f32(ka.w, qv.w, S, 0, 0, 0);
+        }
+        // softmax over j = 4 lg + e for query column n = lr
+        float mx = -INFINITY;
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+            if (4 * lg + e < J) mx = fmaxf(mx, S[e]);
+        mx = fmaxf(mx, __shfl_xor(mx, 16));
+        mx = fmaxf(mx, __shfl_xor(mx, 32));
+        float sum = 0.f;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const float ex = (4 * lg + e < J) ? expf(S[e] - mx) : 0.f;
+            S[e] = ex;
+            sum += ex;
+        }
+        sum += __shfl_xor(sum, 16);
+        sum += __shfl_xor(sum, 32);
+        S *= 1.0f / sum;
+        // O^T[d][n] = sum_j V[j][d] P^T[j][n]
+#pragma unroll
+        for (int dc = 0; dc < 32; dc += 16) {
+            floatx4 vv;
+#pragma unroll
+            for (int s4 = 0; s4 < 4; ++s4) {
+                const int j = 4 * lg + s4;
+                vv[s4] = j < J ? zr[j * ZN + 64 + dc + lr] : 0.f;
+            }
+            floatx4 o = {0.f, 0.f, 0.f, 0.f};
+            o = __builtin_amdgcn_mfma_f32_16x16x4f32(vv.x, S.x, o, 0, 0, 0);
+            o = __builtin_amdgcn_mfma_f32_16x16x4f32(vv.y, S.y, o, 0, 0, 0);
+            o = __builtin_amdgcn_mfma_f32_16x16x4f32(vv.z, S.z, o, 0, 0, 0);
+            o = __builtin_amdgcn_mfma_f32_16x16x4f32(vv.w, S.w, o, 0, 0, 0);
+            if (lr < J && row < p.B)
+                *reinterpret_cast<floatx4*>(p.out + row * p.out_rs + (int64_t)lr * hid + head * 32 + dc + 4 * lg) = o;
+        }
+    }
+}
+
+// MODE 0: StaticGraphLinear with the FiLM / tanh / residual epilogue.
+// MODE 1: to_qkv + Attention fused (attention.py:105-136): the workgroup's three 32-column tiles
+//   are head h's q, k and v columns (tiles h, heads + h, 2 heads + h), and the epilogue runs
+//   softmax(q k^T * dh^-1/2) v per row over the J nodes instead of storing q/k/v; out = the
+//   (B, J, heads * 32) attention output that to_out reads.  qkv never reaches HBM.
+template <int J, int NW, int RT, int CT, bool RMS, int DBG = 0, int MODE = 0>
 __global__ __launch_bounds__(NW * 64, 1) void k_gl4(const GLArgs p) {
+    static_assert(MODE == 0 || (CT == 3 && RT == 1 && J <= 16 && NW == 8), "attention mode: 32 x (q|k|v)");
     constexpr int NPW = (J + NW - 1) / NW;  // nodes per wave
     constexpr int KS = (J + 3) / 4;         // 4-deep k steps of the mixing GEMM (K = J padded)
     constexpr int IB = (J + 15) / 16;       // 16-row i blocks of the mixing GEMM
@@ -138,14 +247,14 @@ __global__ __launch_bounds__(NW * 64, 1) void k_gl4(const GLArgs p) {
     const int l32 = lane & 31, h = lane >> 5, lr = lane & 15, lg = lane >> 4;
     const int stage_h = p.ntypes * CT * 1024;  // halves per weight stage
     const int wfl = stage_h;                   // two stages of halves = stage_h floats
-    const int yfl = J * YS;
+    const int yfl = MODE == 1 ? J * (8 * COLS + 16) + 8 * 16 * 100 : J * YS;  // Y slab (+ Z rows)
     _Float16* sW0 = reinterpret_cast<_Float16*>(smem);
     _Float16* sW1 = sW0 + stage_h;
     float* sY = smem;  // aliases the weight stages after the K loop
     float* sG = smem + (wfl > yfl ? wfl : yfl);
     float* sF = sG + J * J;  // FiLM (scale + 1 | shift) for this workgroup's columns
 
-    const int ntile_c = (p.N + COLS - 1) / COLS;
+    const int ntile_c = MODE == 1 ? p.attn_heads : (p.N + COLS - 1) / COLS;
     const int nwg = gridDim.x, xcd = blockIdx.x & 7, q8 = nwg >> 3, r8 = nwg & 7;
     const int L = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (blockIdx.x >> 3);
     const int ctile = L % ntile_c;
@@ -219,7 +328,9 @@ __global__ __launch_bounds__(NW * 64, 1) void k_gl4(const GLArgs p) {
         for (int q0 = wave * 64; q0 < npieces; q0 += NTH) {
             const int q = min(q0 + lane, npieces - 1);
             const int t = q / per_type, rem = q - t * per_type;
-            const _Float16* src = p.wsp + (((int64_t)t * nchunk + c) * p.wsp_nct + (c0 >> 5)) * 1024 + rem * 8;
+            const int ct = rem >> 7;  // 32-column tile of this piece
+            const int tile = MODE == 1 ? ctile + ct * p.attn_heads : (c0 >> 5) + ct;
+            const _Float16* src = p.wsp + (((int64_t)t * nchunk + c) * p.wsp_nct + tile) * 1024 + (rem & 127) * 8;
             __builtin_amdgcn_global_load_lds((const void*)src, (lds_void*)(dst + (size_t)q0 * 8), 16, 0, 0);
         }
     };
@@ -292,7 +403,7 @@ __global__ __launch_bounds__(NW * 64, 1) void k_gl4(const GLArgs p) {
     for (int m = 0; m < NPW; ++m)
 #pragma unroll
         for (int ct = 0; ct < CT; ++ct) {
-            const int ncol = c0 + 32 * ct + l32;
+            const int ncol = (MODE == 1 ? (ctile + ct * p.attn_heads) * 32 : c0 + 32 * ct) + l32;
             bv[m][ct] = (p.bias && ncol < p.N) ? p.bias[p.wrow[jn[m]] + ncol] : 0.f;
         }
     fill_w(0, sW0);
@@ -342,6 +453,10 @@ __global__ __launch_bounds__(NW * 64, 1) void k_gl4(const GLArgs p) {
     }
 
     if (DBG == 6) ts[3] = wall_clock64();
+    if constexpr (MODE == 1) {
+        attention_epilogue<J, NW, NPW>(p, acc, smem, sG, row0, ctile, wave, lane);
+        return;
+    }
     // ---- mixing + epilogue, one 16-row slab at a time.  Z^T = Y^T G-hat^T on 16x16x4 f32 MFMA
     // with Y^T as the A operand: lane (lr, lg) ends up holding D[rc = 4lg + e][i = lr], i.e. four
     // consecutive columns of one row for node i, so residual loads and output stores are 16 B
@@ -466,17 +581,17 @@ __global__ __launch_bounds__(NW * 64, 1) void k_gl4(const GLArgs p) {
     }
 }
 
-template <int J, int NW, int RT, int CT, int DBG = 0>
+template <int J, int NW, int RT, int CT, int DBG = 0, int MODE = 0>
 static hipError_t gl4_launch(const GLArgs& a, bool rms, hipStream_t s) {
     constexpr int COLS = 32 * CT;
-    const int ntile_c = (a.N + COLS - 1) / COLS;
+    const int ntile_c = MODE == 1 ? a.attn_heads : (a.N + COLS - 1) / COLS;
     const int64_t ntile_r = (a.B + 32 * RT - 1) / (32 * RT);
     const dim3 grid((unsigned)(ntile_c * ntile_r));
     const size_t wfl = (size_t)a.ntypes * CT * 1024;  // two stages of halves, in floats
-    const size_t yfl = (size_t)J * (16 * COLS + 16);
+    const size_t yfl = MODE == 1 ? (size_t)J * (8 * COLS + 16) + 8 * 16 * 100 : (size_t)J * (16 * COLS + 16);
     const size_t lds = ((wfl > yfl ? wfl : yfl) + (size_t)J * J + 2 * COLS) * sizeof(float);
     if (lds > 160 * 1024) return hipErrorNotSupported;
-    auto kt = rms ? k_gl4<J, NW, RT, CT, true, DBG> : k_gl4<J, NW, RT, CT, false, DBG>;
+    auto kt = rms ? k_gl4<J, NW, RT, CT, true, DBG, MODE> : k_gl4<J, NW, RT, CT, false, DBG, MODE>;
     if (lds > 64 * 1024) {
         hipError_t e = hipFuncSetAttribute((const void*)kt, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         if (e != hipSuccess) return e;
@@ -512,6 +627,7 @@ hipError_t launch_graph_linear_v4(const GLArgs& a, bool rms, hipStream_t s) {
             if (cfg == 421) return gl4_launch<16, 4, 2, 1>(a, rms, s);
             if (cfg == 821) return gl4_launch<16, 8, 2, 1>(a, rms, s);
             if (cfg == 812) return gl4_launch<16, 8, 1, 2>(a, rms, s);
+            if (cfg == 813) return gl4_launch<16, 8, 1, 3>(a, rms, s);
             if (cfg == 1) return gl4_launch<16, 8, 2, 2, 1>(a, rms, s);  // timing experiments
             if (cfg == 2) return gl4_launch<16, 8, 2, 2, 2>(a, rms, s);
             if (cfg == 3) return gl4_launch<16, 8, 2, 2, 3>(a, rms, s);
@@ -521,9 +637,27 @@ hipError_t launch_graph_linear_v4(const GLArgs& a, bool rms, hipStream_t s) {
             if (cfg == 7) return gl4_launch<16, 8, 2, 2, 7>(a, rms, s);
             if (cfg == 8) return gl4_launch<16, 8, 2, 2, 8>(a, rms, s);
             if (cfg == 9) return gl4_launch<16, 8, 2, 2, 9>(a, rms, s);
-            return gl4_launch<16, 8, 2, 2>(a, rms, s);
+            if (cfg == 822) return gl4_launch<16, 8, 2, 2>(a, rms, s);
+            // 32 rows x 96 columns: 200 workgroups for an N = 192 layer at B = 3200 (64 x 64 gives
+            // 150, leaving 40 % of the CUs idle); measured 1.28x faster on those layers
+            return gl4_launch<16, 8, 1, 3>(a, rms, s);
+        // J > 16 needs two 16-node blocks in the mixing epilogue: 96 columns spill there
         case 17: return gl4_launch<17, 8, 2, 1>(a, rms, s);
         case 21: return gl4_launch<21, 8, 1, 2>(a, rms, s);
+        default: return hipErrorNotSupported;
+    }
+}
+
+// to_qkv (RMSNorm-scaled, no bias) + Attention fused; a.out = (B, J, heads * 32) attention
+// output.  hipErrorNotSupported where the fused tile does not apply (caller falls back to the
+// graph-linear + k_attention pair).
+hipError_t launch_qkv_attention_v4(const GLArgs& a, bool rms, hipStream_t s) {
+    if (a.B <= 0) return hipSuccess;
+    if (!a.wsp || a.J > 16 || a.attn_heads < 1 || a.N != 3 * a.attn_heads * 32 || a.bias || a.film || a.res ||
+        a.act || (a.K1 + a.K2) % 32 || a.K1 % 16 || ((uintptr_t)a.out & 15) || (a.out_rs & 3))
+        return hipErrorNotSupported;
+    switch (a.J) {
+        case 16: return gl4_launch<16, 8, 1, 3, 0, 1>(a, rms, s);
         default: return hipErrorNotSupported;
     }
 }

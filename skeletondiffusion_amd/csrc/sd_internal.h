@@ -32,12 +32,14 @@ struct GLArgs {
     int ntype[kMaxNodes];                                 // type(j)
     // v4 only: W pre-split into f16 hi/lo B fragments (make_split_weights); null -> v4 unusable
     const _Float16* wsp; int wsp_nct; float wsp_unscale;
+    // fused to_qkv + Attention (launch_qkv_attention_v4): heads of 32 dims, q scale dh^-1/2
+    int attn_heads; float attn_scale;
 };
 
 // f16 hi/lo split of a (types, N, K) f32 weight in MFMA B-fragment order (sd_graph_linear_v4.hip)
 struct SplitW {
     _Float16* w = nullptr;  // device, owned by the caller (hipFree)
-    int nct = 0;            // 32-column tiles in the layout (padded to even)
+    int nct = 0;            // 32-column tiles in the layout (padded to a multiple of 6)
     float scale = 1.f;      // W' = W * scale (a power of two)
     float unscale = 1.f;    // 1 / scale
 };
@@ -66,6 +68,7 @@ hipError_t launch_graph_linear_v1(const GLArgs& a, bool rms, hipStream_t s);
 hipError_t launch_graph_linear_v2(const GLArgs& a, bool rms, hipStream_t s);
 hipError_t launch_graph_linear_v3(const GLArgs& a, bool rms, hipStream_t s);  // J in {16,17,21}
 hipError_t launch_graph_linear_v4(const GLArgs& a, bool rms, hipStream_t s);  // needs a.wsp
+hipError_t launch_qkv_attention_v4(const GLArgs& a, bool rms, hipStream_t s);  // J <= 16, dh 32
 int graph_linear_variant();  // SKELDIFF_GL_VARIANT (0 auto, 1, 2, 3, 4), read at load
 int set_graph_linear_variant(int v);  // returns the previous value, -1 if v is out of range
 int set_gl4_tile(int cfg);            // SKELDIFF_GL4_CFG (<NW><RT><CT>, 0 = auto); returns previous

@@ -67,6 +67,11 @@ struct sd_plan {
     std::vector<Slot> slots;
     std::map<std::string, int> index;
     bool finalized = false;
+    bool fuse_ok = false;  // to_qkv + attention fusable (v4 split weights, J <= 16, dim_head 32)
+    bool fuse_attention_now() const {
+        const int v = sd::graph_linear_variant();
+        return fuse_ok && (v == 0 || v == 4);
+    }
     std::vector<void*> allocs;
 
     GL init_lin;
@@ -261,12 +266,25 @@ int run_denoiser(const sd_plan* p, const float* x_t, const float* x_cond, int64_
         if (!p->has_attn[l]) continue;
         if (p->d.use_attention) {
             // Residual(PreNorm(Attention)): x = to_out(attn(to_qkv(rmsnorm(x)))) + x
-            a = gl_args(p, p->qkv[l], w.x, 1, nullptr, nullptr, nullptr, w.qkv, rows);
-            SD_LAUNCH(prof, 0, sd::launch_graph_linear(a, true, s));
             // q * dim_head ** -0.5 (attention.py:114,128): Python double scalar cast to fp32
-            sd::AttnArgs aa{w.qkv, w.o, rows, p->J, p->d.attn_heads, p->d.attn_dim_head,
-                            (float)std::pow((double)p->d.attn_dim_head, -0.5)};
-            SD_LAUNCH(prof, 1, sd::launch_attention(aa, s));
+            const float qscale = (float)std::pow((double)p->d.attn_dim_head, -0.5);
+            hipError_t fused = hipErrorNotSupported;
+            if (p->fuse_attention_now()) {  // to_qkv + attention in one kernel, qkv stays on chip
+                a = gl_args(p, p->qkv[l], w.x, 1, nullptr, nullptr, nullptr, w.o, rows);
+                a.out_rs = (int64_t)p->J * p->hid;
+                a.attn_heads = p->d.attn_heads;
+                a.attn_scale = qscale;
+                if (prof && prof->pre(0, s)) return fail(SD_E_HIP, "hipEventRecord failed");
+                fused = sd::launch_qkv_attention_v4(a, true, s);
+                if (fused != hipSuccess && fused != hipErrorNotSupported) SD_HIP(fused);
+                if (prof && prof->post(s)) return fail(SD_E_HIP, "hipEventRecord failed");
+            }
+            if (fused == hipErrorNotSupported) {
+                a = gl_args(p, p->qkv[l], w.x, 1, nullptr, nullptr, nullptr, w.qkv, rows);
+                SD_LAUNCH(prof, 0, sd::launch_graph_linear(a, true, s));
+                sd::AttnArgs aa{w.qkv, w.o, rows, p->J, p->d.attn_heads, p->d.attn_dim_head, qscale};
+                SD_LAUNCH(prof, 1, sd::launch_attention(aa, s));
+            }
             a = gl_args(p, p->outp[l], w.o, 1, nullptr, nullptr, w.x, w.x, rows);
             SD_LAUNCH(prof, 0, sd::launch_graph_linear(a, false, s));
         } else {
@@ -516,6 +534,9 @@ int sd_plan_finalize(sd_plan* p, void* stream_) {
     }
     if ((rc = pack_gl(p->fres_res))) return rc;
     if ((rc = pack_gl(p->fglin))) return rc;
+    p->fuse_ok = p->d.use_attention && J <= 16 && p->d.attn_dim_head == 32;
+    for (size_t l = 0; l < p->qkv.size(); ++l)
+        if (p->has_attn[l] && !p->qkv[l].split.w) p->fuse_ok = false;
 
     // time MLP (generator.py:50-55, 97) and per-block FiLM tables (attention.py:81-84, 96-100)
     float *emb = nullptr, *t1 = nullptr, *temb = nullptr;
@@ -816,6 +837,44 @@ int sd_test_graph_linear(const float* x1, int32_t K1, int64_t x1_div, const floa
         (void)hipStreamSynchronize((hipStream_t)stream);
         (void)hipFree(sw.w);
     }
+    SD_HIP(e);
+    return SD_OK;
+}
+
+int sd_test_qkv_attention(const float* x, int32_t K, const float* W, const int64_t* node_types, const float* ghat,
+                          float* out, int64_t rows, int32_t J, int32_t heads, int32_t rms, void* stream) {
+    if (!x || !W || !ghat || !out || !node_types || J < 1 || J > sd::kMaxNodes || heads < 1 || K % 32 || rows < 0)
+        return fail(SD_E_INVALID, "bad arguments");
+    sd::GLArgs a{};
+    const int N = 3 * heads * 32;
+    a.x1 = x;
+    a.K1 = K;
+    a.x1_rs = (int64_t)J * K;
+    a.x1_div = 1;
+    a.G = ghat;
+    a.out = out;
+    a.out_rs = (int64_t)J * heads * 32;
+    a.B = rows;
+    a.N = N;
+    a.J = J;
+    a.ntypes = 1;
+    for (int j = 0; j < J; ++j) {
+        if (node_types[j] < 0) return fail(SD_E_INVALID, "negative node type");
+        a.wrow[j] = (int)node_types[j] * N;
+        a.ntype[j] = (int)node_types[j];
+        a.ntypes = std::max(a.ntypes, (int)node_types[j] + 1);
+    }
+    a.attn_heads = heads;
+    a.attn_scale = (float)std::pow(32.0, -0.5);
+    sd::SplitW sw;
+    SD_HIP(sd::make_split_weights(W, a.ntypes, N, K, &sw, (hipStream_t)stream));
+    a.wsp = sw.w;
+    a.wsp_nct = sw.nct;
+    a.wsp_unscale = sw.unscale;
+    const hipError_t e = sd::launch_qkv_attention_v4(a, rms != 0, (hipStream_t)stream);
+    (void)hipStreamSynchronize((hipStream_t)stream);
+    (void)hipFree(sw.w);
+    if (e == hipErrorNotSupported) return fail(SD_E_INVALID, "fused qkv+attention not available for this shape");
     SD_HIP(e);
     return SD_OK;
 }

@@ -89,7 +89,7 @@ def kernel_variant():
 
 
 # every v4 tile instantiation for J=16 and the exact-f32 generations on the release shapes
-V4_TILES = [0, 412, 421, 821, 812]
+V4_TILES = [0, 412, 421, 821, 812, 813, 822]
 
 
 @pytest.mark.parametrize("case", [c for c in CASES if c[0] == 16])
@@ -141,3 +141,42 @@ def test_attention_kernel(J, heads, dh, cuda):
     torch.cuda.synchronize()
     assert torch.isfinite(out).all()
     assert (out.cpu().double() - ref).abs().max().item() < 2e-5
+
+
+@pytest.mark.parametrize("J,nty,heads,rms", [(16, 10, 8, True), (16, 1, 4, True), (16, 10, 8, False), (16, 3, 2, True)])
+@pytest.mark.parametrize("B", [64, 67])
+def test_qkv_attention_fused(J, nty, heads, rms, B, cuda):
+    """Fused to_qkv + attention kernel vs a float64 torch restatement of the two ops."""
+    g = torch.Generator().manual_seed(J * 100 + heads + B + rms)
+    K, hid = 192, heads * 32
+    r = lambda *s: torch.rand(*s, generator=g) * 2 - 1  # noqa: E731
+    x = r(B, J, K)
+    W = r(nty, 3 * hid, K) / K ** 0.5
+    types = torch.randint(0, nty, (J,), generator=g)
+    ghat = F.normalize(torch.eye(J) + torch.rand(J, J, generator=g) * 0.1, p=1.0, dim=1)
+    qkv = _gl_reference(x, None, W, None, types, ghat, None, 0, None, rms, 1).double()
+    q, k, v = (c.reshape(B, J, heads, 32).permute(0, 2, 3, 1) for c in qkv.chunk(3, dim=-1))
+    sim = torch.einsum("bhcn,bhcj->bhnj", q * 32 ** -0.5, k)
+    ref = torch.einsum("bhnj,bhdj->bhnd", sim.softmax(-1), v).permute(0, 2, 1, 3).reshape(B, J, hid)
+    out = torch.full((B, J, hid), float("nan"), device=cuda)
+    nt = (ctypes.c_int64 * J)(*types.tolist())
+    xd, Wd, gd = x.to(cuda), W.to(cuda), ghat.to(cuda)
+    _lib.check(_lib.lib().sd_test_qkv_attention(xd.data_ptr(), K, Wd.data_ptr(), nt, gd.data_ptr(), out.data_ptr(),
+                                                B, J, heads, int(rms), 0))
+    torch.cuda.synchronize()
+    got = out.cpu().double()
+    assert torch.isfinite(got).all()
+    assert (got - ref).abs().max().item() < 2e-5
+
+
+def test_qkv_attention_rejects_large_J(cuda):
+    J, K, heads, B = 21, 192, 8, 8
+    x = torch.zeros(B, J, K, device=cuda)
+    W = torch.zeros(1, 3 * heads * 32, K, device=cuda)
+    out = torch.zeros(B, J, heads * 32, device=cuda)
+    g = torch.eye(J, device=cuda)
+    nt = (ctypes.c_int64 * J)(*([0] * J))
+    rc = _lib.lib().sd_test_qkv_attention(x.data_ptr(), K, W.data_ptr(), nt, g.data_ptr(), out.data_ptr(), B, J,
+                                          heads, 1, 0)
+    assert rc < 0
+
