@@ -13,9 +13,15 @@ and per-GPU work is fixed as N grows (weak scaling).  Weights are the repo's det
 synthetic filler (no checkpoint can be fetched); conditioning latents are synthetic U(-1, 1).
 
 Rank 0 prints one JSON line.  It also carries:
-  roofline      the dominant kernel (k_graph_linear, fp32 MFMA) measured live with HIP events
-                on the launch stream (sd_profile_step): algorithmic FLOPs / kernel time vs the
-                157.3 TFLOP/s fp32 dense peak;
+  roofline      the dominant kernel class (the graph-linear launches of a denoise step, incl. the
+                fused to_qkv + attention ones) measured live with HIP events on the launch stream
+                (sd_profile_step): algorithmic f32 FLOPs / kernel time.  The default kernels (v4)
+                compute every f32 product as three f16 MFMA products (x_hi W_hi + x_hi W_lo +
+                x_lo W_hi, f32 accumulate), so their ceiling is the f16 dense MFMA peak / 3
+                (2500 / 3 TFLOP/s of f32 work); the exact-f32 generations (SKELDIFF_GL_VARIANT=1..3)
+                are priced against the 157.3 TFLOP/s f32 peak.  "hbm_view" prices the same
+                launches by their algorithmic HBM bytes (activations in and out once, weights once)
+                against 8 TB/s;
   cpu_baseline  the oracle (torch-CPU restatement of the reference path) on this host, bounded
                 sample: a few of the T steps on the same B rows, per-step time x T.
 """
@@ -41,6 +47,7 @@ from skeletondiffusion_amd.skeletons import skeleton  # noqa: E402
 
 METRIC = "generated futures/sec (AMASS 16-joint, 50 futures, T=100) at 1/2/4/8 GPUs"
 FP32_PEAK_TFLOPS = 157.3   # MI355X fp32 dense (vector = matrix), MI355X_MICROARCH.md
+F16_MFMA_PEAK_TFLOPS = 2500.0  # MI355X f16/bf16 dense MFMA (no sparsity), MI355X_MICROARCH.md
 HBM_PEAK_GBS = 8000.0      # MI355X HBM3E spec
 
 # BASELINE.json configs -> (skeleton, T, batch sequences, futures)
@@ -99,6 +106,26 @@ def shard(rank: int, batch: int, futures: int):
     sequence on one rank (eval_prepare_model.py:96 repeat_interleave order).
     Returns (seq0, row0, rows); row0 keys the device noise so outputs are GPU-count invariant."""
     return rank * batch, rank * batch * futures, batch * futures
+
+
+def graph_linear_bytes(d, rows, fused_attn):
+    """Algorithmic HBM bytes of one denoise step's graph-linear launches: every activation read
+    once and written once (f32), every weight read once (f32 or split f16 pair: 4 B either way)."""
+    m = d.model
+    J, H = d.channels, m.dim + m.cond_dim
+    hid = m.attn_heads * m.attn_dim_head if hasattr(m, "attn_heads") else 256
+    total = 0.0
+    for mod in m.modules():
+        if type(mod).__name__ != "StaticGraphLinear":
+            continue
+        N, K = mod.weight.shape[-2], mod.weight.shape[-1]
+        fused_qkv = fused_attn and N == 3 * hid
+        out_n = hid if fused_qkv else N
+        total += 4.0 * rows * J * (K + out_n) + 4.0 * mod.weight.numel()
+    # residual reads: every ResnetBlock's block2 and every attention's to_out add a (B, J, H) residual
+    n_res = sum(type(mod).__name__ in ("ResnetBlock", "Attention") for mod in m.modules())
+    total += 4.0 * rows * J * H * n_res
+    return total
 
 
 def profile_kernels(d, x_cond, rows, reps=5):
@@ -208,7 +235,15 @@ def main():
         ms, cnt, fl = profile_kernels(d, x_cond, rows, args.profile_reps)
 
     value = world * rows * args.steps / elapsed
-    gl_tflops = fl[0] / (ms[0] * 1e-3) / 1e12
+    L = _lib.lib()
+    variant = L.sd_set_kernel_variant(-1, -1)
+    split = variant in (0, 4) and J in (16, 17, 21)
+    fused_attn = ms[1] == 0.0 and cnt[1] == 0   # attention ran inside the graph-linear launches
+    gl_flops = fl[0] + (fl[1] if fused_attn else 0.0)
+    gl_tflops = gl_flops / (ms[0] * 1e-3) / 1e12
+    peak = F16_MFMA_PEAK_TFLOPS / 3.0 if split else FP32_PEAK_TFLOPS
+    gl_bytes = graph_linear_bytes(d, rows, fused_attn)
+    gl_gbs = gl_bytes / (ms[0] * 1e-3) / 1e9
     upd_bytes = 3.0 * rows * J * D * 4        # x0, x_t in, x_{t-1} out (device Philox noise)
     upd_gbs = upd_bytes / (ms[2] * 1e-3) / 1e9
     step_flops = sum(fl)
@@ -224,17 +259,27 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "f32",
+        "arithmetic": ("f32-accurate: 3 x f16 split products on v_mfma_f32_32x32x16_f16, f32 accumulate "
+                       "(end-to-end error within the f32-vs-f64 drift, tools/sim_split_f16.py); "
+                       "exact-f32 kernels via SKELDIFF_GL_VARIANT=3") if split else "exact f32 (f32 MFMA)",
         "data": "synthetic (deterministic synthetic weights of the release Denoiser; U(-1,1) conditioning "
                 "latents; device Philox noise)",
         "config": {"workload": c["workload"], "J": J, "T": T, "sequences_per_gpu": batch,
                    "futures": rows // batch, "rows_per_gpu": rows, "latent_dim": D, "hipgraph": graph,
                    "parallelism": f"dp{world} (sequence-sharded, no data-path collective)"},
         "roofline": {
-            "bound": "mfma", "kernel": "k_graph_linear (v_mfma_f32_16x16x4_f32, fused bias/G-hat/FiLM/tanh/residual)",
-            "achieved": gl_tflops, "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": gl_tflops / FP32_PEAK_TFLOPS,
+            "bound": "mfma",
+            "kernel": ("k_gl4 graph-linear (3xf16 split MFMA, fused bias/RMS/G-hat/FiLM/tanh/residual; "
+                       "to_qkv launches fused with attention)") if split else
+                      "k_gl3/k_gl2 graph-linear (exact f32 MFMA, fused epilogue)",
+            "achieved": gl_tflops, "peak": peak, "unit": "TFLOP/s", "frac": gl_tflops / peak,
+            "peak_basis": "f16 dense MFMA 2500 TFLOP/s / 3 products per f32 product" if split else
+                          "f32 dense 157.3 TFLOP/s",
             "traffic": None,
-            "flops_per_launch": fl[0] / max(cnt[0], 1), "launches_per_denoise_step": cnt[0],
+            "flops_per_launch": gl_flops / max(cnt[0], 1), "launches_per_denoise_step": cnt[0],
             "avg_launch_ms": ms[0] / max(cnt[0], 1),
+            "hbm_view": {"achieved": gl_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": gl_gbs / HBM_PEAK_GBS,
+                         "algorithmic_bytes_per_launch": gl_bytes / max(cnt[0], 1)},
         },
         "kernels_per_denoise_step_ms": {"graph_linear": ms[0], "attention": ms[1], "update": ms[2],
                                         "step_first_to_last_event": ms[3]},

@@ -176,7 +176,8 @@ int sd_test_qkv_attention(const float* x, int32_t K, const float* W, const int64
 /* Kernel-generation selector (tests / tuning; process-wide, affects launches recorded after it):
  * gl_variant 0 = auto (v4 split-f16 where available, else exact-f32 v3/v2), 1..3 = exact-f32
  * generations, 4 = v4; gl4_tile = <waves><row tiles><col tiles> (e.g. 822) or 0 = auto,
- * -1 leaves it.  Returns the previous gl_variant, or -1 for an invalid one (nothing changed). */
+ * -1 leaves it.  Returns the previous gl_variant, or -1 for an invalid one (nothing changed);
+ * gl_variant = -1 only queries (returns the current value). */
 int sd_set_kernel_variant(int32_t gl_variant, int32_t gl4_tile);
 
 #ifdef __cplusplus

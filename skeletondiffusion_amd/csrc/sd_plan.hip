@@ -771,6 +771,7 @@ int sd_profile_step(const sd_plan* p, const float* x_t, const float* x_cond, int
 }
 
 int sd_set_kernel_variant(int32_t gl_variant, int32_t gl4_tile) {
+    if (gl_variant == -1) return sd::graph_linear_variant();  // query
     const int old = sd::set_graph_linear_variant(gl_variant);
     if (old < 0) return fail(SD_E_INVALID, "gl_variant out of range");
     if (gl4_tile >= 0) (void)sd::set_gl4_tile(gl4_tile);

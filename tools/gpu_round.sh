@@ -1,2 +1,6 @@
+#!/bin/bash
+# Round evidence: smoke + GPU tests + default bench (with CPU baseline), then the rocprof
+# kernel-trace summary and PMC traffic passes for profiles/<tag>.
 set -u
-bash tools/gpu_check.sh && PMC=1 BENCH_ARGS="--steps 2 --warmup 1 --no-cpu-baseline" bash tools/profile.sh r01_v3
+TAG=${1:-r01}
+bash tools/gpu_check.sh && PMC=1 bash tools/profile.sh $TAG

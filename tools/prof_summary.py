@@ -31,10 +31,17 @@ ntile_r = (rows_b + 63) // 64
 by_shape = defaultdict(list)
 for r in trace:
     n = r["Kernel_Name"]
-    if "k_gl2" not in n and "k_graph_linear" not in n and "k_gl3" not in n:
+    if "k_gl2" not in n and "k_graph_linear" not in n and "k_gl3" not in n and "k_gl4" not in n:
         continue
     wgs = int(r.get("Grid_Size") or r["Grid_Size_X"]) // 256
-    if "k_gl3" in n:
+    if "k_gl4" in n:  # <J, NW, RT, CT, RMS, DBG, MODE>: tile 32 RT rows x 32 CT columns, NW * 64 threads
+        targs = [t.strip() for t in n.split("<")[1].split(">")[0].split(",")]
+        nw, rt, ctl = int(targs[1]), int(targs[2]), int(targs[3])
+        wgs = int(r.get("Grid_Size") or r["Grid_Size_X"]) // (nw * 64)
+        mode = int(targs[6]) if len(targs) > 6 else 0
+        nt = wgs // ((rows_b + 32 * rt - 1) // (32 * rt))
+        NT = 96 if mode == 1 else 32 * ctl  # mode 1: one head (q|k|v) per column tile
+    elif "k_gl3" in n:
         nt, NT = wgs // ((rows_b + 31) // 32), 32
     else:
         nt = wgs // ntile_r
