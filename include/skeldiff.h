@@ -165,14 +165,23 @@ int sd_test_graph_linear(const float* x1, int32_t K1, int64_t x1_div, const floa
                          const float* W, const float* bias, const int64_t* node_types, const float* ghat,
                          const float* film, int32_t act, const float* res, float* out, int64_t rows,
                          int32_t J, int32_t N, int32_t rms, void* stream);
+/* sd_test_graph_linear_layout: as sd_test_graph_linear with operand layouts: bit 0 x1, bit 1 x2,
+ *   bit 2 res, bit 3 out in the v4 row-blocked layout (per 32-row block and node, features as
+ *   [F/8][2][32 rows][4]; buffers padded to a multiple of 32 rows); needs the v4 kernels. */
+int sd_test_graph_linear_layout(const float* x1, int32_t K1, int64_t x1_div, const float* x2, int32_t K2,
+                                const float* W, const float* bias, const int64_t* node_types, const float* ghat,
+                                const float* film, int32_t act, const float* res, float* out, int64_t rows,
+                                int32_t J, int32_t N, int32_t rms, int32_t layout, void* stream);
 int sd_test_attention(const float* qkv, float* out, int64_t rows, int32_t J, int32_t heads,
                       int32_t dim_head, void* stream);
 /* sd_test_qkv_attention: the fused to_qkv + Attention kernel on caller buffers: qkv = G-hat-mixed
  *   StaticGraphLinear (s_j W[type j] x_j, s_j = RMS scale when rms, no bias) with W (types, 3*heads*32, K),
  *   then out(B,J,heads*32) = softmax(q k^T / sqrt(32)) v per head.  SD_E_INVALID where the fused
- *   kernel does not apply (J > 16).  Replaces to_qkv + Attention, attention.py:105-136. */
+ *   kernel does not apply (J > 16).  layout bit 0 / bit 3: x / out row-blocked (as
+ *   sd_test_graph_linear_layout).  Replaces to_qkv + Attention, attention.py:105-136. */
 int sd_test_qkv_attention(const float* x, int32_t K, const float* W, const int64_t* node_types, const float* ghat,
-                          float* out, int64_t rows, int32_t J, int32_t heads, int32_t rms, void* stream);
+                          float* out, int64_t rows, int32_t J, int32_t heads, int32_t rms, int32_t layout,
+                          void* stream);
 /* Kernel-generation selector (tests / tuning; process-wide, affects launches recorded after it):
  * gl_variant 0 = auto (v4 split-f16 where available, else exact-f32 v3/v2), 1..3 = exact-f32
  * generations, 4 = v4; gl4_tile = <waves><row tiles><col tiles> (e.g. 822) or 0 = auto,

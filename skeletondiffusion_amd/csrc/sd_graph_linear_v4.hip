@@ -58,6 +58,15 @@ __device__ __forceinline__ float tanh4(float x) {
     return 1.0f - 2.0f * __builtin_amdgcn_rcpf(e + 1.0f);
 }
 
+// Row-blocked activation layout of the v4 path: rows in blocks of 32; per (block, node) the F
+// features as [F/8][2][32 rows][4], i.e. one aligned 16-B piece per (row, 4 features).  An x
+// fragment load (32 rows x 8 features of one node) is then 2 x 512 contiguous bytes and an
+// output quad one 16-B store.  Buffers are padded to a multiple of 32 rows.
+__device__ __forceinline__ int64_t blk_off(int64_t row, int node, int f, int J, int F) {
+    return ((((row >> 5) * J + node) * (int64_t)F) << 5) + ((f >> 3) << 8) + (((f >> 2) & 1) << 7) +
+           ((row & 31) << 2) + (f & 3);
+}
+
 // ---- one-time weight preparation ------------------------------------------------------------
 
 __global__ void k_absmax(const float* __restrict__ w, int64_t n, unsigned* __restrict__ out) {
@@ -220,8 +229,11 @@ __device__ __forceinline__ void attention_epilogue(const GLArgs& p, floatx16 (&a
             o = __builtin_amdgcn_mfma_f32_16x16x4f32(vv.y, S.y, o, 0, 0, 0);
             o = __builtin_amdgcn_mfma_f32_16x16x4f32(vv.z, S.z, o, 0, 0, 0);
             o = __builtin_amdgcn_mfma_f32_16x16x4f32(vv.w, S.w, o, 0, 0, 0);
-            if (lr < J && row < p.B)
-                *reinterpret_cast<floatx4*>(p.out + row * p.out_rs + (int64_t)lr * hid + head * 32 + dc + 4 * lg) = o;
+            if (lr < J && row < p.B) {
+                const int f = head * 32 + dc + 4 * lg;
+                float* dst = p.out_blk ? p.out + blk_off(row, lr, f, J, hid) : p.out + row * p.out_rs + (int64_t)lr * hid + f;
+                *reinterpret_cast<floatx4*>(dst) = o;
+            }
         }
     }
 }
@@ -256,21 +268,28 @@ __global__ __launch_bounds__(NW * 64, 1) void k_gl4(const GLArgs p) {
 
     const int ntile_c = MODE == 1 ? p.attn_heads : (p.N + COLS - 1) / COLS;
     const int nwg = gridDim.x, xcd = blockIdx.x & 7, q8 = nwg >> 3, r8 = nwg & 7;
-    const int L = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (blockIdx.x >> 3);
+    // XCD-aware order: consecutive L (the column tiles of one row tile) on one XCD, so x is
+    // fetched into that XCD's L2 once.  attn_order 1 (fused attention): L = blockIdx, i.e. head
+    // h = blockIdx % heads runs on XCD h % 8 and each XCD's L2 keeps only its heads' weights.
+    const int L = (MODE == 1 && p.attn_order == 1)
+                      ? (int)blockIdx.x
+                      : (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (blockIdx.x >> 3);
     const int ctile = L % ntile_c;
     const int64_t row0 = (int64_t)(L / ntile_c) * (32 * RT);
     const int c0 = ctile * COLS;
     const int K = p.K1 + p.K2;
     const int nchunk = K >> 4;  // even (checked at launch)
 
+    // x row pointers: row-major (B, J, K) with the tail rows clamped to row 0 (never stored), or
+    // row-blocked (padded to 32 rows: read as they are) -- see blk_off
     const float* x1r[RT];
     const float* x2r[RT];
 #pragma unroll
     for (int rt = 0; rt < RT; ++rt) {
         const int64_t arow = row0 + 32 * rt + l32;
-        const int64_t ac = arow < p.B ? arow : 0;  // tail rows read row 0, never stored
-        x1r[rt] = p.x1 + ((DBG == 4 ? row0 : ac) / p.x1_div) * p.x1_rs + 8 * h;  // DBG 4: one row per wave
-        x2r[rt] = p.K2 ? p.x2 + (DBG == 4 ? row0 : ac) * p.x2_rs + 8 * h : nullptr;
+        const int64_t ac = arow < p.B ? arow : 0;
+        x1r[rt] = p.x1_blk ? p.x1 + blk_off(arow, 0, 8 * h, J, p.K1) : p.x1 + (ac / p.x1_div) * p.x1_rs + 8 * h;
+        x2r[rt] = !p.K2 ? nullptr : p.x2_blk ? p.x2 + blk_off(arow, 0, 8 * h, J, p.K2) : p.x2 + ac * p.x2_rs + 8 * h;
     }
     int jn[NPW], toff[NPW];  // wave-uniform (SGPR): clamped node, its type's stage offset
 #pragma unroll
@@ -298,26 +317,22 @@ __global__ __launch_bounds__(NW * 64, 1) void k_gl4(const GLArgs p) {
     XBuf X0, X1;
     auto load_x = [&](int c, XBuf& xb) {
         const int k0 = c << 4;
-        if (DBG == 8) {  // timing experiment: x as if stored chunk-blocked (1 KiB per instruction)
-#pragma unroll
-            for (int m = 0; m < NPW; ++m)
-#pragma unroll
-                for (int rt = 0; rt < RT; ++rt) {
-                    const int64_t nblk = max((int64_t)1, (p.B / p.x1_div / 32) * J * (p.K1 / 16));  // stays inside x1
-                    const float* src = p.x1 + (((((L / ntile_c) * RT + rt) * (int64_t)J + jn[m]) * nchunk + c) % nblk) * 512;
-                    xb.a[m][rt] = g4(src + lane * 4);
-                    xb.b[m][rt] = g4(src + 256 + lane * 4);
-                }
-            return;
-        }
 #pragma unroll
         for (int m = 0; m < NPW; ++m)
 #pragma unroll
             for (int rt = 0; rt < RT; ++rt) {
-                const float* src = (k0 < p.K1) ? x1r[rt] + (int64_t)jn[m] * p.K1 + k0
-                                               : x2r[rt] + (int64_t)jn[m] * p.K2 + (k0 - p.K1);
+                const float* src;
+                int step4;  // floats from k..k+3 to k+4..k+7
+                if (k0 < p.K1) {
+                    src = p.x1_blk ? x1r[rt] + (int64_t)jn[m] * p.K1 * 32 + (k0 << 5) : x1r[rt] + (int64_t)jn[m] * p.K1 + k0;
+                    step4 = p.x1_blk ? 128 : 4;
+                } else {
+                    const int k2 = k0 - p.K1;
+                    src = p.x2_blk ? x2r[rt] + (int64_t)jn[m] * p.K2 * 32 + (k2 << 5) : x2r[rt] + (int64_t)jn[m] * p.K2 + k2;
+                    step4 = p.x2_blk ? 128 : 4;
+                }
                 xb.a[m][rt] = g4(src);
-                xb.b[m][rt] = g4(src + 4);
+                xb.b[m][rt] = g4(src + step4);
             }
     };
     // LDS-DMA of chunk c's weight slice for this workgroup's columns: per type one contiguous
@@ -339,7 +354,7 @@ __global__ __launch_bounds__(NW * 64, 1) void k_gl4(const GLArgs p) {
         const bool rms_chunk = RMS && (c << 4) < p.K1;
 #pragma unroll
         for (int m = 0; m < NPW; ++m) {
-            if (wave + NW * m >= J || DBG == 1) continue;  // wave-uniform (DBG 1: loads only)
+            if (wave + NW * m >= J) continue;  // wave-uniform
             const _Float16* wt = cur + toff[m] + lane * 8;
             halfx8 xh[RT], xl[RT];
 #pragma unroll
@@ -350,13 +365,8 @@ __global__ __launch_bounds__(NW * 64, 1) void k_gl4(const GLArgs p) {
                     const floatx8 q = f * f;
                     ss[m][rt] += ((q[0] + q[1]) + (q[2] + q[3])) + ((q[4] + q[5]) + (q[6] + q[7]));
                 }
-                if (DBG == 3) {  // timing experiment: no split VALU (operands are garbage)
-                    xh[rt] = __builtin_bit_cast(halfx8, xb.a[m][rt]);
-                    xl[rt] = __builtin_bit_cast(halfx8, xb.b[m][rt]);
-                } else {
-                    xh[rt] = __builtin_convertvector(f, halfx8);
-                    xl[rt] = __builtin_convertvector(f - __builtin_convertvector(xh[rt], floatx8), halfx8);
-                }
+                xh[rt] = __builtin_convertvector(f, halfx8);
+                xl[rt] = __builtin_convertvector(f - __builtin_convertvector(xh[rt], floatx8), halfx8);
             }
 #pragma unroll
             for (int ct = 0; ct < CT; ++ct) {
@@ -382,7 +392,7 @@ __global__ __launch_bounds__(NW * 64, 1) void k_gl4(const GLArgs p) {
         __builtin_amdgcn_s_waitcnt(VmCnt4<0>::imm);
         __builtin_amdgcn_s_barrier();
         if (c + 1 < nchunk) {
-            if (DBG != 5) fill_w(c + 1, (c & 1) ? sW0 : sW1);  // DBG 5: no weight DMA
+            fill_w(c + 1, (c & 1) ? sW0 : sW1);
             load_x(c + 1, nxt);
         }
         compute(c, cur);
@@ -440,18 +450,6 @@ __global__ __launch_bounds__(NW * 64, 1) void k_gl4(const GLArgs p) {
                 for (int r = 0; r < 16; ++r) acc[m][rt][ct][r] = acc[m][rt][ct][r] * sc[r] + bv[m][ct];
         }
     }
-    if (DBG == 2) {  // timing experiment: K loop only, one store per lane
-        float t = 0.f;
-#pragma unroll
-        for (int m = 0; m < NPW; ++m)
-#pragma unroll
-            for (int rt = 0; rt < RT; ++rt)
-#pragma unroll
-                for (int ct = 0; ct < CT; ++ct) t += acc[m][rt][ct][0];
-        p.out[(int64_t)blockIdx.x * NTH + tid] = t;
-        return;
-    }
-
     if (DBG == 6) ts[3] = wall_clock64();
     if constexpr (MODE == 1) {
         attention_epilogue<J, NW, NPW>(p, acc, smem, sG, row0, ctile, wave, lane);
@@ -482,8 +480,8 @@ __global__ __launch_bounds__(NW * 64, 1) void k_gl4(const GLArgs p) {
 #pragma unroll
             for (int ib = 0; ib < IB; ++ib) {
                 const int i = ib * 16 + lr;
-                rv[k][ib] = (ok && i < J) ? g4(p.res + row * p.res_rs + (int64_t)i * p.N + n)
-                                          : floatx4{0.f, 0.f, 0.f, 0.f};
+                const float* src = p.res_blk ? p.res + blk_off(row, i, n, J, p.N) : p.res + row * p.res_rs + (int64_t)i * p.N + n;
+                rv[k][ib] = (ok && i < J) ? g4(src) : floatx4{0.f, 0.f, 0.f, 0.f};
             }
         }
     };
@@ -555,14 +553,9 @@ __global__ __launch_bounds__(NW * 64, 1) void k_gl4(const GLArgs p) {
                         v.w = tanh4(v.w);
                     }
                     if (p.res) v += rv[k][ib];
-                    if (DBG == 9) {  // timing experiment: no output stores (keep the values live)
-                        if (v.x == 12345.f) p.out[0] = v.y;
-                    } else if (DBG == 7) {  // timing experiment: each store instruction 1 KiB contiguous
-                        const int64_t nblk = max((int64_t)1, p.B * J * p.N / (NTH * 4));  // stays inside out
-                        const int64_t o = (((((int64_t)blockIdx.x * (2 * RT) + hc) * BPW + k) * IB + ib) % nblk) * NTH * 4;
-                        *reinterpret_cast<floatx4*>(p.out + o + (int64_t)tid * 4) = v;
-                    } else if (ok && i < J) {
-                        *reinterpret_cast<floatx4*>(p.out + row * p.out_rs + (int64_t)i * p.N + n) = v;
+                    if (ok && i < J) {
+                        float* dst = p.out_blk ? p.out + blk_off(row, i, n, J, p.N) : p.out + row * p.out_rs + (int64_t)i * p.N + n;
+                        *reinterpret_cast<floatx4*>(dst) = v;
                     }
                 }
             }
@@ -618,7 +611,7 @@ hipError_t launch_graph_linear_v4(const GLArgs& a, bool rms, hipStream_t s) {
     // 16-B row segments in the epilogue: N, row strides and buffers 16-B aligned
     if ((a.N & 3) || ((uintptr_t)a.out & 15) || ((uintptr_t)a.res & 15) || (a.res && (a.res_rs & 3)) || (a.out_rs & 3))
         return hipErrorNotSupported;
-    if (!a.wsp || (a.K1 + a.K2) % 32 || a.K1 % 16) return hipErrorNotSupported;
+    if (!a.wsp || (a.K1 + a.K2) % 32 || a.K1 % 16 || (a.x1_blk && a.x1_div != 1)) return hipErrorNotSupported;
     const int cfg = gl4_cfg();
     switch (a.J) {
         case 16:
@@ -628,15 +621,7 @@ hipError_t launch_graph_linear_v4(const GLArgs& a, bool rms, hipStream_t s) {
             if (cfg == 821) return gl4_launch<16, 8, 2, 1>(a, rms, s);
             if (cfg == 812) return gl4_launch<16, 8, 1, 2>(a, rms, s);
             if (cfg == 813) return gl4_launch<16, 8, 1, 3>(a, rms, s);
-            if (cfg == 1) return gl4_launch<16, 8, 2, 2, 1>(a, rms, s);  // timing experiments
-            if (cfg == 2) return gl4_launch<16, 8, 2, 2, 2>(a, rms, s);
-            if (cfg == 3) return gl4_launch<16, 8, 2, 2, 3>(a, rms, s);
-            if (cfg == 4) return gl4_launch<16, 8, 2, 2, 4>(a, rms, s);
-            if (cfg == 5) return gl4_launch<16, 8, 2, 2, 5>(a, rms, s);
-            if (cfg == 6) return gl4_launch<16, 8, 2, 2, 6>(a, rms, s);
-            if (cfg == 7) return gl4_launch<16, 8, 2, 2, 7>(a, rms, s);
-            if (cfg == 8) return gl4_launch<16, 8, 2, 2, 8>(a, rms, s);
-            if (cfg == 9) return gl4_launch<16, 8, 2, 2, 9>(a, rms, s);
+            if (cfg == 6) return gl4_launch<16, 8, 1, 3, 6>(a, rms, s);  // phase stamps (tools/stamps.py)
             if (cfg == 822) return gl4_launch<16, 8, 2, 2>(a, rms, s);
             // 32 rows x 96 columns: 200 workgroups for an N = 192 layer at B = 3200 (64 x 64 gives
             // 150, leaving 40 % of the CUs idle); measured 1.28x faster on those layers
@@ -656,8 +641,10 @@ hipError_t launch_qkv_attention_v4(const GLArgs& a, bool rms, hipStream_t s) {
     if (!a.wsp || a.J > 16 || a.attn_heads < 1 || a.N != 3 * a.attn_heads * 32 || a.bias || a.film || a.res ||
         a.act || (a.K1 + a.K2) % 32 || a.K1 % 16 || ((uintptr_t)a.out & 15) || (a.out_rs & 3))
         return hipErrorNotSupported;
+    GLArgs b = a;
+    b.attn_order = gl4_cfg() == 100 ? 1 : 0;
     switch (a.J) {
-        case 16: return gl4_launch<16, 8, 1, 3, 0, 1>(a, rms, s);
+        case 16: return gl4_launch<16, 8, 1, 3, 0, 1>(b, rms, s);
         default: return hipErrorNotSupported;
     }
 }

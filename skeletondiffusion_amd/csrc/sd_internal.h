@@ -33,7 +33,10 @@ struct GLArgs {
     // v4 only: W pre-split into f16 hi/lo B fragments (make_split_weights); null -> v4 unusable
     const _Float16* wsp; int wsp_nct; float wsp_unscale;
     // fused to_qkv + Attention (launch_qkv_attention_v4): heads of 32 dims, q scale dh^-1/2
-    int attn_heads; float attn_scale;
+    int attn_heads; float attn_scale; int attn_order;
+    // v4 only: operand / result layouts, 0 = row-major (B, J, F), 1 = row-blocked (blk_off in
+    // sd_graph_linear_v4.hip; rows padded to 32)
+    int x1_blk, x2_blk, res_blk, out_blk;
 };
 
 // f16 hi/lo split of a (types, N, K) f32 weight in MFMA B-fragment order (sd_graph_linear_v4.hip)
@@ -63,7 +66,7 @@ struct UpdArgs {
     int64_t B; int J; int D;
 };
 
-hipError_t launch_graph_linear(const GLArgs& a, bool rms, hipStream_t s);     // dispatches v1 / v2
+hipError_t launch_graph_linear(const GLArgs& a, bool rms, hipStream_t s);     // dispatches v1..v4
 hipError_t launch_graph_linear_v1(const GLArgs& a, bool rms, hipStream_t s);
 hipError_t launch_graph_linear_v2(const GLArgs& a, bool rms, hipStream_t s);
 hipError_t launch_graph_linear_v3(const GLArgs& a, bool rms, hipStream_t s);  // J in {16,17,21}

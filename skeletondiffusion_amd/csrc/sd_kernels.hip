@@ -216,6 +216,8 @@ hipError_t launch_graph_linear(const GLArgs& a, bool rms, hipStream_t s) {
         const hipError_t e = launch_graph_linear_v4(a, rms, s);
         if (e != hipErrorNotSupported) return e;
     }
+    // the exact-f32 generations read and write row-major activations only
+    if (a.x1_blk || a.x2_blk || a.res_blk || a.out_blk) return hipErrorNotSupported;
     if (v == 3 || (v == 0 && a.N < 512)) {
         const hipError_t e = launch_graph_linear_v3(a, rms, s);
         if (e != hipErrorNotSupported) return e;

@@ -68,10 +68,12 @@ struct sd_plan {
     std::map<std::string, int> index;
     bool finalized = false;
     bool fuse_ok = false;  // to_qkv + attention fusable (v4 split weights, J <= 16, dim_head 32)
+    bool blk_ok = false;   // every layer on v4 with row-blocked intermediate activations
     bool fuse_attention_now() const {
         const int v = sd::graph_linear_variant();
         return fuse_ok && (v == 0 || v == 4);
     }
+    bool blocked_now() const { return blk_ok && fuse_attention_now(); }
     std::vector<void*> allocs;
 
     GL init_lin;
@@ -154,9 +156,10 @@ size_t align256(size_t v) { return (v + 255) & ~(size_t)255; }
 
 size_t carve(const sd_plan* p, int64_t rows, char* base, WS* w) {
     const size_t f = sizeof(float);
-    const size_t nH = (size_t)rows * p->J * p->H * f;
-    const size_t nQ = (size_t)rows * p->J * (p->d.use_attention ? 3 * p->hid : p->H) * f;
-    const size_t nO = (size_t)rows * p->J * (p->d.use_attention ? p->hid : 1) * f;
+    const size_t rp = (size_t)((rows + 31) / 32 * 32);  // activations: padded to the 32-row blocks of the v4 layout
+    const size_t nH = rp * p->J * p->H * f;
+    const size_t nQ = rp * p->J * (p->d.use_attention ? 3 * p->hid : p->H) * f;
+    const size_t nO = rp * p->J * (p->d.use_attention ? p->hid : 1) * f;
     const size_t nD = (size_t)rows * p->J * p->D * f;
     size_t off = 0;
     auto take = [&](size_t n) {
@@ -242,6 +245,14 @@ struct Prof {
 int run_denoiser(const sd_plan* p, const float* x_t, const float* x_cond, int64_t cond_repeat,
                  int t, float* x0_out, int64_t rows, const WS& w, hipStream_t s, Prof* prof = nullptr) {
     const int H = p->H;
+    // v4 path: every intermediate activation in the row-blocked layout (coalesced x fragments);
+    // the denoiser's inputs (x_t, x_cond) and output (x0) stay row-major
+    const int B = p->blocked_now() ? 1 : 0;
+    auto lay = [B](sd::GLArgs& g, int in, int res, int out) {
+        g.x1_blk = g.x2_blk = B & in;
+        g.res_blk = B & res;
+        g.out_blk = B & out;
+    };
     // init_lin on cat([x_cond, x]) (generator.py:91-94)
     sd::GLArgs a;
     // The init_lin output is `r` (generator.py:95, r = x.clone()); it is written to w.r and the
@@ -250,6 +261,7 @@ int run_denoiser(const sd_plan* p, const float* x_t, const float* x_cond, int64_
         a = gl_args(p, p->init_lin, x_cond, (int)cond_repeat, x_t, nullptr, nullptr, w.r, rows);
     else
         a = gl_args(p, p->init_lin, x_t, 1, nullptr, nullptr, nullptr, w.r, rows);
+    lay(a, 0, 0, 1);
     SD_LAUNCH(prof, 0, sd::launch_graph_linear(a, false, s));
 
     const int L = 2 * p->depth;
@@ -258,9 +270,11 @@ int run_denoiser(const sd_plan* p, const float* x_t, const float* x_cond, int64_
         const float* xin = (l == 0) ? w.r : w.x;
         // ResnetBlock: h = tanh(FiLM(GL1 x)); x = tanh(GL2 h) + x     (attention.py:96-102)
         a = gl_args(p, p->r1[l], xin, 1, nullptr, film, nullptr, w.h, rows);
+        lay(a, 1, 1, 1);
         a.act = 1;
         SD_LAUNCH(prof, 0, sd::launch_graph_linear(a, false, s));
         a = gl_args(p, p->r2[l], w.h, 1, nullptr, nullptr, xin, w.x, rows);
+        lay(a, 1, 1, 1);
         a.act = 1;
         SD_LAUNCH(prof, 0, sd::launch_graph_linear(a, false, s));
         if (!p->has_attn[l]) continue;
@@ -274,37 +288,45 @@ int run_denoiser(const sd_plan* p, const float* x_t, const float* x_cond, int64_
                 a.out_rs = (int64_t)p->J * p->hid;
                 a.attn_heads = p->d.attn_heads;
                 a.attn_scale = qscale;
+                lay(a, 1, 1, 1);
                 if (prof && prof->pre(0, s)) return fail(SD_E_HIP, "hipEventRecord failed");
                 fused = sd::launch_qkv_attention_v4(a, true, s);
                 if (fused != hipSuccess && fused != hipErrorNotSupported) SD_HIP(fused);
                 if (prof && prof->post(s)) return fail(SD_E_HIP, "hipEventRecord failed");
             }
             if (fused == hipErrorNotSupported) {
+                if (B) return fail(SD_E_INTERNAL, "row-blocked plan without the fused attention kernel");
                 a = gl_args(p, p->qkv[l], w.x, 1, nullptr, nullptr, nullptr, w.qkv, rows);
                 SD_LAUNCH(prof, 0, sd::launch_graph_linear(a, true, s));
                 sd::AttnArgs aa{w.qkv, w.o, rows, p->J, p->d.attn_heads, p->d.attn_dim_head, qscale};
                 SD_LAUNCH(prof, 1, sd::launch_attention(aa, s));
             }
             a = gl_args(p, p->outp[l], w.o, 1, nullptr, nullptr, w.x, w.x, rows);
+            lay(a, 1, 1, 1);
             SD_LAUNCH(prof, 0, sd::launch_graph_linear(a, false, s));
         } else {
             // Residual(PreNorm(StaticGraphLinear)): x = GL(rmsnorm(x)) + x
             a = gl_args(p, p->qkv[l], w.x, 1, nullptr, nullptr, w.x, w.x, rows);
+            lay(a, 1, 1, 1);
             SD_LAUNCH(prof, 0, sd::launch_graph_linear(a, true, s));
         }
     }
     // final_res_block on cat(x, r) (generator.py:104-106)
     const float* film = p->film + ((size_t)L * p->T + t) * 2 * H;
     a = gl_args(p, p->fres_res, w.x, 1, w.r, nullptr, nullptr, w.res, rows);
+    lay(a, 1, 1, 1);
     SD_LAUNCH(prof, 0, sd::launch_graph_linear(a, false, s));
     a = gl_args(p, p->r1[L], w.x, 1, w.r, film, nullptr, w.h, rows);
+    lay(a, 1, 1, 1);
     a.act = 1;
     SD_LAUNCH(prof, 0, sd::launch_graph_linear(a, false, s));
     a = gl_args(p, p->r2[L], w.h, 1, nullptr, nullptr, w.res, w.res, rows);
+    lay(a, 1, 1, 1);
     a.act = 1;
     SD_LAUNCH(prof, 0, sd::launch_graph_linear(a, false, s));
     // final_glin (generator.py:107)
     a = gl_args(p, p->fglin, w.res, 1, nullptr, nullptr, nullptr, x0_out, rows);
+    lay(a, 1, 1, 0);
     SD_LAUNCH(prof, 0, sd::launch_graph_linear(a, false, s));
     return SD_OK;
 }
@@ -537,6 +559,16 @@ int sd_plan_finalize(sd_plan* p, void* stream_) {
     p->fuse_ok = p->d.use_attention && J <= 16 && p->d.attn_dim_head == 32;
     for (size_t l = 0; l < p->qkv.size(); ++l)
         if (p->has_attn[l] && !p->qkv[l].split.w) p->fuse_ok = false;
+    // row-blocked activations need every graph-linear on v4 (split weights, K multiple of 32)
+    p->blk_ok = p->fuse_ok && J == 16;
+    auto v4ok = [](const GL& g) { return g.split.w && (g.K1 + g.K2) % 32 == 0; };
+    if (!v4ok(p->init_lin) || !v4ok(p->fres_res) || !v4ok(p->fglin)) p->blk_ok = false;
+    for (auto& g : p->r1)
+        if (!v4ok(g)) p->blk_ok = false;
+    for (auto& g : p->r2)
+        if (!v4ok(g)) p->blk_ok = false;
+    for (size_t l = 0; l < p->outp.size(); ++l)
+        if (p->has_attn[l] && !v4ok(p->outp[l])) p->blk_ok = false;
 
     // time MLP (generator.py:50-55, 97) and per-block FiLM tables (attention.py:81-84, 96-100)
     float *emb = nullptr, *t1 = nullptr, *temb = nullptr;
@@ -782,6 +814,14 @@ int sd_test_graph_linear(const float* x1, int32_t K1, int64_t x1_div, const floa
                          const float* W, const float* bias, const int64_t* node_types, const float* ghat,
                          const float* film, int32_t act, const float* res, float* out, int64_t rows,
                          int32_t J, int32_t N, int32_t rms, void* stream) {
+    return sd_test_graph_linear_layout(x1, K1, x1_div, x2, K2, W, bias, node_types, ghat, film, act, res, out, rows,
+                                       J, N, rms, 0, stream);
+}
+
+int sd_test_graph_linear_layout(const float* x1, int32_t K1, int64_t x1_div, const float* x2, int32_t K2,
+                                const float* W, const float* bias, const int64_t* node_types, const float* ghat,
+                                const float* film, int32_t act, const float* res, float* out, int64_t rows,
+                                int32_t J, int32_t N, int32_t rms, int32_t layout, void* stream) {
     if (!x1 || !W || !ghat || !out || !node_types || J < 1 || J > sd::kMaxNodes || N < 1 || K1 % 16 ||
         K2 % 16 || x1_div < 1 || rows < 0)
         return fail(SD_E_INVALID, "bad arguments");
@@ -819,6 +859,10 @@ int sd_test_graph_linear(const float* x1, int32_t K1, int64_t x1_div, const floa
         return e && atoi(e) == 1;
     }();
     static std::map<std::tuple<const float*, int, int, int>, sd::SplitW> cached;
+    a.x1_blk = layout & 1;
+    a.x2_blk = (layout >> 1) & 1;
+    a.res_blk = (layout >> 2) & 1;
+    a.out_blk = (layout >> 3) & 1;
     sd::SplitW sw;
     if (sd::graph_linear_variant() == 0 || sd::graph_linear_variant() == 4) {
         const auto key = std::make_tuple(W, a.ntypes, N, K1 + a.K2);
@@ -843,7 +887,8 @@ int sd_test_graph_linear(const float* x1, int32_t K1, int64_t x1_div, const floa
 }
 
 int sd_test_qkv_attention(const float* x, int32_t K, const float* W, const int64_t* node_types, const float* ghat,
-                          float* out, int64_t rows, int32_t J, int32_t heads, int32_t rms, void* stream) {
+                          float* out, int64_t rows, int32_t J, int32_t heads, int32_t rms, int32_t layout,
+                          void* stream) {
     if (!x || !W || !ghat || !out || !node_types || J < 1 || J > sd::kMaxNodes || heads < 1 || K % 32 || rows < 0)
         return fail(SD_E_INVALID, "bad arguments");
     sd::GLArgs a{};
@@ -867,6 +912,8 @@ int sd_test_qkv_attention(const float* x, int32_t K, const float* W, const int64
     }
     a.attn_heads = heads;
     a.attn_scale = (float)std::pow(32.0, -0.5);
+    a.x1_blk = layout & 1;
+    a.out_blk = (layout >> 3) & 1;
     sd::SplitW sw;
     SD_HIP(sd::make_split_weights(W, a.ntypes, N, K, &sw, (hipStream_t)stream));
     a.wsp = sw.w;

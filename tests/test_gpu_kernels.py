@@ -34,6 +34,30 @@ def _gl_reference(x1, x2, W, bias, types, ghat, film, act, res, rms, div):
     return z.float()
 
 
+def to_blocked(t):
+    """(B, J, F) -> the v4 row-blocked layout, flat: per 32-row block and node, [F/8][2][32][4]."""
+    B, J, F = t.shape
+    Bp = (B + 31) // 32 * 32
+    tp = torch.zeros(Bp, J, F, dtype=t.dtype)
+    tp[:B] = t
+    return tp.view(Bp // 32, 32, J, F // 8, 2, 4).permute(0, 2, 3, 4, 1, 5).contiguous().view(-1)
+
+
+def from_blocked(flat, B, J, F):
+    Bp = (B + 31) // 32 * 32
+    return flat.view(Bp // 32, J, F // 8, 2, 32, 4).permute(0, 4, 1, 2, 3, 5).reshape(Bp, J, F)[:B]
+
+
+def test_blocked_layout_helpers():
+    t = torch.arange(67 * 3 * 16, dtype=torch.float32).view(67, 3, 16)
+    b = to_blocked(t)
+    assert b.numel() == 96 * 3 * 16
+    assert torch.equal(from_blocked(b, 67, 3, 16), t)
+    # element (row 33, node 2, feature 13): block 1, octet 1, half 1, row 1, lane 1
+    off = ((1 * 3 + 2) * 16 * 32) + 1 * 256 + 1 * 128 + 1 * 4 + 1
+    assert b[off] == t[33, 2, 13]
+
+
 def _run_gl(dev, x1, x2, W, bias, types, ghat, film, act, res, rms, div):
     B = x1.shape[0] * div
     J, N = x1.shape[1], W.shape[1]
@@ -145,7 +169,8 @@ def test_attention_kernel(J, heads, dh, cuda):
 
 @pytest.mark.parametrize("J,nty,heads,rms", [(16, 10, 8, True), (16, 1, 4, True), (16, 10, 8, False), (16, 3, 2, True)])
 @pytest.mark.parametrize("B", [64, 67])
-def test_qkv_attention_fused(J, nty, heads, rms, B, cuda):
+@pytest.mark.parametrize("blocked", [False, True])
+def test_qkv_attention_fused(J, nty, heads, rms, B, blocked, cuda):
     """Fused to_qkv + attention kernel vs a float64 torch restatement of the two ops."""
     g = torch.Generator().manual_seed(J * 100 + heads + B + rms)
     K, hid = 192, heads * 32
@@ -161,10 +186,14 @@ def test_qkv_attention_fused(J, nty, heads, rms, B, cuda):
     out = torch.full((B, J, hid), float("nan"), device=cuda)
     nt = (ctypes.c_int64 * J)(*types.tolist())
     xd, Wd, gd = x.to(cuda), W.to(cuda), ghat.to(cuda)
-    _lib.check(_lib.lib().sd_test_qkv_attention(xd.data_ptr(), K, Wd.data_ptr(), nt, gd.data_ptr(), out.data_ptr(),
-                                                B, J, heads, int(rms), 0))
+    if blocked:
+        xd = to_blocked(x).to(cuda)
+        outb = torch.full((to_blocked(torch.zeros(B, J, hid)).numel(),), float("nan"), device=cuda)
+    _lib.check(_lib.lib().sd_test_qkv_attention(xd.data_ptr(), K, Wd.data_ptr(), nt, gd.data_ptr(),
+                                                (outb if blocked else out).data_ptr(), B, J, heads, int(rms),
+                                                9 if blocked else 0, 0))
     torch.cuda.synchronize()
-    got = out.cpu().double()
+    got = (from_blocked(outb.cpu(), B, J, hid) if blocked else out.cpu()).double()
     assert torch.isfinite(got).all()
     assert (got - ref).abs().max().item() < 2e-5
 
@@ -177,6 +206,48 @@ def test_qkv_attention_rejects_large_J(cuda):
     g = torch.eye(J, device=cuda)
     nt = (ctypes.c_int64 * J)(*([0] * J))
     rc = _lib.lib().sd_test_qkv_attention(x.data_ptr(), K, W.data_ptr(), nt, g.data_ptr(), out.data_ptr(), B, J,
-                                          heads, 1, 0)
+                                          heads, 1, 0, 0)
     assert rc < 0
+
+
+LAYOUT_CASES = [  # (K1, K2, N, bias, film, act, res, rms, layout bits: x1 | x2 << 1 | res << 2 | out << 3)
+    (192, 0, 192, True, True, 1, False, False, 0b1001),   # block1, blocked in/out
+    (192, 0, 192, True, False, 1, True, False, 0b1101),   # block2 with blocked residual
+    (256, 0, 192, False, False, 0, True, False, 0b1101),  # to_out
+    (192, 192, 192, True, True, 1, False, False, 0b1011),  # final block1 on cat(x, r)
+    (192, 0, 96, True, False, 0, False, False, 0b0001),   # final_glin: blocked in, row-major out
+    (96, 96, 192, True, False, 0, False, False, 0b1000),   # init_lin: row-major in, blocked out
+    (192, 0, 192, True, False, 1, True, False, 0b0101),   # mixed: blocked x / res, row-major out
+]
+
+
+@pytest.mark.parametrize("K1,K2,N,has_bias,has_film,act,has_res,rms,layout", LAYOUT_CASES)
+@pytest.mark.parametrize("B", [64, 67])
+def test_graph_linear_blocked_layout(K1, K2, N, has_bias, has_film, act, has_res, rms, layout, B, cuda):
+    J, nty = 16, 10
+    g = torch.Generator().manual_seed(K1 + K2 + N + layout + B)
+    r = lambda *s: torch.rand(*s, generator=g) * 2 - 1  # noqa: E731
+    x1, x2 = r(B, J, K1), (r(B, J, K2) if K2 else None)
+    W = r(nty, N, K1 + K2) / (K1 + K2) ** 0.5
+    types = torch.tensor([0, 1, 2, 0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 7, 8, 9])
+    bias = r(nty, N) * 0.1 if has_bias else None
+    ghat = F.normalize(torch.eye(J) + torch.rand(J, J, generator=g) * 0.1, p=1.0, dim=1)
+    film = r(2 * N) * 0.5 if has_film else None
+    res = r(B, J, N) if has_res else None
+    ref = _gl_reference(x1, x2, W, bias, types, ghat, film, act, res, rms, 1)
+    lay = lambda t, bit: None if t is None else (to_blocked(t) if layout & bit else t.contiguous())  # noqa: E731
+    dev = lambda t: None if t is None else t.to(cuda)  # noqa: E731
+    d = dict(x1=dev(lay(x1, 1)), x2=dev(lay(x2, 2)), res=dev(lay(res, 4)), W=dev(W), bias=dev(bias), ghat=dev(ghat),
+             film=dev(film))
+    n_out = to_blocked(torch.zeros(B, J, N)).numel() if layout & 8 else B * J * N
+    out = torch.full((n_out,), float("nan"), device=cuda)
+    nt = (ctypes.c_int64 * J)(*types.tolist())
+    p = lambda a: None if a is None else a.data_ptr()  # noqa: E731
+    _lib.check(_lib.lib().sd_test_graph_linear_layout(p(d["x1"]), K1, 1, p(d["x2"]), K2, p(d["W"]), p(d["bias"]), nt,
+                                                      p(d["ghat"]), p(d["film"]), act, p(d["res"]), out.data_ptr(), B,
+                                                      J, N, int(rms), layout, 0))
+    torch.cuda.synchronize()
+    got = from_blocked(out.cpu(), B, J, N) if layout & 8 else out.cpu().view(B, J, N)
+    assert torch.isfinite(got).all()
+    assert (got - ref).abs().max().item() < 2e-5
 
