@@ -388,17 +388,26 @@ __global__ __launch_bounds__(NW * 64, 1) void k_gl4(const GLArgs p) {
     // issue chunk c+1 into the other stage / register buffer -> MFMAs on chunk c.  The waitcnt
     // is a builtin (not inline asm) so the compiler knows x(c) is complete and inserts no
     // further vmcnt waits before the MFMAs.
+    uint64_t cs[5];  // DBG 6: shader-clock stamps inside chunk 5
     auto step = [&](int c, const XBuf& cur, XBuf& nxt) {
+        if (DBG == 6 && c == 5) cs[0] = clock64();
         __builtin_amdgcn_s_waitcnt(VmCnt4<0>::imm);
+        if (DBG == 6 && c == 5) cs[1] = clock64();
         __builtin_amdgcn_s_barrier();
+        if (DBG == 6 && c == 5) cs[2] = clock64();
         if (c + 1 < nchunk) {
             fill_w(c + 1, (c & 1) ? sW0 : sW1);
             load_x(c + 1, nxt);
         }
+        if (DBG == 6 && c == 5) cs[3] = clock64();
         compute(c, cur);
+        if (DBG == 6 && c == 5) {
+            __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): LDS reads of the MFMAs done
+            cs[4] = clock64();
+        }
     };
 
-    uint64_t ts[6];  // DBG 6: phase stamps (s_memrealtime, 100 MHz)
+    uint64_t ts[8];  // DBG 6: phase stamps (s_memrealtime, 100 MHz) + shader clock around the K loop
     if (DBG == 6) ts[0] = wall_clock64();
     // G-hat and FiLM (scale + 1 | shift) for this workgroup's columns -> LDS, bias -> registers:
     // all read by the epilogue only, after the K loop's barriers
@@ -420,9 +429,13 @@ __global__ __launch_bounds__(NW * 64, 1) void k_gl4(const GLArgs p) {
     load_x(0, X0);
     for (int c = 0; c < nchunk; c += 2) {
         step(c, X0, X1);
-        if (DBG == 6 && c == 0) ts[1] = wall_clock64();
+        if (DBG == 6 && c == 0) {
+            ts[1] = wall_clock64();
+            ts[6] = clock64();
+        }
         step(c + 1, X1, X0);
     }
+    if (DBG == 6) ts[7] = clock64();
     if (DBG == 6) ts[2] = wall_clock64();
 
     // ---- unscale, RMS, bias in the accumulator layout:
@@ -565,11 +578,15 @@ __global__ __launch_bounds__(NW * 64, 1) void k_gl4(const GLArgs p) {
         ts[4] = wall_clock64();
         __syncthreads();
         ts[5] = wall_clock64();
+        if (lane == 0) {  // per wave: chunk-5 phase cycles at out[(nwg * 8) + (blockIdx * NW + wave) * 4]
+            unsigned* q = reinterpret_cast<unsigned*>(p.out) + (size_t)gridDim.x * 8 + ((size_t)blockIdx.x * NW + wave) * 4;
+            for (int i = 0; i < 4; ++i) q[i] = (unsigned)(cs[i + 1] - cs[i]);
+        }
         if (tid == 0) {
             unsigned* o = reinterpret_cast<unsigned*>(p.out) + (size_t)blockIdx.x * 8;
             for (int i = 0; i < 6; ++i) o[i] = (unsigned)ts[i];
             o[6] = __smid();
-            o[7] = L;
+            o[7] = (unsigned)(ts[7] - ts[6]);  // shader-clock cycles of chunks 2 .. end
         }
     }
 }
