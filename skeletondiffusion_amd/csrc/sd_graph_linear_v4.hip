@@ -51,6 +51,14 @@ struct VmCnt4 {
 
 __device__ __forceinline__ floatx4 g4(const float* p) { return *reinterpret_cast<const floatx4*>(p); }
 
+// A 16-B global load the compiler does not track: while an LDS-DMA is in flight hipcc drains it
+// with vmcnt(0) at the first use of any ordinary load's result, which would serialise a
+// pipeline that keeps x two chunks ahead.  Loads issued this way are waited for by hand
+// (s_waitcnt vmcnt(N) + a register fence, k_gl4 XP = 1).
+__device__ __forceinline__ void g4_async(floatx4& d, const float* p) {
+    asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(d) : "v"(p) : "memory");
+}
+
 // tanh(x) = 1 - 2 / (exp(2x) + 1) on v_exp_f32 + v_rcp_f32 (no IEEE division sequence):
 // saturates cleanly at +-1, within ~3e-7 absolute of tanhf
 __device__ __forceinline__ float tanh4(float x) {
@@ -243,7 +251,7 @@ __device__ __forceinline__ void attention_epilogue(const GLArgs& p, floatx16 (&a
 //   are head h's q, k and v columns (tiles h, heads + h, 2 heads + h), and the epilogue runs
 //   softmax(q k^T * dh^-1/2) v per row over the J nodes instead of storing q/k/v; out = the
 //   (B, J, heads * 32) attention output that to_out reads.  qkv never reaches HBM.
-template <int J, int NW, int RT, int CT, bool RMS, int DBG = 0, int MODE = 0>
+template <int J, int NW, int RT, int CT, bool RMS, int DBG = 0, int MODE = 0, int XP = 0>
 __global__ __launch_bounds__(NW * 64, 1) void k_gl4(const GLArgs p) {
     static_assert(MODE == 0 || (CT == 3 && RT == 1 && J <= 16 && NW == 8), "attention mode: 32 x (q|k|v)");
     constexpr int NPW = (J + NW - 1) / NW;  // nodes per wave
@@ -314,7 +322,7 @@ __global__ __launch_bounds__(NW * 64, 1) void k_gl4(const GLArgs p) {
     struct XBuf {
         floatx4 a[NPW][RT], b[NPW][RT];
     };
-    XBuf X0, X1;
+    XBuf X0, X1, X2;
     auto load_x = [&](int c, XBuf& xb) {
         const int k0 = c << 4;
 #pragma unroll
@@ -331,8 +339,13 @@ __global__ __launch_bounds__(NW * 64, 1) void k_gl4(const GLArgs p) {
                     src = p.x2_blk ? x2r[rt] + (int64_t)jn[m] * p.K2 * 32 + (k2 << 5) : x2r[rt] + (int64_t)jn[m] * p.K2 + k2;
                     step4 = p.x2_blk ? 128 : 4;
                 }
-                xb.a[m][rt] = g4(src);
-                xb.b[m][rt] = g4(src + step4);
+                if constexpr (XP == 1) {
+                    g4_async(xb.a[m][rt], src);
+                    g4_async(xb.b[m][rt], src + step4);
+                } else {
+                    xb.a[m][rt] = g4(src);
+                    xb.b[m][rt] = g4(src + step4);
+                }
             }
     };
     // LDS-DMA of chunk c's weight slice for this workgroup's columns: per type one contiguous
@@ -425,15 +438,60 @@ __global__ __launch_bounds__(NW * 64, 1) void k_gl4(const GLArgs p) {
             const int ncol = (MODE == 1 ? (ctile + ct * p.attn_heads) * 32 : c0 + 32 * ct) + l32;
             bv[m][ct] = (p.bias && ncol < p.N) ? p.bias[p.wrow[jn[m]] + ncol] : 0.f;
         }
-    fill_w(0, sW0);
-    load_x(0, X0);
-    for (int c = 0; c < nchunk; c += 2) {
-        step(c, X0, X1);
-        if (DBG == 6 && c == 0) {
-            ts[1] = wall_clock64();
-            ts[6] = clock64();
+    if constexpr (XP == 0) {
+        fill_w(0, sW0);
+        load_x(0, X0);
+        for (int c = 0; c < nchunk; c += 2) {
+            step(c, X0, X1);
+            if (DBG == 6 && c == 0) {
+                ts[1] = wall_clock64();
+                ts[6] = clock64();
+            }
+            step(c + 1, X1, X0);
         }
-        step(c + 1, X1, X0);
+    } else {  // XP 1
+        // x two chunks ahead in three register buffers (hand-waited loads), weights one chunk
+        // ahead in two LDS stages.  Issue order in step c: weight DMA (c+1), then x (c+2); at the
+        // top of step c only x(c+1) -- the last 2*RT*NPW loads issued -- stays in flight.
+        constexpr int NX = 2 * RT * NPW;
+        auto fence = [&](XBuf& xb) {
+#pragma unroll
+            for (int m = 0; m < NPW; ++m)
+#pragma unroll
+                for (int rt = 0; rt < RT; ++rt) asm volatile("" : "+v"(xb.a[m][rt]), "+v"(xb.b[m][rt]));
+        };
+        auto step2 = [&](int c, XBuf& cur, XBuf& nxt2) {
+            if (DBG == 6 && c == 5) cs[0] = clock64();
+            if (c + 1 < nchunk) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NX) : "memory");
+            else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            fence(cur);
+            if (DBG == 6 && c == 5) cs[1] = clock64();
+            __builtin_amdgcn_s_barrier();
+            if (DBG == 6 && c == 5) cs[2] = clock64();
+            if (c + 1 < nchunk) fill_w(c + 1, (c & 1) ? sW0 : sW1);
+            if (c + 2 < nchunk) load_x(c + 2, nxt2);
+            if (DBG == 6 && c == 5) cs[3] = clock64();
+            compute(c, cur);
+            if (DBG == 6 && c == 5) {
+                __builtin_amdgcn_s_waitcnt(0xc07f);
+                cs[4] = clock64();
+            }
+        };
+        fill_w(0, sW0);
+        load_x(0, X0);
+        load_x(1, X1);
+        int c = 0;
+        for (; c + 3 <= nchunk; c += 3) {
+            step2(c, X0, X2);
+            if (DBG == 6 && c == 0) {
+                ts[1] = wall_clock64();
+                ts[6] = clock64();
+            }
+            step2(c + 1, X1, X0);
+            step2(c + 2, X2, X1);
+        }
+        if (c < nchunk) step2(c, X0, X2);
+        if (c + 1 < nchunk) step2(c + 1, X1, X0);
     }
     if (DBG == 6) ts[7] = clock64();
     if (DBG == 6) ts[2] = wall_clock64();
@@ -591,7 +649,7 @@ __global__ __launch_bounds__(NW * 64, 1) void k_gl4(const GLArgs p) {
     }
 }
 
-template <int J, int NW, int RT, int CT, int DBG = 0, int MODE = 0>
+template <int J, int NW, int RT, int CT, int DBG = 0, int MODE = 0, int XP = 0>
 static hipError_t gl4_launch(const GLArgs& a, bool rms, hipStream_t s) {
     constexpr int COLS = 32 * CT;
     const int ntile_c = MODE == 1 ? a.attn_heads : (a.N + COLS - 1) / COLS;
@@ -601,7 +659,7 @@ static hipError_t gl4_launch(const GLArgs& a, bool rms, hipStream_t s) {
     const size_t yfl = MODE == 1 ? (size_t)J * (8 * COLS + 16) + 8 * 16 * 100 : (size_t)J * (16 * COLS + 16);
     const size_t lds = ((wfl > yfl ? wfl : yfl) + (size_t)J * J + 2 * COLS) * sizeof(float);
     if (lds > 160 * 1024) return hipErrorNotSupported;
-    auto kt = rms ? k_gl4<J, NW, RT, CT, true, DBG, MODE> : k_gl4<J, NW, RT, CT, false, DBG, MODE>;
+    auto kt = rms ? k_gl4<J, NW, RT, CT, true, DBG, MODE, XP> : k_gl4<J, NW, RT, CT, false, DBG, MODE, XP>;
     if (lds > 64 * 1024) {
         hipError_t e = hipFuncSetAttribute((const void*)kt, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         if (e != hipSuccess) return e;
@@ -639,6 +697,8 @@ hipError_t launch_graph_linear_v4(const GLArgs& a, bool rms, hipStream_t s) {
             if (cfg == 812) return gl4_launch<16, 8, 1, 2>(a, rms, s);
             if (cfg == 813) return gl4_launch<16, 8, 1, 3>(a, rms, s);
             if (cfg == 6) return gl4_launch<16, 8, 1, 3, 6>(a, rms, s);  // phase stamps (tools/stamps.py)
+            if (cfg == 7) return gl4_launch<16, 8, 1, 3, 6, 0, 1>(a, rms, s);  // stamps, x two chunks ahead
+            if (cfg == 1813) return gl4_launch<16, 8, 1, 3, 0, 0, 1>(a, rms, s);
             if (cfg == 822) return gl4_launch<16, 8, 2, 2>(a, rms, s);
             // 32 rows x 96 columns: 200 workgroups for an N = 192 layer at B = 3200 (64 x 64 gives
             // 150, leaving 40 % of the CUs idle); measured 1.28x faster on those layers

@@ -41,6 +41,25 @@ def test_release_sample_matches_reference(name, cuda):
     assert _max_err(noise0, start) == 0.0 and _max_err(noise_t, samp) == 0.0
 
 
+@pytest.mark.parametrize("variant", [3, 2, 1])
+@pytest.mark.parametrize("name", ["release_h36m16_T10", "release_freeman17_T10"])
+def test_exact_f32_generations_match_reference(name, variant, cuda):
+    """The exact-f32 graph-linear generations (row-major activations, separate k_attention) on
+    the whole sampler, against the same reference outputs as the default split-f16 v4 path."""
+    L = _lib.lib()
+    old = L.sd_set_kernel_variant(variant, -1)
+    assert old >= 0
+    try:
+        z = golden(name)
+        d = build_release_diffusion(z, cuda)
+        xcs, fu, start, samp = release_inputs(z)
+        img, _ = d.sample(batch_size=start.shape[0], x_cond=xcs.to(cuda), start_noise=start.to(cuda),
+                          sampling_noise=samp.to(cuda))
+        assert _max_err(img, z["img"]) < TOL
+    finally:
+        L.sd_set_kernel_variant(old, -1)
+
+
 @pytest.mark.parametrize("name", ["release_h36m16_T10", "release_amass21_T10"])
 def test_denoiser_forward_and_activations(name, cuda):
     z = golden(name)
