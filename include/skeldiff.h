@@ -156,6 +156,20 @@ int sd_profile_step(const sd_plan* plan, const float* x_t, const float* x_cond, 
                     int32_t t, int64_t rows, void* workspace, size_t workspace_bytes, int32_t reps,
                     float* ms_out, int32_t* counts_out, void* stream);
 
+/* Evaluation metrics on device, one workgroup per sequence, deterministic
+ * fixed-order reductions, caller-owned device buffers, up to 64 samples per sequence.
+ * sd_pairwise_distances: x (nseq, samples, features) -> per sequence the mean over sample pairs
+ *   i < j of the L1 distance (l1_mean: the reference's lat_apd, src/metrics/multimodal.py:137-151)
+ *   and of the L2 distance (l2_mean: apd, multimodal.py:15-35); either output may be NULL.
+ * sd_ade_fde: pred (nseq, samples, frames, features), target (nseq, frames, features) -> per
+ *   sequence min over samples of the mean-over-frames L2 distance (ade, multimodal.py:44-57) and
+ *   of the last frame's distance (fde, :60-73); per_sample_* (nseq, samples) receive the
+ *   distances before the minimum (reduction != 'mean'); any output may be NULL. */
+int sd_pairwise_distances(const float* x, int64_t nseq, int32_t samples, int64_t features, float* l1_mean,
+                          float* l2_mean, void* stream);
+int sd_ade_fde(const float* pred, const float* target, int64_t nseq, int32_t samples, int32_t frames,
+               int64_t features, float* ade, float* fde, float* per_sample_ade, float* per_sample_fde, void* stream);
+
 /* Test hooks: one kernel on caller buffers, for the per-kernel numerics tests.
  * sd_test_graph_linear: out(B,J,N) = act(FiLM(ghat @ (s_j W[type j] [x1_j | x2_j] + bias[type j]))) + res,
  *   W (types,N,K1+K2), bias (types,N) or NULL, ghat (J,J), film (2N) or NULL, res (B,J,N) or NULL,

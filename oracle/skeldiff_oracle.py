@@ -526,3 +526,47 @@ def readme_config(J: int = 16) -> DenoiserConfig:
 
 
 __all__ += ["denoiser_param_shapes", "synthetic_state_dict", "release_config", "readme_config"]
+
+
+# ---------------------------------------------------------------------------------------------
+# Evaluation metrics (reference src/metrics/multimodal.py), restated for the on-device metric
+# kernels' parity tests.  Pinned by tests/golden/metrics.npz (the reference's own functions).
+
+def _time_slice(x: torch.Tensor, t0: int, t: int, axis: int) -> torch.Tensor:
+    """multimodal.py:4-8."""
+    end = x.shape[axis] if t == -1 else t
+    return x.narrow(axis, t0, end - t0)
+
+
+def metric_lat_apd(lat_pred: torch.Tensor) -> torch.Tensor:
+    """multimodal.py:137-151: mean over sample pairs i < j of the L1 distance."""
+    B, S = lat_pred.shape[:2]
+    x = lat_pred.reshape(B, S, -1).double()
+    d = (x[:, :, None, :] - x[:, None, :, :]).abs().sum(-1)
+    iu = torch.triu_indices(S, S, offset=1)
+    return d[:, iu[0], iu[1]].mean(-1).float()
+
+
+def metric_apd(pred: torch.Tensor, t0: int = 0, t: int = -1) -> torch.Tensor:
+    """multimodal.py:15-35: mean over sample pairs i < j of the L2 distance."""
+    pred = _time_slice(pred, t0, t, 2)
+    B, S = pred.shape[:2]
+    if S == 1:
+        return torch.zeros(B)
+    x = pred.reshape(B, S, -1).double()
+    d = (x[:, :, None, :] - x[:, None, :, :]).pow(2).sum(-1).sqrt()
+    iu = torch.triu_indices(S, S, offset=1)
+    return d[:, iu[0], iu[1]].mean(-1).float()
+
+
+def metric_ade(target, pred, t0=0, t=-1, reduction="mean", last_only=False):
+    """multimodal.py:44-57 (ade) and :60-73 (fde, last_only)."""
+    pred, target = _time_slice(pred, t0, t, 2), _time_slice(target, t0, t, 1)
+    B, S, T = pred.shape[:3]
+    diff = pred.reshape(B, S, T, -1).double() - target.reshape(B, 1, T, -1).double()
+    dist = diff.pow(2).sum(-1).sqrt()
+    dist = dist[..., -1] if last_only else dist.mean(-1)
+    return (dist.min(-1).values if reduction == "mean" else dist).float()
+
+
+__all__ += ["metric_lat_apd", "metric_apd", "metric_ade"]

@@ -85,6 +85,12 @@ hipError_t launch_set_rng(uint64_t* rng_dev, uint64_t seed, int64_t row0, hipStr
 hipError_t launch_copy_rows(float* dst, int64_t dst_rs, const float* src, int64_t src_rs,
                             int64_t rows, int64_t n, hipStream_t s);
 
+// evaluation metrics (sd_metrics.hip)
+hipError_t launch_pairwise(const float* x, int64_t nseq, int S, int64_t X, float* l1_mean, float* l2_mean,
+                           hipStream_t s);
+hipError_t launch_ade_fde(const float* pred, const float* target, int64_t nseq, int S, int T, int64_t F, float* ade,
+                          float* fde, float* per_sample_ade, float* per_sample_fde, hipStream_t s);
+
 // plan-finalize helpers (one-time)
 hipError_t launch_sinusoidal(float* emb, int T, int dim, float neg_scale, hipStream_t s);
 hipError_t launch_linear(const float* x, int M, int K, const float* W, const float* b, int N,

@@ -802,6 +802,27 @@ int sd_profile_step(const sd_plan* p, const float* x_t, const float* x_cond, int
     return SD_OK;
 }
 
+int sd_pairwise_distances(const float* x, int64_t nseq, int32_t samples, int64_t features, float* l1_mean,
+                          float* l2_mean, void* stream) {
+    if (nseq < 0 || samples < 2 || samples > 64 || features < 1)
+        return fail(SD_E_INVALID, "pairwise distances: need 2..64 samples, features >= 1");
+    if (nseq == 0) return SD_OK;
+    if (!x) return fail(SD_E_INVALID, "pairwise distances: null input");
+    SD_HIP(sd::launch_pairwise(x, nseq, samples, features, l1_mean, l2_mean, (hipStream_t)stream));
+    return SD_OK;
+}
+
+int sd_ade_fde(const float* pred, const float* target, int64_t nseq, int32_t samples, int32_t frames,
+               int64_t features, float* ade, float* fde, float* per_sample_ade, float* per_sample_fde, void* stream) {
+    if (nseq < 0 || samples < 1 || samples > 64 || frames < 1 || features < 1)
+        return fail(SD_E_INVALID, "ade/fde: need 1..64 samples, frames >= 1, features >= 1");
+    if (nseq == 0) return SD_OK;
+    if (!pred || !target) return fail(SD_E_INVALID, "ade/fde: null input");
+    SD_HIP(sd::launch_ade_fde(pred, target, nseq, samples, frames, features, ade, fde, per_sample_ade, per_sample_fde,
+                              (hipStream_t)stream));
+    return SD_OK;
+}
+
 int sd_set_kernel_variant(int32_t gl_variant, int32_t gl4_tile) {
     if (gl_variant == -1) return sd::graph_linear_variant();  // query
     const int old = sd::set_graph_linear_variant(gl_variant);

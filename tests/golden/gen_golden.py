@@ -16,7 +16,7 @@ that package's published sinusoidal embedding:
 It is injected into sys.modules for the duration of this script; nothing of the reference is
 copied into the repository.
 
-Usage:  PYTHONDONTWRITEBYTECODE=1 python tests/golden/gen_golden.py
+Usage:  PYTHONDONTWRITEBYTECODE=1 python tests/golden/gen_golden.py [metrics]
 """
 from __future__ import annotations
 
@@ -254,7 +254,27 @@ def gen_release(skel_key, T, B_seq, futures, with_acts, steps_to_keep=None, tag=
     _save(tag or f"release_{skel_key}_T{T}", **out)
 
 
+def gen_metrics():
+    """The reference's multimodal metrics (src/metrics/multimodal.py) on synthetic samples: latent
+    APD (L1) and APD (L2) over 50 futures of (J=16, 96) latents, and ADE / FDE of (frames, J*3)
+    motions against a target, incl. the per-sample (reduction != 'mean') form."""
+    from src.metrics.multimodal import ade, apd, fde, lat_apd
+
+    lat = torch.from_numpy(synthetic.normal((3, 50, 16, 96), seed=31)) * 0.3
+    motion = torch.from_numpy(synthetic.normal((2, 7, 20, 16, 3), seed=32))  # (B, S, T, J, 3)
+    target = torch.from_numpy(synthetic.normal((2, 20, 16, 3), seed=33))
+    # inputs are regenerated from the seeds by the consumers (tests/test_metrics*.py)
+    _save("metrics", lat_apd=lat_apd(lat), lat_apd_l2=apd(lat.unsqueeze(2)),
+          apd=apd(motion), ade=ade(target, motion), fde=fde(target, motion),
+          ade_per_sample=ade(target, motion, reduction="none"), fde_per_sample=fde(target, motion, reduction="none"),
+          ade_t5_15=ade(target, motion, t0=5, t=15), apd_t5_15=apd(motion, t0=5, t=15))
+
+
 def main():
+    if sys.argv[1:] == ["metrics"]:
+        gen_metrics()
+        return
+    gen_metrics()
     gen_covariances()
     gen_readme()
     gen_release("h36m16", 10, B_seq=2, futures=4, with_acts=True)
