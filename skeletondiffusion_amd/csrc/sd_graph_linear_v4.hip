@@ -258,7 +258,8 @@ __global__ __launch_bounds__(NW * 64, 1) void k_gl4(const GLArgs p) {
     constexpr int KS = (J + 3) / 4;         // 4-deep k steps of the mixing GEMM (K = J padded)
     constexpr int IB = (J + 15) / 16;       // 16-row i blocks of the mixing GEMM
     constexpr int COLS = 32 * CT;
-    constexpr int YS = 16 * COLS + 16;      // floats per node in a 16-row Y slab (+16: bank shift)
+    constexpr int YR = COLS + 4;            // floats per Y row (+4: 4x4 blocks read conflict-free)
+    constexpr int YS = 16 * YR + 16;        // floats per node in a 16-row Y slab (+16: bank shift)
     constexpr int NTH = NW * 64;
     constexpr int BPW = (COLS + NW - 1) / NW;  // 16-wide mixing blocks per wave per slab
     extern __shared__ __attribute__((aligned(16))) float smem[];
@@ -538,13 +539,33 @@ __global__ __launch_bounds__(NW * 64, 1) void k_gl4(const GLArgs p) {
             const int i = ib * 16 + lr, jj = 4 * s + lg;
             ga[ib][s] = (i < J && jj < J) ? sG[i * J + jj] : 0.f;
         }
+    // Mixing block b (0 <= b < COLS) of a 16-row slab = 16 (row, column) positions; the A lane lr
+    // reads position lr, the output lane (lr = node, lg) owns positions 4 lg .. 4 lg + 3, which
+    // are always 4 consecutive columns of one row (one 16-B piece).  Row-major output: a block is
+    // 16 consecutive columns of one row, so the 4 lanes of a node cover 64 contiguous bytes.
+    // Row-blocked output: a block is 4 rows x 4 columns (lg -> row), so the 4 lanes of a node
+    // cover 4 consecutive rows of one 4-feature group = 64 contiguous bytes of that layout.
+    const bool blk_out = p.out_blk != 0;  // wave-uniform
+    auto a_off = [&](int b) {             // LDS offset (row * YR + col) of this lane's A position
+        return blk_out ? ((b / (COLS / 4)) * 4 + (lr >> 2)) * YR + (b % (COLS / 4)) * 4 + (lr & 3)
+                       : (b / (COLS / 16)) * YR + (b % (COLS / 16)) * 16 + lr;
+    };
+    auto out_pos = [&](int b, int& r, int& cc) {  // row in the slab and first column of this lane's quad
+        if (blk_out) {
+            r = (b / (COLS / 4)) * 4 + lg;
+            cc = (b % (COLS / 4)) * 4;
+        } else {
+            r = b / (COLS / 16);
+            cc = (b % (COLS / 16)) * 16 + 4 * lg;
+        }
+    };
     floatx4 rv[BPW][IB];
     auto load_res = [&](int hc) {
 #pragma unroll
         for (int k = 0; k < BPW; ++k) {
             const int b = wave + NW * k;
-            const int rc = b * 16 + 4 * lg;
-            const int r = rc / COLS, cc = rc - r * COLS;
+            int r, cc;
+            out_pos(min(b, COLS - 1), r, cc);
             const int64_t row = row0 + 16 * hc + r;
             const int n = c0 + cc;
             const bool ok = b < COLS && row < p.B && n < p.N;  // N % 4 == 0 (checked at launch)
@@ -571,7 +592,7 @@ __global__ __launch_bounds__(NW * 64, 1) void k_gl4(const GLArgs p) {
 #pragma unroll
                 for (int q = 0; q < 8; ++q) {
                     const int r = (q & 3) + 8 * (q >> 2) + 4 * h;
-                    sY[j * YS + r * COLS + 32 * ct + l32] = acc[m][rt][ct][8 * hf + q];
+                    sY[j * YS + r * YR + 32 * ct + l32] = acc[m][rt][ct][8 * hf + q];
                 }
         }
         __syncthreads();
@@ -587,7 +608,7 @@ __global__ __launch_bounds__(NW * 64, 1) void k_gl4(const GLArgs p) {
 #pragma unroll
                 for (int s = 0; s < KS; ++s) {
                     const int jj = 4 * s + lg;
-                    ya[kk][s] = (k0 + kk < BPW && jj < J) ? sY[jj * YS + b * 16 + lr] : 0.f;
+                    ya[kk][s] = (k0 + kk < BPW && jj < J) ? sY[jj * YS + a_off(b)] : 0.f;
                 }
             }
             floatx4 z[PG][IB];
@@ -606,8 +627,8 @@ __global__ __launch_bounds__(NW * 64, 1) void k_gl4(const GLArgs p) {
                 const int k = k0 + kk;
                 if (k >= BPW) continue;
                 const int b = wave + NW * k;
-                const int rc = b * 16 + 4 * lg;
-                const int r = rc / COLS, cc = rc - r * COLS;
+                int r, cc;
+                out_pos(min(b, COLS - 1), r, cc);
                 const int64_t row = row0 + 16 * hc + r;
                 const int n = c0 + cc;
                 const bool ok = b < COLS && row < p.B && n < p.N;
@@ -656,7 +677,7 @@ static hipError_t gl4_launch(const GLArgs& a, bool rms, hipStream_t s) {
     const int64_t ntile_r = (a.B + 32 * RT - 1) / (32 * RT);
     const dim3 grid((unsigned)(ntile_c * ntile_r));
     const size_t wfl = (size_t)a.ntypes * CT * 1024;  // two stages of halves, in floats
-    const size_t yfl = MODE == 1 ? (size_t)J * (8 * COLS + 16) + 8 * 16 * 100 : (size_t)J * (16 * COLS + 16);
+    const size_t yfl = MODE == 1 ? (size_t)J * (8 * COLS + 16) + 8 * 16 * 100 : (size_t)J * (16 * (COLS + 4) + 16);
     const size_t lds = ((wfl > yfl ? wfl : yfl) + (size_t)J * J + 2 * COLS) * sizeof(float);
     if (lds > 160 * 1024) return hipErrorNotSupported;
     auto kt = rms ? k_gl4<J, NW, RT, CT, true, DBG, MODE, XP> : k_gl4<J, NW, RT, CT, false, DBG, MODE, XP>;
