@@ -61,6 +61,7 @@ struct UpdArgs {
     float c1s, c2s, sigs;                  // isotropic scalars
     int iso; int act; int noise_mode;      // noise_mode: 0 none (t == 0), 1 given, 2 Philox
     uint64_t seed; int64_t row0; int step; const uint64_t* rng_dev;  // rng_dev: {seed,row0} or null
+    int64_t row_shift;                     // added to row0 (either source): a row chunk's first row
     float* out; float* out2; int64_t out2_rs;
     float* mean_out; int64_t mean_rs; float* noise_out; int64_t noise_rs;
     int64_t B; int J; int D;
@@ -78,7 +79,8 @@ int set_gl4_tile(int cfg);            // SKELDIFF_GL4_CFG (<NW><RT><CT>, 0 = aut
 hipError_t launch_attention(const AttnArgs& a, hipStream_t s);
 hipError_t launch_update(const UpdArgs& a, hipStream_t s);
 hipError_t launch_noise_fill(float* out, int64_t rows, int64_t n_per_row, uint64_t seed,
-                             int64_t row0, int step, const uint64_t* rng_dev, hipStream_t s);
+                             int64_t row0, int step, const uint64_t* rng_dev, hipStream_t s,
+                             int64_t row_shift = 0);  // row_shift: added to row0 (either source)
 hipError_t launch_philox_raw(uint32_t* out, int64_t rows, int64_t quads, uint64_t seed,
                              int64_t row0, int step, hipStream_t s);
 hipError_t launch_set_rng(uint64_t* rng_dev, uint64_t seed, int64_t row0, hipStream_t s);

@@ -397,13 +397,14 @@ __device__ __forceinline__ floatx2 noise_pair(uint64_t seed, uint64_t row, int s
 
 __global__ __launch_bounds__(256) void k_noise_fill(float* out, int64_t rows, int64_t quads,
                                                     uint64_t seed, int64_t row0, int step,
-                                                    const uint64_t* rng_dev) {
+                                                    const uint64_t* rng_dev, int64_t row_shift) {
     const int64_t g = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (g >= rows * quads) return;
     if (rng_dev) {
         seed = rng_dev[0];
         row0 = (int64_t)rng_dev[1];
     }
+    row0 += row_shift;
     const int64_t r = g / quads;
     const uint32_t q = (uint32_t)(g % quads);
     const uint4 x = philox_at(seed, (uint64_t)(row0 + r), step, q);
@@ -412,12 +413,13 @@ __global__ __launch_bounds__(256) void k_noise_fill(float* out, int64_t rows, in
 }
 
 hipError_t launch_noise_fill(float* out, int64_t rows, int64_t n_per_row, uint64_t seed,
-                             int64_t row0, int step, const uint64_t* rng_dev, hipStream_t s) {
+                             int64_t row0, int step, const uint64_t* rng_dev, hipStream_t s,
+                             int64_t row_shift) {
     const int64_t quads = n_per_row / 4;
     const int64_t n = rows * quads;
     if (n <= 0) return hipSuccess;
     hipLaunchKernelGGL(k_noise_fill, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, out, rows,
-                       quads, seed, row0, step, rng_dev);
+                       quads, seed, row0, step, rng_dev, row_shift);
     return hipGetLastError();
 }
 
@@ -501,6 +503,7 @@ __global__ __launch_bounds__(256) void k_update(const UpdArgs p) {
         seed = p.rng_dev[0];
         row0 = (int64_t)p.rng_dev[1];
     }
+    row0 += p.row_shift;
 
     floatx2 x0v[JM], xtv[JM], ev[JM];
 #pragma unroll

@@ -9,6 +9,7 @@
 #include <map>
 #include <memory>
 #include <mutex>
+#include <numeric>
 #include <string>
 #include <tuple>
 #include <vector>
@@ -54,6 +55,7 @@ struct GraphKey {
     const void* ptrs[10];
     int64_t cond_repeat;
     int32_t flags;
+    int32_t chains;
     void* stream;
     bool operator<(const GraphKey& o) const { return std::memcmp(this, &o, sizeof(GraphKey)) < 0; }
 };
@@ -90,10 +92,21 @@ struct sd_plan {
     std::vector<float> iso_c1, iso_c2, iso_sig;  // host copies of the scalar tables (isotropic)
 
     std::mutex gmu;
-    std::map<GraphKey, hipGraphExec_t> graphs;
+    std::map<GraphKey, std::vector<hipGraphExec_t>> graphs;  // one graph per row chain
+    // row chains (record_loop): auxiliary streams + fork/join events, created on first use
+    static constexpr int kMaxChains = 8;
+    std::mutex cmu;
+    hipStream_t aux[kMaxChains] = {};
+    hipEvent_t ev_fork = nullptr, ev_join[kMaxChains] = {};
 
     ~sd_plan() {
-        for (auto& kv : graphs) (void)hipGraphExecDestroy(kv.second);
+        for (auto& kv : graphs)
+            for (auto x : kv.second) (void)hipGraphExecDestroy(x);
+        for (int i = 0; i < kMaxChains; ++i) {
+            if (aux[i]) (void)hipStreamDestroy(aux[i]);
+            if (ev_join[i]) (void)hipEventDestroy(ev_join[i]);
+        }
+        if (ev_fork) (void)hipEventDestroy(ev_fork);
         for (auto& s : slots)
             if (s.dev) (void)hipFree(s.dev);
         for (void* p : allocs) (void)hipFree(p);
@@ -335,7 +348,7 @@ int run_update(const sd_plan* p, const float* x0, const float* xt, const float* 
                int64_t eps_rs, int noise_mode, uint64_t seed, int64_t row0,
                const uint64_t* rng_dev, int t, float* out, float* out2, int64_t out2_rs,
                float* mean_out, int64_t mean_rs, float* noise_out, int64_t noise_rs, int64_t rows,
-               hipStream_t s, Prof* prof = nullptr) {
+               hipStream_t s, Prof* prof = nullptr, int64_t row_shift = 0) {
     sd::UpdArgs u{};
     u.x0 = x0;
     u.xt = xt;
@@ -348,6 +361,7 @@ int run_update(const sd_plan* p, const float* x0, const float* xt, const float* 
     u.row0 = row0;
     u.step = t;
     u.rng_dev = rng_dev;
+    u.row_shift = row_shift;
     u.out = out;
     u.out2 = out2;
     u.out2_rs = out2_rs;
@@ -664,34 +678,123 @@ int sd_p_sample_update(const sd_plan* p, const float* x0_raw, const float* x_t, 
                       noise_out ? noise_rs : JD, rows, (hipStream_t)stream);
 }
 
+// Row chains.  Rows never interact inside the Denoiser or the posterior update, so the T-step
+// chain of rows [r0, r1) is independent of every other row range: record_loop splits the batch
+// into `chains` row ranges (multiples of 32 rows and of cond_repeat) and records each range's
+// T steps on its own stream, forked from and joined back into the caller's stream.  Kernels of
+// different chains then run concurrently, so one chain's idle CUs (a 200-workgroup graph linear
+// on 256 CUs, the last wave of a 800-workgroup attention launch) take the other chain's
+// workgroups instead of waiting for the next kernel boundary.
+static int g_chains = [] {
+    const char* e = getenv("SKELDIFF_CHAINS");
+    return e ? atoi(e) : 2;
+}();
+
+static WS shift_ws(const sd_plan* p, const WS& w, int64_t r0) {
+    WS o = w;
+    const int64_t J = p->J;
+    o.x += r0 * J * p->H;
+    o.r += r0 * J * p->H;
+    o.h += r0 * J * p->H;
+    o.res += r0 * J * p->H;
+    o.qkv += r0 * J * (p->d.use_attention ? 3 * p->hid : p->H);
+    o.o += r0 * J * (p->d.use_attention ? p->hid : 1);
+    o.x0 += r0 * J * p->D;
+    o.img0 += r0 * J * p->D;
+    o.img1 += r0 * J * p->D;
+    return o;
+}
+
+// number of row chains for `rows` rows and the first row of chain i (i = 0 .. n)
+static int chain_count(const sd_plan* p, int64_t rows, int64_t cond_repeat, int64_t* unit) {
+    int64_t g = 32;
+    if (p->C > 0) g = g / std::gcd(g, cond_repeat) * cond_repeat;  // lcm(32, cond_repeat)
+    *unit = g;
+    const int64_t units = rows / g;
+    int n = std::max(1, std::min(g_chains, (int)sd_plan::kMaxChains));
+    if (units < n) n = (int)std::max<int64_t>(1, units);
+    return n;
+}
+static int64_t chain_row(int i, int n, int64_t rows, int64_t unit) {
+    return i >= n ? rows : (rows / unit) * i / n * unit;
+}
+
+// Creates the auxiliary streams / fork-join events chains 1 .. n-1 use (caller holds cmu).
+static int ensure_chains(sd_plan* mp, int n) {
+    if (!mp->ev_fork) SD_HIP(hipEventCreateWithFlags(&mp->ev_fork, hipEventDisableTiming));
+    for (int i = 1; i < n; ++i) {
+        if (!mp->aux[i]) SD_HIP(hipStreamCreateWithFlags(&mp->aux[i], hipStreamNonBlocking));
+        if (!mp->ev_join[i]) SD_HIP(hipEventCreateWithFlags(&mp->ev_join[i], hipEventDisableTiming));
+    }
+    return SD_OK;
+}
+
+// The whole T-step chain: start noise, then per step Denoiser + posterior update.  only = -1
+// records every row chain (chain i on cs[i]; steps outer, chains inner, so an eager caller feeds
+// every chain from the start); only = i records chain i alone on cs[i] (one captured graph per
+// chain, see sd_sample_loop).
 static int record_loop(const sd_plan* p, const float* x_T, const float* x_cond, int64_t cond_repeat,
                        const float* eps_all, uint64_t seed, int64_t row0, float* out, float* means,
                        float* noise_out, float* timages, float* start_out, int64_t rows, const WS& w,
-                       int32_t flags, bool use_rng_dev, hipStream_t s) {
+                       int32_t flags, bool use_rng_dev, const hipStream_t* cs, int nch, int64_t unit, int only) {
     const int T = p->T;
     const int64_t JD = (int64_t)p->J * p->D;
     const int64_t step_rs = (int64_t)(T > 1 ? T - 1 : 1) * JD;  // row stride of (B, T-1, J, D)
     const uint64_t* rng = use_rng_dev ? w.rng : nullptr;
-    const float* cur = x_T;
-    if (flags & SD_FLAG_DEVICE_START) {
-        SD_HIP(sd::launch_noise_fill(w.img1, rows, JD, seed, row0, T, rng, s));
-        cur = w.img1;
-    }
-    if (start_out) SD_HIP(sd::launch_copy_rows(start_out, JD, cur, JD, rows, JD, s));
+    const bool dev_start = (flags & SD_FLAG_DEVICE_START) != 0;
     const bool dev_noise = (flags & SD_FLAG_DEVICE_NOISE) != 0;
+    struct Chain {
+        int64_t r0, n;
+        WS w;
+        const float* cur;
+    } ch[sd_plan::kMaxChains];
+    const int c0 = only < 0 ? 0 : only, c1 = only < 0 ? nch : only + 1;
+    for (int i = c0; i < c1; ++i) {
+        Chain& c = ch[i];
+        c.r0 = chain_row(i, nch, rows, unit);
+        c.n = chain_row(i + 1, nch, rows, unit) - c.r0;
+        c.w = shift_ws(p, w, c.r0);
+        c.cur = dev_start ? c.w.img1 : x_T + c.r0 * JD;
+        if (dev_start) SD_HIP(sd::launch_noise_fill(c.w.img1, c.n, JD, seed, row0, T, rng, cs[i], c.r0));
+        if (start_out) SD_HIP(sd::launch_copy_rows(start_out + c.r0 * JD, JD, c.cur, JD, c.n, JD, cs[i]));
+    }
     for (int t = T - 1; t >= 0; --t) {
-        int rc = run_denoiser(p, cur, x_cond, cond_repeat, t, w.x0, rows, w, s);
-        if (rc) return rc;
-        float* nxt = (t == 0) ? out : (((T - 1 - t) & 1) ? w.img1 : w.img0);
         const int64_t k = T - 1 - t;  // index into the (B, T-1, ...) records
-        const float* eps = (!dev_noise && t > 0) ? eps_all + k * JD : nullptr;
         const bool rec = t > 0;
-        rc = run_update(p, w.x0, cur, eps, step_rs, dev_noise ? 2 : 1, seed, row0, rng, t, nxt,
-                        (rec && timages) ? timages + k * JD : nullptr, step_rs,
-                        (rec && means) ? means + k * JD : nullptr, step_rs,
-                        (rec && noise_out) ? noise_out + k * JD : nullptr, step_rs, rows, s);
-        if (rc) return rc;
-        cur = nxt;
+        for (int i = c0; i < c1; ++i) {
+            Chain& c = ch[i];
+            const int64_t r0 = c.r0;
+            const float* xc = (p->C > 0) ? x_cond + (r0 / cond_repeat) * p->J * p->C : x_cond;
+            int rc = run_denoiser(p, c.cur, xc, cond_repeat, t, c.w.x0, c.n, c.w, cs[i]);
+            if (rc) return rc;
+            float* nxt = (t == 0) ? out + r0 * JD : (((T - 1 - t) & 1) ? c.w.img1 : c.w.img0);
+            const float* eps = (!dev_noise && t > 0) ? eps_all + r0 * step_rs + k * JD : nullptr;
+            rc = run_update(p, c.w.x0, c.cur, eps, step_rs, dev_noise ? 2 : 1, seed, row0, rng, t, nxt,
+                            (rec && timages) ? timages + r0 * step_rs + k * JD : nullptr, step_rs,
+                            (rec && means) ? means + r0 * step_rs + k * JD : nullptr, step_rs,
+                            (rec && noise_out) ? noise_out + r0 * step_rs + k * JD : nullptr, step_rs, c.n,
+                            cs[i], nullptr, r0);
+            if (rc) return rc;
+            c.cur = nxt;
+        }
+    }
+    return SD_OK;
+}
+
+// fork chains 1 .. n-1 off s (caller holds cmu, ensure_chains done)
+static int fork_chains(sd_plan* mp, hipStream_t s, int n, hipStream_t* cs) {
+    cs[0] = s;
+    if (n > 1) SD_HIP(hipEventRecord(mp->ev_fork, s));
+    for (int i = 1; i < n; ++i) {
+        SD_HIP(hipStreamWaitEvent(mp->aux[i], mp->ev_fork, 0));
+        cs[i] = mp->aux[i];
+    }
+    return SD_OK;
+}
+static int join_chains(sd_plan* mp, hipStream_t s, int n, const hipStream_t* cs) {
+    for (int i = 1; i < n; ++i) {
+        SD_HIP(hipEventRecord(mp->ev_join[i], cs[i]));
+        SD_HIP(hipStreamWaitEvent(s, mp->ev_join[i], 0));
     }
     return SD_OK;
 }
@@ -713,12 +816,29 @@ int sd_sample_loop(const sd_plan* p, const float* x_T, const float* x_cond, int6
     if (cond_repeat < 1) return fail(SD_E_INVALID, "cond_repeat must be >= 1");
     if (rows == 0) return SD_OK;
     hipStream_t s = (hipStream_t)stream;
-    if (!(flags & SD_FLAG_GRAPH))
-        return record_loop(p, x_T, x_cond, cond_repeat, eps_all, seed, row0, out, means_out, noise_out,
-                           timages_out, start_out, rows, w, flags, false, s);
+    sd_plan* mp = const_cast<sd_plan*>(p);
+    int64_t unit = 32;
+    const int nch = chain_count(p, rows, cond_repeat, &unit);
+    std::unique_lock<std::mutex> lk(mp->cmu, std::defer_lock);  // fork/join objects are shared
+    hipStream_t cs[sd_plan::kMaxChains];
+    cs[0] = s;
+    if (nch > 1) {
+        lk.lock();
+        if ((rc = ensure_chains(mp, nch))) return rc;
+        for (int i = 1; i < nch; ++i) cs[i] = mp->aux[i];
+    }
+    if (!(flags & SD_FLAG_GRAPH)) {
+        if ((rc = fork_chains(mp, s, nch, cs))) return rc;
+        rc = record_loop(p, x_T, x_cond, cond_repeat, eps_all, seed, row0, out, means_out, noise_out, timages_out,
+                         start_out, rows, w, flags, false, cs, nch, unit, -1);
+        if (rc) return rc;
+        return join_chains(mp, s, nch, cs);
+    }
 
-    // Graph mode: the chain is captured once per (rows, pointers, flags, stream) and replayed;
-    // seed / row0 live in the workspace so a replay can draw fresh noise.
+    // Graph mode: each row chain is captured once per (rows, pointers, flags, stream, chains) as a
+    // graph of its own and replayed on its own stream (the chains' graphs overlap on the GPU, where
+    // one graph holding parallel branches would be replayed in order); seed / row0 live in the
+    // workspace so a replay can draw fresh noise.
     GraphKey key;
     std::memset(&key, 0, sizeof(key));
     key.rows = rows;
@@ -726,38 +846,46 @@ int sd_sample_loop(const sd_plan* p, const float* x_T, const float* x_cond, int6
     std::memcpy(key.ptrs, ptrs, sizeof(ptrs));
     key.cond_repeat = cond_repeat;
     key.flags = flags;
+    key.chains = nch;
     key.stream = stream;
     SD_HIP(sd::launch_set_rng(w.rng, seed, row0, s));
-    hipGraphExec_t exec = nullptr;
+    std::vector<hipGraphExec_t> execs;
     {
-        std::lock_guard<std::mutex> lk(const_cast<sd_plan*>(p)->gmu);
+        std::lock_guard<std::mutex> g(mp->gmu);
         auto it = p->graphs.find(key);
-        if (it != p->graphs.end()) exec = it->second;
+        if (it != p->graphs.end()) execs = it->second;
     }
-    if (!exec) {
-        hipGraph_t graph = nullptr;
-        SD_HIP(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
-        rc = record_loop(p, x_T, x_cond, cond_repeat, eps_all, seed, row0, out, means_out, noise_out,
-                         timages_out, start_out, rows, w, flags, true, s);
-        hipError_t e = hipStreamEndCapture(s, &graph);
-        if (rc) {
-            if (graph) (void)hipGraphDestroy(graph);
-            return rc;
+    if (execs.empty()) {
+        for (int i = 0; i < nch; ++i) {
+            hipGraph_t graph = nullptr;
+            hipGraphExec_t exec = nullptr;
+            hipError_t e = hipStreamBeginCapture(cs[i], hipStreamCaptureModeThreadLocal);
+            if (e == hipSuccess) {
+                rc = record_loop(p, x_T, x_cond, cond_repeat, eps_all, seed, row0, out, means_out, noise_out,
+                                 timages_out, start_out, rows, w, flags, true, cs, nch, unit, i);
+                e = hipStreamEndCapture(cs[i], &graph);
+                if (!rc && e == hipSuccess) e = hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0);
+                if (graph) (void)hipGraphDestroy(graph);
+            }
+            if (rc || e != hipSuccess) {
+                for (auto x : execs) (void)hipGraphExecDestroy(x);
+                if (rc) return rc;
+                return fail(SD_E_HIP, std::string("graph capture: ") + hipGetErrorString(e));
+            }
+            execs.push_back(exec);
         }
-        if (e != hipSuccess) return fail(SD_E_HIP, std::string("hipStreamEndCapture: ") + hipGetErrorString(e));
-        e = hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0);
-        (void)hipGraphDestroy(graph);
-        if (e != hipSuccess) return fail(SD_E_HIP, std::string("hipGraphInstantiate: ") + hipGetErrorString(e));
-        std::lock_guard<std::mutex> lk(const_cast<sd_plan*>(p)->gmu);
-        auto& cache = const_cast<sd_plan*>(p)->graphs;
+        std::lock_guard<std::mutex> g(mp->gmu);
+        auto& cache = mp->graphs;
         if (cache.size() >= 8) {  // bounded cache: callers that reuse buffers hit it every call
-            for (auto& kv : cache) (void)hipGraphExecDestroy(kv.second);
+            for (auto& kv : cache)
+                for (auto x : kv.second) (void)hipGraphExecDestroy(x);
             cache.clear();
         }
-        cache[key] = exec;
+        cache[key] = execs;
     }
-    SD_HIP(hipGraphLaunch(exec, s));
-    return SD_OK;
+    if ((rc = fork_chains(mp, s, nch, cs))) return rc;
+    for (int i = 0; i < nch; ++i) SD_HIP(hipGraphLaunch(execs[i], cs[i]));
+    return join_chains(mp, s, nch, cs);
 }
 
 int sd_plan_step_flops(const sd_plan* p, int64_t rows, double* flops_out) {
@@ -828,6 +956,14 @@ int sd_set_kernel_variant(int32_t gl_variant, int32_t gl4_tile) {
     const int old = sd::set_graph_linear_variant(gl_variant);
     if (old < 0) return fail(SD_E_INVALID, "gl_variant out of range");
     if (gl4_tile >= 0) (void)sd::set_gl4_tile(gl4_tile);
+    return old;
+}
+
+int sd_set_row_chains(int32_t n) {
+    if (n == -1) return g_chains;
+    if (n < 1 || n > sd_plan::kMaxChains) return fail(SD_E_INVALID, "row chains must be in [1, 8]");
+    const int old = g_chains;
+    g_chains = n;
     return old;
 }
 

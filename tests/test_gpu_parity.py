@@ -236,3 +236,36 @@ def test_full_size_config2_step_and_properties(cuda):
     assert a.abs().max() <= 1.0 + 1e-5  # t = 0: C1[0] = I, C2[0] = 0, no noise -> clamp(x0)
     part = d.sample(batch_size=100, x_cond=x_cond[6:8], seed=11, row0=300)[0]
     assert torch.equal(part, a[300:400])
+
+
+@pytest.mark.parametrize("graph", [False, True])
+def test_row_chains_bitwise_invariant(graph, cuda):
+    """sd_set_row_chains: the batch is split into row ranges whose T-step chains run on forked
+    streams.  Rows are independent, so latents and every per-step record are bitwise those of a
+    single chain -- device noise (row0-shifted Philox) and given noise (row-offset eps) alike."""
+    z = golden("release_h36m16_T10")
+    d = build_release_diffusion(z, cuda)
+    J, T = 16, 10
+    g = torch.Generator().manual_seed(3)
+    xc = (torch.rand((24, J, 96), generator=g) * 2 - 1).to(cuda)  # 24 sequences x 4 futures
+    rows = 96                                                        # = 3 chain units of 32 rows
+    start = torch.randn((rows, J, 96), generator=g).to(cuda)
+    samp = torch.randn((rows, T - 1, J, 96), generator=g).to(cuda)
+    L = _lib.lib()
+    old = L.sd_set_row_chains(1)
+    assert old >= 1
+    try:
+        res = {}
+        for n in (1, 2, 3, 8):
+            assert L.sd_set_row_chains(n) >= 1
+            a = d.engine.sample_loop(rows, x_cond=xc, seed=21, row0=7, record=(True, False), graph=graph)
+            b = d.engine.sample_loop(rows, x_cond=xc, start_noise=start, sampling_noise=samp, record=(False, True),
+                                     graph=graph)
+            torch.cuda.synchronize()
+            res[n] = [t.clone() for t in (a[0], a[1], a[2], a[3], b[0], b[4])]
+        for n in (2, 3, 8):
+            for x, y in zip(res[1], res[n]):
+                assert torch.equal(x, y), n
+        assert L.sd_set_row_chains(0) < 0 and L.sd_set_row_chains(9) < 0
+    finally:
+        L.sd_set_row_chains(old)
