@@ -266,7 +266,8 @@ def main():
                 "latents; device Philox noise)",
         "config": {"workload": c["workload"], "J": J, "T": T, "sequences_per_gpu": batch,
                    "futures": rows // batch, "rows_per_gpu": rows, "latent_dim": D, "hipgraph": graph,
-                   "parallelism": f"dp{world} (sequence-sharded, no data-path collective)"},
+                   "parallelism": f"dp{world} (sequence-sharded, no data-path collective)",
+                   "row_chains": min(L.sd_set_row_chains(-1), max(1, rows // 32))},
         "roofline": {
             "bound": "mfma",
             "kernel": ("k_gl4 graph-linear (3xf16 split MFMA, fused bias/RMS/G-hat/FiLM/tanh/residual; "
@@ -278,6 +279,9 @@ def main():
             "traffic": None,
             "flops_per_launch": gl_flops / max(cnt[0], 1), "launches_per_denoise_step": cnt[0],
             "avg_launch_ms": ms[0] / max(cnt[0], 1),
+            "measured_on": ("one denoise step at the full batch on one stream (sd_profile_step: HIP events "
+                            "around each launch, kernels alone on the GPU); the timed region runs the same "
+                            "kernels as concurrent row chains (config.row_chains) with 32x64 graph-linear tiles"),
             "hbm_view": {"achieved": gl_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": gl_gbs / HBM_PEAK_GBS,
                          "algorithmic_bytes_per_launch": gl_bytes / max(cnt[0], 1)},
         },

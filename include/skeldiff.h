@@ -202,8 +202,8 @@ int sd_test_qkv_attention(const float* x, int32_t K, const float* W, const int64
  * -1 leaves it.  Returns the previous gl_variant, or -1 for an invalid one (nothing changed);
  * gl_variant = -1 only queries (returns the current value). */
 int sd_set_kernel_variant(int32_t gl_variant, int32_t gl4_tile);
-/* Row chains of sd_sample_loop (process-wide; SKELDIFF_CHAINS, default 2): the batch is split into
- * n row ranges (multiples of 32 rows and of cond_repeat; fewer when the batch is small) whose
+/* Row chains of sd_sample_loop (process-wide; SKELDIFF_CHAINS, default 3): the batch is split into
+ * n row ranges (multiples of 32 rows; fewer when the batch is small) whose
  * T-step chains run on forked streams and overlap on the GPU.  Rows are independent, so the
  * results do not depend on n.  Returns the previous n; n = -1 only queries; SD_E_INVALID
  * outside [1, 8]. */

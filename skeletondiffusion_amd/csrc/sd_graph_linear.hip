@@ -86,7 +86,7 @@ __global__ __launch_bounds__(256, MINW) void k_gl2(const GLArgs p) {
     const int64_t arow = row0 + lr;
     const bool rok = arow < p.B;
     const int64_t arow_c = rok ? arow : 0;
-    const float* x1r = p.x1 + (arow_c / p.x1_div) * p.x1_rs + 4 * lg;
+    const float* x1r = p.x1 + ((arow_c + p.x1_row0) / p.x1_div) * p.x1_rs + 4 * lg;
     const float* x2r = p.K2 ? p.x2 + arow_c * p.x2_rs + 4 * lg : nullptr;
     // Tail rows read row 0 (valid memory) and are never stored, so every wave issues exactly J
     // x loads per chunk - the counted vmcnt below relies on that count.

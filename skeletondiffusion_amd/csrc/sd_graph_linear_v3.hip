@@ -90,7 +90,7 @@ __global__ __launch_bounds__(256, 2) void k_gl3(const GLArgs p) {
 
     const int64_t arow = row0 + l32;
     const int64_t arow_c = arow < p.B ? arow : 0;  // tail rows read row 0, never stored
-    const float* x1r = p.x1 + (arow_c / p.x1_div) * p.x1_rs + 8 * h;
+    const float* x1r = p.x1 + ((arow_c + p.x1_row0) / p.x1_div) * p.x1_rs + 8 * h;
     const float* x2r = p.K2 ? p.x2 + arow_c * p.x2_rs + 8 * h : nullptr;
 
     floatx16 acc[NPW];

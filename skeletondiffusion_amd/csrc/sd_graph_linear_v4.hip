@@ -297,7 +297,7 @@ __global__ __launch_bounds__(NW * 64, 1) void k_gl4(const GLArgs p) {
     for (int rt = 0; rt < RT; ++rt) {
         const int64_t arow = row0 + 32 * rt + l32;
         const int64_t ac = arow < p.B ? arow : 0;
-        x1r[rt] = p.x1_blk ? p.x1 + blk_off(arow, 0, 8 * h, J, p.K1) : p.x1 + (ac / p.x1_div) * p.x1_rs + 8 * h;
+        x1r[rt] = p.x1_blk ? p.x1 + blk_off(arow, 0, 8 * h, J, p.K1) : p.x1 + ((ac + p.x1_row0) / p.x1_div) * p.x1_rs + 8 * h;
         x2r[rt] = !p.K2 ? nullptr : p.x2_blk ? p.x2 + blk_off(arow, 0, 8 * h, J, p.K2) : p.x2 + ac * p.x2_rs + 8 * h;
     }
     int jn[NPW], toff[NPW];  // wave-uniform (SGPR): clamped node, its type's stage offset
@@ -678,8 +678,19 @@ static hipError_t gl4_launch(const GLArgs& a, bool rms, hipStream_t s) {
     const dim3 grid((unsigned)(ntile_c * ntile_r));
     const size_t wfl = (size_t)a.ntypes * CT * 1024;  // two stages of halves, in floats
     const size_t yfl = MODE == 1 ? (size_t)J * (8 * COLS + 16) + 8 * 16 * 100 : (size_t)J * (16 * (COLS + 4) + 16);
-    const size_t lds = ((wfl > yfl ? wfl : yfl) + (size_t)J * J + 2 * COLS) * sizeof(float);
+    size_t lds = ((wfl > yfl ? wfl : yfl) + (size_t)J * J + 2 * COLS) * sizeof(float);
     if (lds > 160 * 1024) return hipErrorNotSupported;
+    // Every k_gl4 launch takes a CU's whole LDS, so no other kernel's workgroup shares its CU
+    // (the tiles run one workgroup per CU anyway: registers).  Measured with row chains
+    // (concurrent kernels of independent row ranges): k_gl4 workgroups co-resident with other
+    // kernels' workgroups gave wrong, run-to-run different rows (fused attention at 122 KB LDS:
+    // up to 0.15 off in a T = 2 sampler; the 32 x 64 tile at 82 KB: ~1e-3 over T = 100); with
+    // the whole LDS reserved every chain count is bitwise equal to one chain, at the same
+    // throughput.  The K loop follows the LDS-DMA ordering rules (counted vmcnt + barrier before
+    // a read, one phase between the last read and a restage); the cause is not identified
+    // (DESIGN.md §4c).  SKELDIFF_FULL_LDS (bit MODE) overrides for experiments.
+    static const int full_lds = getenv("SKELDIFF_FULL_LDS") ? atoi(getenv("SKELDIFF_FULL_LDS")) : 3;
+    if (full_lds & (1 << MODE)) lds = 160 * 1024;
     auto kt = rms ? k_gl4<J, NW, RT, CT, true, DBG, MODE, XP> : k_gl4<J, NW, RT, CT, false, DBG, MODE, XP>;
     if (lds > 64 * 1024) {
         hipError_t e = hipFuncSetAttribute((const void*)kt, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
@@ -708,7 +719,7 @@ hipError_t launch_graph_linear_v4(const GLArgs& a, bool rms, hipStream_t s) {
     if ((a.N & 3) || ((uintptr_t)a.out & 15) || ((uintptr_t)a.res & 15) || (a.res && (a.res_rs & 3)) || (a.out_rs & 3))
         return hipErrorNotSupported;
     if (!a.wsp || (a.K1 + a.K2) % 32 || a.K1 % 16 || (a.x1_blk && a.x1_div != 1)) return hipErrorNotSupported;
-    const int cfg = gl4_cfg();
+    const int cfg = gl4_cfg() ? gl4_cfg() : a.tile_hint;
     switch (a.J) {
         case 16:
             if (cfg == 422) return gl4_launch<16, 4, 2, 2>(a, rms, s);

@@ -15,7 +15,9 @@ constexpr int kMaxNodes = 64;
 //   z     = act(z)                               (tanh)
 //   z    += res                                  (residual, attention.py:16 / :102)
 struct GLArgs {
-    const float* x1; int64_t x1_rs; int K1; int x1_div;   // row b reads x1 row b / x1_div
+    const float* x1; int64_t x1_rs; int K1; int x1_div;   // row b reads x1 row (b + x1_row0) / x1_div
+    int64_t x1_row0;                                      // 0 <= x1_row0 < x1_div (a row chunk's phase)
+    int tile_hint;                                        // v4 tile <NW><RT><CT> when SKELDIFF_GL4_CFG is unset (0: per shape)
     const float* x2; int64_t x2_rs; int K2;               // optional second input (cat along K)
     const float* W;                                       // (types, N, K1+K2), K contiguous
     const float* bias;                                    // (types, N) or null

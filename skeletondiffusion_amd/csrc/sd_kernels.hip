@@ -100,7 +100,7 @@ __global__ __launch_bounds__(256) void k_graph_linear(const GLArgs p) {
     const int64_t arow = row0 + lr;
     const bool row_ok = arow < p.B;
     const int64_t arow_c = row_ok ? arow : 0;
-    gl_accumulate<JM, EXACT, NCB, RMS>(acc, ss, p.x1 + (arow_c / p.x1_div) * p.x1_rs, row_ok,
+    gl_accumulate<JM, EXACT, NCB, RMS>(acc, ss, p.x1 + ((arow_c + p.x1_row0) / p.x1_div) * p.x1_rs, row_ok,
                                        p.K1, 0, K, J, p, c0, lr, lg);
     if (p.K2 > 0) {
         float dummy[JM];

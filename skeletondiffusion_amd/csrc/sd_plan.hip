@@ -72,10 +72,14 @@ struct sd_plan {
     bool fuse_ok = false;  // to_qkv + attention fusable (v4 split weights, J <= 16, dim_head 32)
     bool blk_ok = false;   // every layer on v4 with row-blocked intermediate activations
     bool fuse_attention_now() const {
+        static const bool no_fuse = getenv("SKELDIFF_NO_FUSE") != nullptr;  // diagnostic
         const int v = sd::graph_linear_variant();
-        return fuse_ok && (v == 0 || v == 4);
+        return fuse_ok && !no_fuse && (v == 0 || v == 4);
     }
-    bool blocked_now() const { return blk_ok && fuse_attention_now(); }
+    bool blocked_now() const {
+        static const bool no_block = getenv("SKELDIFF_NO_BLOCK") != nullptr;  // diagnostic
+        return blk_ok && !no_block && fuse_attention_now();
+    }
     std::vector<void*> allocs;
 
     GL init_lin;
@@ -255,13 +259,16 @@ struct Prof {
     } while (0)
 
 // Denoiser.forward (generator.py:86-107) for `rows` rows at time t.
+// cond_phase: row 0 of this call is row cond_phase of a cond_repeat group (row chains)
 int run_denoiser(const sd_plan* p, const float* x_t, const float* x_cond, int64_t cond_repeat,
-                 int t, float* x0_out, int64_t rows, const WS& w, hipStream_t s, Prof* prof = nullptr) {
+                 int t, float* x0_out, int64_t rows, const WS& w, hipStream_t s, Prof* prof = nullptr,
+                 int64_t cond_phase = 0, int tile_hint = 0) {
     const int H = p->H;
     // v4 path: every intermediate activation in the row-blocked layout (coalesced x fragments);
     // the denoiser's inputs (x_t, x_cond) and output (x0) stay row-major
     const int B = p->blocked_now() ? 1 : 0;
-    auto lay = [B](sd::GLArgs& g, int in, int res, int out) {
+    auto lay = [B, tile_hint](sd::GLArgs& g, int in, int res, int out) {
+        g.tile_hint = tile_hint;
         g.x1_blk = g.x2_blk = B & in;
         g.res_blk = B & res;
         g.out_blk = B & out;
@@ -270,10 +277,12 @@ int run_denoiser(const sd_plan* p, const float* x_t, const float* x_cond, int64_
     sd::GLArgs a;
     // The init_lin output is `r` (generator.py:95, r = x.clone()); it is written to w.r and the
     // first ResnetBlock reads it from there and writes its result to w.x, so no copy is needed.
-    if (p->C > 0)
+    if (p->C > 0) {
         a = gl_args(p, p->init_lin, x_cond, (int)cond_repeat, x_t, nullptr, nullptr, w.r, rows);
-    else
+        a.x1_row0 = cond_phase;
+    } else {
         a = gl_args(p, p->init_lin, x_t, 1, nullptr, nullptr, nullptr, w.r, rows);
+    }
     lay(a, 0, 0, 1);
     SD_LAUNCH(prof, 0, sd::launch_graph_linear(a, false, s));
 
@@ -680,14 +689,14 @@ int sd_p_sample_update(const sd_plan* p, const float* x0_raw, const float* x_t, 
 
 // Row chains.  Rows never interact inside the Denoiser or the posterior update, so the T-step
 // chain of rows [r0, r1) is independent of every other row range: record_loop splits the batch
-// into `chains` row ranges (multiples of 32 rows and of cond_repeat) and records each range's
+// into `chains` row ranges (multiples of 32 rows) and records each range's
 // T steps on its own stream, forked from and joined back into the caller's stream.  Kernels of
 // different chains then run concurrently, so one chain's idle CUs (a 200-workgroup graph linear
 // on 256 CUs, the last wave of a 800-workgroup attention launch) take the other chain's
 // workgroups instead of waiting for the next kernel boundary.
 static int g_chains = [] {
     const char* e = getenv("SKELDIFF_CHAINS");
-    return e ? atoi(e) : 2;
+    return e ? atoi(e) : 3;  // 3 chains + the caller's stream fit HIP's default 4 hardware queues
 }();
 
 static WS shift_ws(const sd_plan* p, const WS& w, int64_t r0) {
@@ -707,8 +716,7 @@ static WS shift_ws(const sd_plan* p, const WS& w, int64_t r0) {
 
 // number of row chains for `rows` rows and the first row of chain i (i = 0 .. n)
 static int chain_count(const sd_plan* p, int64_t rows, int64_t cond_repeat, int64_t* unit) {
-    int64_t g = 32;
-    if (p->C > 0) g = g / std::gcd(g, cond_repeat) * cond_repeat;  // lcm(32, cond_repeat)
+    const int64_t g = 32;  // a chain starts on a row block; x_cond rows via x1_row0
     *unit = g;
     const int64_t units = rows / g;
     int n = std::max(1, std::min(g_chains, (int)sd_plan::kMaxChains));
@@ -765,7 +773,10 @@ static int record_loop(const sd_plan* p, const float* x_T, const float* x_cond, 
             Chain& c = ch[i];
             const int64_t r0 = c.r0;
             const float* xc = (p->C > 0) ? x_cond + (r0 / cond_repeat) * p->J * p->C : x_cond;
-            int rc = run_denoiser(p, c.cur, xc, cond_repeat, t, c.w.x0, c.n, c.w, cs[i]);
+            // concurrent chains: 32 x 64 tiles (more, smaller workgroups to interleave) measured
+            // 5 % faster than the single-chain 32 x 96 choice at B = 3200, 3 chains
+            int rc = run_denoiser(p, c.cur, xc, cond_repeat, t, c.w.x0, c.n, c.w, cs[i], nullptr, r0 % cond_repeat,
+                                  nch > 1 ? 812 : 0);
             if (rc) return rc;
             float* nxt = (t == 0) ? out + r0 * JD : (((T - 1 - t) & 1) ? c.w.img1 : c.w.img0);
             const float* eps = (!dev_noise && t > 0) ? eps_all + r0 * step_rs + k * JD : nullptr;
@@ -829,6 +840,8 @@ int sd_sample_loop(const sd_plan* p, const float* x_T, const float* x_cond, int6
     }
     if (!(flags & SD_FLAG_GRAPH)) {
         if ((rc = fork_chains(mp, s, nch, cs))) return rc;
+        if (getenv("SKELDIFF_CHAIN_SERIAL"))  // diagnostic: same row split, one stream
+            for (int i = 1; i < nch; ++i) cs[i] = s;
         rc = record_loop(p, x_T, x_cond, cond_repeat, eps_all, seed, row0, out, means_out, noise_out, timages_out,
                          start_out, rows, w, flags, false, cs, nch, unit, -1);
         if (rc) return rc;

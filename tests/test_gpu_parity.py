@@ -247,8 +247,10 @@ def test_row_chains_bitwise_invariant(graph, cuda):
     d = build_release_diffusion(z, cuda)
     J, T = 16, 10
     g = torch.Generator().manual_seed(3)
-    xc = (torch.rand((24, J, 96), generator=g) * 2 - 1).to(cuda)  # 24 sequences x 4 futures
-    rows = 96                                                        # = 3 chain units of 32 rows
+    # 17 sequences x 6 futures = 102 rows: 3 chain units of 32 rows + a ragged tail; chains start
+    # inside a sequence's futures (row 32 = sequence 5, future 2), exercising the x_cond phase
+    xc = (torch.rand((17, J, 96), generator=g) * 2 - 1).to(cuda)
+    rows = 102
     start = torch.randn((rows, J, 96), generator=g).to(cuda)
     samp = torch.randn((rows, T - 1, J, 96), generator=g).to(cuda)
     L = _lib.lib()
