@@ -77,8 +77,44 @@ if traffic:
         f = traffic["fetch"].get(k, 0.0)
         w = traffic.get("write", {}).get(k, 0.0)
         lines.append(f"| `{k[:60]}` | {f:.0f} | {w:.0f} | {(2 * f + w) * 1024 / 1e6:.1f} |")
+    # the launches bench.py's roofline times (sd_profile_step: one denoise step at the full batch,
+    # one stream): graph-linear dispatches whose grid covers all rows_b rows.  With row chains the
+    # timed sampler's launches cover a third of the rows each and are summarised separately.
+    full = defaultdict(lambda: [0.0, 0.0, 0])  # kernel -> [fetch sum, write sum, n]
+    for kind, col in (("fetch", 0), ("write", 1)):
+        path = os.path.join(src, f"pmc_{kind}", "run_counter_collection.csv")
+        if not os.path.exists(path):
+            continue
+        for r in csv.DictReader(open(path)):
+            n = r["Kernel_Name"]
+            if "k_gl4" not in n:
+                continue
+            targs = [t.strip() for t in n.split("<")[1].split(">")[0].split(",")]
+            nw, rt, mode = int(targs[1]), int(targs[2]), int(targs[6])
+            wgs = int(r["Grid_Size"]) // (nw * 64)
+            ntile_r = (rows_b + 32 * rt - 1) // (32 * rt)
+            if wgs < ntile_r or wgs % ntile_r:
+                continue  # a row-chain launch
+            full[short(n)][col] += float(r["Counter_Value"])
+            if col == 0:
+                full[short(n)][2] += 1
     gl = [k for k in traffic.get("fetch", {}) if "k_gl" in k or "k_graph_linear" in k]
-    if gl:
+    if full:
+        tot_n = sum(v[2] for v in full.values())
+        avg = sum((2 * v[0] + v[1]) * 1024 for v in full.values()) / max(tot_n, 1)
+        lines += ["", "## full-batch graph-linear launches (the launches bench.py's roofline times)", "",
+                  "| kernel | launches | HBM MB per launch (2*FETCH + WRITE) |", "|---|---|---|"]
+        for k, v in full.items():
+            lines.append(f"| `{k[:60]}` | {v[2]} | {(2 * v[0] + v[1]) * 1024 / max(v[2], 1) / 1e6:.1f} |")
+        out = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "profiles", "pmc_traffic.json")
+        data = json.load(open(out)) if os.path.exists(out) else {}
+        data["amass16"] = {"graph_linear_bytes_per_launch": avg, "source": tag,
+                           "note": "2*FETCH_SIZE + WRITE_SIZE per launch, averaged over the full-batch "
+                                   "graph-linear launches of sd_profile_step (the launches the roofline times)"}
+        json.dump(data, open(out, "w"), indent=1)
+        lines += ["", f"full-batch graph-linear average HBM bytes per launch: {avg/1e6:.1f} MB "
+                      "(written to profiles/pmc_traffic.json)"]
+    elif gl:
         calls = {short(s["Name"]): int(s["Calls"]) for s in stats}
         tot_calls = sum(calls.get(k, 0) for k in gl)
         avg = sum((2 * traffic["fetch"][k] + traffic.get("write", {}).get(k, 0.0)) * 1024 * calls.get(k, 0)
