@@ -62,6 +62,11 @@ CONFIGS = {
                        workload="Human3.6M J=16, T=1000, 50 futures, 1 sequence, hipGraph (config 4)"),
     "freeman17": dict(skel="freeman17", T=100, batch=64, futures=50,
                       workload="FreeMan J=17, T=100, 50 futures, batch=64, fp32 (config 5 shape)"),
+    # config 5 as BASELINE.json states it: 11,015 test sequences x 50 futures over 8 GPUs (1,377 per
+    # GPU), T=10 (release), reduced precision (here: the half mode, one f16 product per MAC)
+    "freeman17_half": dict(skel="freeman17", T=10, batch=1377, futures=50, precision="half",
+                           workload="FreeMan J=17, T=10, 50 futures, 1,377 sequences per GPU, half precision "
+                                    "(config 5)"),
 }
 
 RELEASE_ARCH = dict(use_attention=True, self_condition=False, norm_type="none", depth=4, attn_dim_head=32,
@@ -202,6 +207,7 @@ def main():
     d, x_cond, rows = build_config(args.config, dev, T=args.T, batch=batch, futures=futures, seq0=seq0)
     J, D, T = d.channels, d.seq_length, d.num_timesteps
     eng = d.engine
+    eng.set_precision(c.get("precision", "f32"))
     eng.plan()
     graph = not args.no_graph
     stream = torch.cuda.Stream(dev)
@@ -238,10 +244,11 @@ def main():
     L = _lib.lib()
     variant = L.sd_set_kernel_variant(-1, -1)
     split = variant in (0, 4) and J in (16, 17, 21)
+    half = split and eng.precision == "half"
     fused_attn = ms[1] == 0.0 and cnt[1] == 0   # attention ran inside the graph-linear launches
     gl_flops = fl[0] + (fl[1] if fused_attn else 0.0)
     gl_tflops = gl_flops / (ms[0] * 1e-3) / 1e12
-    peak = F16_MFMA_PEAK_TFLOPS / 3.0 if split else FP32_PEAK_TFLOPS
+    peak = F16_MFMA_PEAK_TFLOPS if half else F16_MFMA_PEAK_TFLOPS / 3.0 if split else FP32_PEAK_TFLOPS
     gl_bytes = graph_linear_bytes(d, rows, fused_attn)
     gl_gbs = gl_bytes / (ms[0] * 1e-3) / 1e9
     upd_bytes = 3.0 * rows * J * D * 4        # x0, x_t in, x_{t-1} out (device Philox noise)
@@ -258,8 +265,10 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "f32",
-        "arithmetic": ("f32-accurate: 3 x f16 split products on v_mfma_f32_32x32x16_f16, f32 accumulate "
+        "dtype": "f16" if half else "f32",
+        "arithmetic": ("half: one f16 product per multiply-add on v_mfma_f32_32x32x16_f16, f32 accumulate, f32 "
+                       "activations in HBM (latent ADE/APD within 1 % of the f32 mode, tests/test_precision.py)")
+        if half else ("f32-accurate: 3 x f16 split products on v_mfma_f32_32x32x16_f16, f32 accumulate "
                        "(end-to-end error within the f32-vs-f64 drift, tools/sim_split_f16.py); "
                        "exact-f32 kernels via SKELDIFF_GL_VARIANT=3") if split else "exact f32 (f32 MFMA)",
         "data": "synthetic (deterministic synthetic weights of the release Denoiser; U(-1,1) conditioning "
@@ -274,7 +283,8 @@ def main():
                        "to_qkv launches fused with attention)") if split else
                       "k_gl3/k_gl2 graph-linear (exact f32 MFMA, fused epilogue)",
             "achieved": gl_tflops, "peak": peak, "unit": "TFLOP/s", "frac": gl_tflops / peak,
-            "peak_basis": "f16 dense MFMA 2500 TFLOP/s / 3 products per f32 product" if split else
+            "peak_basis": "f16 dense MFMA 2500 TFLOP/s (one product per multiply-add)" if half else
+                          "f16 dense MFMA 2500 TFLOP/s / 3 products per f32 product" if split else
                           "f32 dense 157.3 TFLOP/s",
             "traffic": None,
             "flops_per_launch": gl_flops / max(cnt[0], 1), "launches_per_denoise_step": cnt[0],

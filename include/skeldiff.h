@@ -208,6 +208,13 @@ int sd_set_kernel_variant(int32_t gl_variant, int32_t gl4_tile);
  * results do not depend on n.  Returns the previous n; n = -1 only queries; SD_E_INVALID
  * outside [1, 8]. */
 int sd_set_row_chains(int32_t n);
+/* Arithmetic of the plan's graph-linear launches.  mode 0 (default):
+ * f32-accurate -- 3 split f16 products per f32 product, within the f32-vs-f64 drift.  mode 1:
+ * half -- one f16 product (x and W rounded to f16), f32 accumulate, f32 activations in HBM; the
+ * latent ADE / APD stay within 1 % of mode 0 (tests/test_precision.py).  Applies to the split-f16
+ * (v4) kernels (J in 16, 17, 21); plans on the exact-f32 kernels stay exact.  Affects launches
+ * recorded after the call; SD_E_INVALID for another mode. */
+int sd_plan_set_precision(sd_plan* plan, int32_t mode);
 
 #ifdef __cplusplus
 }

@@ -251,7 +251,10 @@ __device__ __forceinline__ void attention_epilogue(const GLArgs& p, floatx16 (&a
 //   are head h's q, k and v columns (tiles h, heads + h, 2 heads + h), and the epilogue runs
 //   softmax(q k^T * dh^-1/2) v per row over the J nodes instead of storing q/k/v; out = the
 //   (B, J, heads * 32) attention output that to_out reads.  qkv never reaches HBM.
-template <int J, int NW, int RT, int CT, bool RMS, int DBG = 0, int MODE = 0, int XP = 0>
+// PREC 1 ("half" precision mode): one product x_hi W'_hi per k step, so
+//   only the hi halves of the weight fragments are streamed (half the weight bytes, a third of
+//   the MFMAs); f32 accumulate, f32 activations in HBM, same epilogue.
+template <int J, int NW, int RT, int CT, bool RMS, int DBG = 0, int MODE = 0, int XP = 0, int PREC = 0>
 __global__ __launch_bounds__(NW * 64, 1) void k_gl4(const GLArgs p) {
     static_assert(MODE == 0 || (CT == 3 && RT == 1 && J <= 16 && NW == 8), "attention mode: 32 x (q|k|v)");
     constexpr int NPW = (J + NW - 1) / NW;  // nodes per wave
@@ -266,7 +269,8 @@ __global__ __launch_bounds__(NW * 64, 1) void k_gl4(const GLArgs p) {
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int l32 = lane & 31, h = lane >> 5, lr = lane & 15, lg = lane >> 4;
-    const int stage_h = p.ntypes * CT * 1024;  // halves per weight stage
+    constexpr int TILE_H = PREC ? 512 : 1024;   // halves of one 32-column tile per k chunk (hi | hi+lo)
+    const int stage_h = p.ntypes * CT * TILE_H;  // halves per weight stage
     const int wfl = stage_h;                   // two stages of halves = stage_h floats
     const int yfl = MODE == 1 ? J * (8 * COLS + 16) + 8 * 16 * 100 : J * YS;  // Y slab (+ Z rows)
     _Float16* sW0 = reinterpret_cast<_Float16*>(smem);
@@ -304,7 +308,7 @@ __global__ __launch_bounds__(NW * 64, 1) void k_gl4(const GLArgs p) {
 #pragma unroll
     for (int m = 0; m < NPW; ++m) {
         jn[m] = min(wave + NW * m, J - 1);
-        toff[m] = p.ntype[jn[m]] * (CT * 1024);
+        toff[m] = p.ntype[jn[m]] * (CT * TILE_H);
     }
 
     floatx16 acc[NPW][RT][CT];
@@ -352,14 +356,15 @@ __global__ __launch_bounds__(NW * 64, 1) void k_gl4(const GLArgs p) {
     // LDS-DMA of chunk c's weight slice for this workgroup's columns: per type one contiguous
     // span of CT * 2 KiB starting at tile (c0 / 32)
     auto fill_w = [&](int c, _Float16* dst) {
-        const int per_type = CT * 128;  // 16-B pieces
+        constexpr int PPT = TILE_H / 8;     // 16-B pieces per tile (hi | hi+lo)
+        const int per_type = CT * PPT;
         const int npieces = p.ntypes * per_type;
         for (int q0 = wave * 64; q0 < npieces; q0 += NTH) {
             const int q = min(q0 + lane, npieces - 1);
             const int t = q / per_type, rem = q - t * per_type;
-            const int ct = rem >> 7;  // 32-column tile of this piece
+            const int ct = rem / PPT;  // 32-column tile of this piece
             const int tile = MODE == 1 ? ctile + ct * p.attn_heads : (c0 >> 5) + ct;
-            const _Float16* src = p.wsp + (((int64_t)t * nchunk + c) * p.wsp_nct + tile) * 1024 + (rem & 127) * 8;
+            const _Float16* src = p.wsp + (((int64_t)t * nchunk + c) * p.wsp_nct + tile) * 1024 + (rem % PPT) * 8;
             __builtin_amdgcn_global_load_lds((const void*)src, (lds_void*)(dst + (size_t)q0 * 8), 16, 0, 0);
         }
     };
@@ -380,18 +385,20 @@ __global__ __launch_bounds__(NW * 64, 1) void k_gl4(const GLArgs p) {
                     ss[m][rt] += ((q[0] + q[1]) + (q[2] + q[3])) + ((q[4] + q[5]) + (q[6] + q[7]));
                 }
                 xh[rt] = __builtin_convertvector(f, halfx8);
-                xl[rt] = __builtin_convertvector(f - __builtin_convertvector(xh[rt], floatx8), halfx8);
+                if constexpr (!PREC) xl[rt] = __builtin_convertvector(f - __builtin_convertvector(xh[rt], floatx8), halfx8);
             }
 #pragma unroll
             for (int ct = 0; ct < CT; ++ct) {
-                const halfx8 wh = *reinterpret_cast<const halfx8*>(wt + ct * 1024);
-                const halfx8 wl = *reinterpret_cast<const halfx8*>(wt + ct * 1024 + 512);
+                const halfx8 wh = *reinterpret_cast<const halfx8*>(wt + ct * TILE_H);
 #pragma unroll
                 for (int rt = 0; rt < RT; ++rt) {
                     floatx16 a = acc[m][rt][ct];
                     a = __builtin_amdgcn_mfma_f32_32x32x16_f16(xh[rt], wh, a, 0, 0, 0);
-                    a = __builtin_amdgcn_mfma_f32_32x32x16_f16(xh[rt], wl, a, 0, 0, 0);
-                    a = __builtin_amdgcn_mfma_f32_32x32x16_f16(xl[rt], wh, a, 0, 0, 0);
+                    if constexpr (!PREC) {
+                        const halfx8 wl = *reinterpret_cast<const halfx8*>(wt + ct * TILE_H + 512);
+                        a = __builtin_amdgcn_mfma_f32_32x32x16_f16(xh[rt], wl, a, 0, 0, 0);
+                        a = __builtin_amdgcn_mfma_f32_32x32x16_f16(xl[rt], wh, a, 0, 0, 0);
+                    }
                     acc[m][rt][ct] = a;
                 }
             }
@@ -670,13 +677,13 @@ __global__ __launch_bounds__(NW * 64, 1) void k_gl4(const GLArgs p) {
     }
 }
 
-template <int J, int NW, int RT, int CT, int DBG = 0, int MODE = 0, int XP = 0>
+template <int J, int NW, int RT, int CT, int DBG = 0, int MODE = 0, int XP = 0, int PREC = 0>
 static hipError_t gl4_launch(const GLArgs& a, bool rms, hipStream_t s) {
     constexpr int COLS = 32 * CT;
     const int ntile_c = MODE == 1 ? a.attn_heads : (a.N + COLS - 1) / COLS;
     const int64_t ntile_r = (a.B + 32 * RT - 1) / (32 * RT);
     const dim3 grid((unsigned)(ntile_c * ntile_r));
-    const size_t wfl = (size_t)a.ntypes * CT * 1024;  // two stages of halves, in floats
+    const size_t wfl = (size_t)a.ntypes * CT * (PREC ? 512 : 1024);  // two stages of halves, in floats
     const size_t yfl = MODE == 1 ? (size_t)J * (8 * COLS + 16) + 8 * 16 * 100 : (size_t)J * (16 * (COLS + 4) + 16);
     size_t lds = ((wfl > yfl ? wfl : yfl) + (size_t)J * J + 2 * COLS) * sizeof(float);
     if (lds > 160 * 1024) return hipErrorNotSupported;
@@ -691,7 +698,7 @@ static hipError_t gl4_launch(const GLArgs& a, bool rms, hipStream_t s) {
     // (DESIGN.md §4c).  SKELDIFF_FULL_LDS (bit MODE) overrides for experiments.
     static const int full_lds = getenv("SKELDIFF_FULL_LDS") ? atoi(getenv("SKELDIFF_FULL_LDS")) : 3;
     if (full_lds & (1 << MODE)) lds = 160 * 1024;
-    auto kt = rms ? k_gl4<J, NW, RT, CT, true, DBG, MODE, XP> : k_gl4<J, NW, RT, CT, false, DBG, MODE, XP>;
+    auto kt = rms ? k_gl4<J, NW, RT, CT, true, DBG, MODE, XP, PREC> : k_gl4<J, NW, RT, CT, false, DBG, MODE, XP, PREC>;
     if (lds > 64 * 1024) {
         hipError_t e = hipFuncSetAttribute((const void*)kt, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         if (e != hipSuccess) return e;
@@ -720,6 +727,16 @@ hipError_t launch_graph_linear_v4(const GLArgs& a, bool rms, hipStream_t s) {
         return hipErrorNotSupported;
     if (!a.wsp || (a.K1 + a.K2) % 32 || a.K1 % 16 || (a.x1_blk && a.x1_div != 1)) return hipErrorNotSupported;
     const int cfg = gl4_cfg() ? gl4_cfg() : a.tile_hint;
+    if (a.prec == 1) {  // half precision mode: the default tiles only
+        switch (a.J) {
+            case 16:
+                if (cfg == 812) return gl4_launch<16, 8, 1, 2, 0, 0, 0, 1>(a, rms, s);
+                return gl4_launch<16, 8, 1, 3, 0, 0, 0, 1>(a, rms, s);
+            case 17: return gl4_launch<17, 8, 2, 1, 0, 0, 0, 1>(a, rms, s);
+            case 21: return gl4_launch<21, 8, 1, 2, 0, 0, 0, 1>(a, rms, s);
+            default: return hipErrorNotSupported;
+        }
+    }
     switch (a.J) {
         case 16:
             if (cfg == 422) return gl4_launch<16, 4, 2, 2>(a, rms, s);
@@ -736,7 +753,9 @@ hipError_t launch_graph_linear_v4(const GLArgs& a, bool rms, hipStream_t s) {
             // 150, leaving 40 % of the CUs idle); measured 1.28x faster on those layers
             return gl4_launch<16, 8, 1, 3>(a, rms, s);
         // J > 16 needs two 16-node blocks in the mixing epilogue: 96 columns spill there
-        case 17: return gl4_launch<17, 8, 2, 1>(a, rms, s);
+        case 17:
+            if (cfg == 812) return gl4_launch<17, 8, 1, 2>(a, rms, s);
+            return gl4_launch<17, 8, 2, 1>(a, rms, s);
         case 21: return gl4_launch<21, 8, 1, 2>(a, rms, s);
         default: return hipErrorNotSupported;
     }
@@ -753,7 +772,7 @@ hipError_t launch_qkv_attention_v4(const GLArgs& a, bool rms, hipStream_t s) {
     GLArgs b = a;
     b.attn_order = gl4_cfg() == 100 ? 1 : 0;
     switch (a.J) {
-        case 16: return gl4_launch<16, 8, 1, 3, 0, 1>(b, rms, s);
+        case 16: return a.prec == 1 ? gl4_launch<16, 8, 1, 3, 0, 1, 0, 1>(b, rms, s) : gl4_launch<16, 8, 1, 3, 0, 1>(b, rms, s);
         default: return hipErrorNotSupported;
     }
 }

@@ -34,6 +34,7 @@ struct GLArgs {
     int ntype[kMaxNodes];                                 // type(j)
     // v4 only: W pre-split into f16 hi/lo B fragments (make_split_weights); null -> v4 unusable
     const _Float16* wsp; int wsp_nct; float wsp_unscale;
+    int prec;  // v4 products: 0 f32-accurate (3 split f16 products), 1 half (x_hi W'_hi only)
     // fused to_qkv + Attention (launch_qkv_attention_v4): heads of 32 dims, q scale dh^-1/2
     int attn_heads; float attn_scale; int attn_order;
     // v4 only: operand / result layouts, 0 = row-major (B, J, F), 1 = row-blocked (blk_off in

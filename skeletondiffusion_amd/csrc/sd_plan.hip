@@ -56,6 +56,7 @@ struct GraphKey {
     int64_t cond_repeat;
     int32_t flags;
     int32_t chains;
+    int32_t prec;
     void* stream;
     bool operator<(const GraphKey& o) const { return std::memcmp(this, &o, sizeof(GraphKey)) < 0; }
 };
@@ -71,6 +72,7 @@ struct sd_plan {
     bool finalized = false;
     bool fuse_ok = false;  // to_qkv + attention fusable (v4 split weights, J <= 16, dim_head 32)
     bool blk_ok = false;   // every layer on v4 with row-blocked intermediate activations
+    int prec = 0;          // sd_plan_set_precision: 0 f32-accurate, 1 half (f16 products)
     bool fuse_attention_now() const {
         static const bool no_fuse = getenv("SKELDIFF_NO_FUSE") != nullptr;  // diagnostic
         const int v = sd::graph_linear_variant();
@@ -229,6 +231,7 @@ sd::GLArgs gl_args(const sd_plan* p, const GL& g, const float* x1, int x1_div, c
     a.wsp = g.split.w;
     a.wsp_nct = g.split.nct;
     a.wsp_unscale = g.split.unscale;
+    a.prec = p->prec;
     return a;
 }
 
@@ -860,6 +863,7 @@ int sd_sample_loop(const sd_plan* p, const float* x_T, const float* x_cond, int6
     key.cond_repeat = cond_repeat;
     key.flags = flags;
     key.chains = nch;
+    key.prec = p->prec;
     key.stream = stream;
     SD_HIP(sd::launch_set_rng(w.rng, seed, row0, s));
     std::vector<hipGraphExec_t> execs;
@@ -970,6 +974,13 @@ int sd_set_kernel_variant(int32_t gl_variant, int32_t gl4_tile) {
     if (old < 0) return fail(SD_E_INVALID, "gl_variant out of range");
     if (gl4_tile >= 0) (void)sd::set_gl4_tile(gl4_tile);
     return old;
+}
+
+int sd_plan_set_precision(sd_plan* p, int32_t mode) {
+    if (!p) return fail(SD_E_INVALID, "null plan");
+    if (mode != 0 && mode != 1) return fail(SD_E_INVALID, "precision mode must be 0 (f32) or 1 (half)");
+    p->prec = mode;
+    return SD_OK;
 }
 
 int sd_set_row_chains(int32_t n) {

@@ -30,6 +30,7 @@ class SamplingEngine:
         self._device = None
         self._ws = {}
         self._graph = False
+        self._precision = 0
 
     # ---------------------------------------------------------------------------------------
     def __del__(self):
@@ -92,6 +93,22 @@ class SamplingEngine:
         d.sinusoidal_theta = float(m.sinusoidal_pos_emb_theta)
         return d
 
+    PRECISIONS = {"f32": 0, "half": 1}
+
+    def set_precision(self, precision: str) -> None:
+        """Arithmetic of the graph-linear launches: "f32" (default; f32-accurate split-f16
+        products) or "half" (one f16 product per multiply-add, f32 accumulate; SURVEY.md §8d
+        config 5).  See sd_plan_set_precision."""
+        if precision not in self.PRECISIONS:
+            raise SkelDiffError(f"precision must be one of {sorted(self.PRECISIONS)}, got {precision!r}")
+        self._precision = self.PRECISIONS[precision]
+        if self._plan is not None:
+            check(_lib.lib().sd_plan_set_precision(self._plan, self._precision))
+
+    @property
+    def precision(self) -> str:
+        return {v: k for k, v in self.PRECISIONS.items()}[self._precision]
+
     def plan(self):
         dev = self._device_of_module()
         key = (dev, self._fingerprint())
@@ -118,6 +135,7 @@ class SamplingEngine:
                     keep.append(t)
                     check(L.sd_plan_set_tensor(handle, name.encode(), ptr(t), t.numel(), stream))
                 check(L.sd_plan_finalize(handle, stream))
+                check(L.sd_plan_set_precision(handle, self._precision))
             except Exception:
                 L.sd_plan_destroy(handle)
                 raise
