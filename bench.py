@@ -184,6 +184,8 @@ def main():
     ap.add_argument("--batch", type=int, default=None, help="sequences per GPU")
     ap.add_argument("--futures", type=int, default=None)
     ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--precision", choices=["f32", "half"], default=None,
+                    help="graph-linear arithmetic (default: the config's; f32 for the BASELINE metric)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-steps", type=int, default=4)
     ap.add_argument("--cpu-threads", type=int, default=min(16, os.cpu_count() or 1))
@@ -207,7 +209,7 @@ def main():
     d, x_cond, rows = build_config(args.config, dev, T=args.T, batch=batch, futures=futures, seq0=seq0)
     J, D, T = d.channels, d.seq_length, d.num_timesteps
     eng = d.engine
-    eng.set_precision(c.get("precision", "f32"))
+    eng.set_precision(args.precision or c.get("precision", "f32"))
     eng.plan()
     graph = not args.no_graph
     stream = torch.cuda.Stream(dev)
