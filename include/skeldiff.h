@@ -169,6 +169,16 @@ int sd_pairwise_distances(const float* x, int64_t nseq, int32_t samples, int64_t
                           float* l2_mean, void* stream);
 int sd_ade_fde(const float* pred, const float* target, int64_t nseq, int32_t samples, int32_t frames,
                int64_t features, float* ade, float* fde, float* per_sample_ade, float* per_sample_fde, void* stream);
+/* Multimodal ADE / FDE (src/metrics/multimodal.py:108-135): sequence i has the ground truths
+ * gts[seq_offsets[i] .. seq_offsets[i+1]) (each (frames, features); pair_seq[p] = the sequence
+ * of ground truth p, npairs = seq_offsets[nseq]); per pair the min over samples of the ADE /
+ * FDE against that ground truth (pair_ade / pair_fde, npairs each), then per sequence their
+ * mean (mmade / mmfde, nseq; NaN for a sequence without ground truths, as the reference's
+ * mean of an empty tensor).  pred (nseq, samples, frames, features).  seq_offsets and
+ * pair_seq are device int64 arrays. */
+int sd_mm_ade_fde(const float* pred, const float* gts, const int64_t* pair_seq, int64_t npairs,
+                  const int64_t* seq_offsets, int64_t nseq, int32_t samples, int32_t frames, int64_t features,
+                  float* pair_ade, float* pair_fde, float* mmade, float* mmfde, void* stream);
 
 /* Test hooks: one kernel on caller buffers, for the per-kernel numerics tests.
  * sd_test_graph_linear: out(B,J,N) = act(FiLM(ghat @ (s_j W[type j] [x1_j | x2_j] + bias[type j]))) + res,

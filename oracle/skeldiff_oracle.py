@@ -569,4 +569,18 @@ def metric_ade(target, pred, t0=0, t=-1, reduction="mean", last_only=False):
     return (dist.min(-1).values if reduction == "mean" else dist).float()
 
 
-__all__ += ["metric_lat_apd", "metric_apd", "metric_ade"]
+def metric_mmade(pred, mm_gt, t0=0, t=-1, last_only=False):
+    """multimodal.py:108-120 (mmade) and :122-135 (mmfde, last_only): per sequence the mean over
+    its ground truths of the min over samples of the ADE (FDE); NaN without ground truths."""
+    pred = _time_slice(pred, t0, t, 2)
+    B, S, T = pred.shape[:3]
+    out = torch.zeros(B)
+    for i in range(B):
+        g = _time_slice(mm_gt[i], t0, t, 1).reshape(mm_gt[i].shape[0], 1, T, -1).double()
+        dist = (pred[i].reshape(1, S, T, -1).double() - g).pow(2).sum(-1).sqrt()
+        dist = dist[..., -1] if last_only else dist.mean(-1)
+        out[i] = dist.min(-1).values.mean() if g.shape[0] else float("nan")
+    return out
+
+
+__all__ += ["metric_lat_apd", "metric_apd", "metric_ade", "metric_mmade"]

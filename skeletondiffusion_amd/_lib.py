@@ -26,7 +26,7 @@ EXPORTED = (
     "sd_noise_fill", "sd_philox_raw", "sd_plan_kernels_per_step", "sd_plan_step_flops", "sd_profile_step",
     "sd_test_graph_linear", "sd_test_attention", "sd_set_kernel_variant", "sd_test_qkv_attention",
     "sd_test_graph_linear_layout", "sd_pairwise_distances", "sd_ade_fde", "sd_set_row_chains",
-    "sd_plan_set_precision",
+    "sd_plan_set_precision", "sd_mm_ade_fde",
 )
 
 
@@ -85,6 +85,7 @@ def _declare(lib: ctypes.CDLL) -> None:
         "sd_set_kernel_variant": (ctypes.c_int, [i32, i32]),
         "sd_set_row_chains": (ctypes.c_int, [i32]),
         "sd_plan_set_precision": (ctypes.c_int, [vp, i32]),
+        "sd_mm_ade_fde": (ctypes.c_int, [vp, vp, vp, i64, vp, i64, i32, i32, i64, vp, vp, vp, vp, vp]),
         "sd_pairwise_distances": (ctypes.c_int, [vp, i64, i32, i64, vp, vp, vp]),
         "sd_ade_fde": (ctypes.c_int, [vp, vp, i64, i32, i32, i64, vp, vp, vp, vp, vp]),
         "sd_test_qkv_attention": (ctypes.c_int, [vp, i32, vp, ctypes.POINTER(ctypes.c_int64), vp, vp, i64, i32, i32,

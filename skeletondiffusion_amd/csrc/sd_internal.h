@@ -95,6 +95,9 @@ hipError_t launch_pairwise(const float* x, int64_t nseq, int S, int64_t X, float
                            hipStream_t s);
 hipError_t launch_ade_fde(const float* pred, const float* target, int64_t nseq, int S, int T, int64_t F, float* ade,
                           float* fde, float* per_sample_ade, float* per_sample_fde, hipStream_t s);
+hipError_t launch_mm_ade_fde(const float* pred, const float* gts, const int64_t* pair_seq, int64_t npairs,
+                             const int64_t* seq_off, int64_t nseq, int S, int T, int64_t F, float* pair_ade,
+                             float* pair_fde, float* mmade, float* mmfde, hipStream_t s);
 
 // plan-finalize helpers (one-time)
 hipError_t launch_sinusoidal(float* emb, int T, int dim, float neg_scale, hipStream_t s);

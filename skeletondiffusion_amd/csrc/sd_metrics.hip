@@ -4,7 +4,10 @@
 //   pairwise: mean over the sample pairs i < j of the L1 (lat_apd, multimodal.py:137-151) and
 //             L2 (apd, multimodal.py:15-35) distances between the flattened samples;
 //   ade / fde: per sample the mean over frames (ade, multimodal.py:44-57) or the last frame
-//             (fde, :60-73) of the L2 distance to the target, then the minimum over samples.
+//             (fde, :60-73) of the L2 distance to the target, then the minimum over samples;
+//   mmade / mmfde: the same minimum against each of a sequence's multimodal ground truths,
+//             averaged over them (multimodal.py:108-135): one workgroup per (sequence, gt) pair,
+//             then a fixed-order mean per sequence.
 // Samples are (S, X) rows of one sequence, X = T_frames * F (flattened frame-major, as
 // `pred.reshape(batch, n_samples, seq_length, -1)`).
 #include <hip/hip_runtime.h>
@@ -94,13 +97,16 @@ __global__ __launch_bounds__(256) void k_pairwise(const float* __restrict__ x, i
 
 // pred (S, T, F) per sequence, target (T, F): per sample mean_t ||pred - target|| (ade) and the
 // last frame's distance (fde), minimum over samples
+// pair_seq (nullable): workgroup b compares target b with pred sequence pair_seq[b] (mm metrics)
 __global__ __launch_bounds__(256) void k_ade_fde(const float* __restrict__ pred, const float* __restrict__ target,
                                                  int S, int T, int64_t F, float* __restrict__ ade,
                                                  float* __restrict__ fde, float* __restrict__ per_sample_ade,
-                                                 float* __restrict__ per_sample_fde) {
+                                                 float* __restrict__ per_sample_fde,
+                                                 const int64_t* __restrict__ pair_seq) {
     __shared__ float sum_t[kMaxSamples], last_t[kMaxSamples];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const float* ps = pred + (int64_t)blockIdx.x * S * T * F;
+    const int64_t seq = pair_seq ? pair_seq[blockIdx.x] : (int64_t)blockIdx.x;
+    const float* ps = pred + seq * S * T * F;
     const float* tg = target + (int64_t)blockIdx.x * T * F;
     for (int s = wave; s < S; s += 4) {
         float acc_t = 0.f, last = 0.f;
@@ -136,6 +142,18 @@ __global__ __launch_bounds__(256) void k_ade_fde(const float* __restrict__ pred,
     }
 }
 
+// per sequence the mean of its pairs' values in pair order (offsets: nseq + 1); 0 pairs -> NaN
+// (the mean of an empty tensor, as torch)
+__global__ __launch_bounds__(256) void k_segment_mean(const float* __restrict__ v, const int64_t* __restrict__ off,
+                                                      int64_t nseq, float* __restrict__ out) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= nseq) return;
+    const int64_t a = off[i], b = off[i + 1];
+    float acc = 0.f;
+    for (int64_t k = a; k < b; ++k) acc += v[k];
+    out[i] = b > a ? acc / (float)(b - a) : __builtin_nanf("");
+}
+
 }  // namespace
 
 hipError_t launch_pairwise(const float* x, int64_t nseq, int S, int64_t X, float* l1_mean, float* l2_mean,
@@ -151,7 +169,21 @@ hipError_t launch_ade_fde(const float* pred, const float* target, int64_t nseq, 
     if (nseq <= 0) return hipSuccess;
     if (S < 1 || S > kMaxSamples || T < 1 || F <= 0) return hipErrorInvalidValue;
     hipLaunchKernelGGL(k_ade_fde, dim3((unsigned)nseq), dim3(256), 0, s, pred, target, S, T, F, ade, fde,
-                       per_sample_ade, per_sample_fde);
+                       per_sample_ade, per_sample_fde, (const int64_t*)nullptr);
+    return hipGetLastError();
+}
+
+hipError_t launch_mm_ade_fde(const float* pred, const float* gts, const int64_t* pair_seq, int64_t npairs,
+                             const int64_t* seq_off, int64_t nseq, int S, int T, int64_t F, float* pair_ade,
+                             float* pair_fde, float* mmade, float* mmfde, hipStream_t s) {
+    if (nseq <= 0) return hipSuccess;
+    if (S < 1 || S > kMaxSamples || T < 1 || F <= 0 || npairs < 0) return hipErrorInvalidValue;
+    if (npairs > 0)
+        hipLaunchKernelGGL(k_ade_fde, dim3((unsigned)npairs), dim3(256), 0, s, pred, gts, S, T, F, pair_ade, pair_fde,
+                           (float*)nullptr, (float*)nullptr, pair_seq);
+    const dim3 g((unsigned)((nseq + 255) / 256));
+    if (mmade) hipLaunchKernelGGL(k_segment_mean, g, dim3(256), 0, s, pair_ade, seq_off, nseq, mmade);
+    if (mmfde) hipLaunchKernelGGL(k_segment_mean, g, dim3(256), 0, s, pair_fde, seq_off, nseq, mmfde);
     return hipGetLastError();
 }
 

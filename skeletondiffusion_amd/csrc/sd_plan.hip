@@ -968,6 +968,19 @@ int sd_ade_fde(const float* pred, const float* target, int64_t nseq, int32_t sam
     return SD_OK;
 }
 
+int sd_mm_ade_fde(const float* pred, const float* gts, const int64_t* pair_seq, int64_t npairs,
+                  const int64_t* seq_offsets, int64_t nseq, int32_t samples, int32_t frames, int64_t features,
+                  float* pair_ade, float* pair_fde, float* mmade, float* mmfde, void* stream) {
+    if (nseq < 0 || npairs < 0 || samples < 1 || samples > 64 || frames < 1 || features < 1)
+        return fail(SD_E_INVALID, "mmade/mmfde: need 1..64 samples, frames >= 1, features >= 1");
+    if (nseq == 0) return SD_OK;
+    if (!seq_offsets || (npairs > 0 && (!pred || !gts || !pair_seq)) || (mmade && !pair_ade) || (mmfde && !pair_fde))
+        return fail(SD_E_INVALID, "mmade/mmfde: null input (pair outputs are required for the means)");
+    SD_HIP(sd::launch_mm_ade_fde(pred, gts, pair_seq, npairs, seq_offsets, nseq, samples, frames, features, pair_ade,
+                                 pair_fde, mmade, mmfde, (hipStream_t)stream));
+    return SD_OK;
+}
+
 int sd_set_kernel_variant(int32_t gl_variant, int32_t gl4_tile) {
     if (gl_variant == -1) return sd::graph_linear_variant();  // query
     const int old = sd::set_graph_linear_variant(gl_variant);

@@ -92,4 +92,47 @@ def fde(target: torch.Tensor, pred: torch.Tensor, t0: int = 0, t: int = -1, redu
     return _ade_fde(target, pred, t0, t, reduction, False)
 
 
-__all__ = ["lat_apd", "apd", "ade", "fde"]
+def _mm(target, pred, mm_gt, t0, t, want_ade):
+    pred = _time_slice(pred, t0, t, 2)
+    B, S, T = pred.shape[:3]
+    if len(mm_gt) != B:
+        raise ValueError(f"mm_gt has {len(mm_gt)} entries for {B} sequences")
+    p = _device_tensor(pred.reshape(B, S, T, _flat(pred.shape[3:])), "pred")
+    dev, F = p.device, p.shape[3]
+    counts = [int(g.shape[0]) for g in mm_gt]
+    if min(counts, default=1) == 0:  # the reference's reshape of an empty set raises (multimodal.py:113)
+        raise RuntimeError("mmade/mmfde: a sequence has no multimodal ground truths")
+    parts = [_time_slice(_device_tensor(g, "mm_gt"), t0, t, 1).reshape(g.shape[0], T, -1) for g in mm_gt if g.shape[0]]
+    for g in parts:
+        if g.shape[2] != F:
+            raise ValueError(f"mm_gt frames have {g.shape[2]} features, pred frames {F}")
+    gts = torch.cat(parts).contiguous() if parts else torch.empty((0, T, F), device=dev)
+    npairs = gts.shape[0]
+    cnt = torch.tensor(counts, dtype=torch.int64)
+    off = torch.zeros(B + 1, dtype=torch.int64)
+    off[1:] = torch.cumsum(cnt, 0)
+    off = off.to(dev)
+    pair_seq = torch.repeat_interleave(torch.arange(B, dtype=torch.int64), cnt).to(dev)
+    pair = torch.empty(max(npairs, 1), device=dev, dtype=torch.float32)
+    out = torch.empty(B, device=dev, dtype=torch.float32)
+    stream = torch.cuda.current_stream(dev).cuda_stream
+    args = (pair, None, out, None) if want_ade else (None, pair, None, out)
+    check(_lib.lib().sd_mm_ade_fde(p.data_ptr(), gts.data_ptr() if npairs else None, pair_seq.data_ptr() if npairs else None,
+                                   npairs, off.data_ptr(), B, S, T, F, *(_lib.ptr(a) for a in args), stream))
+    return out
+
+
+def mmade(target: torch.Tensor, pred: torch.Tensor, mm_gt, t0: int = 0, t: int = -1, **kwargs) -> torch.Tensor:
+    """Multimodal ADE (multimodal.py:108-120): pred (batch, num_samples, seq_length, ...), mm_gt a
+    sequence of batch tensors (n_gts_i, seq_length, ...): per sequence the mean over its ground
+    truths of the min over samples of the mean-over-frames L2 distance (RuntimeError for a
+    sequence without ground truths, as the reference).  `target` is unused, as in the reference."""
+    return _mm(target, pred, mm_gt, t0, t, True)
+
+
+def mmfde(target: torch.Tensor, pred: torch.Tensor, mm_gt, t0: int = 0, t: int = -1, **kwargs) -> torch.Tensor:
+    """Multimodal FDE (multimodal.py:122-135): as mmade on the last frame of the slice."""
+    return _mm(target, pred, mm_gt, t0, t, False)
+
+
+__all__ = ["lat_apd", "apd", "ade", "fde", "mmade", "mmfde"]

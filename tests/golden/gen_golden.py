@@ -258,7 +258,7 @@ def gen_metrics():
     """The reference's multimodal metrics (src/metrics/multimodal.py) on synthetic samples: latent
     APD (L1) and APD (L2) over 50 futures of (J=16, 96) latents, and ADE / FDE of (frames, J*3)
     motions against a target, incl. the per-sample (reduction != 'mean') form."""
-    from src.metrics.multimodal import ade, apd, fde, lat_apd
+    from src.metrics.multimodal import ade, apd, fde, lat_apd, mmade, mmfde
 
     lat = torch.from_numpy(synthetic.normal((3, 50, 16, 96), seed=31)) * 0.3
     motion = torch.from_numpy(synthetic.normal((2, 7, 20, 16, 3), seed=32))  # (B, S, T, J, 3)
@@ -267,7 +267,27 @@ def gen_metrics():
     _save("metrics", lat_apd=lat_apd(lat), lat_apd_l2=apd(lat.unsqueeze(2)),
           apd=apd(motion), ade=ade(target, motion), fde=fde(target, motion),
           ade_per_sample=ade(target, motion, reduction="none"), fde_per_sample=fde(target, motion, reduction="none"),
-          ade_t5_15=ade(target, motion, t0=5, t=15), apd_t5_15=apd(motion, t0=5, t=15))
+          ade_t5_15=ade(target, motion, t0=5, t=15), apd_t5_15=apd(motion, t0=5, t=15),
+          **gen_mm(motion, target, mmade, mmfde))
+
+
+def mm_inputs():
+    """Multimodal ground truths for the 3 sequences of mm_motion: 3, 1 and 2 of them (ragged)."""
+    motion = torch.from_numpy(synthetic.normal((3, 7, 20, 16, 3), seed=34))
+    gts = torch.from_numpy(synthetic.normal((4, 20, 16, 3), seed=35))
+    target = torch.from_numpy(synthetic.normal((3, 20, 16, 3), seed=36))  # sliced, otherwise unused
+    return motion, [gts[:3], gts[3:4], gts[1:3]], target
+
+
+def gen_mm(motion, target, mmade, mmfde):
+    mm_motion, mm_gt, mm_target = mm_inputs()
+    try:  # a sequence without ground truths: the reference's reshape raises
+        mmade(mm_target, mm_motion, [mm_gt[0], mm_gt[1], mm_gt[2][:0]])
+        empty_raises = False
+    except RuntimeError:
+        empty_raises = True
+    return dict(mmade=mmade(mm_target, mm_motion, mm_gt), mmfde=mmfde(mm_target, mm_motion, mm_gt),
+                mmade_t5_15=mmade(mm_target, mm_motion, mm_gt, t0=5, t=15), mm_empty_raises=empty_raises)
 
 
 def main():

@@ -98,3 +98,49 @@ def test_lat_apd_of_sampled_futures(cuda):
     lat = img.view(2, 50, 16, 96)
     _close(M.lat_apd(lat), O.metric_lat_apd(lat.cpu()).numpy())
     _close(M.apd(lat.unsqueeze(2)), O.metric_apd(lat.unsqueeze(2).cpu()).numpy())
+
+
+def _mm_inputs():
+    """tests/golden/gen_golden.py:mm_inputs (3 sequences, 3 / 1 / 2 multimodal ground truths)."""
+    motion = torch.from_numpy(synthetic.normal((3, 7, 20, 16, 3), seed=34))
+    gts = torch.from_numpy(synthetic.normal((4, 20, 16, 3), seed=35))
+    target = torch.from_numpy(synthetic.normal((3, 20, 16, 3), seed=36))
+    return motion, [gts[:3], gts[3:4], gts[1:3]], target
+
+
+def test_oracle_mm_metrics_match_reference():
+    z = golden("metrics")
+    motion, mm_gt, _ = _mm_inputs()
+    _close(O.metric_mmade(motion, mm_gt), z["mmade"])
+    _close(O.metric_mmade(motion, mm_gt, last_only=True), z["mmfde"])
+    _close(O.metric_mmade(motion, mm_gt, 5, 15), z["mmade_t5_15"])
+    assert bool(z["mm_empty_raises"])  # the reference raises for a sequence without ground truths
+
+
+@pytest.mark.gpu
+def test_device_mm_metrics_match_reference(cuda):
+    from skeletondiffusion_amd import _lib
+    from skeletondiffusion_amd import metrics as M
+
+    z = golden("metrics")
+    motion, mm_gt, target = _mm_inputs()
+    motion, target = motion.to(cuda), target.to(cuda)
+    mm_gt = [g.to(cuda) for g in mm_gt]
+    _close(M.mmade(target, motion, mm_gt), z["mmade"])
+    _close(M.mmfde(target, motion, mm_gt), z["mmfde"])
+    _close(M.mmade(target, motion, mm_gt, t0=5, t=15), z["mmade_t5_15"])
+    with pytest.raises(RuntimeError):
+        M.mmade(target, motion, [mm_gt[0], mm_gt[1], mm_gt[2][:0]])
+    # the C ABI itself: a sequence without ground truths -> NaN; nseq == 0 is a no-op
+    p = motion.reshape(3, 7, 20, 48).contiguous()
+    g = torch.cat([mm_gt[0], mm_gt[1]]).reshape(4, 20, 48).contiguous()
+    off = torch.tensor([0, 3, 4, 4], dtype=torch.int64, device=cuda)
+    seq = torch.tensor([0, 0, 0, 1], dtype=torch.int64, device=cuda)
+    pa, out = torch.empty(4, device=cuda), torch.empty(3, device=cuda)
+    L = _lib.lib()
+    assert L.sd_mm_ade_fde(p.data_ptr(), g.data_ptr(), seq.data_ptr(), 4, off.data_ptr(), 3, 7, 20, 48,
+                           pa.data_ptr(), None, out.data_ptr(), None, 0) == 0
+    torch.cuda.synchronize()
+    _close(out[:2], z["mmade"][:2])
+    assert torch.isnan(out[2])
+    assert L.sd_mm_ade_fde(None, None, None, 0, None, 0, 7, 20, 48, None, None, None, None, 0) == 0
