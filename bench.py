@@ -208,6 +208,9 @@ def main():
     seq0, row0, rows = shard(rank, batch, futures)
     d, x_cond, rows = build_config(args.config, dev, T=args.T, batch=batch, futures=futures, seq0=seq0)
     J, D, T = d.channels, d.seq_length, d.num_timesteps
+    if dist:  # every rank samples with rank 0's parameters (RCCL broadcast over xGMI, untimed setup)
+        from skeletondiffusion_amd.sharded import broadcast_state
+        broadcast_state(d)
     eng = d.engine
     eng.set_precision(args.precision or c.get("precision", "f32"))
     eng.plan()

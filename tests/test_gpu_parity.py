@@ -271,3 +271,18 @@ def test_row_chains_bitwise_invariant(graph, cuda):
         assert L.sd_set_row_chains(0) < 0 and L.sd_set_row_chains(9) < 0
     finally:
         L.sd_set_row_chains(old)
+
+
+def test_sharded_eval_single_rank(cuda):
+    """skeletondiffusion_amd.sharded on one rank: the shard is the whole batch, row0 = 0, and the
+    metric reduction is the plain mean (the world > 1 paths run under gloo in test_distributed)."""
+    from skeletondiffusion_amd import metrics, sharded
+
+    z = golden("release_h36m16_T10")
+    d = build_release_diffusion(z, cuda)
+    xcs = release_inputs(z)[0].to(cuda)
+    out, s0 = sharded.sample_sharded(lambda **kw: d.sample(**kw)[0], xcs, 4, seed=9)
+    ref = d.sample(batch_size=8, x_cond=xcs, seed=9, row0=0)[0]
+    assert s0 == 0 and torch.equal(out, ref)
+    v = metrics.lat_apd(out.view(2, 4, 16, 96))
+    assert abs(sharded.reduce_metric(v, nseq_total=2).item() - v.double().mean().item()) < 1e-6
