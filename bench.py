@@ -194,13 +194,19 @@ def main():
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    # one rank per GPU; the modulo only matters for a rehearsal with more ranks than GPUs
+    local = int(os.environ.get("LOCAL_RANK", "0")) % max(torch.cuda.device_count(), 1)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     dist = None
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=dev)   # RCCL over xGMI
+        # "nccl" = RCCL over xGMI; SKELDIFF_DIST_BACKEND=gloo rehearses the multi-rank path on one GPU
+        backend = os.environ.get("SKELDIFF_DIST_BACKEND", "nccl")
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
 
     c = CONFIGS[args.config]
     batch = args.batch or c["batch"]
