@@ -212,6 +212,28 @@ int sd_test_qkv_attention(const float* x, int32_t K, const float* W, const int64
  * -1 leaves it.  Returns the previous gl_variant, or -1 for an invalid one (nothing changed);
  * gl_variant = -1 only queries (returns the current value). */
 int sd_set_kernel_variant(int32_t gl_variant, int32_t gl4_tile);
+
+/* Graph-GRU latent decoder: AutoEncoder.decode -> Decoder.forward
+ * (src/core/network/nn/decoder.py:60-104) with the StaticGraphGRU cell
+ * (src/core/network/layers/recurrent.py:321-366), recurrent_arch_decoder = StaticGraphGRU, one
+ * layer, clockwork off.  Tensors are the reference's `decoder.*` state_dict entries on the device
+ * (types = num_node_types, or 1 with shared weights when num_node_types == 0):
+ *   init_*  initial_hidden_h: G (J,J), weight (types, H, F+L), bias (types, H) or NULL
+ *   G, G_add, weight_ih (types, 3H, F+L), weight_hh (types, 3H, H), bias_ih, bias_hh (types, 3H)
+ *           rnn.layers.0 (G_add may be NULL: no additive influence)
+ *   fc_*    fc: G (J,J), weight (types, F, H), bias (types, F) or NULL
+ * x (rows, 2, J, F) = the last two observed frames (x[:, -2:]), h (rows, J, L) = the sampled
+ * latents -> out (rows, ph, J, F).  F <= 16, L and H multiples of 16. */
+typedef struct sd_gru_decoder_desc {
+    int32_t num_nodes, feature_size, latent_size, hidden_size, num_node_types;
+    const int64_t* node_types; /* host array[J] (ignored when num_node_types == 0) */
+    const float *init_G, *init_weight, *init_bias;
+    const float *G, *G_add, *weight_ih, *weight_hh, *bias_ih, *bias_hh;
+    const float *fc_G, *fc_weight, *fc_bias;
+} sd_gru_decoder_desc;
+size_t sd_gru_decode_workspace_bytes(const sd_gru_decoder_desc* desc, int64_t rows, int32_t ph);
+int sd_gru_decode(const sd_gru_decoder_desc* desc, const float* x, const float* h, int64_t rows, int32_t ph,
+                  float* out, void* workspace, size_t workspace_bytes, void* stream);
 /* Row chains of sd_sample_loop (process-wide; SKELDIFF_CHAINS, default 3): the batch is split into
  * n row ranges (multiples of 32 rows; fewer when the batch is small) whose
  * T-step chains run on forked streams and overlap on the GPU.  Rows are independent, so the

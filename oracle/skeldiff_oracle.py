@@ -583,4 +583,60 @@ def metric_mmade(pred, mm_gt, t0=0, t=-1, last_only=False):
     return out
 
 
-__all__ += ["metric_lat_apd", "metric_apd", "metric_ade", "metric_mmade"]
+# ---- graph-GRU autoencoder, float64 -------------------------------------
+
+
+def _l1_rows(G: torch.Tensor) -> torch.Tensor:
+    """F.normalize(G, p=1, dim=1)."""
+    return G / G.abs().sum(1, keepdim=True).clamp_min(1e-12)
+
+
+def _sgl(sd, pre, x, types):
+    """StaticGraphLinear with learn_influence (graph_structural.py:30-43): Ghat (W[type] x + b)."""
+    W = sd[pre + "weight"].double()[types]
+    y = torch.einsum("nod,bnd->bno", W, x)
+    if pre + "bias" in sd:
+        y = y + sd[pre + "bias"].double()[types]
+    return _l1_rows(sd[pre + "G"].double()) @ y
+
+
+def _gru_cell(sd, pre, x, hx, gx, types, additive: bool):
+    """recurrent.py:321-366 (clockwork off): one step, returns (hy, next gx)."""
+    H = hx.shape[-1]
+    xr = gx @ (torch.einsum("nod,bnd->bno", sd[pre + "weight_ih"].double()[types], x) + sd[pre + "bias_ih"].double()[types])
+    hr = gx @ (torch.einsum("nod,bnd->bno", sd[pre + "weight_hh"].double()[types], hx) + sd[pre + "bias_hh"].double()[types])
+    r = torch.sigmoid(xr[..., :H] + hr[..., :H])
+    z = torch.sigmoid(xr[..., H:2 * H] + hr[..., H:2 * H])
+    n = torch.tanh(xr[..., 2 * H:] + r * hr[..., 2 * H:])
+    hy = n - n * z + z * hx
+    g = gx + sd[pre + "G_add"].double() if additive else gx
+    return hy, _l1_rows(g)
+
+
+def gru_decode(sd, node_types, x2, h, ph, prefix="decoder."):
+    """AutoEncoder.decode -> Decoder.forward (decoder.py:60-104): x2 (B, 2, J, F) the last two
+    observed frames, h (B, J, L) the latent -> (B, ph, J, F)."""
+    types = torch.as_tensor(node_types, dtype=torch.long)
+    x2, h = x2.double(), h.double()
+    hx = _sgl(sd, prefix + "initial_hidden_h.", torch.cat([x2[:, 0], h], -1), types)
+    rec = torch.cat([x2[:, 1], h], -1)
+    gx = _l1_rows(sd[prefix + "rnn.layers.0.G"].double())
+    out = []
+    for _ in range(ph):
+        hx, gx = _gru_cell(sd, prefix + "rnn.layers.0.", rec, hx, gx, types, additive=True)
+        out.append(torch.tanh(_sgl(sd, prefix + "fc.", hx, types)))
+    return torch.stack(out, 1).float()
+
+
+def gru_encode(sd, node_types, x, prefix="encoder."):
+    """Encoder.forward (encoder.py:75-80) + z_activation tanh (autoencoder.py:47-51): x (B, T, J, F)."""
+    types = torch.as_tensor(node_types, dtype=torch.long)
+    x = x.double()
+    hx = _sgl(sd, prefix + "initial_hidden1.", x[:, 0], types)
+    gx = _l1_rows(sd[prefix + "rnn.layers.0.G"].double())
+    for t in range(x.shape[1]):
+        hx, gx = _gru_cell(sd, prefix + "rnn.layers.0.", x[:, t], hx, gx, types, additive=False)
+    return torch.tanh(torch.tanh(_sgl(sd, prefix + "fc.", hx, types))).float()
+
+
+__all__ += ["metric_lat_apd", "metric_apd", "metric_ade", "metric_mmade", "gru_decode", "gru_encode"]

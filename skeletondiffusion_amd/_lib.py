@@ -26,7 +26,7 @@ EXPORTED = (
     "sd_noise_fill", "sd_philox_raw", "sd_plan_kernels_per_step", "sd_plan_step_flops", "sd_profile_step",
     "sd_test_graph_linear", "sd_test_attention", "sd_set_kernel_variant", "sd_test_qkv_attention",
     "sd_test_graph_linear_layout", "sd_pairwise_distances", "sd_ade_fde", "sd_set_row_chains",
-    "sd_plan_set_precision", "sd_mm_ade_fde",
+    "sd_plan_set_precision", "sd_mm_ade_fde", "sd_gru_decode_workspace_bytes", "sd_gru_decode",
 )
 
 
@@ -49,6 +49,15 @@ class SDPlanDesc(ctypes.Structure):
         ("activation", ctypes.c_int32),
         ("sinusoidal_theta", ctypes.c_float),
     ]
+
+
+class SDGruDecoderDesc(ctypes.Structure):
+    """mirrors struct sd_gru_decoder_desc (include/skeldiff.h)"""
+    _fields_ = [(n, ctypes.c_int32) for n in ("num_nodes", "feature_size", "latent_size", "hidden_size",
+                                              "num_node_types")] + \
+               [("node_types", ctypes.POINTER(ctypes.c_int64))] + \
+               [(n, ctypes.c_void_p) for n in ("init_G", "init_weight", "init_bias", "G", "G_add", "weight_ih",
+                                               "weight_hh", "bias_ih", "bias_hh", "fc_G", "fc_weight", "fc_bias")]
 
 
 class SkelDiffError(RuntimeError):
@@ -86,6 +95,9 @@ def _declare(lib: ctypes.CDLL) -> None:
         "sd_set_row_chains": (ctypes.c_int, [i32]),
         "sd_plan_set_precision": (ctypes.c_int, [vp, i32]),
         "sd_mm_ade_fde": (ctypes.c_int, [vp, vp, vp, i64, vp, i64, i32, i32, i64, vp, vp, vp, vp, vp]),
+        "sd_gru_decode_workspace_bytes": (ctypes.c_size_t, [ctypes.POINTER(SDGruDecoderDesc), i64, i32]),
+        "sd_gru_decode": (ctypes.c_int, [ctypes.POINTER(SDGruDecoderDesc), vp, vp, i64, i32, vp, vp,
+                                         ctypes.c_size_t, vp]),
         "sd_pairwise_distances": (ctypes.c_int, [vp, i64, i32, i64, vp, vp, vp]),
         "sd_ade_fde": (ctypes.c_int, [vp, vp, i64, i32, i32, i64, vp, vp, vp, vp, vp]),
         "sd_test_qkv_attention": (ctypes.c_int, [vp, i32, vp, ctypes.POINTER(ctypes.c_int64), vp, vp, i64, i32, i32,

@@ -2,6 +2,8 @@
 // (sd_kernels.hip).  Not part of the public ABI (see include/skeldiff.h).
 #pragma once
 #include <hip/hip_runtime.h>
+
+#include <string>
 #include <stdint.h>
 
 namespace sd {
@@ -104,6 +106,8 @@ hipError_t launch_sinusoidal(float* emb, int T, int dim, float neg_scale, hipStr
 hipError_t launch_linear(const float* x, int M, int K, const float* W, const float* b, int N,
                          float* y, int in_act, int out_act, hipStream_t s);
 hipError_t launch_ghat(const float* G, float* Ghat, int J, int normalize, hipStream_t s);
+// sets the thread-local message sd_last_error() returns; returns `code` (sd_plan.hip)
+int set_error(int code, const std::string& msg);
 hipError_t launch_fold_gain(const float* W, const float* g, float mult, float* out,
                             int64_t rows, int K, hipStream_t s);
 hipError_t launch_sigma(const float* logvar, float* sig, int64_t n, hipStream_t s);

@@ -26,6 +26,12 @@ int fail(int code, const std::string& msg) {
     return code;
 }
 
+}  // namespace
+
+int sd::set_error(int code, const std::string& msg) { return fail(code, msg); }
+
+namespace {
+
 #define SD_HIP(x)                                                                              \
     do {                                                                                       \
         hipError_t e_ = (x);                                                                   \

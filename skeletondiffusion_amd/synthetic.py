@@ -32,10 +32,12 @@ def fill_parameters(named_shapes: Iterable[Tuple[str, Tuple[int, ...]]], seed: i
             a = np.eye(shape[0], shape[1]) + rng.uniform(0.0, 0.1, size=shape)
         elif leaf == "g":
             a = 1.0 + rng.uniform(-0.1, 0.1, size=shape)
-        elif leaf == "weight":
+        elif leaf == "G_add":  # additive graph influence of the GRU cells (recurrent.py:236-245)
+            a = rng.uniform(-0.05, 0.05, size=shape)
+        elif leaf in ("weight", "weight_ih", "weight_hh"):
             bound = 1.0 / math.sqrt(shape[-1])
             a = rng.uniform(-bound, bound, size=shape)
-        elif leaf == "bias":
+        elif leaf in ("bias", "bias_ih", "bias_hh"):
             a = rng.uniform(-0.1, 0.1, size=shape)
         else:
             raise KeyError(f"synthetic filler has no rule for parameter {name!r}")

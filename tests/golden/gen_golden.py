@@ -290,11 +290,39 @@ def gen_mm(motion, target, mmade, mmfde):
                 mmade_t5_15=mmade(mm_target, mm_motion, mm_gt, t0=5, t=15), mm_empty_raises=empty_raises)
 
 
+AE_KW = dict(num_nodes=16, encoder_hidden_size=96, decoder_hidden_size=96, latent_size=96, input_size=3,
+             z_activation="tanh", enc_num_layers=1, output_size=3, recurrent_arch_enc="StaticGraphGRU",
+             recurrent_arch_decoder="StaticGraphGRU", if_consider_hip=False)
+AE_SEED = 4321
+
+
+def gen_decoder():
+    """The reference's AutoEncoder (src/core/network/nn/autoencoder.py, release autoencoder.yaml
+    sizes, H36M 16-joint node types) with synthetic weights: the encoder's past embedding of 3
+    observed sequences, and AutoEncoder.decode of 3 x 4 sampled latents for 120 frames."""
+    from src.core.network.nn.autoencoder import AutoEncoder
+    from skeletondiffusion_amd.skeletons import skeleton
+
+    _, _, _, types = skeleton("h36m16")
+    m = AutoEncoder(node_types=torch.from_numpy(types), **AE_KW).eval()
+    synthetic.fill_module_(m, AE_SEED)
+    past = torch.from_numpy(synthetic.normal((3, 30, 16, 3), seed=41)) * 0.3
+    lat = torch.from_numpy(synthetic.uniform((12, 16, 96), seed=42))
+    with torch.no_grad():
+        z_past = m.get_past_embedding(past)
+        out = m.decode(past.repeat_interleave(4, 0), lat, z_past.repeat_interleave(4, 0), ph=120)
+    _save("decoder", out=out, z_past=z_past, keys=np.array(sorted(m.state_dict().keys())))
+
+
 def main():
     if sys.argv[1:] == ["metrics"]:
         gen_metrics()
         return
+    if sys.argv[1:] == ["decoder"]:
+        gen_decoder()
+        return
     gen_metrics()
+    gen_decoder()
     gen_covariances()
     gen_readme()
     gen_release("h36m16", 10, B_seq=2, futures=4, with_acts=True)
