@@ -745,10 +745,15 @@ hipError_t launch_graph_linear_v4(const GLArgs& a, bool rms, hipStream_t s) {
             if (cfg == 821) return gl4_launch<16, 8, 2, 1>(a, rms, s);
             if (cfg == 812) return gl4_launch<16, 8, 1, 2>(a, rms, s);
             if (cfg == 813) return gl4_launch<16, 8, 1, 3>(a, rms, s);
+            if (cfg == 811) return gl4_launch<16, 8, 1, 1>(a, rms, s);  // small batches: 3x the workgroups
             if (cfg == 6) return gl4_launch<16, 8, 1, 3, 6>(a, rms, s);  // phase stamps (tools/stamps.py)
             if (cfg == 7) return gl4_launch<16, 8, 1, 3, 6, 0, 1>(a, rms, s);  // stamps, x two chunks ahead
             if (cfg == 1813) return gl4_launch<16, 8, 1, 3, 0, 0, 1>(a, rms, s);
             if (cfg == 822) return gl4_launch<16, 8, 2, 2>(a, rms, s);
+            // small grids (a few sequences: config 4, one sequence x 50 futures): 32 x 32 tiles give
+            // 3x the workgroups of 32 x 96 and a third of the per-workgroup weight bytes; measured
+            // 1.69x (59.0 vs 34.9 futures/s at 50 rows, T = 1000), but 0.91x at B = 3200
+            if (cfg == 0 && (a.B + 31) / 32 * ((a.N + 95) / 96) < 32) return gl4_launch<16, 8, 1, 1>(a, rms, s);
             // 32 rows x 96 columns: 200 workgroups for an N = 192 layer at B = 3200 (64 x 64 gives
             // 150, leaving 40 % of the CUs idle); measured 1.28x faster on those layers
             return gl4_launch<16, 8, 1, 3>(a, rms, s);

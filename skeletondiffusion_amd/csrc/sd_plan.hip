@@ -784,8 +784,9 @@ static int record_loop(const sd_plan* p, const float* x_T, const float* x_cond, 
             const float* xc = (p->C > 0) ? x_cond + (r0 / cond_repeat) * p->J * p->C : x_cond;
             // concurrent chains: 32 x 64 tiles (more, smaller workgroups to interleave) measured
             // 5 % faster than the single-chain 32 x 96 choice at B = 3200, 3 chains
+            const int64_t wg813 = (c.n + 31) / 32 * 2;  // 32 x 96 workgroups of an N = 192 layer
             int rc = run_denoiser(p, c.cur, xc, cond_repeat, t, c.w.x0, c.n, c.w, cs[i], nullptr, r0 % cond_repeat,
-                                  nch > 1 ? 812 : 0);
+                                  (nch > 1 && wg813 >= 32) ? 812 : 0);
             if (rc) return rc;
             float* nxt = (t == 0) ? out + r0 * JD : (((T - 1 - t) & 1) ? c.w.img1 : c.w.img0);
             const float* eps = (!dev_noise && t > 0) ? eps_all + r0 * step_rs + k * JD : nullptr;

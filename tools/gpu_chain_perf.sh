@@ -3,7 +3,5 @@ run() {  # name, env...
   env "$@" timeout -k 10 240 python -u bench.py --steps 3 --warmup 1 --no-cpu-baseline > gpurun_out/cp_$name.log 2>&1 || { tail -20 gpurun_out/cp_$name.log; exit 1; }
   echo "$name $(grep '^{' gpurun_out/cp_$name.log | python -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["value"], d["ms_per_step"], d["kernels_per_denoise_step_ms"]["graph_linear"])')"
 }
-timeout -k 10 600 python -u -m pytest tests/test_gpu_kernels.py tests/test_gpu_parity.py -x -q --timeout 120 --timeout-method thread > gpurun_out/ldss_tests.log 2>&1 || { tail -30 gpurun_out/ldss_tests.log; exit 1; }
-tail -1 gpurun_out/ldss_tests.log
-run c3
-run c1 SKELDIFF_CHAINS=1
+run c3_811 SKELDIFF_GL4_CFG=811
+run c1_811 SKELDIFF_GL4_CFG=811 SKELDIFF_CHAINS=1
