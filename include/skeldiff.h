@@ -234,6 +234,14 @@ typedef struct sd_gru_decoder_desc {
 size_t sd_gru_decode_workspace_bytes(const sd_gru_decoder_desc* desc, int64_t rows, int32_t ph);
 int sd_gru_decode(const sd_gru_decoder_desc* desc, const float* x, const float* h, int64_t rows, int32_t ph,
                   float* out, void* workspace, size_t workspace_bytes, void* stream);
+/* Graph-GRU encoder + z_activation (src/core/network/nn/encoder.py:75-80, autoencoder.py:47-51,
+ * encoder_act = z_activation = tanh): x (rows, frames, J, F) observed frames -> z (rows, J, L) =
+ * tanh(tanh(fc(GRU over the frames from initial_hidden1(x[:, 0])))).  Same descriptor with the
+ * `encoder.*` tensors: init_* = initial_hidden1 (weight (types, H, F)), weight_ih (types, 3H, F),
+ * G_add = NULL, fc weight (types, L, H); latent_size = L. */
+size_t sd_gru_encode_workspace_bytes(const sd_gru_decoder_desc* desc, int64_t rows, int32_t frames);
+int sd_gru_encode(const sd_gru_decoder_desc* desc, const float* x, int64_t rows, int32_t frames, float* z,
+                  void* workspace, size_t workspace_bytes, void* stream);
 /* Row chains of sd_sample_loop (process-wide; SKELDIFF_CHAINS, default 3): the batch is split into
  * n row ranges (multiples of 32 rows; fewer when the batch is small) whose
  * T-step chains run on forked streams and overlap on the GPU.  Rows are independent, so the

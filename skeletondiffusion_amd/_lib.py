@@ -27,6 +27,7 @@ EXPORTED = (
     "sd_test_graph_linear", "sd_test_attention", "sd_set_kernel_variant", "sd_test_qkv_attention",
     "sd_test_graph_linear_layout", "sd_pairwise_distances", "sd_ade_fde", "sd_set_row_chains",
     "sd_plan_set_precision", "sd_mm_ade_fde", "sd_gru_decode_workspace_bytes", "sd_gru_decode",
+    "sd_gru_encode_workspace_bytes", "sd_gru_encode",
 )
 
 
@@ -98,6 +99,8 @@ def _declare(lib: ctypes.CDLL) -> None:
         "sd_gru_decode_workspace_bytes": (ctypes.c_size_t, [ctypes.POINTER(SDGruDecoderDesc), i64, i32]),
         "sd_gru_decode": (ctypes.c_int, [ctypes.POINTER(SDGruDecoderDesc), vp, vp, i64, i32, vp, vp,
                                          ctypes.c_size_t, vp]),
+        "sd_gru_encode_workspace_bytes": (ctypes.c_size_t, [ctypes.POINTER(SDGruDecoderDesc), i64, i32]),
+        "sd_gru_encode": (ctypes.c_int, [ctypes.POINTER(SDGruDecoderDesc), vp, i64, i32, vp, vp, ctypes.c_size_t, vp]),
         "sd_pairwise_distances": (ctypes.c_int, [vp, i64, i32, i64, vp, vp, vp]),
         "sd_ade_fde": (ctypes.c_int, [vp, vp, i64, i32, i32, i64, vp, vp, vp, vp, vp]),
         "sd_test_qkv_attention": (ctypes.c_int, [vp, i32, vp, ctypes.POINTER(ctypes.c_int64), vp, vp, i64, i32, i32,

@@ -5,9 +5,10 @@ decoder}.py`, `src/core/network/layers/recurrent.py:208-401`).  Same constructor
 state_dict keys as the reference, so its autoencoder checkpoints load strictly.
 
 `AutoEncoder.decode` -- the step after `sample()` in the evaluation (`eval_prepare_model.py:
-106-116`), run on bs x 50 rows for ph frames -- goes to the HIP decoder (`sd_gru_decode`) when
-the module lives on a ROCm device; on the CPU it raises (no CPU sampling path).  The encoder
-(bs rows, once per sequence) and the training-time `autoencode` stay torch ops (autograd).
+106-116`), run on bs x 50 rows for ph frames -- goes to the HIP decoder (`sd_gru_decode`) and
+`get_past_embedding` (the conditioning latents) to the HIP encoder (`sd_gru_encode`) when the
+module lives on a ROCm device; on the CPU they raise (no CPU evaluation path).  `forward` /
+`autoencode` (training, autograd) stay torch ops.
 """
 from __future__ import annotations
 
@@ -253,10 +254,20 @@ class AutoEncoder(nn.Module):
         h, _ = self.encoder(x)
         return h
 
+    def _hip(self):
+        from ... import decoder_engine
+
+        if self._engine is None:
+            self._engine = decoder_engine.DecoderEngine(self.decoder, self.encoder,
+                                                        z_tanh=isinstance(self.z_activation, nn.Tanh))
+        return self._engine
+
     def get_past_embedding(self, past, state=None):
-        with torch.no_grad():
-            h_hat_embedding = self(past)
-        return self.z_activation(h_hat_embedding)
+        """z_activation(encoder(past)) on the HIP encoder (the conditioning latents of sample(),
+        eval_prepare_model.py:89-99); no_grad as the reference."""
+        if state is not None:
+            raise NotImplementedError("get_past_embedding(state=...) is not used by the evaluation and not built")
+        return self._hip().encode(past)
 
     def get_embedding(self, future, state=None):
         return self.forward(future)
@@ -269,15 +280,13 @@ class AutoEncoder(nn.Module):
         (decoder.py:85-104 semantics; `z` is unused there too)."""
         if state is not None:
             raise NotImplementedError("decode(state=...) is not used by the evaluation and not built")
-        from ... import decoder_engine
-
-        if self._engine is None:
-            self._engine = decoder_engine.DecoderEngine(self.decoder)
-        return self._engine.decode(x[:, -2:], h, ph)
+        return self._hip().decode(x[:, -2:], h, ph)
 
     def autoencode(self, y, past, ph=1, state=None):
         """Training-time reconstruction on torch ops (autograd)."""
-        z_past, z = self.get_train_embeddings(y, past, state=state)
+        with torch.no_grad():
+            z_past = self.z_activation(self(past))
+        z = self.get_embedding(y, state=state)
         out, _ = self.decoder(x=past[:, -2:], h=z, z=z_past, ph=ph, state=state)
         return out, z_past, z
 

@@ -73,6 +73,22 @@ __global__ void k_pad_frame(const float* __restrict__ x, int64_t rows, int J, in
     xp[g] = k < F ? x[((r * 2 + f) * J + j) * F + k] : 0.f;
 }
 
+// frame `f` of x (rows, T, J, F) -> (rows, J, KF) zero-padded (encoder input)
+__global__ void k_pad_frame_t(const float* __restrict__ x, int64_t rows, int T, int J, int F, int f,
+                              float* __restrict__ xp) {
+    const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= rows * J * KF) return;
+    const int k = (int)(g % KF);
+    const int64_t rj = g / KF, r = rj / J;
+    const int j = (int)(rj % J);
+    xp[g] = k < F ? x[((r * T + f) * J + j) * F + k] : 0.f;
+}
+
+__global__ void k_tanh_inplace(float* __restrict__ v, int64_t n) {
+    const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (g < n) v[g] = tanhf(v[g]);
+}
+
 // One workgroup per row: x_res (J, 3H) and gx_t in LDS; thread -> (node i, feature c) outputs.
 __global__ __launch_bounds__(256) void k_gru_gate(const float* __restrict__ xres, const float* __restrict__ hres,
                                                   const float* __restrict__ gx, const float* __restrict__ hx,
@@ -244,6 +260,75 @@ int sd_gru_decode(const sd_gru_decoder_desc* d, const float* x, const float* h, 
         hx = hn;
         hn = tmp;
     }
+#undef DHIP
+    return SD_OK;
+}
+
+size_t sd_gru_encode_workspace_bytes(const sd_gru_decoder_desc* d, int64_t rows, int32_t frames) {
+    if (check_desc(d) || rows < 0 || frames < 1) return 0;
+    return sd::carve(d, rows, frames, nullptr, nullptr) + 256;
+}
+
+// Encoder.forward + z_activation (encoder.py:75-80, autoencoder.py:47-51): the GRU over `frames`
+// observed frames from hx_0 = initial_hidden1(x[:, 0]), then z = tanh(tanh(fc(hx_T))).  The
+// descriptor's init_* are initial_hidden1 (input F), weight_ih is (types, 3H, F), latent_size is
+// the fc output width (the latent), G_add must be NULL (no additive influence in the encoder).
+int sd_gru_encode(const sd_gru_decoder_desc* d, const float* x, int64_t rows, int32_t frames, float* z,
+                  void* workspace, size_t ws_bytes, void* stream) {
+    int rc = check_desc(d);
+    if (rc) return rc;
+    if (rows < 0 || frames < 1) return dfail(SD_E_INVALID, "rows >= 0 and frames >= 1 required");
+    if (rows == 0) return SD_OK;
+    if (!x || !z) return dfail(SD_E_INVALID, "null input / output");
+    if (d->G_add) return dfail(SD_E_INVALID, "the encoder GRU has no additive graph influence (G_add must be NULL)");
+    const size_t need = sd::carve(d, rows, frames, nullptr, nullptr);
+    char* base = (char*)(((uintptr_t)workspace + 255) & ~(uintptr_t)255);
+    if (!workspace || (size_t)(base - (char*)workspace) + need > ws_bytes)
+        return dfail(SD_E_INVALID, "workspace too small: need " + std::to_string(need + 256));
+    sd::DecWS w;
+    sd::carve(d, rows, frames, base, &w);
+    hipStream_t s = (hipStream_t)stream;
+    const int J = d->num_nodes, F = d->feature_size, L = d->latent_size, H = d->hidden_size;
+    const int nt = d->num_node_types > 0 ? d->num_node_types : 1;
+#define DHIP(expr)                                                                              \
+    do {                                                                                        \
+        hipError_t e_ = (expr);                                                                 \
+        if (e_ != hipSuccess) return dfail(SD_E_HIP, std::string(#expr) + ": " + hipGetErrorString(e_)); \
+    } while (0)
+    auto grid = [](int64_t n) { return dim3((unsigned)((n + 255) / 256)); };
+    // F-wide weights padded to KF (no latent part: L' = 0); frames padded one at a time into xprev
+    hipLaunchKernelGGL(sd::k_pad_w, grid((int64_t)nt * H * sd::KF), dim3(256), 0, s, d->init_weight, (int64_t)nt * H, F, 0, w.winit);
+    hipLaunchKernelGGL(sd::k_pad_w, grid((int64_t)nt * 3 * H * sd::KF), dim3(256), 0, s, d->weight_ih, (int64_t)nt * 3 * H, F, 0, w.wih);
+    hipLaunchKernelGGL(sd::k_identity, grid((int64_t)J * J), dim3(256), 0, s, w.ident, J);
+    hipLaunchKernelGGL(sd::k_gx_table, dim3(1), dim3(64), 0, s, d->G, (const float*)nullptr, J, (int)frames, w.gx);
+    DHIP(hipGetLastError());
+    DHIP(sd::launch_ghat(d->init_G, w.ghat_init, J, 1, s));
+    DHIP(sd::launch_ghat(d->fc_G, w.ghat_fc, J, 1, s));
+    const int64_t JH = (int64_t)J * H, JH3 = 3 * JH;
+    const size_t gate_lds = ((size_t)J * 3 * H + (size_t)J * J) * sizeof(float);
+    if (gate_lds > 64 * 1024)
+        DHIP(hipFuncSetAttribute((const void*)sd::k_gru_gate, hipFuncAttributeMaxDynamicSharedMemorySize, (int)gate_lds));
+    // x (rows, frames, J, F): frame t -> xprev via k_pad_frame's (rows, 2, J, F) view at stride
+    // frames: done with a strided copy kernel of its own
+    hipLaunchKernelGGL(sd::k_pad_frame_t, grid(rows * J * sd::KF), dim3(256), 0, s, x, rows, frames, J, F, 0, w.xprev);
+    DHIP(sd::launch_graph_linear(sd::gl(d, w.xprev, sd::KF, nullptr, 0, w.winit, d->init_bias, w.ghat_init, H, w.h0, JH, rows, 0), false, s));
+    float* hx = w.h0;
+    float* hn = w.h1;
+    for (int t = 0; t < frames; ++t) {
+        const float* gxt = w.gx + (size_t)t * J * J;
+        if (t > 0) hipLaunchKernelGGL(sd::k_pad_frame_t, grid(rows * J * sd::KF), dim3(256), 0, s, x, rows, frames, J, F, t, w.xprev);
+        DHIP(sd::launch_graph_linear(sd::gl(d, w.xprev, sd::KF, nullptr, 0, w.wih, d->bias_ih, w.ident, 3 * H, w.xres, JH3, rows, 0), false, s));
+        DHIP(sd::launch_graph_linear(sd::gl(d, hx, H, nullptr, 0, d->weight_hh, d->bias_hh, gxt, 3 * H, w.hres, JH3, rows, 0), false, s));
+        hipLaunchKernelGGL(sd::k_gru_gate, dim3((unsigned)rows), dim3(256), gate_lds, s, w.xres, w.hres, gxt, hx, hn, J, H);
+        DHIP(hipGetLastError());
+        float* tmp = hx;
+        hx = hn;
+        hn = tmp;
+    }
+    // z = tanh(tanh(Ghat_fc (W_fc hx + b_fc))): the fc launch's tanh epilogue, then one more tanh
+    DHIP(sd::launch_graph_linear(sd::gl(d, hx, H, nullptr, 0, d->fc_weight, d->fc_bias, w.ghat_fc, L, z, (int64_t)J * L, rows, 1), false, s));
+    hipLaunchKernelGGL(sd::k_tanh_inplace, grid(rows * J * L), dim3(256), 0, s, z, rows * J * L);
+    DHIP(hipGetLastError());
 #undef DHIP
     return SD_OK;
 }

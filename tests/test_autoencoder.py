@@ -54,19 +54,38 @@ def test_module_torch_paths_match_reference():
     m, _ = _model()
     past, lat = _inputs()
     with torch.no_grad():
-        zp = m.get_past_embedding(past)
+        zp = m.z_activation(m(past))  # the torch encoder (training path)
         out, _ = m.decoder(x=past.repeat_interleave(4, 0)[:, -2:], h=lat, z=None, ph=120)
     assert (zp - torch.from_numpy(z["z_past"])).abs().max().item() < 1e-5
     assert (out - torch.from_numpy(z["out"])).abs().max().item() < 1e-5
 
 
-def test_decode_refuses_cpu():
+def test_decode_and_encode_refuse_cpu():
     from skeletondiffusion_amd._lib import SkelDiffError
 
     m, _ = _model()
     past, lat = _inputs()
     with pytest.raises(SkelDiffError):
         m.decode(past[:1], lat[:1], None, ph=3)
+    with pytest.raises(SkelDiffError):
+        m.get_past_embedding(past[:1])
+
+
+@pytest.mark.gpu
+def test_hip_encode_matches_reference(cuda):
+    z = golden("decoder")
+    m, types = _model(cuda)
+    past, _ = _inputs()
+    zp = m.get_past_embedding(past.to(cuda))
+    torch.cuda.synchronize()
+    assert (zp.cpu() - torch.from_numpy(z["z_past"])).abs().max().item() < TOL
+    g = torch.Generator().manual_seed(5)
+    x = torch.randn((7, 9, 16, 3), generator=g) * 0.3  # ragged batch, other length
+    sd = {k: v.detach().cpu() for k, v in m.state_dict().items()}
+    ref = O.gru_encode(sd, types, x)
+    got = m.get_past_embedding(x.to(cuda))
+    torch.cuda.synchronize()
+    assert (got.cpu() - ref).abs().max().item() < TOL
 
 
 @pytest.mark.gpu
