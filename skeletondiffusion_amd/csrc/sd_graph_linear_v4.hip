@@ -566,11 +566,17 @@ __global__ __launch_bounds__(NW * 64, 1) void k_gl4(const GLArgs p) {
             cc = (b % (COLS / 16)) * 16 + 4 * lg;
         }
     };
-    floatx4 rv[BPW][IB];
-    auto load_res = [&](int hc) {
+    // J <= 16: a slab's residual pieces are all loaded before the Y exchange (latency hidden);
+    // J > 16 (two node blocks): per group of PG blocks, halving the registers they hold
+    constexpr bool RES_EARLY = IB == 1;
+    constexpr int PG0 = (IB == 1 && BPW <= 8) ? BPW : (BPW < 4 ? BPW : 4);
+    floatx4 rv[RES_EARLY ? BPW : PG0][IB];
+    auto load_res = [&](int hc, int kfirst, int kcount) {
 #pragma unroll
-        for (int k = 0; k < BPW; ++k) {
-            const int b = wave + NW * k;
+        for (int kk = 0; kk < (RES_EARLY ? BPW : PG0); ++kk) {
+            if (kk >= kcount) continue;
+            const int k = kfirst + kk;
+            const int b = k < BPW ? wave + NW * k : COLS;
             int r, cc;
             out_pos(min(b, COLS - 1), r, cc);
             const int64_t row = row0 + 16 * hc + r;
@@ -580,7 +586,7 @@ __global__ __launch_bounds__(NW * 64, 1) void k_gl4(const GLArgs p) {
             for (int ib = 0; ib < IB; ++ib) {
                 const int i = ib * 16 + lr;
                 const float* src = p.res_blk ? p.res + blk_off(row, i, n, J, p.N) : p.res + row * p.res_rs + (int64_t)i * p.N + n;
-                rv[k][ib] = (ok && i < J) ? g4(src) : floatx4{0.f, 0.f, 0.f, 0.f};
+                rv[kk][ib] = (ok && i < J) ? g4(src) : floatx4{0.f, 0.f, 0.f, 0.f};
             }
         }
     };
@@ -588,7 +594,7 @@ __global__ __launch_bounds__(NW * 64, 1) void k_gl4(const GLArgs p) {
 #pragma unroll
     for (int hc = 0; hc < 2 * RT; ++hc) {
         const int rt = hc >> 1, hf = hc & 1;
-        if (p.res) load_res(hc);  // latency hides under the Y exchange below
+        if (RES_EARLY && p.res) load_res(hc, 0, BPW);  // latency hides under the Y exchange below
         __syncthreads();          // K loop / previous slab done with the LDS that sY aliases
 #pragma unroll
         for (int m = 0; m < NPW; ++m) {
@@ -606,8 +612,10 @@ __global__ __launch_bounds__(NW * 64, 1) void k_gl4(const GLArgs p) {
         // per group of PG blocks: phase 1 every LDS read, phase 2 the mixing MFMAs, phase 3
         // FiLM / tanh / residual / 16-B stores -- no dependent chain per block
         constexpr int PG = (IB == 1 && BPW <= 8) ? BPW : (BPW < 4 ? BPW : 4);
+        static_assert(PG == PG0, "residual group size");
 #pragma unroll
         for (int k0 = 0; k0 < BPW; k0 += PG) {
+            if (!RES_EARLY && p.res) load_res(hc, k0, min(PG, BPW - k0));
             float ya[PG][KS];  // A operand: Y^T[row = rc = 16b + lr][k = j = 4s + lg]
 #pragma unroll
             for (int kk = 0; kk < PG; ++kk) {
@@ -651,7 +659,7 @@ __global__ __launch_bounds__(NW * 64, 1) void k_gl4(const GLArgs p) {
                         v.z = tanh4(v.z);
                         v.w = tanh4(v.w);
                     }
-                    if (p.res) v += rv[k][ib];
+                    if (p.res) v += rv[RES_EARLY ? k : kk][ib];
                     if (ok && i < J) {
                         float* dst = p.out_blk ? p.out + blk_off(row, i, n, J, p.N) : p.out + row * p.out_rs + (int64_t)i * p.N + n;
                         *reinterpret_cast<floatx4*>(dst) = v;
@@ -759,8 +767,8 @@ hipError_t launch_graph_linear_v4(const GLArgs& a, bool rms, hipStream_t s) {
             return gl4_launch<16, 8, 1, 3>(a, rms, s);
         // J > 16 needs two 16-node blocks in the mixing epilogue: 96 columns spill there
         case 17:
-            if (cfg == 812) return gl4_launch<17, 8, 1, 2>(a, rms, s);
-            return gl4_launch<17, 8, 2, 1>(a, rms, s);
+            if (cfg == 821) return gl4_launch<17, 8, 2, 1>(a, rms, s);
+            return gl4_launch<17, 8, 1, 2>(a, rms, s);
         case 21: return gl4_launch<21, 8, 1, 2>(a, rms, s);
         default: return hipErrorNotSupported;
     }
