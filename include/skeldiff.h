@@ -256,6 +256,27 @@ int sd_set_row_chains(int32_t n);
  * recorded after the call; SD_E_INVALID for another mode. */
 int sd_plan_set_precision(sd_plan* plan, int32_t mode);
 
+/* Training-side StaticGraphLinear (SURVEY.md §8f "next" #4): replaces GraphLinear.forward
+ * (src/core/network/layers/graph_structural.py:30-43, StaticGraphLinear :105-114) and the backward
+ * torch autograd derives for it in NonisotropicGaussianDiffusion.forward / p_losses training
+ * (src/core/diffusion/base.py:262-307).  Caller-owned device buffers, row-major:
+ *   x (rows, J, K), W (types, N, K), bias (types, N) or NULL, node_types device int64 (J) with
+ *   values in [0, n_types) (n_types = 0: shared weights, W (1, N, K), node_types ignored),
+ *   ghat (J, J) = the mixing matrix actually applied (G, or G / rowsum|G| when learn_influence).
+ * sd_gl_train_forward: z = W[type j] x_j + bias[type j] (pre-mix, kept for backward), y = ghat @ z.
+ * sd_gl_train_backward: from dy (rows, J, N) and the forward's z: dx (rows, J, K), dW (types, N, K),
+ *   dbias (types, N), dghat (J, J); any output may be NULL (not computed).  Deterministic (fixed
+ *   reduction order).  workspace >= sd_gl_train_workspace_bytes(rows, J, K, N, n_types).
+ *   1 <= J <= 64. */
+size_t sd_gl_train_workspace_bytes(int64_t rows, int32_t J, int32_t K, int32_t N, int32_t n_types);
+int sd_gl_train_forward(const float* x, const float* W, const float* bias, const int64_t* node_types,
+                        int32_t n_types, const float* ghat, int64_t rows, int32_t J, int32_t K, int32_t N,
+                        float* z, float* y, void* stream);
+int sd_gl_train_backward(const float* x, const float* z, const float* dy, const float* W, const int64_t* node_types,
+                         int32_t n_types, const float* ghat, int64_t rows, int32_t J, int32_t K, int32_t N, float* dx,
+                         float* dW, float* dbias, float* dghat, void* workspace, size_t workspace_bytes,
+                         void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -27,7 +27,8 @@ EXPORTED = (
     "sd_test_graph_linear", "sd_test_attention", "sd_set_kernel_variant", "sd_test_qkv_attention",
     "sd_test_graph_linear_layout", "sd_pairwise_distances", "sd_ade_fde", "sd_set_row_chains",
     "sd_plan_set_precision", "sd_mm_ade_fde", "sd_gru_decode_workspace_bytes", "sd_gru_decode",
-    "sd_gru_encode_workspace_bytes", "sd_gru_encode",
+    "sd_gru_encode_workspace_bytes", "sd_gru_encode", "sd_gl_train_workspace_bytes", "sd_gl_train_forward",
+    "sd_gl_train_backward",
 )
 
 
@@ -107,6 +108,10 @@ def _declare(lib: ctypes.CDLL) -> None:
                                                  i32, i32, vp]),
         "sd_test_graph_linear_layout": (ctypes.c_int, [vp, i32, i64, vp, i32, vp, vp, ctypes.POINTER(ctypes.c_int64),
                                                        vp, vp, i32, vp, vp, i64, i32, i32, i32, i32, vp]),
+        "sd_gl_train_workspace_bytes": (sz, [i64, i32, i32, i32, i32]),
+        "sd_gl_train_forward": (ctypes.c_int, [vp, vp, vp, vp, i32, vp, i64, i32, i32, i32, vp, vp, vp]),
+        "sd_gl_train_backward": (ctypes.c_int, [vp, vp, vp, vp, vp, i32, vp, i64, i32, i32, i32, vp, vp, vp, vp, vp,
+                                                sz, vp]),
         "sd_profile_step": (ctypes.c_int, [vp, vp, vp, i64, i32, i64, vp, sz, i32, ctypes.POINTER(ctypes.c_float),
                                            ctypes.POINTER(ctypes.c_int32), vp]),
     }

@@ -3,8 +3,10 @@
 Module / attribute names are fixed by the reference's state_dict (strict loading,
 reference src/eval_prepare_model.py:72), so they match
 src/core/network/layers/{graph_structural,attention}.py; the code itself is written for this
-engine.  These torch implementations serve `NonisotropicGaussianDiffusion.forward()`
-(training, autograd).  Sampling never calls them: it runs on the HIP engine (engine.py).
+engine.  These modules serve `NonisotropicGaussianDiffusion.forward()` (training, autograd); on
+the device every StaticGraphLinear runs forward and backward on the HIP training kernels
+(training.py, sd_train.hip), the rest on torch ops.  Sampling never calls them: it runs on the
+HIP engine (engine.py).
 """
 from __future__ import annotations
 
@@ -15,6 +17,8 @@ import torch
 import torch.nn.functional as F
 from torch import nn
 from torch.nn import Parameter, init
+
+from ... import training as _training
 
 
 class StaticGraphLinear(nn.Module):
@@ -81,6 +85,10 @@ class StaticGraphLinear(nn.Module):
 
     def forward(self, x: torch.Tensor, g: Optional[torch.Tensor] = None) -> torch.Tensor:
         g = self.ghat() if g is None else g
+        if (x.is_cuda and torch.is_grad_enabled() and x.dtype == torch.float32
+                and self.weight.dtype == torch.float32 and _training.hip_training_enabled()):
+            # training on the device: forward + backward on the HIP kernels (sd_train.hip)
+            return _training.graph_linear(x, self.weight, self.bias, g, self.node_type_index)
         if self.node_type_index is not None:
             w = self.weight[self.node_type_index.to(self.weight.device)]       # (J, out, in)
             y = torch.einsum("noi,bni->bno", w, x)

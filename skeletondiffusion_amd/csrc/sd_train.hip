@@ -1,0 +1,379 @@
+// Training side of the StaticGraphLinear (SURVEY.md §8f "next" #4): forward with the pre-mix
+// activations kept for backward, and the backward the reference gets from torch autograd over
+// GraphLinear.forward (src/core/network/layers/graph_structural.py:30-43, 105-114):
+//   z[r, j, :] = W[type j] x[r, j, :] + bias[type j]         (per-node GEMM, rows x K -> rows x N)
+//   y[r, i, :] = sum_j ghat[i, j] z[r, j, :]                  (node mixing)
+// backward from dy:
+//   dz[r, j, :] = sum_i ghat[i, j] dy[r, i, :]                (mixing with ghat^T)
+//   dx[:, j, :] = dz[:, j, :] W[type j]                       (per-node GEMM)
+//   dW[t]       = sum_{j: type j = t} dz[:, j, :]^T x[:, j, :] (per-type GEMM, reduction over rows)
+//   dbias[t]    = sum_{r, j: type j = t} dz[r, j, :]
+//   dghat[i, j] = sum_{r, n} dy[r, i, n] z[r, j, n]
+// The three GEMMs are one strided kernel on v_mfma_f32_32x32x2_f32 (exact f32 products, f32
+// accumulate): 64x64 C tile per 256-thread workgroup (2x2 waves of 32x32), K staged 16 at a time
+// through LDS; the reduction over rows (dW) is split over row ranges into partial tiles that a
+// fixed-order pass sums (deterministic, no float atomics).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <string>
+
+#include "../../include/skeldiff.h"
+#include "sd_internal.h"
+
+namespace sd {
+namespace {
+
+constexpr int TM = 64, TN = 64, TK = 16;
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+// Strided batched GEMM: for batch z (grid.z = nbatch * splits):
+//   node mode (by_type = 0): group = {node j = batch}, t = type(j)
+//   type mode (by_type = 1): group = {nodes j with type(j) = batch}, t = batch
+// C[c_off + m*cm + n] (+)= sum over the group, k of A[a_off + m*am + k*ak] * B[b_off + k*bk + n*bn]
+// with a_off = j*aj + t*at, b_off = j*bj + t*bt, c_off = (by_type ? t : j)*cz + split*cs.
+// splits > 1 (dW, where the reduction index k is the row index): split s takes k in
+// [s*kchunk, min(K, (s+1)*kchunk)) and writes its own partial slab (c_off += s*cs).
+struct GemmArgs {
+    const float* A;
+    const float* B;
+    float* C;
+    const float* bias;  // node mode only: C += bias[t*bt_bias + n]
+    const int64_t* types;
+    int M, N, K, J, by_type, splits, kchunk;
+    int64_t am, ak, aj, at, bk, bn, bj, bt, cm, cz, cs, bias_t;
+};
+
+__global__ __launch_bounds__(256) void k_gemm(GemmArgs g) {
+    __shared__ float As[TK][TM + 4];
+    __shared__ float Bs[TK][TN + 4];
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int wm = w >> 1, wn = w & 1;
+    const int m0 = blockIdx.y * TM, n0 = blockIdx.x * TN;
+    const int batch = blockIdx.z / g.splits, split = blockIdx.z % g.splits;
+    const int kbeg = split * g.kchunk;
+    const int kend = min(g.K, kbeg + g.kchunk);
+
+    f32x16 acc;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) acc[i] = 0.f;
+
+    const int jbeg = g.by_type ? 0 : batch, jend = g.by_type ? g.J : batch + 1;
+    for (int j = jbeg; j < jend; ++j) {
+        const int t = g.types ? (int)g.types[j] : 0;
+        if (g.by_type && t != batch) continue;  // uniform over the workgroup
+        const float* A = g.A + j * g.aj + t * g.at;
+        const float* B = g.B + j * g.bj + t * g.bt;
+        for (int k0 = kbeg; k0 < kend; k0 += TK) {
+            // stage A (TM x TK) and B (TK x TN): 1024 elements each, 4 per thread; the unit-stride
+            // dimension runs over consecutive threads
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int idx = tid + 256 * q;
+                int mm, kk;
+                if (g.am == 1) { mm = idx & 63; kk = idx >> 6; } else { kk = idx & 15; mm = idx >> 4; }
+                const int gm = m0 + mm, gk = k0 + kk;
+                As[kk][mm] = (gm < g.M && gk < kend) ? A[gm * g.am + (int64_t)gk * g.ak] : 0.f;
+                int nn, kb;
+                if (g.bn == 1) { nn = idx & 63; kb = idx >> 6; } else { kb = idx & 15; nn = idx >> 4; }
+                const int gn = n0 + nn, gkb = k0 + kb;
+                Bs[kb][nn] = (gn < g.N && gkb < kend) ? B[(int64_t)gkb * g.bk + gn * g.bn] : 0.f;
+            }
+            __syncthreads();
+#pragma unroll
+            for (int kk = 0; kk < TK; kk += 2) {
+                const float a = As[kk + (lane >> 5)][wm * 32 + (lane & 31)];
+                const float b = Bs[kk + (lane >> 5)][wn * 32 + (lane & 31)];
+                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, acc, 0, 0, 0);
+            }
+            __syncthreads();
+        }
+    }
+    // C/D map: col = lane & 31, row = (reg & 3) + 8 * (reg >> 2) + 4 * (lane >> 5)
+    float* C = g.C + batch * g.cz + split * g.cs;  // node j's or type t's output slab
+    const int n = n0 + wn * 32 + (lane & 31);
+    if (n >= g.N) return;
+    float bv = 0.f;
+    if (g.bias) {
+        const int t = g.types ? (int)g.types[batch] : 0;
+        bv = g.bias[t * g.bias_t + n];
+    }
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        const int m = m0 + wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+        if (m < g.M) C[m * g.cm + n] = acc[r] + bv;
+    }
+}
+
+// out[r, i, n] = sum_j M[i, j] in[r, j, n], M = ghat (transpose = 0) or ghat^T (transpose = 1).
+// One workgroup per (row, 64-column chunk); the J x 64 input slab and ghat in LDS.
+__global__ __launch_bounds__(256) void k_mix(const float* __restrict__ in, const float* __restrict__ ghat,
+                                             float* __restrict__ out, int J, int N, int transpose) {
+    __shared__ float s_in[64][64];
+    __shared__ float s_g[64][65];
+    const int r = blockIdx.x, n0 = blockIdx.y * 64, tid = threadIdx.x;
+    const int64_t base = (int64_t)r * J * N;
+    for (int e = tid; e < J * J; e += 256) {
+        const int i = e / J, j = e % J;
+        s_g[i][j] = transpose ? ghat[j * J + i] : ghat[i * J + j];
+    }
+    for (int e = tid; e < J * 64; e += 256) {
+        const int j = e >> 6, c = e & 63;
+        s_in[j][c] = (n0 + c < N) ? in[base + (int64_t)j * N + n0 + c] : 0.f;
+    }
+    __syncthreads();
+    const int c = tid & 63;
+    if (n0 + c >= N) return;
+    for (int i = tid >> 6; i < J; i += 4) {
+        float acc = 0.f;
+        for (int j = 0; j < J; ++j) acc = fmaf(s_g[i][j], s_in[j][c], acc);
+        out[base + (int64_t)i * N + n0 + c] = acc;
+    }
+}
+
+// partial dghat over a row range on v_mfma_f32_32x32x2_f32:
+//   part[chunk][i][j] = sum_{r in chunk} (dY_r Z_r^T)[i][j],  dY_r, Z_r = (J x N) slabs of row r.
+// Each wave takes every 4th row of the chunk; per 8-feature step a lane (node i or j = l & 31 of a
+// 32-node tile, half h = l >> 5) loads 4 consecutive features k = k0 + 4h + s of its dy and z rows
+// (16 B) and feeds them as MFMA k-step s: A and B use the same k permutation, so the sum over k
+// is exact.  TI x TI 32x32 tiles cover J <= 32 * TI.  The 4 waves' tiles are summed in LDS in wave
+// order (deterministic).
+template <int TI>
+__global__ __launch_bounds__(256) void k_dghat_part(const float* __restrict__ dy, const float* __restrict__ z,
+                                                    float* __restrict__ part, int64_t rows, int J, int N,
+                                                    int rows_per_chunk) {
+    __shared__ float s_acc[TI * 32][TI * 32 + 1];
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int li = lane & 31, h = lane >> 5;
+    f32x16 acc[TI][TI];
+#pragma unroll
+    for (int a = 0; a < TI; ++a)
+#pragma unroll
+        for (int b = 0; b < TI; ++b)
+#pragma unroll
+            for (int q = 0; q < 16; ++q) acc[a][b][q] = 0.f;
+    const int64_t r0 = (int64_t)blockIdx.x * rows_per_chunk;
+    const int64_t r1 = min(rows, r0 + rows_per_chunk);
+    const bool vec = (N & 7) == 0;
+    for (int64_t r = r0 + w; r < r1; r += 4) {
+        const float* dyr = dy + r * J * N;
+        const float* zr = z + r * J * N;
+        for (int k0 = 0; k0 < N; k0 += 8) {
+            float av[TI][4], bv[TI][4];
+#pragma unroll
+            for (int a = 0; a < TI; ++a) {
+                const int i = a * 32 + li;
+                const int k = k0 + 4 * h;
+                if (vec) {
+                    float4 va = make_float4(0.f, 0.f, 0.f, 0.f), vb = va;
+                    if (i < J) {
+                        va = *(const float4*)(dyr + (int64_t)i * N + k);
+                        vb = *(const float4*)(zr + (int64_t)i * N + k);
+                    }
+                    av[a][0] = va.x; av[a][1] = va.y; av[a][2] = va.z; av[a][3] = va.w;
+                    bv[a][0] = vb.x; bv[a][1] = vb.y; bv[a][2] = vb.z; bv[a][3] = vb.w;
+                } else {
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) {
+                        const bool ok = i < J && k + q < N;
+                        av[a][q] = ok ? dyr[(int64_t)i * N + k + q] : 0.f;
+                        bv[a][q] = ok ? zr[(int64_t)i * N + k + q] : 0.f;
+                    }
+                }
+            }
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+#pragma unroll
+                for (int a = 0; a < TI; ++a)
+#pragma unroll
+                    for (int b = 0; b < TI; ++b)
+                        acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[a][q], bv[b][q], acc[a][b], 0, 0, 0);
+        }
+    }
+    // C/D map: col = lane & 31, row = (reg & 3) + 8 * (reg >> 2) + 4 * (lane >> 5)
+    for (int ww = 0; ww < 4; ++ww) {
+        if (w == ww) {
+#pragma unroll
+            for (int a = 0; a < TI; ++a)
+#pragma unroll
+                for (int b = 0; b < TI; ++b)
+#pragma unroll
+                    for (int q = 0; q < 16; ++q) {
+                        const int i = a * 32 + (q & 3) + 8 * (q >> 2) + 4 * h, j = b * 32 + li;
+                        s_acc[i][j] = (ww == 0 ? 0.f : s_acc[i][j]) + acc[a][b][q];
+                    }
+        }
+        __syncthreads();
+    }
+    for (int p = tid; p < J * J; p += 256) part[(int64_t)blockIdx.x * J * J + p] = s_acc[p / J][p % J];
+}
+
+// partial dbias over a row range: part[chunk][t][n] = sum_{r in chunk, j: type j = t} dz[r,j,n]
+__global__ __launch_bounds__(256) void k_dbias_part(const float* __restrict__ dz, const int64_t* __restrict__ types,
+                                                    float* __restrict__ part, int64_t rows, int J, int N,
+                                                    int n_types, int rows_per_chunk) {
+    const int n = blockIdx.x * 256 + threadIdx.x, t = blockIdx.y;
+    if (n >= N) return;
+    const int64_t r0 = (int64_t)blockIdx.z * rows_per_chunk;
+    const int64_t r1 = min(rows, r0 + rows_per_chunk);
+    float acc = 0.f;
+    for (int64_t r = r0; r < r1; ++r)
+        for (int j = 0; j < J; ++j)
+            if ((types ? (int)types[j] : 0) == t) acc += dz[(r * J + j) * N + n];
+    part[((int64_t)blockIdx.z * n_types + t) * N + n] = acc;
+}
+
+// out[e] = sum_s part[s][e] in split order (deterministic)
+__global__ __launch_bounds__(256) void k_sum_parts(const float* __restrict__ part, int splits, int64_t n,
+                                                   float* __restrict__ out) {
+    const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (e >= n) return;
+    float acc = 0.f;
+    for (int s = 0; s < splits; ++s) acc += part[s * n + e];
+    out[e] = acc;
+}
+
+constexpr int kRowsPerChunk = 16;  // dbias partials
+constexpr int kDghatRows = 8;      // dghat partials (2 rows per wave)
+
+int splits_for(int64_t rows) {
+    // dW reduction: about 64 rows per split, at most 32 splits
+    int64_t s = (rows + 255) / 256;
+    return (int)(s < 1 ? 1 : (s > 32 ? 32 : s));
+}
+
+int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
+
+}  // namespace
+}  // namespace sd
+
+using sd::GemmArgs;
+
+#define TR_HIP(x)                                                                                     \
+    do {                                                                                              \
+        hipError_t e_ = (x);                                                                          \
+        if (e_ != hipSuccess) return sd::set_error(SD_E_HIP, std::string(#x) + ": " + hipGetErrorString(e_)); \
+    } while (0)
+
+extern "C" {
+
+size_t sd_gl_train_workspace_bytes(int64_t rows, int32_t J, int32_t K, int32_t N, int32_t n_types) {
+    if (rows < 0 || J < 1 || K < 1 || N < 1) return 0;
+    const int types = n_types < 1 ? 1 : n_types;
+    const int64_t s = sd::splits_for(rows);
+    const int64_t chunks = sd::ceil_div(rows, sd::kRowsPerChunk);
+    const int64_t gchunks = sd::ceil_div(rows, sd::kDghatRows);
+    int64_t part = s * types * (int64_t)N * K;                    // dW partials
+    part = part > gchunks * (int64_t)J * J ? part : gchunks * (int64_t)J * J;   // dghat partials
+    part = part > chunks * (int64_t)types * N ? part : chunks * (int64_t)types * N;  // dbias partials
+    return (size_t)(rows * J * (int64_t)N + part) * sizeof(float);
+}
+
+int sd_gl_train_forward(const float* x, const float* W, const float* bias, const int64_t* node_types,
+                        int32_t n_types, const float* ghat, int64_t rows, int32_t J, int32_t K, int32_t N,
+                        float* z, float* y, void* stream) {
+    if (rows < 0 || J < 1 || J > 64 || K < 1 || N < 1 || n_types < 0)
+        return sd::set_error(SD_E_INVALID, "gl_train_forward: need rows >= 0, 1 <= J <= 64, K, N >= 1");
+    if (rows == 0) return SD_OK;
+    if (!x || !W || !ghat || !z || !y) return sd::set_error(SD_E_INVALID, "gl_train_forward: null buffer");
+    if (n_types > 0 && !node_types) return sd::set_error(SD_E_INVALID, "gl_train_forward: node_types missing");
+    if (rows > INT32_MAX / 2) return sd::set_error(SD_E_INVALID, "gl_train_forward: too many rows");
+    hipStream_t s = (hipStream_t)stream;
+    GemmArgs g{};
+    g.A = x; g.B = W; g.C = z; g.bias = bias; g.types = n_types > 0 ? node_types : nullptr;
+    g.M = (int)rows; g.N = N; g.K = K; g.J = J; g.by_type = 0; g.splits = 1; g.kchunk = K;
+    g.am = (int64_t)J * K; g.ak = 1; g.aj = K; g.at = 0;            // A[m][k] = x[m, j, k]
+    g.bk = 1; g.bn = K; g.bj = 0; g.bt = (int64_t)N * K;            // B[k][n] = W[t][n][k]
+    g.cm = (int64_t)J * N; g.cz = N; g.cs = 0; g.bias_t = N;        // C[m][n] = z[m, j, n]
+    hipLaunchKernelGGL(sd::k_gemm, dim3((unsigned)sd::ceil_div(N, sd::TN), (unsigned)sd::ceil_div(rows, sd::TM), J),
+                       dim3(256), 0, s, g);
+    TR_HIP(hipGetLastError());
+    hipLaunchKernelGGL(sd::k_mix, dim3((unsigned)rows, (unsigned)sd::ceil_div(N, 64)), dim3(256), 0, s, z, ghat, y, J,
+                       N, 0);
+    TR_HIP(hipGetLastError());
+    return SD_OK;
+}
+
+int sd_gl_train_backward(const float* x, const float* z, const float* dy, const float* W, const int64_t* node_types,
+                         int32_t n_types, const float* ghat, int64_t rows, int32_t J, int32_t K, int32_t N, float* dx,
+                         float* dW, float* dbias, float* dghat, void* workspace, size_t workspace_bytes,
+                         void* stream) {
+    if (rows < 0 || J < 1 || J > 64 || K < 1 || N < 1 || n_types < 0)
+        return sd::set_error(SD_E_INVALID, "gl_train_backward: need rows >= 0, 1 <= J <= 64, K, N >= 1");
+    if (rows > INT32_MAX / 2) return sd::set_error(SD_E_INVALID, "gl_train_backward: too many rows");
+    const int types = n_types > 0 ? n_types : 1;
+    const int64_t* tp = n_types > 0 ? node_types : nullptr;
+    if (n_types > 0 && !node_types) return sd::set_error(SD_E_INVALID, "gl_train_backward: node_types missing");
+    hipStream_t s = (hipStream_t)stream;
+    if (rows == 0) {  // empty batch: zero parameter gradients
+        if (dW) TR_HIP(hipMemsetAsync(dW, 0, (size_t)types * N * K * sizeof(float), s));
+        if (dbias) TR_HIP(hipMemsetAsync(dbias, 0, (size_t)types * N * sizeof(float), s));
+        if (dghat) TR_HIP(hipMemsetAsync(dghat, 0, (size_t)J * J * sizeof(float), s));
+        return SD_OK;
+    }
+    if (!x || !z || !dy || !W || !ghat) return sd::set_error(SD_E_INVALID, "gl_train_backward: null input");
+    if (!workspace || workspace_bytes < sd_gl_train_workspace_bytes(rows, J, K, N, n_types))
+        return sd::set_error(SD_E_INVALID, "gl_train_backward: workspace too small");
+    float* dz = (float*)workspace;
+    float* part = dz + rows * J * (int64_t)N;
+
+    // dghat first (reads dy and z, independent of dz)
+    if (dghat) {
+        const int64_t chunks = sd::ceil_div(rows, sd::kDghatRows);
+        if (J <= 32)
+            hipLaunchKernelGGL(sd::k_dghat_part<1>, dim3((unsigned)chunks), dim3(256), 0, s, dy, z, part, rows, J, N,
+                               sd::kDghatRows);
+        else
+            hipLaunchKernelGGL(sd::k_dghat_part<2>, dim3((unsigned)chunks), dim3(256), 0, s, dy, z, part, rows, J, N,
+                               sd::kDghatRows);
+        TR_HIP(hipGetLastError());
+        hipLaunchKernelGGL(sd::k_sum_parts, dim3((unsigned)sd::ceil_div((int64_t)J * J, 256)), dim3(256), 0, s, part,
+                           (int)chunks, (int64_t)J * J, dghat);
+        TR_HIP(hipGetLastError());
+    }
+    if (!dx && !dW && !dbias) return SD_OK;
+    hipLaunchKernelGGL(sd::k_mix, dim3((unsigned)rows, (unsigned)sd::ceil_div(N, 64)), dim3(256), 0, s, dy, ghat, dz,
+                       J, N, 1);
+    TR_HIP(hipGetLastError());
+    if (dx) {
+        GemmArgs g{};
+        g.A = dz; g.B = W; g.C = dx; g.bias = nullptr; g.types = tp;
+        g.M = (int)rows; g.N = K; g.K = N; g.J = J; g.by_type = 0; g.splits = 1; g.kchunk = N;
+        g.am = (int64_t)J * N; g.ak = 1; g.aj = N; g.at = 0;         // A[m][n] = dz[m, j, n]
+        g.bk = K; g.bn = 1; g.bj = 0; g.bt = (int64_t)N * K;         // B[n][k] = W[t][n][k]
+        g.cm = (int64_t)J * K; g.cz = K; g.cs = 0;                   // C[m][k] = dx[m, j, k]
+        hipLaunchKernelGGL(sd::k_gemm, dim3((unsigned)sd::ceil_div(K, sd::TN), (unsigned)sd::ceil_div(rows, sd::TM), J),
+                           dim3(256), 0, s, g);
+        TR_HIP(hipGetLastError());
+    }
+    if (dW) {
+        const int splits = sd::splits_for(rows);
+        const int kchunk = (int)sd::ceil_div(sd::ceil_div(rows, splits), sd::TK) * sd::TK;
+        GemmArgs g{};
+        g.A = dz; g.B = x; g.C = part; g.bias = nullptr; g.types = tp;
+        g.M = N; g.N = K; g.K = (int)rows; g.J = J; g.by_type = 1; g.splits = splits; g.kchunk = kchunk;
+        g.am = 1; g.ak = (int64_t)J * N; g.aj = N; g.at = 0;         // A[n][r] = dz[r, j, n]
+        g.bk = (int64_t)J * K; g.bn = 1; g.bj = K; g.bt = 0;         // B[r][k] = x[r, j, k]
+        g.cm = K; g.cz = (int64_t)N * K; g.cs = (int64_t)types * N * K;  // C[n][k] = part[s][t][n][k]
+        hipLaunchKernelGGL(sd::k_gemm,
+                           dim3((unsigned)sd::ceil_div(K, sd::TN), (unsigned)sd::ceil_div(N, sd::TM), types * splits),
+                           dim3(256), 0, s, g);
+        TR_HIP(hipGetLastError());
+        const int64_t n = (int64_t)types * N * K;
+        hipLaunchKernelGGL(sd::k_sum_parts, dim3((unsigned)sd::ceil_div(n, 256)), dim3(256), 0, s, part, splits, n, dW);
+        TR_HIP(hipGetLastError());
+    }
+    if (dbias) {
+        const int64_t chunks = sd::ceil_div(rows, sd::kRowsPerChunk);
+        hipLaunchKernelGGL(sd::k_dbias_part, dim3((unsigned)sd::ceil_div(N, 256), types, (unsigned)chunks), dim3(256), 0,
+                           s, dz, tp, part, rows, J, N, types, sd::kRowsPerChunk);
+        TR_HIP(hipGetLastError());
+        const int64_t n = (int64_t)types * N;
+        hipLaunchKernelGGL(sd::k_sum_parts, dim3((unsigned)sd::ceil_div(n, 256)), dim3(256), 0, s, part, (int)chunks, n,
+                           dbias);
+        TR_HIP(hipGetLastError());
+    }
+    return SD_OK;
+}
+
+}  // extern "C"

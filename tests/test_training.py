@@ -1,0 +1,190 @@
+"""Training-side StaticGraphLinear on HIP (SURVEY.md §8f "next" #4; csrc/sd_train.hip,
+skeletondiffusion_amd/training.py).
+
+Kernel parity: forward y and the backward's dx / dW / dbias / dG against float64 torch autograd
+over the reference's GraphLinear math (graph_structural.py:30-43: per-type W, bias before the
+G-hat mixing, G-hat = G / rowsum|G|), at the Denoiser's shapes (per-type H->H, 2H->H, to_qkv
+H->768, README shared weights) and ragged / empty / one-row batches.  Tolerance: max |diff| <=
+2e-5 x max |reference| (f32 products, f32 accumulate over <= a few thousand terms).
+Training step parity: the release Denoiser's p_losses on the device (HIP graph-linears) against
+the reference's own loss (golden fixture) and every parameter's gradient against the CPU torch
+path of the same module."""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from conftest import build_release_diffusion, golden, release_inputs
+from skeletondiffusion_amd import synthetic, training
+from skeletondiffusion_amd.core.network.layers import StaticGraphLinear
+
+REL_TOL = 2e-5
+
+
+def _ref_graph_linear(x, W, b, G, types, learn):
+    gh = F.normalize(G, p=1.0, dim=1) if learn else G
+    if types is not None:
+        z = torch.einsum("noi,rni->rno", W[types], x)
+        if b is not None:
+            z = z + b[types]
+    else:
+        z = x @ W.t()
+        if b is not None:
+            z = z + b
+    return gh.matmul(z)
+
+
+def _close(got, ref, what):
+    got = got.detach().double().cpu()
+    ref = ref.detach().double().cpu()
+    scale = float(ref.abs().max()) if ref.numel() else 0.0
+    err = float((got - ref).abs().max()) if ref.numel() else 0.0
+    assert err <= REL_TOL * max(scale, 1e-30) + 1e-12, f"{what}: max |diff| {err:.3e} vs max |ref| {scale:.3e}"
+
+
+CASES = [  # J, K, N, n_types (0 = shared), bias, learn_influence, rows
+    (16, 192, 192, 10, True, True, 257),
+    (16, 192, 768, 10, False, True, 64),
+    (21, 384, 192, 13, True, True, 100),
+    (17, 192, 96, 9, True, True, 65),
+    (51, 192, 96, 43, True, True, 33),
+    (16, 96, 96, 0, True, False, 8),
+    (16, 192, 192, 10, True, True, 1),
+]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("J,K,N,nt,bias,learn,rows", CASES)
+def test_gl_train_kernel_vs_autograd(J, K, N, nt, bias, learn, rows):
+    g = torch.Generator().manual_seed(J * 1000 + K + N + rows)
+    x = torch.rand(rows, J, K, generator=g, dtype=torch.float64) * 2 - 1
+    W = (torch.rand((nt, N, K) if nt else (N, K), generator=g, dtype=torch.float64) * 2 - 1) / K ** 0.5
+    b = (torch.rand((nt, N) if nt else (N,), generator=g, dtype=torch.float64) - 0.5) if bias else None
+    G = torch.eye(J, dtype=torch.float64) + 0.1 * torch.rand(J, J, generator=g, dtype=torch.float64)
+    types = torch.randint(0, nt, (J,), generator=g) if nt else None
+    if nt:
+        types[:nt] = torch.arange(nt)[: min(nt, J)]
+    dy = torch.rand(rows, J, N, generator=g, dtype=torch.float64) * 2 - 1
+
+    leaves = [t.clone().requires_grad_(True) for t in (x, W, G)] + ([b.clone().requires_grad_(True)] if bias else [])
+    y_ref = _ref_graph_linear(leaves[0], leaves[1], leaves[3] if bias else None, leaves[2], types, learn)
+    y_ref.backward(dy)
+
+    dev = torch.device("cuda:0")
+    dl = [t.float().to(dev).requires_grad_(True) for t in (x, W, G)] + \
+         ([b.float().to(dev).requires_grad_(True)] if bias else [])
+    gh = F.normalize(dl[2], p=1.0, dim=1) if learn else dl[2]
+    y = training.graph_linear(dl[0], dl[1], dl[3] if bias else None, gh,
+                              None if types is None else types.to(dev))
+    y.backward(dy.float().to(dev))
+    torch.cuda.synchronize()
+    _close(y, y_ref, "y")
+    _close(dl[0].grad, leaves[0].grad, "dx")
+    _close(dl[1].grad, leaves[1].grad, "dW")
+    if learn:
+        _close(dl[2].grad, leaves[2].grad, "dG")
+    if bias:
+        _close(dl[3].grad, leaves[3].grad, "dbias")
+
+
+@pytest.mark.gpu
+def test_gl_train_empty_batch():
+    dev = torch.device("cuda:0")
+    x = torch.zeros(0, 16, 64, device=dev, requires_grad=True)
+    W = torch.rand(3, 32, 64, device=dev, requires_grad=True)
+    b = torch.rand(3, 32, device=dev, requires_grad=True)
+    G = torch.eye(16, device=dev, requires_grad=True)
+    types = (torch.arange(16) % 3).to(dev)
+    y = training.graph_linear(x, W, b, G, types)
+    assert y.shape == (0, 16, 32)
+    y.sum().backward()
+    torch.cuda.synchronize()
+    assert x.grad.shape == x.shape
+    assert float(W.grad.abs().max()) == 0.0 and float(b.grad.abs().max()) == 0.0 and float(G.grad.abs().max()) == 0.0
+
+
+@pytest.mark.gpu
+def test_gl_train_deterministic():
+    dev = torch.device("cuda:0")
+    g = torch.Generator().manual_seed(7)
+    x = torch.rand(300, 16, 192, generator=g).to(dev).requires_grad_(True)
+    W = torch.rand(10, 192, 192, generator=g).to(dev).requires_grad_(True)
+    G = torch.rand(16, 16, generator=g).to(dev).requires_grad_(True)
+    types = (torch.arange(16) % 10).to(dev)
+    grads = []
+    for _ in range(2):
+        for t in (x, W, G):
+            t.grad = None
+        training.graph_linear(x, W, None, G, types).pow(2).sum().backward()
+        grads.append([t.grad.clone() for t in (x, W, G)])
+    for a, c in zip(*grads):
+        assert torch.equal(a, c)
+
+
+def _grad_fn_names(t):
+    seen, out, stack = set(), set(), [t.grad_fn]
+    while stack:
+        f = stack.pop()
+        if f is None or f in seen:
+            continue
+        seen.add(f)
+        out.add(type(f).__name__)
+        stack.extend(n for n, _ in f.next_functions)
+    return out
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["release_h36m16_T10", "release_amass21_T10"])
+def test_release_training_step_on_hip(name):
+    z = golden(name)
+    xcs, fu, start, _ = release_inputs(z)
+    xc = xcs.repeat_interleave(fu, 0)
+    B, J = start.shape[0], start.shape[1]
+    T = int(z["T"])
+    t_train = torch.arange(B) % T
+    noise = torch.from_numpy(synthetic.normal((B, J, 96), 24))
+    xs = torch.from_numpy(synthetic.uniform((B, J, 96), 25))
+
+    d_cpu = build_release_diffusion(z)
+    loss_c, _, _ = d_cpu.p_losses(xs, t_train, noise=noise, x_cond=xc)
+    loss_c.mean().backward()
+
+    dev = torch.device("cuda:0")
+    d_gpu = build_release_diffusion(z, device=dev)
+    assert training.hip_training_enabled()
+    loss_g, lw, mout = d_gpu.p_losses(xs.to(dev), t_train.to(dev), noise=noise.to(dev), x_cond=xc.to(dev))
+    assert "GraphLinearFunctionBackward" in _grad_fn_names(loss_g), "HIP graph-linear not on the training path"
+    loss_g.mean().backward()
+    torch.cuda.synchronize()
+    # the reference's own loss (gen_golden.py, reference p_losses on CPU)
+    np.testing.assert_allclose(loss_g.detach().cpu().numpy(), z["train_loss"], atol=1e-5, rtol=1e-5)
+    np.testing.assert_allclose(mout.detach().cpu().numpy(), z["train_model_out"], atol=1e-5, rtol=0)
+    pc = dict(d_cpu.named_parameters())
+    n_checked = 0
+    for k, p in d_gpu.named_parameters():
+        if pc[k].grad is None:
+            assert p.grad is None or float(p.grad.abs().max()) == 0.0, k
+            continue
+        # gradients of a mean L1 loss: compare against the CPU path's scale per tensor
+        got, ref = p.grad.double().cpu(), pc[k].grad.double()
+        err, scale = float((got - ref).abs().max()), float(ref.abs().max())
+        assert err <= 1e-3 * scale + 1e-9, f"{k}: max |diff| {err:.3e} vs max |ref| {scale:.3e}"
+        n_checked += 1
+    assert n_checked > 100
+
+
+def test_graph_linear_needs_device_tensors():
+    x = torch.zeros(2, 16, 8)
+    with pytest.raises(ValueError):
+        training.graph_linear(x, torch.zeros(4, 8), None, torch.eye(16), None)
+
+
+def test_cpu_module_keeps_torch_path():
+    m = StaticGraphLinear(8, 4, num_nodes=5, node_types=torch.tensor([0, 1, 0, 2, 1]), learn_influence=True)
+    x = torch.rand(3, 5, 8)
+    y = m(x)
+    ref = _ref_graph_linear(x, m.weight, m.bias, m.G, m.node_type_index, True)
+    torch.testing.assert_close(y, ref)
+    prev = training.set_hip_training(False)
+    assert prev is True and not training.hip_training_enabled()
+    training.set_hip_training(prev)
