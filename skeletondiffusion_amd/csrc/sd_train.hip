@@ -24,7 +24,8 @@
 namespace sd {
 namespace {
 
-constexpr int TM = 64, TN = 64, TK = 16;
+constexpr int TM = 64, TN = 64, TK = 32;
+constexpr int TE = TM * TK / 256;  // staged elements per thread and operand
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 // Strided batched GEMM: for batch z (grid.z = nbatch * splits):
@@ -44,9 +45,43 @@ struct GemmArgs {
     int64_t am, ak, aj, at, bk, bn, bj, bt, cm, cz, cs, bias_t;
 };
 
+// Tile staging: TK = 32 deep (measured: 64-deep tiles halve the workgroups per CU through LDS and
+// run 45 % slower), two LDS buffers, the next tile's global loads held in registers
+// while the MFMAs of the current one run (one barrier per tile).  The unit-stride dimension of
+// each operand runs over consecutive threads (am == 1 / bn == 1 select the mapping).
+struct TileRegs {
+    float a[TE], b[TE];
+};
+
+__device__ __forceinline__ void load_tile(const GemmArgs& g, const float* A, const float* B, int m0, int n0, int k0,
+                                          int kend, int tid, TileRegs& r) {
+#pragma unroll
+    for (int q = 0; q < TE; ++q) {
+        const int idx = tid + 256 * q;
+        int mm, kk;
+        if (g.am == 1) { mm = idx & 63; kk = idx >> 6; } else { kk = idx & (TK - 1); mm = idx / TK; }
+        const int gm = m0 + mm, gk = k0 + kk;
+        r.a[q] = (gm < g.M && gk < kend) ? A[gm * g.am + (int64_t)gk * g.ak] : 0.f;
+        int nn, kb;
+        if (g.bn == 1) { nn = idx & 63; kb = idx >> 6; } else { kb = idx & (TK - 1); nn = idx / TK; }
+        const int gn = n0 + nn, gkb = k0 + kb;
+        r.b[q] = (gn < g.N && gkb < kend) ? B[(int64_t)gkb * g.bk + gn * g.bn] : 0.f;
+    }
+}
+
+__device__ __forceinline__ void store_tile(const GemmArgs& g, float (*As)[TM + 4], float (*Bs)[TN + 4], int tid,
+                                           const TileRegs& r) {
+#pragma unroll
+    for (int q = 0; q < TE; ++q) {
+        const int idx = tid + 256 * q;
+        if (g.am == 1) As[idx >> 6][idx & 63] = r.a[q]; else As[idx & (TK - 1)][idx / TK] = r.a[q];
+        if (g.bn == 1) Bs[idx >> 6][idx & 63] = r.b[q]; else Bs[idx & (TK - 1)][idx / TK] = r.b[q];
+    }
+}
+
 __global__ __launch_bounds__(256) void k_gemm(GemmArgs g) {
-    __shared__ float As[TK][TM + 4];
-    __shared__ float Bs[TK][TN + 4];
+    __shared__ float As[2][TK][TM + 4];
+    __shared__ float Bs[2][TK][TN + 4];
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int wm = w >> 1, wn = w & 1;
     const int m0 = blockIdx.y * TM, n0 = blockIdx.x * TN;
@@ -62,31 +97,26 @@ __global__ __launch_bounds__(256) void k_gemm(GemmArgs g) {
     for (int j = jbeg; j < jend; ++j) {
         const int t = g.types ? (int)g.types[j] : 0;
         if (g.by_type && t != batch) continue;  // uniform over the workgroup
+        if (kbeg >= kend) continue;
         const float* A = g.A + j * g.aj + t * g.at;
         const float* B = g.B + j * g.bj + t * g.bt;
+        TileRegs r;
+        load_tile(g, A, B, m0, n0, kbeg, kend, tid, r);
+        store_tile(g, As[0], Bs[0], tid, r);
+        __syncthreads();
+        int cur = 0;
         for (int k0 = kbeg; k0 < kend; k0 += TK) {
-            // stage A (TM x TK) and B (TK x TN): 1024 elements each, 4 per thread; the unit-stride
-            // dimension runs over consecutive threads
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const int idx = tid + 256 * q;
-                int mm, kk;
-                if (g.am == 1) { mm = idx & 63; kk = idx >> 6; } else { kk = idx & 15; mm = idx >> 4; }
-                const int gm = m0 + mm, gk = k0 + kk;
-                As[kk][mm] = (gm < g.M && gk < kend) ? A[gm * g.am + (int64_t)gk * g.ak] : 0.f;
-                int nn, kb;
-                if (g.bn == 1) { nn = idx & 63; kb = idx >> 6; } else { kb = idx & 15; nn = idx >> 4; }
-                const int gn = n0 + nn, gkb = k0 + kb;
-                Bs[kb][nn] = (gn < g.N && gkb < kend) ? B[(int64_t)gkb * g.bk + gn * g.bn] : 0.f;
-            }
-            __syncthreads();
+            const bool more = k0 + TK < kend;
+            if (more) load_tile(g, A, B, m0, n0, k0 + TK, kend, tid, r);
 #pragma unroll
             for (int kk = 0; kk < TK; kk += 2) {
-                const float a = As[kk + (lane >> 5)][wm * 32 + (lane & 31)];
-                const float b = Bs[kk + (lane >> 5)][wn * 32 + (lane & 31)];
+                const float a = As[cur][kk + (lane >> 5)][wm * 32 + (lane & 31)];
+                const float b = Bs[cur][kk + (lane >> 5)][wn * 32 + (lane & 31)];
                 acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, acc, 0, 0, 0);
             }
+            if (more) store_tile(g, As[cur ^ 1], Bs[cur ^ 1], tid, r);
             __syncthreads();
+            cur ^= 1;
         }
     }
     // C/D map: col = lane & 31, row = (reg & 3) + 8 * (reg >> 2) + 4 * (lane >> 5)
@@ -233,6 +263,27 @@ __global__ __launch_bounds__(256) void k_sum_parts(const float* __restrict__ par
     out[e] = acc;
 }
 
+// out[e] = sum_s part[s][e] for few elements over many parts: one wave per element, lane l sums
+// parts l, l + 64, ..., then a fixed xor-shuffle tree (deterministic)
+__global__ __launch_bounds__(64) void k_sum_parts_wave(const float* __restrict__ part, int splits, int64_t n,
+                                                       float* __restrict__ out) {
+    const int64_t e = blockIdx.x;
+    const int l = threadIdx.x;
+    float acc = 0.f;
+    for (int s = l; s < splits; s += 64) acc += part[s * n + e];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o, 64);
+    if (l == 0) out[e] = acc;
+}
+
+hipError_t sum_parts(const float* part, int splits, int64_t n, float* out, hipStream_t s) {
+    if (splits >= 16 && n <= 65536)
+        hipLaunchKernelGGL(k_sum_parts_wave, dim3((unsigned)n), dim3(64), 0, s, part, splits, n, out);
+    else
+        hipLaunchKernelGGL(k_sum_parts, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, part, splits, n, out);
+    return hipGetLastError();
+}
+
 constexpr int kRowsPerChunk = 16;  // dbias partials
 constexpr int kDghatRows = 8;      // dghat partials (2 rows per wave)
 
@@ -327,9 +378,7 @@ int sd_gl_train_backward(const float* x, const float* z, const float* dy, const 
             hipLaunchKernelGGL(sd::k_dghat_part<2>, dim3((unsigned)chunks), dim3(256), 0, s, dy, z, part, rows, J, N,
                                sd::kDghatRows);
         TR_HIP(hipGetLastError());
-        hipLaunchKernelGGL(sd::k_sum_parts, dim3((unsigned)sd::ceil_div((int64_t)J * J, 256)), dim3(256), 0, s, part,
-                           (int)chunks, (int64_t)J * J, dghat);
-        TR_HIP(hipGetLastError());
+        TR_HIP(sd::sum_parts(part, (int)chunks, (int64_t)J * J, dghat, s));
     }
     if (!dx && !dW && !dbias) return SD_OK;
     hipLaunchKernelGGL(sd::k_mix, dim3((unsigned)rows, (unsigned)sd::ceil_div(N, 64)), dim3(256), 0, s, dy, ghat, dz,
@@ -360,8 +409,7 @@ int sd_gl_train_backward(const float* x, const float* z, const float* dy, const 
                            dim3(256), 0, s, g);
         TR_HIP(hipGetLastError());
         const int64_t n = (int64_t)types * N * K;
-        hipLaunchKernelGGL(sd::k_sum_parts, dim3((unsigned)sd::ceil_div(n, 256)), dim3(256), 0, s, part, splits, n, dW);
-        TR_HIP(hipGetLastError());
+        TR_HIP(sd::sum_parts(part, splits, n, dW, s));
     }
     if (dbias) {
         const int64_t chunks = sd::ceil_div(rows, sd::kRowsPerChunk);
@@ -369,9 +417,7 @@ int sd_gl_train_backward(const float* x, const float* z, const float* dy, const 
                            s, dz, tp, part, rows, J, N, types, sd::kRowsPerChunk);
         TR_HIP(hipGetLastError());
         const int64_t n = (int64_t)types * N;
-        hipLaunchKernelGGL(sd::k_sum_parts, dim3((unsigned)sd::ceil_div(n, 256)), dim3(256), 0, s, part, (int)chunks, n,
-                           dbias);
-        TR_HIP(hipGetLastError());
+        TR_HIP(sd::sum_parts(part, (int)chunks, n, dbias, s));
     }
     return SD_OK;
 }
