@@ -1,7 +1,7 @@
 #!/bin/bash
 # One bench line per BASELINE config shape (1 GPU), for DESIGN.md / profiles.
 mkdir -p gpurun_out
-for cfg in amass16 amass21 freeman17 mano51 h36m_t1000; do
+for cfg in ${CFGS:-amass16 amass21 freeman17 freeman17_half mano51 h36m_t1000}; do
   steps=2; [ $cfg = h36m_t1000 ] && steps=3
   timeout -k 10 300 python -u bench.py --config $cfg --steps $steps --warmup 1 --no-cpu-baseline > gpurun_out/cfg_$cfg.log 2>&1
   rc=$?; echo "$cfg rc=$rc"; [ $rc -eq 0 ] || exit $rc
