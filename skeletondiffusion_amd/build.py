@@ -9,7 +9,7 @@ import subprocess
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 OUT = os.path.join(HERE, "libskeldiff.so")
-SOURCES = ["sd_kernels.hip", "sd_graph_linear.hip", "sd_graph_linear_v3.hip", "sd_graph_linear_v4.hip",
+SOURCES = ["sd_kernels.hip", "sd_graph_linear.hip", "sd_graph_linear_v3.hip", "sd_graph_linear_v4.hip", "sd_graph_linear_v5.hip",
            "sd_metrics.hip", "sd_decoder.hip", "sd_train.hip", "sd_plan.hip"]
 HEADERS = ["sd_internal.h", os.path.join("..", "..", "include", "skeldiff.h")]
 

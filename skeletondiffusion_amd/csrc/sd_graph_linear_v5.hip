@@ -1,0 +1,190 @@
+// v5: StaticGraphLinear (graph_structural.py:30-43) + fused epilogue for LARGE skeletons
+// (J > 21: AMASS-MANO J = 51 with 43 node types, config 3).  Exact f32.
+//
+// The one-kernel generations keep all J nodes of a row tile in one workgroup, so every k chunk
+// stages the weights of every node type: at J = 51 that is 43 types (v3/v4 do not fit the LDS;
+// v2 fits with 16-column tiles only and reaches 17.7 TF/s).  v5 splits the layer in two:
+//   k_gl5_gemm   z[b, j, :] = s_bj W[type j] [x1_bj | x2_bj] + bias[type j]    per node j:
+//                a row-batched GEMM (64 rows x 64 columns per workgroup, 2 x 2 waves of
+//                v_mfma_f32_32x32x2_f32, K staged 32 deep, double-buffered with register
+//                prefetch), one weight slab per workgroup; s_bj = 1 / max(||x1_bj||, 1e-12) (RMS)
+//                from the staged x1 elements; z goes straight into `out`;
+//   k_gl5_mix    out[b, i, :] = act(FiLM(sum_j G-hat[i, j] z[b, j, :])) + res[b, i, :]   in place:
+//                one workgroup per (row, 64 columns) stages the row's J x 64 z slab in LDS before
+//                it writes the same slab (each element read and written by its own workgroup).
+// x1/x2 must not alias out.  When res aliases out (x = GL(h) + x), z goes to the caller's scratch
+// (GLArgs::zs, a dead activation buffer of the step) instead, so the residual is read intact.
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdint.h>
+
+#include "sd_internal.h"
+
+namespace sd {
+namespace {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+constexpr int TM = 64, TN = 64, TK = 32;
+constexpr int TE = TM * TK / 256;  // staged elements per thread and operand
+
+struct Regs {
+    float a[TE], b[TE];
+};
+
+// A (rows x K, k contiguous): thread element q is row (tid >> 5) + 8q, k = k0 + (tid & 31)
+__device__ __forceinline__ float x_elem(const GLArgs& p, int j, int64_t b, int k) {
+    if (k < p.K1) return p.x1[((b + p.x1_row0) / p.x1_div) * p.x1_rs + (int64_t)j * p.K1 + k];
+    return p.x2[b * p.x2_rs + (int64_t)j * p.K2 + (k - p.K1)];
+}
+
+template <bool RMS>
+__device__ __forceinline__ void load_stage(const GLArgs& p, const float* W, int j, int64_t m0, int n0, int k0, int K,
+                                           int tid, Regs& r, float* ssq) {
+    const int kk = tid & 31, mr = tid >> 5;
+    const int gk = k0 + kk;
+#pragma unroll
+    for (int q = 0; q < TE; ++q) {
+        const int64_t b = m0 + mr + 8 * q;
+        const float v = (b < p.B && gk < K) ? x_elem(p, j, b, gk) : 0.f;
+        r.a[q] = v;
+        if (RMS && gk < p.K1) ssq[q] = fmaf(v, v, ssq[q]);
+        const int n = n0 + mr + 8 * q;
+        r.b[q] = (n < p.N && gk < K) ? W[(int64_t)n * K + gk] : 0.f;
+    }
+}
+
+__device__ __forceinline__ void store_stage(float (*As)[TM + 4], float (*Bs)[TN + 4], int tid, const Regs& r) {
+    const int kk = tid & 31, mr = tid >> 5;
+#pragma unroll
+    for (int q = 0; q < TE; ++q) {
+        As[kk][mr + 8 * q] = r.a[q];
+        Bs[kk][mr + 8 * q] = r.b[q];
+    }
+}
+
+template <bool RMS>
+__global__ __launch_bounds__(256) void k_gl5_gemm(const GLArgs p, float* __restrict__ z, int64_t z_rs) {
+    __shared__ float As[2][TK][TM + 4];
+    __shared__ float Bs[2][TK][TN + 4];
+    __shared__ float s_scale[TM];
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int wm = w >> 1, wn = w & 1;
+    const int j = blockIdx.z;
+    const int64_t m0 = (int64_t)blockIdx.y * TM;
+    const int n0 = blockIdx.x * TN;
+    const int K = p.K1 + p.K2;
+    const float* W = p.W + (int64_t)p.wrow[j] * K;
+
+    f32x16 acc;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) acc[i] = 0.f;
+    float ssq[TE];
+#pragma unroll
+    for (int q = 0; q < TE; ++q) ssq[q] = 0.f;
+
+    Regs r;
+    load_stage<RMS>(p, W, j, m0, n0, 0, K, tid, r, ssq);
+    store_stage(As[0], Bs[0], tid, r);
+    __syncthreads();
+    int cur = 0;
+    for (int k0 = 0; k0 < K; k0 += TK) {
+        const bool more = k0 + TK < K;
+        if (more) load_stage<RMS>(p, W, j, m0, n0, k0 + TK, K, tid, r, ssq);
+#pragma unroll
+        for (int kk = 0; kk < TK; kk += 2) {
+            const float a = As[cur][kk + (lane >> 5)][wm * 32 + (lane & 31)];
+            const float b = Bs[cur][kk + (lane >> 5)][wn * 32 + (lane & 31)];
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, acc, 0, 0, 0);
+        }
+        if (more) store_stage(As[cur ^ 1], Bs[cur ^ 1], tid, r);
+        __syncthreads();
+        cur ^= 1;
+    }
+    if (RMS) {  // F.normalize(x1, dim=-1): the 32 lanes of a half-wave hold one row's k slice
+#pragma unroll
+        for (int q = 0; q < TE; ++q) {
+            float t = ssq[q];
+#pragma unroll
+            for (int o = 1; o < 32; o <<= 1) t += __shfl_xor(t, o, 64);
+            if ((tid & 31) == 0) s_scale[(tid >> 5) + 8 * q] = 1.0f / fmaxf(sqrtf(t), 1e-12f);
+        }
+        __syncthreads();
+    }
+    // C/D map: col = lane & 31, row = (reg & 3) + 8 * (reg >> 2) + 4 * (lane >> 5)
+    const int n = n0 + wn * 32 + (lane & 31);
+    if (n >= p.N) return;
+    const float bv = p.bias ? p.bias[p.wrow[j] + n] : 0.f;
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+        const int m = wm * 32 + (e & 3) + 8 * (e >> 2) + 4 * (lane >> 5);
+        const int64_t b = m0 + m;
+        if (b < p.B) {
+            const float v = RMS ? acc[e] * s_scale[m] : acc[e];
+            z[b * z_rs + (int64_t)j * p.N + n] = v + bv;
+        }
+    }
+}
+
+__global__ __launch_bounds__(256) void k_gl5_mix(const GLArgs p, const float* z, int64_t z_rs) {
+    __shared__ float s_z[kMaxNodes][64];
+    __shared__ float s_g[kMaxNodes][kMaxNodes + 1];
+    const int tid = threadIdx.x, J = p.J, N = p.N;
+    const int64_t b = blockIdx.x;
+    const int n0 = blockIdx.y * 64;
+    float* orow = p.out + b * p.out_rs;
+    const float* zrow = z + b * z_rs;
+    for (int e = tid; e < J * J; e += 256) s_g[e / J][e % J] = p.G[e];
+    for (int e = tid; e < J * 64; e += 256) {
+        const int jj = e >> 6, c = e & 63;
+        s_z[jj][c] = (n0 + c < N) ? zrow[(int64_t)jj * N + n0 + c] : 0.f;
+    }
+    __syncthreads();
+    const int c = tid & 63, n = n0 + c;
+    if (n >= N) return;
+    float fa = 1.f, fb = 0.f;
+    if (p.film) {
+        fa = p.film[n] + 1.0f;
+        fb = p.film[N + n];
+    }
+    for (int i = tid >> 6; i < J; i += 4) {
+        float v = 0.f;
+        for (int jj = 0; jj < J; ++jj) v = fmaf(s_g[i][jj], s_z[jj][c], v);
+        if (p.film) v = v * fa + fb;
+        if (p.act == 1) v = tanhf(v);
+        if (p.res) v += p.res[b * p.res_rs + (int64_t)i * N + n];
+        orow[(int64_t)i * N + n] = v;
+    }
+}
+
+}  // namespace
+
+// Row-major operands only; J <= kMaxNodes.  hipErrorNotSupported where v5 does not apply.
+hipError_t launch_graph_linear_v5(const GLArgs& a, bool rms, hipStream_t s) {
+    if (a.B <= 0) return hipSuccess;
+    if (a.J < 1 || a.J > kMaxNodes || a.x1_blk || a.x2_blk || a.res_blk || a.out_blk) return hipErrorNotSupported;
+    if (a.x1 == a.out || (a.x2 && a.x2 == a.out)) return hipErrorNotSupported;  // in-place GEMM would race
+    float* z = a.out;
+    int64_t z_rs = a.out_rs;
+    if (a.res && a.res == a.out) {  // the residual must survive the GEMM: z into the scratch
+        if (!a.zs || a.zs_cap < a.B * a.J * (int64_t)a.N || a.zs == a.x1 || a.zs == a.x2) return hipErrorNotSupported;
+        z = a.zs;
+        z_rs = (int64_t)a.J * a.N;
+    } else if (a.res && a.res < a.out + a.B * a.out_rs && a.out < a.res + a.B * a.res_rs) {
+        return hipErrorNotSupported;  // partial overlap
+    }
+    const int64_t row_tiles = (a.B + TM - 1) / TM;
+    if (row_tiles > 65535 || a.B > 65535 * 1024LL) return hipErrorNotSupported;
+    const dim3 g1((unsigned)((a.N + TN - 1) / TN), (unsigned)row_tiles, (unsigned)a.J);
+    if (rms)
+        hipLaunchKernelGGL(k_gl5_gemm<true>, g1, dim3(256), 0, s, a, z, z_rs);
+    else
+        hipLaunchKernelGGL(k_gl5_gemm<false>, g1, dim3(256), 0, s, a, z, z_rs);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    const dim3 g2((unsigned)a.B, (unsigned)((a.N + 63) / 64));
+    hipLaunchKernelGGL(k_gl5_mix, g2, dim3(256), 0, s, a, (const float*)z, z_rs);
+    return hipGetLastError();
+}
+
+}  // namespace sd

@@ -42,6 +42,8 @@ struct GLArgs {
     // v4 only: operand / result layouts, 0 = row-major (B, J, F), 1 = row-blocked (blk_off in
     // sd_graph_linear_v4.hip; rows padded to 32)
     int x1_blk, x2_blk, res_blk, out_blk;
+    // v5 only: scratch for the pre-mix activations when res aliases out (zs_cap floats), or null
+    float* zs; int64_t zs_cap;
 };
 
 // f16 hi/lo split of a (types, N, K) f32 weight in MFMA B-fragment order (sd_graph_linear_v4.hip)
@@ -72,7 +74,8 @@ struct UpdArgs {
     int64_t B; int J; int D;
 };
 
-hipError_t launch_graph_linear(const GLArgs& a, bool rms, hipStream_t s);     // dispatches v1..v4
+hipError_t launch_graph_linear(const GLArgs& a, bool rms, hipStream_t s);     // dispatches v1..v5
+hipError_t launch_graph_linear_v5(const GLArgs& a, bool rms, hipStream_t s);  // J > 21: GEMM + mixing pass
 hipError_t launch_graph_linear_v1(const GLArgs& a, bool rms, hipStream_t s);
 hipError_t launch_graph_linear_v2(const GLArgs& a, bool rms, hipStream_t s);
 hipError_t launch_graph_linear_v3(const GLArgs& a, bool rms, hipStream_t s);  // J in {16,17,21}

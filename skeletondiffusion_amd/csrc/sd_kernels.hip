@@ -193,13 +193,13 @@ static hipError_t gl_dispatch_rms(const GLArgs& a, bool rms, hipStream_t s) {
 static int g_gl_variant = [] {
     const char* e = getenv("SKELDIFF_GL_VARIANT");
     const int x = e ? atoi(e) : 0;
-    return (x >= 0 && x <= 4) ? x : 0;
+    return (x >= 0 && x <= 5) ? x : 0;
 }();
 
 int graph_linear_variant() { return g_gl_variant; }
 
 int set_graph_linear_variant(int v) {
-    if (v < 0 || v > 4) return -1;
+    if (v < 0 || v > 5) return -1;
     const int old = g_gl_variant;
     g_gl_variant = v;
     return old;
@@ -208,7 +208,9 @@ int set_graph_linear_variant(int v) {
 // 0 (default): v4 (f32-accurate split-f16 MFMA) where the plan prepared split weights and the
 // skeleton has an instantiation; otherwise the exact-f32 kernels per shape: v3 (node-split
 // waves, 32x32 f32 MFMA) for N < 512, where it measured 1.15-1.25x faster than v2; v2 with
-// 32-column tiles for the wide to_qkv layer (N = 768).  1/2/3/4 force one generation.
+// 32-column tiles for the wide to_qkv layer (N = 768); v5 (node-batched GEMM + mixing pass) for
+// J > 21, where every one-kernel tile must stage all node types' weights.  1..5 force one
+// generation (falling through to v2 where the forced one does not apply).
 hipError_t launch_graph_linear(const GLArgs& a, bool rms, hipStream_t s) {
     const int v = graph_linear_variant();
     if (v == 1) return launch_graph_linear_v1(a, rms, s);
@@ -218,6 +220,11 @@ hipError_t launch_graph_linear(const GLArgs& a, bool rms, hipStream_t s) {
     }
     // the exact-f32 generations read and write row-major activations only
     if (a.x1_blk || a.x2_blk || a.res_blk || a.out_blk) return hipErrorNotSupported;
+    // large skeletons (J > 21, MANO J = 51: 43 node types): node-batched GEMM + mixing pass
+    if (v == 5 || (v == 0 && a.J > 21)) {
+        const hipError_t e = launch_graph_linear_v5(a, rms, s);
+        if (e != hipErrorNotSupported) return e;
+    }
     if (v == 3 || (v == 0 && a.N < 512)) {
         const hipError_t e = launch_graph_linear_v3(a, rms, s);
         if (e != hipErrorNotSupported) return e;

@@ -276,7 +276,12 @@ int run_denoiser(const sd_plan* p, const float* x_t, const float* x_cond, int64_
     // v4 path: every intermediate activation in the row-blocked layout (coalesced x fragments);
     // the denoiser's inputs (x_t, x_cond) and output (x0) stay row-major
     const int B = p->blocked_now() ? 1 : 0;
-    auto lay = [B, tile_hint](sd::GLArgs& g, int in, int res, int out) {
+    // v5 scratch (pre-mix activations of layers whose residual aliases their output): the qkv
+    // buffer, dead outside the attention block (>= rows * J * H floats)
+    const int64_t zs_cap = rows * p->J * (int64_t)(p->d.use_attention ? 3 * p->hid : p->H);
+    auto lay = [B, tile_hint, &w, zs_cap](sd::GLArgs& g, int in, int res, int out) {
+        g.zs = w.qkv;
+        g.zs_cap = zs_cap;
         g.tile_hint = tile_hint;
         g.x1_blk = g.x2_blk = B & in;
         g.res_blk = B & res;

@@ -123,6 +123,13 @@ def test_graph_linear_generations(case, variant, tile, kernel_variant, cuda):
     _check_gl(*case, 67, cuda)
 
 
+@pytest.mark.parametrize("case", CASES)
+def test_graph_linear_v5(case, kernel_variant, cuda):
+    """v5 (node-batched GEMM + mixing pass; the default for J > 21) forced on every shape."""
+    kernel_variant(5, 0)
+    _check_gl(*case, 67, cuda)
+
+
 def test_kernel_variant_rejects_bad_value():
     L = _lib.lib()
     assert L.sd_set_kernel_variant(9, -1) < 0
