@@ -126,30 +126,53 @@ __global__ __launch_bounds__(256) void k_gl5_gemm(const GLArgs p, float* __restr
     }
 }
 
+// Each thread owns one column and the 16 rows i = 16 * wave + q: per source node one LDS read of
+// z and four 16-B broadcast reads of G-hat^T[j][16 wave .. +15] feed 16 multiply-adds (the
+// one-row-per-step form issued two LDS reads per multiply-add and was LDS-bound at ~1.3 TB/s).
 __global__ __launch_bounds__(256) void k_gl5_mix(const GLArgs p, const float* z, int64_t z_rs) {
     __shared__ float s_z[kMaxNodes][64];
-    __shared__ float s_g[kMaxNodes][kMaxNodes + 1];
+    __shared__ __attribute__((aligned(16))) float s_gt[kMaxNodes][kMaxNodes + 4];
     const int tid = threadIdx.x, J = p.J, N = p.N;
     const int64_t b = blockIdx.x;
     const int n0 = blockIdx.y * 64;
     float* orow = p.out + b * p.out_rs;
     const float* zrow = z + b * z_rs;
-    for (int e = tid; e < J * J; e += 256) s_g[e / J][e % J] = p.G[e];
+    for (int e = tid; e < J * kMaxNodes; e += 256) {
+        const int jj = e / kMaxNodes, i = e % kMaxNodes;
+        s_gt[jj][i] = i < J ? p.G[i * J + jj] : 0.f;
+    }
     for (int e = tid; e < J * 64; e += 256) {
         const int jj = e >> 6, c = e & 63;
         s_z[jj][c] = (n0 + c < N) ? zrow[(int64_t)jj * N + n0 + c] : 0.f;
     }
     __syncthreads();
-    const int c = tid & 63, n = n0 + c;
-    if (n >= N) return;
+    const int c = tid & 63, n = n0 + c, i0 = 16 * (tid >> 6);
+    if (n >= N || i0 >= J) return;
+    float acc[16];
+#pragma unroll
+    for (int q = 0; q < 16; ++q) acc[q] = 0.f;
+    for (int jj = 0; jj < J; ++jj) {
+        const float zv = s_z[jj][c];
+        const float4* g4 = reinterpret_cast<const float4*>(&s_gt[jj][i0]);
+#pragma unroll
+        for (int v = 0; v < 4; ++v) {
+            const float4 g = g4[v];
+            acc[4 * v + 0] = fmaf(g.x, zv, acc[4 * v + 0]);
+            acc[4 * v + 1] = fmaf(g.y, zv, acc[4 * v + 1]);
+            acc[4 * v + 2] = fmaf(g.z, zv, acc[4 * v + 2]);
+            acc[4 * v + 3] = fmaf(g.w, zv, acc[4 * v + 3]);
+        }
+    }
     float fa = 1.f, fb = 0.f;
     if (p.film) {
         fa = p.film[n] + 1.0f;
         fb = p.film[N + n];
     }
-    for (int i = tid >> 6; i < J; i += 4) {
-        float v = 0.f;
-        for (int jj = 0; jj < J; ++jj) v = fmaf(s_g[i][jj], s_z[jj][c], v);
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+        const int i = i0 + q;
+        if (i >= J) break;
+        float v = acc[q];
         if (p.film) v = v * fa + fb;
         if (p.act == 1) v = tanhf(v);
         if (p.res) v += p.res[b * p.res_rs + (int64_t)i * N + n];
