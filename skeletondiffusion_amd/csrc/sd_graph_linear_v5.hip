@@ -129,8 +129,8 @@ __global__ __launch_bounds__(256) void k_gl5_gemm(const GLArgs p, float* __restr
 // Each thread owns one column and the 16 rows i = 16 * wave + q: per source node one LDS read of
 // z and four 16-B broadcast reads of G-hat^T[j][16 wave .. +15] feed 16 multiply-adds (the
 // one-row-per-step form issued two LDS reads per multiply-add and was LDS-bound at ~1.3 TB/s).
-__global__ __launch_bounds__(256) void k_gl5_mix(const GLArgs p, const float* z, int64_t z_rs) {
-    __shared__ float s_z[kMaxNodes][64];
+__global__ __launch_bounds__(256) void k_gl5_mix(const GLArgs p, const float* z, int64_t z_rs, int vec) {
+    __shared__ __attribute__((aligned(16))) float s_z[kMaxNodes][64];
     __shared__ __attribute__((aligned(16))) float s_gt[kMaxNodes][kMaxNodes + 4];
     const int tid = threadIdx.x, J = p.J, N = p.N;
     const int64_t b = blockIdx.x;
@@ -141,9 +141,17 @@ __global__ __launch_bounds__(256) void k_gl5_mix(const GLArgs p, const float* z,
         const int jj = e / kMaxNodes, i = e % kMaxNodes;
         s_gt[jj][i] = i < J ? p.G[i * J + jj] : 0.f;
     }
-    for (int e = tid; e < J * 64; e += 256) {
-        const int jj = e >> 6, c = e & 63;
-        s_z[jj][c] = (n0 + c < N) ? zrow[(int64_t)jj * N + n0 + c] : 0.f;
+    if (vec && n0 + 64 <= N) {  // 16-B pieces (z, N and z_rs 16-B aligned: checked at launch)
+        for (int e = tid; e < J * 16; e += 256) {
+            const int jj = e >> 4, c4 = (e & 15) * 4;
+            *reinterpret_cast<float4*>(&s_z[jj][c4]) =
+                *reinterpret_cast<const float4*>(zrow + (int64_t)jj * N + n0 + c4);
+        }
+    } else {
+        for (int e = tid; e < J * 64; e += 256) {
+            const int jj = e >> 6, c = e & 63;
+            s_z[jj][c] = (n0 + c < N) ? zrow[(int64_t)jj * N + n0 + c] : 0.f;
+        }
     }
     __syncthreads();
     const int c = tid & 63, n = n0 + c, i0 = 16 * (tid >> 6);
@@ -206,7 +214,8 @@ hipError_t launch_graph_linear_v5(const GLArgs& a, bool rms, hipStream_t s) {
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     const dim3 g2((unsigned)a.B, (unsigned)((a.N + 63) / 64));
-    hipLaunchKernelGGL(k_gl5_mix, g2, dim3(256), 0, s, a, (const float*)z, z_rs);
+    const int vec = ((uintptr_t)z & 15) == 0 && (a.N & 3) == 0 && (z_rs & 3) == 0;
+    hipLaunchKernelGGL(k_gl5_mix, g2, dim3(256), 0, s, a, (const float*)z, z_rs, vec);
     return hipGetLastError();
 }
 
