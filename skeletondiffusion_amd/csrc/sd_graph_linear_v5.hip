@@ -6,8 +6,8 @@
 // v2 fits with 16-column tiles only and reaches 17.7 TF/s).  v5 splits the layer in two:
 //   k_gl5_gemm   z[b, j, :] = s_bj W[type j] [x1_bj | x2_bj] + bias[type j]    per node j:
 //                a row-batched GEMM (64 rows x 64 columns per workgroup, 2 x 2 waves of
-//                v_mfma_f32_32x32x2_f32, K staged 32 deep, double-buffered with register
-//                prefetch), one weight slab per workgroup; s_bj = 1 / max(||x1_bj||, 1e-12) (RMS)
+//                v_mfma_f32_32x32x2_f32, K staged 32 deep in 16-B pieces, double-buffered with
+//                register prefetch), one weight slab per workgroup; s_bj = 1 / max(||x1_bj||, 1e-12) (RMS)
 //                from the staged x1 elements; z goes straight into `out`;
 //   k_gl5_mix    out[b, i, :] = act(FiLM(sum_j G-hat[i, j] z[b, j, :])) + res[b, i, :]   in place:
 //                one workgroup per (row, 64 columns) stages the row's J x 64 z slab in LDS before
@@ -26,40 +26,43 @@ namespace {
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 constexpr int TM = 64, TN = 64, TK = 32;
-constexpr int TE = TM * TK / 256;  // staged elements per thread and operand
 
 struct Regs {
-    float a[TE], b[TE];
+    float4 a[2], b[2];
 };
 
-// A (rows x K, k contiguous): thread element q is row (tid >> 5) + 8q, k = k0 + (tid & 31)
-__device__ __forceinline__ float x_elem(const GLArgs& p, int j, int64_t b, int k) {
-    if (k < p.K1) return p.x1[((b + p.x1_row0) / p.x1_div) * p.x1_rs + (int64_t)j * p.K1 + k];
-    return p.x2[b * p.x2_rs + (int64_t)j * p.K2 + (k - p.K1)];
+// A (rows x K, k contiguous), 16-B pieces: thread piece q is row (tid >> 3) + 32q, k = k0 + 4 (tid & 7)
+// (K1, K2, row strides and bases 16-B aligned: checked at launch; a piece never straddles K1)
+__device__ __forceinline__ float4 x_piece(const GLArgs& p, int j, int64_t b, int k) {
+    if (k < p.K1)
+        return *reinterpret_cast<const float4*>(p.x1 + ((b + p.x1_row0) / p.x1_div) * p.x1_rs + (int64_t)j * p.K1 + k);
+    return *reinterpret_cast<const float4*>(p.x2 + b * p.x2_rs + (int64_t)j * p.K2 + (k - p.K1));
 }
 
 template <bool RMS>
 __device__ __forceinline__ void load_stage(const GLArgs& p, const float* W, int j, int64_t m0, int n0, int k0, int K,
                                            int tid, Regs& r, float* ssq) {
-    const int kk = tid & 31, mr = tid >> 5;
-    const int gk = k0 + kk;
+    const int kq = 4 * (tid & 7), mr = tid >> 3;
+    const int gk = k0 + kq;
+    const float4 zero = make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
-    for (int q = 0; q < TE; ++q) {
-        const int64_t b = m0 + mr + 8 * q;
-        const float v = (b < p.B && gk < K) ? x_elem(p, j, b, gk) : 0.f;
+    for (int q = 0; q < 2; ++q) {
+        const int64_t b = m0 + mr + 32 * q;
+        const float4 v = (b < p.B && gk < K) ? x_piece(p, j, b, gk) : zero;
         r.a[q] = v;
-        if (RMS && gk < p.K1) ssq[q] = fmaf(v, v, ssq[q]);
-        const int n = n0 + mr + 8 * q;
-        r.b[q] = (n < p.N && gk < K) ? W[(int64_t)n * K + gk] : 0.f;
+        if (RMS && gk < p.K1) ssq[q] += v.x * v.x + v.y * v.y + v.z * v.z + v.w * v.w;
+        const int n = n0 + mr + 32 * q;
+        r.b[q] = (n < p.N && gk < K) ? *reinterpret_cast<const float4*>(W + (int64_t)n * K + gk) : zero;
     }
 }
 
 __device__ __forceinline__ void store_stage(float (*As)[TM + 4], float (*Bs)[TN + 4], int tid, const Regs& r) {
-    const int kk = tid & 31, mr = tid >> 5;
+    const int kq = 4 * (tid & 7), mr = tid >> 3;
 #pragma unroll
-    for (int q = 0; q < TE; ++q) {
-        As[kk][mr + 8 * q] = r.a[q];
-        Bs[kk][mr + 8 * q] = r.b[q];
+    for (int q = 0; q < 2; ++q) {
+        const int m = mr + 32 * q;
+        As[kq + 0][m] = r.a[q].x; As[kq + 1][m] = r.a[q].y; As[kq + 2][m] = r.a[q].z; As[kq + 3][m] = r.a[q].w;
+        Bs[kq + 0][m] = r.b[q].x; Bs[kq + 1][m] = r.b[q].y; Bs[kq + 2][m] = r.b[q].z; Bs[kq + 3][m] = r.b[q].w;
     }
 }
 
@@ -79,9 +82,7 @@ __global__ __launch_bounds__(256) void k_gl5_gemm(const GLArgs p, float* __restr
     f32x16 acc;
 #pragma unroll
     for (int i = 0; i < 16; ++i) acc[i] = 0.f;
-    float ssq[TE];
-#pragma unroll
-    for (int q = 0; q < TE; ++q) ssq[q] = 0.f;
+    float ssq[2] = {0.f, 0.f};
 
     Regs r;
     load_stage<RMS>(p, W, j, m0, n0, 0, K, tid, r, ssq);
@@ -101,13 +102,13 @@ __global__ __launch_bounds__(256) void k_gl5_gemm(const GLArgs p, float* __restr
         __syncthreads();
         cur ^= 1;
     }
-    if (RMS) {  // F.normalize(x1, dim=-1): the 32 lanes of a half-wave hold one row's k slice
+    if (RMS) {  // F.normalize(x1, dim=-1): 8 consecutive lanes hold one row's k slice
 #pragma unroll
-        for (int q = 0; q < TE; ++q) {
+        for (int q = 0; q < 2; ++q) {
             float t = ssq[q];
 #pragma unroll
-            for (int o = 1; o < 32; o <<= 1) t += __shfl_xor(t, o, 64);
-            if ((tid & 31) == 0) s_scale[(tid >> 5) + 8 * q] = 1.0f / fmaxf(sqrtf(t), 1e-12f);
+            for (int o = 1; o < 8; o <<= 1) t += __shfl_xor(t, o, 64);
+            if ((tid & 7) == 0) s_scale[(tid >> 3) + 32 * q] = 1.0f / fmaxf(sqrtf(t), 1e-12f);
         }
         __syncthreads();
     }
@@ -195,6 +196,10 @@ hipError_t launch_graph_linear_v5(const GLArgs& a, bool rms, hipStream_t s) {
     if (a.B <= 0) return hipSuccess;
     if (a.J < 1 || a.J > kMaxNodes || a.x1_blk || a.x2_blk || a.res_blk || a.out_blk) return hipErrorNotSupported;
     if (a.x1 == a.out || (a.x2 && a.x2 == a.out)) return hipErrorNotSupported;  // in-place GEMM would race
+    // 16-B operand pieces
+    if ((a.K1 & 3) || (a.K2 & 3) || (a.x1_rs & 3) || (a.K2 && (a.x2_rs & 3)) || ((uintptr_t)a.x1 & 15) ||
+        ((uintptr_t)a.x2 & 15) || ((uintptr_t)a.W & 15))
+        return hipErrorNotSupported;
     float* z = a.out;
     int64_t z_rs = a.out_rs;
     if (a.res && a.res == a.out) {  // the residual must survive the GEMM: z into the scratch
