@@ -154,9 +154,14 @@ __global__ __launch_bounds__(256) void k_gl5_mix(const GLArgs p, const float* z,
             s_z[jj][c] = (n0 + c < N) ? zrow[(int64_t)jj * N + n0 + c] : 0.f;
         }
     }
-    __syncthreads();
+    // the residual pieces are loaded before the barrier, so their latency overlaps the mixing
     const int c = tid & 63, n = n0 + c, i0 = 16 * (tid >> 6);
-    if (n >= N || i0 >= J) return;
+    const bool live = n < N && i0 < J;
+    float rv[16];
+#pragma unroll
+    for (int q = 0; q < 16; ++q) rv[q] = (p.res && live && i0 + q < J) ? p.res[b * p.res_rs + (int64_t)(i0 + q) * N + n] : 0.f;
+    __syncthreads();
+    if (!live) return;
     float acc[16];
 #pragma unroll
     for (int q = 0; q < 16; ++q) acc[q] = 0.f;
@@ -184,8 +189,7 @@ __global__ __launch_bounds__(256) void k_gl5_mix(const GLArgs p, const float* z,
         float v = acc[q];
         if (p.film) v = v * fa + fb;
         if (p.act == 1) v = tanhf(v);
-        if (p.res) v += p.res[b * p.res_rs + (int64_t)i * N + n];
-        orow[(int64_t)i * N + n] = v;
+        orow[(int64_t)i * N + n] = v + rv[q];
     }
 }
 
