@@ -79,9 +79,52 @@ __device__ __forceinline__ void store_tile(const GemmArgs& g, float (*As)[TM + 4
     }
 }
 
+// 16-B pieces (VEC): 512 float4 per operand tile, 2 per thread, along the operand's unit-stride
+// dimension (k: kq = 4 (tid & 7), row (tid >> 3) + 32 q;  m / n: 4 (tid & 15), k (tid >> 4) + 16 q).
+// The host checks strides, extents and bases are multiples of 4 floats / 16 B (gemm_vec_ok).
+struct TileRegs4 {
+    float4 a[2], b[2];
+};
+
+__device__ __forceinline__ void load_tile4(const GemmArgs& g, const float* A, const float* B, int m0, int n0, int k0,
+                                           int kend, int tid, TileRegs4& r) {
+    const float4 zero = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+        int mm, kk;
+        if (g.ak == 1) { kk = 4 * (tid & 7); mm = (tid >> 3) + 32 * q; } else { mm = 4 * (tid & 15); kk = (tid >> 4) + 16 * q; }
+        const int gm = m0 + mm, gk = k0 + kk;
+        r.a[q] = (gm < g.M && gk < kend) ? *reinterpret_cast<const float4*>(A + gm * g.am + (int64_t)gk * g.ak) : zero;
+        int nn, kb;
+        if (g.bk == 1) { kb = 4 * (tid & 7); nn = (tid >> 3) + 32 * q; } else { nn = 4 * (tid & 15); kb = (tid >> 4) + 16 * q; }
+        const int gn = n0 + nn, gkb = k0 + kb;
+        r.b[q] = (gn < g.N && gkb < kend) ? *reinterpret_cast<const float4*>(B + (int64_t)gkb * g.bk + gn * g.bn) : zero;
+    }
+}
+
+__device__ __forceinline__ void store_tile4(const GemmArgs& g, float (*As)[TM + 4], float (*Bs)[TN + 4], int tid,
+                                            const TileRegs4& r) {
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+        if (g.ak == 1) {
+            const int kk = 4 * (tid & 7), mm = (tid >> 3) + 32 * q;
+            As[kk][mm] = r.a[q].x; As[kk + 1][mm] = r.a[q].y; As[kk + 2][mm] = r.a[q].z; As[kk + 3][mm] = r.a[q].w;
+        } else {
+            *reinterpret_cast<float4*>(&As[(tid >> 4) + 16 * q][4 * (tid & 15)]) = r.a[q];
+        }
+        if (g.bk == 1) {
+            const int kb = 4 * (tid & 7), nn = (tid >> 3) + 32 * q;
+            Bs[kb][nn] = r.b[q].x; Bs[kb + 1][nn] = r.b[q].y; Bs[kb + 2][nn] = r.b[q].z; Bs[kb + 3][nn] = r.b[q].w;
+        } else {
+            *reinterpret_cast<float4*>(&Bs[(tid >> 4) + 16 * q][4 * (tid & 15)]) = r.b[q];
+        }
+    }
+}
+
+template <bool VEC>
 __global__ __launch_bounds__(256) void k_gemm(GemmArgs g) {
-    __shared__ float As[2][TK][TM + 4];
-    __shared__ float Bs[2][TK][TN + 4];
+    __shared__ __attribute__((aligned(16))) float As[2][TK][TM + 4];
+    __shared__ __attribute__((aligned(16))) float Bs[2][TK][TN + 4];
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int wm = w >> 1, wn = w & 1;
     const int m0 = blockIdx.y * TM, n0 = blockIdx.x * TN;
@@ -101,20 +144,32 @@ __global__ __launch_bounds__(256) void k_gemm(GemmArgs g) {
         const float* A = g.A + j * g.aj + t * g.at;
         const float* B = g.B + j * g.bj + t * g.bt;
         TileRegs r;
-        load_tile(g, A, B, m0, n0, kbeg, kend, tid, r);
-        store_tile(g, As[0], Bs[0], tid, r);
+        TileRegs4 r4;
+        if (VEC) {
+            load_tile4(g, A, B, m0, n0, kbeg, kend, tid, r4);
+            store_tile4(g, As[0], Bs[0], tid, r4);
+        } else {
+            load_tile(g, A, B, m0, n0, kbeg, kend, tid, r);
+            store_tile(g, As[0], Bs[0], tid, r);
+        }
         __syncthreads();
         int cur = 0;
         for (int k0 = kbeg; k0 < kend; k0 += TK) {
             const bool more = k0 + TK < kend;
-            if (more) load_tile(g, A, B, m0, n0, k0 + TK, kend, tid, r);
+            if (more) {
+                if (VEC) load_tile4(g, A, B, m0, n0, k0 + TK, kend, tid, r4);
+                else load_tile(g, A, B, m0, n0, k0 + TK, kend, tid, r);
+            }
 #pragma unroll
             for (int kk = 0; kk < TK; kk += 2) {
                 const float a = As[cur][kk + (lane >> 5)][wm * 32 + (lane & 31)];
                 const float b = Bs[cur][kk + (lane >> 5)][wn * 32 + (lane & 31)];
                 acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, acc, 0, 0, 0);
             }
-            if (more) store_tile(g, As[cur ^ 1], Bs[cur ^ 1], tid, r);
+            if (more) {
+                if (VEC) store_tile4(g, As[cur ^ 1], Bs[cur ^ 1], tid, r4);
+                else store_tile(g, As[cur ^ 1], Bs[cur ^ 1], tid, r);
+            }
             __syncthreads();
             cur ^= 1;
         }
@@ -284,6 +339,24 @@ hipError_t sum_parts(const float* part, int splits, int64_t n, float* out, hipSt
     return hipGetLastError();
 }
 
+// 16-B pieces apply when each operand has a unit-stride dimension whose extent is a multiple of
+// 4 and every other stride / offset / base is 16-B aligned
+bool gemm_vec_ok(const GemmArgs& g) {
+    auto m4 = [](int64_t v) { return (v & 3) == 0; };
+    const bool a_ok = (g.ak == 1 && m4(g.K) && m4(g.kchunk) && m4(g.am)) || (g.am == 1 && m4(g.M) && m4(g.ak));
+    const bool b_ok = (g.bk == 1 && m4(g.K) && m4(g.kchunk) && m4(g.bn)) || (g.bn == 1 && m4(g.N) && m4(g.bk));
+    return a_ok && b_ok && m4(g.aj) && m4(g.at) && m4(g.bj) && m4(g.bt) && ((uintptr_t)g.A & 15) == 0 &&
+           ((uintptr_t)g.B & 15) == 0;
+}
+
+hipError_t launch_gemm(const GemmArgs& g, dim3 grid, hipStream_t s) {
+    if (gemm_vec_ok(g))
+        hipLaunchKernelGGL(k_gemm<true>, grid, dim3(256), 0, s, g);
+    else
+        hipLaunchKernelGGL(k_gemm<false>, grid, dim3(256), 0, s, g);
+    return hipGetLastError();
+}
+
 constexpr int kRowsPerChunk = 16;  // dbias partials
 constexpr int kDghatRows = 8;      // dghat partials (2 rows per wave)
 
@@ -336,9 +409,7 @@ int sd_gl_train_forward(const float* x, const float* W, const float* bias, const
     g.am = (int64_t)J * K; g.ak = 1; g.aj = K; g.at = 0;            // A[m][k] = x[m, j, k]
     g.bk = 1; g.bn = K; g.bj = 0; g.bt = (int64_t)N * K;            // B[k][n] = W[t][n][k]
     g.cm = (int64_t)J * N; g.cz = N; g.cs = 0; g.bias_t = N;        // C[m][n] = z[m, j, n]
-    hipLaunchKernelGGL(sd::k_gemm, dim3((unsigned)sd::ceil_div(N, sd::TN), (unsigned)sd::ceil_div(rows, sd::TM), J),
-                       dim3(256), 0, s, g);
-    TR_HIP(hipGetLastError());
+    TR_HIP(sd::launch_gemm(g, dim3((unsigned)sd::ceil_div(N, sd::TN), (unsigned)sd::ceil_div(rows, sd::TM), J), s));
     hipLaunchKernelGGL(sd::k_mix, dim3((unsigned)rows, (unsigned)sd::ceil_div(N, 64)), dim3(256), 0, s, z, ghat, y, J,
                        N, 0);
     TR_HIP(hipGetLastError());
@@ -391,9 +462,7 @@ int sd_gl_train_backward(const float* x, const float* z, const float* dy, const 
         g.am = (int64_t)J * N; g.ak = 1; g.aj = N; g.at = 0;         // A[m][n] = dz[m, j, n]
         g.bk = K; g.bn = 1; g.bj = 0; g.bt = (int64_t)N * K;         // B[n][k] = W[t][n][k]
         g.cm = (int64_t)J * K; g.cz = K; g.cs = 0;                   // C[m][k] = dx[m, j, k]
-        hipLaunchKernelGGL(sd::k_gemm, dim3((unsigned)sd::ceil_div(K, sd::TN), (unsigned)sd::ceil_div(rows, sd::TM), J),
-                           dim3(256), 0, s, g);
-        TR_HIP(hipGetLastError());
+        TR_HIP(sd::launch_gemm(g, dim3((unsigned)sd::ceil_div(K, sd::TN), (unsigned)sd::ceil_div(rows, sd::TM), J), s));
     }
     if (dW) {
         const int splits = sd::splits_for(rows);
@@ -404,10 +473,8 @@ int sd_gl_train_backward(const float* x, const float* z, const float* dy, const 
         g.am = 1; g.ak = (int64_t)J * N; g.aj = N; g.at = 0;         // A[n][r] = dz[r, j, n]
         g.bk = (int64_t)J * K; g.bn = 1; g.bj = K; g.bt = 0;         // B[r][k] = x[r, j, k]
         g.cm = K; g.cz = (int64_t)N * K; g.cs = (int64_t)types * N * K;  // C[n][k] = part[s][t][n][k]
-        hipLaunchKernelGGL(sd::k_gemm,
-                           dim3((unsigned)sd::ceil_div(K, sd::TN), (unsigned)sd::ceil_div(N, sd::TM), types * splits),
-                           dim3(256), 0, s, g);
-        TR_HIP(hipGetLastError());
+        TR_HIP(sd::launch_gemm(
+            g, dim3((unsigned)sd::ceil_div(K, sd::TN), (unsigned)sd::ceil_div(N, sd::TM), types * splits), s));
         const int64_t n = (int64_t)types * N * K;
         TR_HIP(sd::sum_parts(part, splits, n, dW, s));
     }
