@@ -188,3 +188,21 @@ def test_cpu_module_keeps_torch_path():
     prev = training.set_hip_training(False)
     assert prev is True and not training.hip_training_enabled()
     training.set_hip_training(prev)
+
+
+def test_gl_train_abi_validation_on_host():
+    """Argument checks of the training ABI run before any device work (no GPU needed)."""
+    from skeletondiffusion_amd import _lib
+    L = _lib.lib()
+    ws = L.sd_gl_train_workspace_bytes(1024, 16, 192, 192, 10)
+    # dz (rows, J, N) plus the largest partial buffer (dW split partials)
+    assert ws >= 1024 * 16 * 192 * 4 + 192 * 192 * 10 * 4
+    assert L.sd_gl_train_workspace_bytes(2048, 16, 192, 192, 10) > ws
+    assert L.sd_gl_train_workspace_bytes(-1, 16, 192, 192, 10) == 0
+    assert L.sd_gl_train_forward(None, None, None, None, 0, None, 4, 0, 8, 8, None, None, None) < 0   # J = 0
+    assert b"J" in L.sd_last_error()
+    assert L.sd_gl_train_forward(None, None, None, None, 0, None, 4, 65, 8, 8, None, None, None) < 0  # J > 64
+    assert L.sd_gl_train_forward(None, None, None, None, 0, None, 0, 16, 8, 8, None, None, None) == 0  # empty
+    assert L.sd_gl_train_forward(None, None, None, None, 0, None, 4, 16, 8, 8, None, None, None) < 0   # null buffers
+    assert L.sd_gl_train_backward(None, None, None, None, None, 0, None, 4, 16, 8, 8, None, None, None, None,
+                                  None, 0, None) < 0                                                  # null input
