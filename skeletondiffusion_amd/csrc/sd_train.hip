@@ -191,29 +191,54 @@ __global__ __launch_bounds__(256) void k_gemm(GemmArgs g) {
 }
 
 // out[r, i, n] = sum_j M[i, j] in[r, j, n], M = ghat (transpose = 0) or ghat^T (transpose = 1).
-// One workgroup per (row, 64-column chunk); the J x 64 input slab and ghat in LDS.
+// One workgroup per (row, 64-column chunk): the J x 64 input slab and M^T in LDS; each thread owns
+// one column and RPT consecutive output rows (RPT * 4 >= J), fed per source node by one LDS read
+// of the input and RPT / 4 16-B broadcast reads of M^T[j][i0 ..] (not two LDS reads per FMA).
+template <int RPT>
 __global__ __launch_bounds__(256) void k_mix(const float* __restrict__ in, const float* __restrict__ ghat,
                                              float* __restrict__ out, int J, int N, int transpose) {
-    __shared__ float s_in[64][64];
-    __shared__ float s_g[64][65];
+    __shared__ __attribute__((aligned(16))) float s_in[64][64];
+    __shared__ __attribute__((aligned(16))) float s_mt[64][68];
     const int r = blockIdx.x, n0 = blockIdx.y * 64, tid = threadIdx.x;
     const int64_t base = (int64_t)r * J * N;
-    for (int e = tid; e < J * J; e += 256) {
-        const int i = e / J, j = e % J;
-        s_g[i][j] = transpose ? ghat[j * J + i] : ghat[i * J + j];
+    for (int e = tid; e < J * 4 * RPT; e += 256) {
+        const int jj = e / (4 * RPT), i = e % (4 * RPT);
+        s_mt[jj][i] = i < J ? (transpose ? ghat[jj * J + i] : ghat[i * J + jj]) : 0.f;
     }
     for (int e = tid; e < J * 64; e += 256) {
         const int j = e >> 6, c = e & 63;
         s_in[j][c] = (n0 + c < N) ? in[base + (int64_t)j * N + n0 + c] : 0.f;
     }
     __syncthreads();
-    const int c = tid & 63;
-    if (n0 + c >= N) return;
-    for (int i = tid >> 6; i < J; i += 4) {
-        float acc = 0.f;
-        for (int j = 0; j < J; ++j) acc = fmaf(s_g[i][j], s_in[j][c], acc);
-        out[base + (int64_t)i * N + n0 + c] = acc;
+    const int c = tid & 63, i0 = RPT * (tid >> 6);
+    if (n0 + c >= N || i0 >= J) return;
+    float acc[RPT];
+#pragma unroll
+    for (int q = 0; q < RPT; ++q) acc[q] = 0.f;
+    for (int j = 0; j < J; ++j) {
+        const float x = s_in[j][c];
+        const float4* m4 = reinterpret_cast<const float4*>(&s_mt[j][i0]);
+#pragma unroll
+        for (int v = 0; v < RPT / 4; ++v) {
+            const float4 m = m4[v];
+            acc[4 * v + 0] = fmaf(m.x, x, acc[4 * v + 0]);
+            acc[4 * v + 1] = fmaf(m.y, x, acc[4 * v + 1]);
+            acc[4 * v + 2] = fmaf(m.z, x, acc[4 * v + 2]);
+            acc[4 * v + 3] = fmaf(m.w, x, acc[4 * v + 3]);
+        }
     }
+#pragma unroll
+    for (int q = 0; q < RPT; ++q)
+        if (i0 + q < J) out[base + (int64_t)(i0 + q) * N + n0 + c] = acc[q];
+}
+
+hipError_t launch_mix(const float* in, const float* ghat, float* out, int64_t rows, int J, int N, int transpose,
+                      hipStream_t s) {
+    const dim3 grid((unsigned)rows, (unsigned)((N + 63) / 64));
+    if (J <= 16) hipLaunchKernelGGL(k_mix<4>, grid, dim3(256), 0, s, in, ghat, out, J, N, transpose);
+    else if (J <= 32) hipLaunchKernelGGL(k_mix<8>, grid, dim3(256), 0, s, in, ghat, out, J, N, transpose);
+    else hipLaunchKernelGGL(k_mix<16>, grid, dim3(256), 0, s, in, ghat, out, J, N, transpose);
+    return hipGetLastError();
 }
 
 // partial dghat over a row range on v_mfma_f32_32x32x2_f32:
@@ -410,9 +435,7 @@ int sd_gl_train_forward(const float* x, const float* W, const float* bias, const
     g.bk = 1; g.bn = K; g.bj = 0; g.bt = (int64_t)N * K;            // B[k][n] = W[t][n][k]
     g.cm = (int64_t)J * N; g.cz = N; g.cs = 0; g.bias_t = N;        // C[m][n] = z[m, j, n]
     TR_HIP(sd::launch_gemm(g, dim3((unsigned)sd::ceil_div(N, sd::TN), (unsigned)sd::ceil_div(rows, sd::TM), J), s));
-    hipLaunchKernelGGL(sd::k_mix, dim3((unsigned)rows, (unsigned)sd::ceil_div(N, 64)), dim3(256), 0, s, z, ghat, y, J,
-                       N, 0);
-    TR_HIP(hipGetLastError());
+    TR_HIP(sd::launch_mix(z, ghat, y, rows, J, N, 0, s));
     return SD_OK;
 }
 
@@ -452,9 +475,7 @@ int sd_gl_train_backward(const float* x, const float* z, const float* dy, const 
         TR_HIP(sd::sum_parts(part, (int)chunks, (int64_t)J * J, dghat, s));
     }
     if (!dx && !dW && !dbias) return SD_OK;
-    hipLaunchKernelGGL(sd::k_mix, dim3((unsigned)rows, (unsigned)sd::ceil_div(N, 64)), dim3(256), 0, s, dy, ghat, dz,
-                       J, N, 1);
-    TR_HIP(hipGetLastError());
+    TR_HIP(sd::launch_mix(dy, ghat, dz, rows, J, N, 1, s));
     if (dx) {
         GemmArgs g{};
         g.A = dz; g.B = W; g.C = dx; g.bias = nullptr; g.types = tp;
