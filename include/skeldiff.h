@@ -108,6 +108,24 @@ int sd_denoiser_forward(const sd_plan* plan, const float* x_t, const float* x_co
                         int64_t cond_repeat, int32_t t, float* x0_out, int64_t rows,
                         void* workspace, size_t workspace_bytes, void* stream);
 
+/* Status of the last sd_sample_loop / sd_denoiser_forward / sd_denoiser_trace on `workspace`
+ * (synchronises `stream`): flags bit 0 (SD_STATUS_F16_RANGE) = an activation reached |x| >= 65504,
+ * outside the f16 range of the split-f16 (v4) products, so the results are not f32-accurate; run
+ * again with SD_OPT_KERNEL_VARIANT = 3 (exact f32).  The word is cleared at the start of each
+ * of those calls. */
+enum { SD_STATUS_F16_RANGE = 1 };
+int sd_workspace_status(const sd_plan* plan, const void* workspace, size_t workspace_bytes, uint32_t* flags,
+                        void* stream);
+
+/* sd_denoiser_forward that also copies every block output (rows, J, D + cond_dim), row-major,
+ * into acts[0 .. 2 + 4 * depth): init_lin, then per layer i < 2 * depth the ResnetBlock output and
+ * the Residual(PreNorm(Attention)) output (nn.Identity for the last layer: a copy of the
+ * ResnetBlock output), then final_res_block -- the module outputs of generator.py:94-106 (test
+ * hook: the per-layer parity against the reference's forward hooks). */
+int sd_denoiser_trace(const sd_plan* plan, const float* x_t, const float* x_cond, int64_t cond_repeat,
+                      int32_t t, float* x0_out, int64_t rows, void* workspace, size_t workspace_bytes,
+                      float* const* acts, int32_t nacts, void* stream);
+
 /* One reverse step for B rows at time t:
  *   x0 = clamp(act(x0_raw), -1, 1); mean = C1[t] x0 + C2[t] x_t;
  *   x_prev = mean + U (sigma_t * eps)   (nonisotropic)   |  c1 x0 + c2 x_t + sigma_t eps (iso)
@@ -206,12 +224,30 @@ int sd_test_attention(const float* qkv, float* out, int64_t rows, int32_t J, int
 int sd_test_qkv_attention(const float* x, int32_t K, const float* W, const int64_t* node_types, const float* ghat,
                           float* out, int64_t rows, int32_t J, int32_t heads, int32_t rms, int32_t layout,
                           void* stream);
-/* Kernel-generation selector (tests / tuning; process-wide, affects launches recorded after it):
- * gl_variant 0 = auto (v4 split-f16 where available, else exact-f32 v3/v2), 1..3 = exact-f32
- * generations, 4 = v4; gl4_tile = <waves><row tiles><col tiles> (e.g. 822) or 0 = auto,
+/* Process DEFAULT of the kernel generation for plans created afterwards and for the sd_test_*
+ * hooks (a plan keeps its own copy: SD_OPT_KERNEL_VARIANT / SD_OPT_GL4_TILE):
+ * gl_variant 0 = auto (v4 split-f16 where available, else exact-f32 v3/v2/v5), 1..3 = exact-f32
+ * generations, 4 = v4, 5 = v5; gl4_tile = <waves><row tiles><col tiles> (e.g. 822) or 0 = auto,
  * -1 leaves it.  Returns the previous gl_variant, or -1 for an invalid one (nothing changed);
  * gl_variant = -1 only queries (returns the current value). */
 int sd_set_kernel_variant(int32_t gl_variant, int32_t gl4_tile);
+
+/* Per-plan kernel options (read by the launches recorded after the call; part of the graph
+ * cache key).  A plan starts from the process defaults (sd_set_kernel_variant,
+ * sd_set_row_chains, SKELDIFF_* environment at load); two plans may hold different options and
+ * sample concurrently.  SD_E_INVALID for an unknown option or value. */
+enum {
+    SD_OPT_KERNEL_VARIANT = 1,  /* 0 auto, 1..5 force a graph-linear generation */
+    SD_OPT_GL4_TILE = 2,        /* v4 tile <waves><row tiles><col tiles>, 0 = per shape */
+    SD_OPT_ROW_CHAINS = 3,      /* 1..8 concurrent row chains in sd_sample_loop */
+    SD_OPT_PRECISION = 4,       /* as sd_plan_set_precision */
+    SD_OPT_GL4_STAGING = 5      /* v4 weight stages: 0 LDS-DMA, workgroup holds its CU's whole
+                                   LDS (default); 1 register-staged, CU shareable;
+                                   2 DIAGNOSTIC ONLY: LDS-DMA with the CU shareable -- reproduces the
+                                   §4c co-residency corruption, never for production use */
+};
+int sd_plan_set_option(sd_plan* plan, int32_t option, int64_t value);
+int sd_plan_get_option(const sd_plan* plan, int32_t option, int64_t* value);
 
 /* Graph-GRU latent decoder: AutoEncoder.decode -> Decoder.forward
  * (src/core/network/nn/decoder.py:60-104) with the StaticGraphGRU cell
@@ -242,7 +278,8 @@ int sd_gru_decode(const sd_gru_decoder_desc* desc, const float* x, const float* 
 size_t sd_gru_encode_workspace_bytes(const sd_gru_decoder_desc* desc, int64_t rows, int32_t frames);
 int sd_gru_encode(const sd_gru_decoder_desc* desc, const float* x, int64_t rows, int32_t frames, float* z,
                   void* workspace, size_t workspace_bytes, void* stream);
-/* Row chains of sd_sample_loop (process-wide; SKELDIFF_CHAINS, default 3): the batch is split into
+/* Process DEFAULT of the row chains of sd_sample_loop for plans created afterwards (a plan keeps
+ * its own: SD_OPT_ROW_CHAINS; SKELDIFF_CHAINS at load, default 3): the batch is split into
  * n row ranges (multiples of 32 rows; fewer when the batch is small) whose
  * T-step chains run on forked streams and overlap on the GPU.  Rows are independent, so the
  * results do not depend on n.  Returns the previous n; n = -1 only queries; SD_E_INVALID

@@ -34,7 +34,7 @@ import torch.nn.functional as F
 __all__ = [
     "beta_schedule", "schedule_buffers", "covariance_diagonals", "nonisotropic_buffers",
     "isotropic_buffers", "get_cov_from_corr", "DenoiserConfig", "denoiser_forward",
-    "sinusoidal_embedding", "p_sample_loop", "philox4x32_10", "philox_normal",
+    "sinusoidal_embedding", "p_sample_loop", "p_sample_step", "philox4x32_10", "philox_normal",
     "device_noise", "ORACLE_IS_TEST_INFRASTRUCTURE",
 ]
 
@@ -338,20 +338,38 @@ def denoiser_forward(sd: Dict[str, torch.Tensor], cfg: DenoiserConfig, x: torch.
 #        isotropic.py:85-95)
 
 
+def p_sample_step(sd, cfg: DenoiserConfig, bufs: Dict[str, torch.Tensor], img: torch.Tensor, t: int,
+                  noise, x_cond: Optional[torch.Tensor] = None, activation: str = "identity"):
+    """One nonisotropic reverse step at time t from x_t = img (base.py:314-341,
+    nonisotropic.py:196-210); noise (B, J, D) or 0 at t = 0.  Returns (x_{t-1}, mean)."""
+    B = img.shape[0]
+    if x_cond is not None and B > x_cond.shape[0]:
+        x_cond = x_cond.repeat_interleave(B // x_cond.shape[0], 0)
+    out = denoiser_forward(sd, cfg, img, torch.full((B,), t, dtype=torch.long), x_cond)
+    x0 = (torch.tanh(out) if activation == "tanh" else out).clamp(-1.0, 1.0)
+    mean = bufs["posterior_mean_coef1_x0"][t] @ x0 + bufs["posterior_mean_coef2_xt"][t] @ img
+    lv = bufs["Lambda_posterior_log_variance_clipped"][t].unsqueeze(-1)
+    return mean + bufs["U"] @ ((0.5 * lv).exp() * noise), mean
+
+
 def p_sample_loop(sd, cfg: DenoiserConfig, bufs: Dict[str, torch.Tensor], start_noise: torch.Tensor,
                   sampling_noise: Optional[torch.Tensor], x_cond: Optional[torch.Tensor] = None,
                   isotropic: bool = False, activation: str = "identity", record_means: bool = False,
-                  steps: Optional[int] = None):
-    """Reverse diffusion with host-supplied noise.  Returns (img, [mean_t for t=T-1..1]).
+                  steps: Optional[int] = None, record_imgs: bool = False,
+                  noise2interpolate: Optional[torch.Tensor] = None, interpolate_funct=None):
+    """Reverse diffusion with host-supplied noise.  Returns (img, [mean_t for t=T-1..1]), or
+    (img, means, [x_t for t=T-1..1]) with `record_imgs` (return_timages, base.py:371-389).
 
     `steps` runs only the first `steps` iterations (t = T-1 .. T-steps) for bounded CPU
-    baselines; the per-step cost is constant in t."""
+    baselines; the per-step cost is constant in t.
+    `noise2interpolate` + `interpolate_funct`: the reference's noise interpolation
+    (base.py:335-338; nonisotropic.py:218-227): x = mean + f(U(s*n1), U(s*n2))."""
     T = bufs["betas"].shape[0]
     img = start_noise.clone()
     B = img.shape[0]
     if x_cond is not None and B > x_cond.shape[0]:
         x_cond = x_cond.repeat_interleave(B // x_cond.shape[0], 0)  # base.py:246-248
-    means = []
+    means, imgs = [], []
     for it, t in enumerate(reversed(range(T))):
         if steps is not None and it >= steps:
             break
@@ -370,13 +388,22 @@ def p_sample_loop(sd, cfg: DenoiserConfig, bufs: Dict[str, torch.Tensor], start_
                 else torch.randn_like(img)
         else:
             noise = 0.0
-        if isotropic:
+        if noise2interpolate is not None and t > 0:  # base.py:335-338, nonisotropic.py:218-227
+            n2 = noise2interpolate[:, sampling_noise.shape[1] - t]
+            s = (0.5 * lv).exp()
+            img = mean + interpolate_funct(bufs["U"] @ (s * noise), bufs["U"] @ (s * n2))
+        elif isotropic:
             img = mean + (0.5 * lv).exp() * noise
         else:
             img = mean + bufs["U"] @ ((0.5 * lv).exp() * noise)
         if record_means and t != 0:
             means.append(mean)
-    return img, (torch.stack(means, dim=1) if record_means and means else None)
+        if record_imgs and t != 0:
+            imgs.append(img)
+    ms = torch.stack(means, dim=1) if record_means and means else None
+    if record_imgs:
+        return img, ms, (torch.stack(imgs, dim=1) if imgs else None)
+    return img, ms
 
 
 # ---------------------------------------------------------------------------------------------

@@ -12,7 +12,8 @@ import threading
 from typing import Optional
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libskeldiff.so")
+# SKELDIFF_LIB: load another build of the library (e.g. the libskeldiff_dbg.so diagnostic variant)
+LIB_PATH = os.environ.get("SKELDIFF_LIB") or os.path.join(HERE, "libskeldiff.so")
 
 SD_FLAG_GRAPH = 1
 SD_FLAG_DEVICE_START = 2
@@ -28,8 +29,13 @@ EXPORTED = (
     "sd_test_graph_linear_layout", "sd_pairwise_distances", "sd_ade_fde", "sd_set_row_chains",
     "sd_plan_set_precision", "sd_mm_ade_fde", "sd_gru_decode_workspace_bytes", "sd_gru_decode",
     "sd_gru_encode_workspace_bytes", "sd_gru_encode", "sd_gl_train_workspace_bytes", "sd_gl_train_forward",
-    "sd_gl_train_backward",
+    "sd_gl_train_backward", "sd_plan_set_option", "sd_plan_get_option", "sd_denoiser_trace",
+    "sd_workspace_status",
 )
+
+# sd_plan_set_option keys (include/skeldiff.h)
+SD_OPT_KERNEL_VARIANT, SD_OPT_GL4_TILE, SD_OPT_ROW_CHAINS, SD_OPT_PRECISION, SD_OPT_GL4_STAGING = 1, 2, 3, 4, 5
+SD_STATUS_F16_RANGE = 1
 
 
 class SDPlanDesc(ctypes.Structure):
@@ -84,6 +90,8 @@ def _declare(lib: ctypes.CDLL) -> None:
         "sd_plan_finalize": (ctypes.c_int, [vp, vp]),
         "sd_workspace_bytes": (sz, [vp, i64]),
         "sd_denoiser_forward": (ctypes.c_int, [vp, vp, vp, i64, i32, vp, i64, vp, sz, vp]),
+        "sd_workspace_status": (ctypes.c_int, [vp, vp, sz, ctypes.POINTER(ctypes.c_uint32), vp]),
+        "sd_denoiser_trace": (ctypes.c_int, [vp, vp, vp, i64, i32, vp, i64, vp, sz, ctypes.POINTER(vp), i32, vp]),
         "sd_p_sample_update": (ctypes.c_int, [vp, vp, vp, vp, i64, u64, i64, i32, vp, vp, i64, vp, i64, i64, vp]),
         "sd_sample_loop": (ctypes.c_int, [vp, vp, vp, i64, vp, u64, i64, vp, vp, vp, vp, vp, i64, vp, sz, i32, vp]),
         "sd_noise_fill": (ctypes.c_int, [vp, i64, i64, u64, i64, i32, vp]),
@@ -96,6 +104,8 @@ def _declare(lib: ctypes.CDLL) -> None:
         "sd_set_kernel_variant": (ctypes.c_int, [i32, i32]),
         "sd_set_row_chains": (ctypes.c_int, [i32]),
         "sd_plan_set_precision": (ctypes.c_int, [vp, i32]),
+        "sd_plan_set_option": (ctypes.c_int, [vp, i32, i64]),
+        "sd_plan_get_option": (ctypes.c_int, [vp, i32, ctypes.POINTER(ctypes.c_int64)]),
         "sd_mm_ade_fde": (ctypes.c_int, [vp, vp, vp, i64, vp, i64, i32, i32, i64, vp, vp, vp, vp, vp]),
         "sd_gru_decode_workspace_bytes": (ctypes.c_size_t, [ctypes.POINTER(SDGruDecoderDesc), i64, i32]),
         "sd_gru_decode": (ctypes.c_int, [ctypes.POINTER(SDGruDecoderDesc), vp, vp, i64, i32, vp, vp,

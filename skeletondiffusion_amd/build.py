@@ -28,14 +28,17 @@ def _stale() -> bool:
     return any(os.path.getmtime(os.path.join(CSRC, f)) > t for f in SOURCES + HEADERS)
 
 
-def build_library(force: bool = False, verbose: bool = False) -> str:
-    if not force and not _stale():
+def build_library(force: bool = False, verbose: bool = False, debug_lds: bool = False, extra=(), tag="_dbg") -> str:
+    """debug_lds: the diagnostic variant libskeldiff_dbg.so (-DSD_DEBUG_LDS: LDS integrity
+    counters in k_gl4 / k_update, sd_debug_lds_counters); load it with SKELDIFF_LIB."""
+    out = OUT.replace(".so", tag + ".so") if debug_lds else OUT
+    if not force and not debug_lds and not _stale():
         return OUT
     objs, procs = [], []
     for src in SOURCES:  # one hipcc per translation unit, in parallel
-        obj = os.path.join(CSRC, src.replace(".hip", ".o"))
+        obj = os.path.join(CSRC, src.replace(".hip", tag + ".o" if debug_lds else ".o"))
         cmd = [_hipcc(), "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-c",
-               "-Wno-pass-failed", os.path.join(CSRC, src), "-o", obj]
+               "-Wno-pass-failed"] + (["-DSD_DEBUG_LDS"] + list(extra) if debug_lds else []) + [os.path.join(CSRC, src), "-o", obj]
         if verbose:
             print(" ".join(cmd))
         procs.append((src, subprocess.Popen(cmd)))
@@ -43,13 +46,15 @@ def build_library(force: bool = False, verbose: bool = False) -> str:
     failed = [src for src, pr in procs if pr.wait() != 0]
     if failed:
         raise RuntimeError("hipcc failed: " + ", ".join(failed))
-    tmp = OUT + ".tmp"
+    tmp = out + ".tmp"
     subprocess.run([_hipcc(), "--offload-arch=gfx950", "-shared", "-fPIC", "-o", tmp] + objs, check=True)
-    os.replace(tmp, OUT)
+    os.replace(tmp, out)
     for o in objs:
         os.remove(o)
-    return OUT
+    return out
 
 
 if __name__ == "__main__":
-    print(build_library(force=True, verbose=True))
+    import sys
+
+    print(build_library(force=True, verbose=True, debug_lds="--debug-lds" in sys.argv))

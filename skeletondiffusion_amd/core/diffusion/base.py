@@ -9,12 +9,14 @@ stays on torch ops so that it keeps autograd.
 from __future__ import annotations
 
 import math
+import warnings
 from typing import Dict, Optional
 
 import torch
 import torch.nn.functional as F
 from torch import nn
 
+from ... import _lib
 from ... import engine as _engine
 
 __all__ = ["LatentDiffusion", "extract", "default", "exists", "identity", "linear_beta_schedule",
@@ -281,10 +283,27 @@ class LatentDiffusion(nn.Module):
                                                    noise2interpolate, interpolation_kwargs)
         if self.self_condition:
             raise NotImplementedError("self_condition=True is not supported by the sampling engine")
-        res = self.engine.sample_loop(shape[0], x_cond=x_cond, start_noise=start_noise,
-                                      sampling_noise=sampling_noise,
-                                      record=(return_sampling_noise, return_timages),
-                                      seed=seed, row0=row0)
+        if seed is None and (start_noise is None or sampling_noise is None):
+            seed = int(torch.randint(0, 2 ** 62, (1,)).item())  # fixed, so a re-run draws the same noise
+
+        def run():
+            return self.engine.sample_loop(shape[0], x_cond=x_cond, start_noise=start_noise,
+                                           sampling_noise=sampling_noise,
+                                           record=(return_sampling_noise, return_timages),
+                                           seed=seed, row0=row0)
+
+        res = run()
+        if self.engine.status(shape[0]) & _lib.SD_STATUS_F16_RANGE:
+            # an activation left the f16 range of the split-f16 kernels: the whole chain again on
+            # the exact-f32 kernels (same seed / noise, so the same sample)
+            warnings.warn("activation outside the f16 range of the split-f16 kernels: re-sampling with the "
+                          "exact-f32 kernels (kernel_variant=3)")
+            old = self.engine.get_option("kernel_variant")
+            self.engine.set_option("kernel_variant", 3)
+            try:
+                res = run()
+            finally:
+                self.engine.set_option("kernel_variant", old)
         img, start, noise_t, mean_t, imgs = res
         noise = start
         if return_sampling_noise:

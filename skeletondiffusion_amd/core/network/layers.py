@@ -86,7 +86,8 @@ class StaticGraphLinear(nn.Module):
     def forward(self, x: torch.Tensor, g: Optional[torch.Tensor] = None) -> torch.Tensor:
         g = self.ghat() if g is None else g
         if (x.is_cuda and torch.is_grad_enabled() and x.dtype == torch.float32
-                and self.weight.dtype == torch.float32 and _training.hip_training_enabled()):
+                and self.weight.dtype == torch.float32 and _training.hip_training_enabled()
+                and _training.hip_shapes_ok(x, self.weight, g, self.node_type_index)):
             # training on the device: forward + backward on the HIP kernels (sd_train.hip)
             return _training.graph_linear(x, self.weight, self.bias, g, self.node_type_index)
         if self.node_type_index is not None:

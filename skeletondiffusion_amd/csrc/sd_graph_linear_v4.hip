@@ -112,6 +112,26 @@ __global__ void k_split_w(const float* __restrict__ W, int ntypes, int N, int K,
 
 }  // namespace
 
+// row-blocked (blk_off) -> row-major (rows, J, F) copy (sd_denoiser_trace)
+__global__ void k_unblock(float* __restrict__ out, const float* __restrict__ in, int64_t rows, int J, int F) {
+    const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t n4 = rows * J * (F / 4);
+    if (g >= n4) return;
+    const int f = (int)(g % (F / 4)) * 4;
+    const int64_t rj = g / (F / 4);
+    const int j = (int)(rj % J);
+    const int64_t row = rj / J;
+    *reinterpret_cast<floatx4*>(out + (row * J + j) * F + f) = *reinterpret_cast<const floatx4*>(in + blk_off(row, j, f, J, F));
+}
+
+hipError_t launch_unblock(float* out, const float* in, int64_t rows, int J, int F, hipStream_t s) {
+    const int64_t n4 = rows * J * (F / 4);
+    if (n4 <= 0) return hipSuccess;
+    if (F % 4) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_unblock, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, s, out, in, rows, J, F);
+    return hipGetLastError();
+}
+
 hipError_t make_split_weights(const float* W, int ntypes, int N, int K, SplitW* out, hipStream_t s) {
     out->nct = ((N + 31) / 32 + 5) / 6 * 6;  // 32-col tiles, padded to a multiple of 6 (CT in 1, 2, 3)
     const int64_t n = (int64_t)ntypes * N * K;
@@ -254,7 +274,9 @@ __device__ __forceinline__ void attention_epilogue(const GLArgs& p, floatx16 (&a
 // PREC 1 ("half" precision mode): one product x_hi W'_hi per k step, so
 //   only the hi halves of the weight fragments are streamed (half the weight bytes, a third of
 //   the MFMAs); f32 accumulate, f32 activations in HBM, same epilogue.
-template <int J, int NW, int RT, int CT, bool RMS, int DBG = 0, int MODE = 0, int XP = 0, int PREC = 0>
+// STG 0: weight stages filled by LDS-DMA (global_load_lds_dwordx4); STG 1: register-staged
+//   (global_load_dwordx4 a chunk ahead, ds_write_b128 after the chunk's MFMAs).
+template <int J, int NW, int RT, int CT, bool RMS, int DBG = 0, int MODE = 0, int XP = 0, int PREC = 0, int STG = 0>
 __global__ __launch_bounds__(NW * 64, 1) void k_gl4(const GLArgs p) {
     static_assert(MODE == 0 || (CT == 3 && RT == 1 && J <= 16 && NW == 8), "attention mode: 32 x (q|k|v)");
     constexpr int NPW = (J + NW - 1) / NW;  // nodes per wave
@@ -313,6 +335,7 @@ __global__ __launch_bounds__(NW * 64, 1) void k_gl4(const GLArgs p) {
 
     floatx16 acc[NPW][RT][CT];
     float ss[NPW][RT];
+    float amx = 0.f;  // max |x| this lane split to f16 (range guard, GLArgs::status)
 #pragma unroll
     for (int m = 0; m < NPW; ++m)
 #pragma unroll
@@ -368,6 +391,26 @@ __global__ __launch_bounds__(NW * 64, 1) void k_gl4(const GLArgs p) {
             __builtin_amdgcn_global_load_lds((const void*)src, (lds_void*)(dst + (size_t)q0 * 8), 16, 0, 0);
         }
     };
+#ifdef SD_DEBUG_LDS
+    // stage c against its global source, read in the phase that reads the stage anyway
+    auto check_stage = [&](int c) {
+        constexpr int PPT = TILE_H / 8;
+        const int per_type = CT * PPT;
+        const int npieces = p.ntypes * per_type;
+        const _Float16* st = (c & 1) ? sW1 : sW0;
+        unsigned bad = 0;
+        for (int q = tid; q < npieces; q += NTH) {
+            const int t = q / per_type, rem = q - t * per_type;
+            const int ct = rem / PPT;
+            const int tile = MODE == 1 ? ctile + ct * p.attn_heads : (c0 >> 5) + ct;
+            const uint4 g = *reinterpret_cast<const uint4*>(p.wsp + (((int64_t)t * nchunk + c) * p.wsp_nct + tile) * 1024 +
+                                                            (rem % PPT) * 8);
+            const uint4 l = *reinterpret_cast<const uint4*>(st + (size_t)q * 8);
+            bad += (g.x != l.x) + (g.y != l.y) + (g.z != l.z) + (g.w != l.w);
+        }
+        if (bad) atomicAdd(&p.dbg[0], bad);
+    };
+#endif
     auto compute = [&](int c, const XBuf& xb) {
         const _Float16* cur = (c & 1) ? sW1 : sW0;
         const bool rms_chunk = RMS && (c << 4) < p.K1;
@@ -383,6 +426,11 @@ __global__ __launch_bounds__(NW * 64, 1) void k_gl4(const GLArgs p) {
                 if (rms_chunk) {
                     const floatx8 q = f * f;
                     ss[m][rt] += ((q[0] + q[1]) + (q[2] + q[3])) + ((q[4] + q[5]) + (q[6] + q[7]));
+                }
+                {
+                    const floatx8 a = __builtin_elementwise_abs(f);
+                    amx = fmaxf(amx, fmaxf(fmaxf(fmaxf(a[0], a[1]), fmaxf(a[2], a[3])),
+                                           fmaxf(fmaxf(a[4], a[5]), fmaxf(a[6], a[7]))));
                 }
                 xh[rt] = __builtin_convertvector(f, halfx8);
                 if constexpr (!PREC) xl[rt] = __builtin_convertvector(f - __builtin_convertvector(xh[rt], floatx8), halfx8);
@@ -426,6 +474,9 @@ __global__ __launch_bounds__(NW * 64, 1) void k_gl4(const GLArgs p) {
             __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): LDS reads of the MFMAs done
             cs[4] = clock64();
         }
+#if defined(SD_DEBUG_LDS) && !defined(SD_DEBUG_NO_GL)
+        check_stage(c);
+#endif
     };
 
     uint64_t ts[8];  // DBG 6: phase stamps (s_memrealtime, 100 MHz) + shader clock around the K loop
@@ -446,7 +497,56 @@ __global__ __launch_bounds__(NW * 64, 1) void k_gl4(const GLArgs p) {
             const int ncol = (MODE == 1 ? (ctile + ct * p.attn_heads) * 32 : c0 + 32 * ct) + l32;
             bv[m][ct] = (p.bias && ncol < p.N) ? p.bias[p.wrow[jn[m]] + ncol] : 0.f;
         }
-    if constexpr (XP == 0) {
+    if constexpr (STG == 1) {
+        // register-staged weights: the pieces of chunk c+1 this thread carries are loaded right
+        // after barrier c (with x(c+1)) and written to the other stage after compute(c); its
+        // last reads were in phase c-1, before barrier c.  lgkmcnt(0) + barrier c+1 makes the
+        // writes visible to every wave (no LDS-DMA anywhere in the K loop).
+        constexpr int MAXP = 8;  // checked at launch: ntypes * CT * TILE_H / 8 <= MAXP * NTH
+        constexpr int PPT = TILE_H / 8;
+        const int per_type = CT * PPT;
+        const int npieces = p.ntypes * per_type;
+        // per carried piece: its offset in chunk 0's slice (halves; chunk c adds c * cstride)
+        int woff[MAXP];
+#pragma unroll
+        for (int k = 0; k < MAXP; ++k) {
+            const int q = min(tid + k * NTH, npieces - 1);
+            const int t = q / per_type, rem = q - t * per_type;
+            const int ct = rem / PPT;
+            const int tile = MODE == 1 ? ctile + ct * p.attn_heads : (c0 >> 5) + ct;
+            woff[k] = ((t * nchunk) * p.wsp_nct + tile) * 1024 + (rem % PPT) * 8;
+        }
+        const int cstride = p.wsp_nct * 1024;
+        // the carried pieces as MAXP named registers (an array here was kept in scratch)
+        uint4 w0, w1, w2, w3, w4, w5, w6, w7;
+#define SD_W8(OP) OP(0, w0) OP(1, w1) OP(2, w2) OP(3, w3) OP(4, w4) OP(5, w5) OP(6, w6) OP(7, w7)
+#define SD_WLOAD(k, w) \
+    if (tid + k * NTH < npieces) w = *reinterpret_cast<const uint4*>(p.wsp + woff[k] + c * cstride);
+#define SD_WSTORE(k, w) \
+    if (tid + k * NTH < npieces) *reinterpret_cast<uint4*>(dst + (size_t)(tid + k * NTH) * 8) = w;
+        auto load_w = [&](int c) { SD_W8(SD_WLOAD) };
+        auto store_w = [&](_Float16* dst) { SD_W8(SD_WSTORE) };
+#undef SD_WLOAD
+#undef SD_WSTORE
+#undef SD_W8
+        auto step_r = [&](int c, const XBuf& cur, XBuf& nxt) {
+            __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this wave's stage writes landed
+            __builtin_amdgcn_s_barrier();
+            if (c + 1 < nchunk) {
+                load_w(c + 1);
+                load_x(c + 1, nxt);
+            }
+            compute(c, cur);
+            if (c + 1 < nchunk) store_w((c & 1) ? sW0 : sW1);
+        };
+        load_w(0);
+        load_x(0, X0);
+        store_w(sW0);
+        for (int c = 0; c < nchunk; c += 2) {
+            step_r(c, X0, X1);
+            step_r(c + 1, X1, X0);
+        }
+    } else if constexpr (XP == 0) {
         fill_w(0, sW0);
         load_x(0, X0);
         for (int c = 0; c < nchunk; c += 2) {
@@ -503,6 +603,9 @@ __global__ __launch_bounds__(NW * 64, 1) void k_gl4(const GLArgs p) {
     }
     if (DBG == 6) ts[7] = clock64();
     if (DBG == 6) ts[2] = wall_clock64();
+    // f16 range guard: an activation the split cannot represent (the caller re-runs on the
+    // exact-f32 kernels, engine.py); one atomic per wave at most, none in range
+    if (p.status && __builtin_amdgcn_ballot_w64(amx >= 65504.0f) != 0 && lane == 0) atomicOr(p.status, 1u);
 
     // ---- unscale, RMS, bias in the accumulator layout:
     //      D[row = (r&3) + 8(r>>2) + 4h][col = l32] for register r of a 32x32 tile
@@ -530,6 +633,13 @@ __global__ __launch_bounds__(NW * 64, 1) void k_gl4(const GLArgs p) {
         }
     }
     if (DBG == 6) ts[3] = wall_clock64();
+#if defined(SD_DEBUG_LDS) && !defined(SD_DEBUG_NO_G)
+    {
+        unsigned bad = 0;
+        for (int i = tid; i < J * J; i += NTH) bad += sG[i] != p.G[i];
+        if (bad) atomicAdd(&p.dbg[2], bad);
+    }
+#endif
     if constexpr (MODE == 1) {
         attention_epilogue<J, NW, NPW>(p, acc, smem, sG, row0, ctile, wave, lane);
         return;
@@ -685,8 +795,35 @@ __global__ __launch_bounds__(NW * 64, 1) void k_gl4(const GLArgs p) {
     }
 }
 
+// v4 weight staging (GLArgs::gl4_stage): 0 = LDS-DMA stages, the workgroup holds
+// its CU's whole LDS; 1 = register-staged stages, exact LDS size (CU shareable).  Process default
+// SKELDIFF_GL4_STAGE for new plans.
+static int g_gl4_stage = [] {
+    const char* e = getenv("SKELDIFF_GL4_STAGE");
+    const int v = e ? atoi(e) : 0;
+    return (v >= 0 && v <= 2) ? v : 0;
+}();
+int gl4_stage_default() { return g_gl4_stage; }
+int set_gl4_stage(int stage) {
+    if (stage < 0 || stage > 2) return -1;
+    const int old = g_gl4_stage;
+    g_gl4_stage = stage;
+    return old;
+}
+
+template <int J, int NW, int RT, int CT, int DBG = 0, int MODE = 0, int XP = 0, int PREC = 0, int STG = 0>
+static hipError_t gl4_launch_t(const GLArgs& a, bool rms, hipStream_t s);
+
 template <int J, int NW, int RT, int CT, int DBG = 0, int MODE = 0, int XP = 0, int PREC = 0>
 static hipError_t gl4_launch(const GLArgs& a, bool rms, hipStream_t s) {
+    constexpr int TILE_H = PREC ? 512 : 1024;
+    if (a.gl4_stage == 1 && XP == 0 && DBG == 0 && a.ntypes * CT * (TILE_H / 8) <= 8 * NW * 64)
+        return gl4_launch_t<J, NW, RT, CT, DBG, MODE, XP, PREC, 1>(a, rms, s);
+    return gl4_launch_t<J, NW, RT, CT, DBG, MODE, XP, PREC, 0>(a, rms, s);
+}
+
+template <int J, int NW, int RT, int CT, int DBG, int MODE, int XP, int PREC, int STG>
+static hipError_t gl4_launch_t(const GLArgs& a, bool rms, hipStream_t s) {
     constexpr int COLS = 32 * CT;
     const int ntile_c = MODE == 1 ? a.attn_heads : (a.N + COLS - 1) / COLS;
     const int64_t ntile_r = (a.B + 32 * RT - 1) / (32 * RT);
@@ -695,18 +832,17 @@ static hipError_t gl4_launch(const GLArgs& a, bool rms, hipStream_t s) {
     const size_t yfl = MODE == 1 ? (size_t)J * (8 * COLS + 16) + 8 * 16 * 100 : (size_t)J * (16 * (COLS + 4) + 16);
     size_t lds = ((wfl > yfl ? wfl : yfl) + (size_t)J * J + 2 * COLS) * sizeof(float);
     if (lds > 160 * 1024) return hipErrorNotSupported;
-    // Every k_gl4 launch takes a CU's whole LDS, so no other kernel's workgroup shares its CU
-    // (the tiles run one workgroup per CU anyway: registers).  Measured with row chains
-    // (concurrent kernels of independent row ranges): k_gl4 workgroups co-resident with other
-    // kernels' workgroups gave wrong, run-to-run different rows (fused attention at 122 KB LDS:
-    // up to 0.15 off in a T = 2 sampler; the 32 x 64 tile at 82 KB: ~1e-3 over T = 100); with
-    // the whole LDS reserved every chain count is bitwise equal to one chain, at the same
-    // throughput.  The K loop follows the LDS-DMA ordering rules (counted vmcnt + barrier before
-    // a read, one phase between the last read and a restage); the cause is not identified
-    // (DESIGN.md §4c).  SKELDIFF_FULL_LDS (bit MODE) overrides for experiments.
-    static const int full_lds = getenv("SKELDIFF_FULL_LDS") ? atoi(getenv("SKELDIFF_FULL_LDS")) : 3;
-    if (full_lds & (1 << MODE)) lds = 160 * 1024;
-    auto kt = rms ? k_gl4<J, NW, RT, CT, true, DBG, MODE, XP, PREC> : k_gl4<J, NW, RT, CT, false, DBG, MODE, XP, PREC>;
+    // LDS-DMA staging (STG 0): the workgroup takes its CU's whole LDS, so no other kernel's
+    // workgroup shares the CU (these tiles run one workgroup per CU anyway, by registers).  With
+    // concurrent row chains, STG-0 workgroups co-resident with another kernel's LDS-holding
+    // workgroups (k_update's tables) gave wrong, run-to-run different elements; the same
+    // co-residency with register-staged stages (STG 1) is bitwise correct, as is STG 0 alone on
+    // its CU.  DESIGN.md §4c has the measurements and the probes that rule out LDS-DMA addressing,
+    // placement and the vmcnt / barrier ordering of the K loop.
+    // gl4_stage 2 (diagnostic only): LDS-DMA stages at their exact size, so the hazard can be
+    // reproduced (tools/lds_hazard.py)
+    if (STG == 0 && a.gl4_stage != 2) lds = 160 * 1024;
+    auto kt = rms ? k_gl4<J, NW, RT, CT, true, DBG, MODE, XP, PREC, STG> : k_gl4<J, NW, RT, CT, false, DBG, MODE, XP, PREC, STG>;
     if (lds > 64 * 1024) {
         hipError_t e = hipFuncSetAttribute((const void*)kt, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         if (e != hipSuccess) return e;
@@ -715,12 +851,13 @@ static hipError_t gl4_launch(const GLArgs& a, bool rms, hipStream_t s) {
     return hipGetLastError();
 }
 
-// SKELDIFF_GL4_CFG = <NW><RT><CT> (e.g. 822) forces a tile for tuning; 0/unset = per shape.
+// SKELDIFF_GL4_CFG = <NW><RT><CT> (e.g. 822): process default of the plans' v4 tile (tuning);
+// 0/unset = per shape.
 static int g_gl4_cfg = [] {
     const char* e = getenv("SKELDIFF_GL4_CFG");
     return e ? atoi(e) : 0;
 }();
-static int gl4_cfg() { return g_gl4_cfg; }
+int gl4_tile_default() { return g_gl4_cfg; }
 int set_gl4_tile(int cfg) {
     const int old = g_gl4_cfg;
     g_gl4_cfg = cfg;
@@ -734,7 +871,7 @@ hipError_t launch_graph_linear_v4(const GLArgs& a, bool rms, hipStream_t s) {
     if ((a.N & 3) || ((uintptr_t)a.out & 15) || ((uintptr_t)a.res & 15) || (a.res && (a.res_rs & 3)) || (a.out_rs & 3))
         return hipErrorNotSupported;
     if (!a.wsp || (a.K1 + a.K2) % 32 || a.K1 % 16 || (a.x1_blk && a.x1_div != 1)) return hipErrorNotSupported;
-    const int cfg = gl4_cfg() ? gl4_cfg() : a.tile_hint;
+    const int cfg = a.gl4_cfg ? a.gl4_cfg : a.tile_hint;
     if (a.prec == 1) {  // half precision mode: the default tiles only
         switch (a.J) {
             case 16:
@@ -783,7 +920,7 @@ hipError_t launch_qkv_attention_v4(const GLArgs& a, bool rms, hipStream_t s) {
         a.act || (a.K1 + a.K2) % 32 || a.K1 % 16 || ((uintptr_t)a.out & 15) || (a.out_rs & 3))
         return hipErrorNotSupported;
     GLArgs b = a;
-    b.attn_order = gl4_cfg() == 100 ? 1 : 0;
+    b.attn_order = a.gl4_cfg == 100 ? 1 : 0;
     switch (a.J) {
         case 16: return a.prec == 1 ? gl4_launch<16, 8, 1, 3, 0, 1, 0, 1>(b, rms, s) : gl4_launch<16, 8, 1, 3, 0, 1>(b, rms, s);
         default: return hipErrorNotSupported;

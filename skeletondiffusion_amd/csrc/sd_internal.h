@@ -10,6 +10,13 @@ namespace sd {
 
 constexpr int kMaxNodes = 64;
 
+#ifdef SD_DEBUG_LDS
+// diagnostic build only (build.py debug=True): LDS integrity counters (device, 8 words) that
+// GLArgs::dbg / UpdArgs::dbg point to: [0] k_gl4 weight stages vs their global source,
+// [1] k_update tables vs global, [2] k_gl4 G-hat table
+unsigned* debug_counters();
+#endif
+
 // One StaticGraphLinear (graph_structural.py:30-43) with its fused epilogue:
 //   y_j   = s_j * (W_type(j) [x1_j | x2_j]) + bias_type(j)        (s_j = 1/max(|x1_j|,1e-12) if RMS)
 //   z_i   = sum_j Ghat[i][j] y_j
@@ -19,7 +26,11 @@ constexpr int kMaxNodes = 64;
 struct GLArgs {
     const float* x1; int64_t x1_rs; int K1; int x1_div;   // row b reads x1 row (b + x1_row0) / x1_div
     int64_t x1_row0;                                      // 0 <= x1_row0 < x1_div (a row chunk's phase)
-    int tile_hint;                                        // v4 tile <NW><RT><CT> when SKELDIFF_GL4_CFG is unset (0: per shape)
+    int tile_hint;                                        // v4 tile <NW><RT><CT> when gl4_cfg is 0 (0: per shape)
+    // per-launch kernel selection (the plan's options, sd_plan_set_option; process defaults for
+    // the test entry points): generation 0 auto / 1..5 forced, v4 tile <NW><RT><CT> (0 auto),
+    // v4 weight staging 0 LDS-DMA (CU held exclusively) / 1 register-staged (CU shareable)
+    int variant, gl4_cfg, gl4_stage;
     const float* x2; int64_t x2_rs; int K2;               // optional second input (cat along K)
     const float* W;                                       // (types, N, K1+K2), K contiguous
     const float* bias;                                    // (types, N) or null
@@ -44,6 +55,10 @@ struct GLArgs {
     int x1_blk, x2_blk, res_blk, out_blk;
     // v5 only: scratch for the pre-mix activations when res aliases out (zs_cap floats), or null
     float* zs; int64_t zs_cap;
+    unsigned* dbg;  // SD_DEBUG_LDS builds only: integrity counters (else unused)
+    // v4: bit 0 set (atomicOr) when an activation is outside the f16 range of the split
+    // (|x| >= 65504: x_hi would be inf); null = not checked
+    unsigned* status;
 };
 
 // f16 hi/lo split of a (types, N, K) f32 weight in MFMA B-fragment order (sd_graph_linear_v4.hip)
@@ -72,6 +87,7 @@ struct UpdArgs {
     float* out; float* out2; int64_t out2_rs;
     float* mean_out; int64_t mean_rs; float* noise_out; int64_t noise_rs;
     int64_t B; int J; int D;
+    unsigned* dbg;  // SD_DEBUG_LDS builds only
 };
 
 hipError_t launch_graph_linear(const GLArgs& a, bool rms, hipStream_t s);     // dispatches v1..v5
@@ -81,9 +97,14 @@ hipError_t launch_graph_linear_v2(const GLArgs& a, bool rms, hipStream_t s);
 hipError_t launch_graph_linear_v3(const GLArgs& a, bool rms, hipStream_t s);  // J in {16,17,21}
 hipError_t launch_graph_linear_v4(const GLArgs& a, bool rms, hipStream_t s);  // needs a.wsp
 hipError_t launch_qkv_attention_v4(const GLArgs& a, bool rms, hipStream_t s);  // J <= 16, dh 32
-int graph_linear_variant();  // SKELDIFF_GL_VARIANT (0 auto, 1, 2, 3, 4), read at load
+// process defaults that new plans (and the sd_test_* hooks) start from: SKELDIFF_GL_VARIANT
+// (0 auto, 1..5), SKELDIFF_GL4_CFG (<NW><RT><CT>, 0 auto), SKELDIFF_GL4_STAGE (0 / 1), read at load
+int graph_linear_variant();
 int set_graph_linear_variant(int v);  // returns the previous value, -1 if v is out of range
-int set_gl4_tile(int cfg);            // SKELDIFF_GL4_CFG (<NW><RT><CT>, 0 = auto); returns previous
+int gl4_tile_default();
+int set_gl4_tile(int cfg);            // returns the previous value
+int gl4_stage_default();
+int set_gl4_stage(int stage);         // returns the previous value, -1 if out of range
 hipError_t launch_attention(const AttnArgs& a, hipStream_t s);
 hipError_t launch_update(const UpdArgs& a, hipStream_t s);
 hipError_t launch_noise_fill(float* out, int64_t rows, int64_t n_per_row, uint64_t seed,
@@ -94,6 +115,8 @@ hipError_t launch_philox_raw(uint32_t* out, int64_t rows, int64_t quads, uint64_
 hipError_t launch_set_rng(uint64_t* rng_dev, uint64_t seed, int64_t row0, hipStream_t s);
 hipError_t launch_copy_rows(float* dst, int64_t dst_rs, const float* src, int64_t src_rs,
                             int64_t rows, int64_t n, hipStream_t s);
+// row-blocked v4 activation layout -> row-major (rows, J, F)
+hipError_t launch_unblock(float* out, const float* in, int64_t rows, int J, int F, hipStream_t s);
 
 // evaluation metrics (sd_metrics.hip)
 hipError_t launch_pairwise(const float* x, int64_t nseq, int S, int64_t X, float* l1_mean, float* l2_mean,

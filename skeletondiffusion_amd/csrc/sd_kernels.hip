@@ -212,7 +212,10 @@ int set_graph_linear_variant(int v) {
 // J > 21, where every one-kernel tile must stage all node types' weights.  1..5 force one
 // generation (falling through to v2 where the forced one does not apply).
 hipError_t launch_graph_linear(const GLArgs& a, bool rms, hipStream_t s) {
-    const int v = graph_linear_variant();
+    const int v = a.variant;
+    // every generation computes a column tile from the whole K extent of its rows: an input that
+    // aliases the output would be overwritten by sibling column tiles while still being read
+    if (a.B > 0 && (a.x1 == a.out || (a.x2 && a.x2 == a.out))) return hipErrorInvalidValue;
     if (v == 1) return launch_graph_linear_v1(a, rms, s);
     if (v == 4 || v == 0) {
         const hipError_t e = launch_graph_linear_v4(a, rms, s);
@@ -566,6 +569,13 @@ __global__ __launch_bounds__(256) void k_update(const UpdArgs p) {
         if (p.out2) st2(p.out2 + row * p.out2_rs + i * D + d, v);
         if (p.mean_out) st2(p.mean_out + row * p.mean_rs + i * D + d, mean);
     }
+#if defined(SD_DEBUG_LDS) && !defined(SD_DEBUG_NO_UPD)
+    {
+        unsigned bad = 0;
+        for (int i = (int)(g % DP); i < J * J; i += DP) bad += (sC1[i] != p.C1[i]) + (sC2[i] != p.C2[i]) + (sU[i] != p.U[i]);
+        if (bad) atomicAdd(&p.dbg[1], bad);
+    }
+#endif
 }
 
 hipError_t launch_update(const UpdArgs& a, hipStream_t s) {

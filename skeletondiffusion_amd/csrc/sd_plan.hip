@@ -30,6 +30,17 @@ int fail(int code, const std::string& msg) {
 
 int sd::set_error(int code, const std::string& msg) { return fail(code, msg); }
 
+#ifdef SD_DEBUG_LDS
+unsigned* sd::debug_counters() {
+    static unsigned* buf = [] {
+        unsigned* b = nullptr;
+        if (hipMalloc(&b, 8 * sizeof(unsigned)) != hipSuccess || hipMemset(b, 0, 8 * sizeof(unsigned)) != hipSuccess) abort();
+        return b;
+    }();
+    return buf;
+}
+#endif
+
 namespace {
 
 #define SD_HIP(x)                                                                              \
@@ -63,11 +74,37 @@ struct GraphKey {
     int32_t flags;
     int32_t chains;
     int32_t prec;
+    int32_t variant, gl4_cfg, gl4_stage;  // the plan's kernel options at capture time
     void* stream;
     bool operator<(const GraphKey& o) const { return std::memcmp(this, &o, sizeof(GraphKey)) < 0; }
 };
 
+// The captured graphs of one sd_sample_loop shape (one per row chain).  Shared by the cache and
+// every caller that is about to launch them, so an eviction by another thread never destroys an
+// exec a caller still holds; the last holder destroys them after the device has drained.
+struct GraphSet {
+    std::vector<hipGraphExec_t> execs;
+    ~GraphSet() {
+        if (execs.empty()) return;
+        (void)hipDeviceSynchronize();  // an exec may still be running on a caller's stream
+        for (auto x : execs) (void)hipGraphExecDestroy(x);
+    }
+};
+
 }  // namespace
+
+// Row chains.  Rows never interact inside the Denoiser or the posterior update, so the T-step
+// chain of rows [r0, r1) is independent of every other row range: record_loop splits the batch
+// into `chains` row ranges (multiples of 32 rows) and records each range's
+// T steps on its own stream, forked from and joined back into the caller's stream.  Kernels of
+// different chains then run concurrently, so one chain's idle CUs (a 200-workgroup graph linear
+// on 256 CUs, the last wave of a 800-workgroup attention launch) take the other chain's
+// workgroups instead of waiting for the next kernel boundary.
+static int g_chains = [] {
+    const char* e = getenv("SKELDIFF_CHAINS");
+    return e ? atoi(e) : 3;  // 3 chains + the caller's stream fit HIP's default 4 hardware queues
+}();
+
 
 struct sd_plan {
     sd_plan_desc d{};
@@ -79,15 +116,10 @@ struct sd_plan {
     bool fuse_ok = false;  // to_qkv + attention fusable (v4 split weights, J <= 16, dim_head 32)
     bool blk_ok = false;   // every layer on v4 with row-blocked intermediate activations
     int prec = 0;          // sd_plan_set_precision: 0 f32-accurate, 1 half (f16 products)
-    bool fuse_attention_now() const {
-        static const bool no_fuse = getenv("SKELDIFF_NO_FUSE") != nullptr;  // diagnostic
-        const int v = sd::graph_linear_variant();
-        return fuse_ok && !no_fuse && (v == 0 || v == 4);
-    }
-    bool blocked_now() const {
-        static const bool no_block = getenv("SKELDIFF_NO_BLOCK") != nullptr;  // diagnostic
-        return blk_ok && !no_block && fuse_attention_now();
-    }
+    // kernel options (sd_plan_set_option), initialised from the process defaults at creation
+    int variant = 0, gl4_cfg = 0, gl4_stage = 0, chains = 3;
+    bool fuse_attention_now() const { return fuse_ok && (variant == 0 || variant == 4); }
+    bool blocked_now() const { return blk_ok && fuse_attention_now(); }
     std::vector<void*> allocs;
 
     GL init_lin;
@@ -104,7 +136,7 @@ struct sd_plan {
     std::vector<float> iso_c1, iso_c2, iso_sig;  // host copies of the scalar tables (isotropic)
 
     std::mutex gmu;
-    std::map<GraphKey, std::vector<hipGraphExec_t>> graphs;  // one graph per row chain
+    std::map<GraphKey, std::shared_ptr<GraphSet>> graphs;  // one graph per row chain
     // row chains (record_loop): auxiliary streams + fork/join events, created on first use
     static constexpr int kMaxChains = 8;
     std::mutex cmu;
@@ -112,8 +144,7 @@ struct sd_plan {
     hipEvent_t ev_fork = nullptr, ev_join[kMaxChains] = {};
 
     ~sd_plan() {
-        for (auto& kv : graphs)
-            for (auto x : kv.second) (void)hipGraphExecDestroy(x);
+        graphs.clear();
         for (int i = 0; i < kMaxChains; ++i) {
             if (aux[i]) (void)hipStreamDestroy(aux[i]);
             if (ev_join[i]) (void)hipEventDestroy(ev_join[i]);
@@ -173,7 +204,7 @@ int dalloc(sd_plan* p, T** out, size_t n) {
 
 // workspace carve (all offsets 256-B aligned)
 struct WS {
-    uint64_t* rng;
+    uint64_t* rng;      // {seed, row0} of the device noise (graph replays); rng + 4: status word
     float *x, *r, *h, *qkv, *o, *res, *x0, *img0, *img1;
 };
 
@@ -184,7 +215,7 @@ size_t carve(const sd_plan* p, int64_t rows, char* base, WS* w) {
     const size_t rp = (size_t)((rows + 31) / 32 * 32);  // activations: padded to the 32-row blocks of the v4 layout
     const size_t nH = rp * p->J * p->H * f;
     const size_t nQ = rp * p->J * (p->d.use_attention ? 3 * p->hid : p->H) * f;
-    const size_t nO = rp * p->J * (p->d.use_attention ? p->hid : 1) * f;
+    const size_t nO = rp * p->J * (p->d.use_attention ? p->hid : p->H) * f;  // no attention: GL output
     const size_t nD = (size_t)rows * p->J * p->D * f;
     size_t off = 0;
     auto take = [&](size_t n) {
@@ -206,6 +237,9 @@ size_t carve(const sd_plan* p, int64_t rows, char* base, WS* w) {
     W.img1 = (float*)take(nD);
     return off;
 }
+
+// the workspace's status word (range-guard flags, sd_workspace_status)
+unsigned* ws_status(const WS& w) { return reinterpret_cast<unsigned*>(w.rng + 4); }
 
 sd::GLArgs gl_args(const sd_plan* p, const GL& g, const float* x1, int x1_div, const float* x2,
                    const float* film, const float* res, float* out, int64_t rows) {
@@ -238,6 +272,12 @@ sd::GLArgs gl_args(const sd_plan* p, const GL& g, const float* x1, int x1_div, c
     a.wsp_nct = g.split.nct;
     a.wsp_unscale = g.split.unscale;
     a.prec = p->prec;
+    a.variant = p->variant;
+    a.gl4_cfg = p->gl4_cfg;
+    a.gl4_stage = p->gl4_stage;
+#ifdef SD_DEBUG_LDS
+    a.dbg = sd::debug_counters();
+#endif
     return a;
 }
 
@@ -271,15 +311,25 @@ struct Prof {
 // cond_phase: row 0 of this call is row cond_phase of a cond_repeat group (row chains)
 int run_denoiser(const sd_plan* p, const float* x_t, const float* x_cond, int64_t cond_repeat,
                  int t, float* x0_out, int64_t rows, const WS& w, hipStream_t s, Prof* prof = nullptr,
-                 int64_t cond_phase = 0, int tile_hint = 0) {
+                 int64_t cond_phase = 0, int tile_hint = 0, float* const* trace = nullptr) {
     const int H = p->H;
     // v4 path: every intermediate activation in the row-blocked layout (coalesced x fragments);
     // the denoiser's inputs (x_t, x_cond) and output (x0) stay row-major
     const int B = p->blocked_now() ? 1 : 0;
+    // sd_denoiser_trace: block outputs (rows, J, H) row-major, in the reference's module order
+    int ntr = 0;
+    auto record = [&](const float* buf) -> int {
+        if (!trace) return SD_OK;
+        float* dst = trace[ntr++];
+        if (B) SD_HIP(sd::launch_unblock(dst, buf, rows, p->J, H, s));
+        else SD_HIP(sd::launch_copy_rows(dst, (int64_t)p->J * H, buf, (int64_t)p->J * H, rows, (int64_t)p->J * H, s));
+        return SD_OK;
+    };
     // v5 scratch (pre-mix activations of layers whose residual aliases their output): the qkv
     // buffer, dead outside the attention block (>= rows * J * H floats)
     const int64_t zs_cap = rows * p->J * (int64_t)(p->d.use_attention ? 3 * p->hid : p->H);
     auto lay = [B, tile_hint, &w, zs_cap](sd::GLArgs& g, int in, int res, int out) {
+        g.status = ws_status(w);
         g.zs = w.qkv;
         g.zs_cap = zs_cap;
         g.tile_hint = tile_hint;
@@ -299,6 +349,8 @@ int run_denoiser(const sd_plan* p, const float* x_t, const float* x_cond, int64_
     }
     lay(a, 0, 0, 1);
     SD_LAUNCH(prof, 0, sd::launch_graph_linear(a, false, s));
+    int rc = record(w.r);
+    if (rc) return rc;
 
     const int L = 2 * p->depth;
     for (int l = 0; l < L; ++l) {
@@ -313,7 +365,11 @@ int run_denoiser(const sd_plan* p, const float* x_t, const float* x_cond, int64_
         lay(a, 1, 1, 1);
         a.act = 1;
         SD_LAUNCH(prof, 0, sd::launch_graph_linear(a, false, s));
-        if (!p->has_attn[l]) continue;
+        if ((rc = record(w.x))) return rc;
+        if (!p->has_attn[l]) {
+            if ((rc = record(w.x))) return rc;  // nn.Identity in place of the last attention
+            continue;
+        }
         if (p->d.use_attention) {
             // Residual(PreNorm(Attention)): x = to_out(attn(to_qkv(rmsnorm(x)))) + x
             // q * dim_head ** -0.5 (attention.py:114,128): Python double scalar cast to fp32
@@ -341,11 +397,16 @@ int run_denoiser(const sd_plan* p, const float* x_t, const float* x_cond, int64_
             lay(a, 1, 1, 1);
             SD_LAUNCH(prof, 0, sd::launch_graph_linear(a, false, s));
         } else {
-            // Residual(PreNorm(StaticGraphLinear)): x = GL(rmsnorm(x)) + x
-            a = gl_args(p, p->qkv[l], w.x, 1, nullptr, nullptr, w.x, w.x, rows);
+            // Residual(PreNorm(StaticGraphLinear)): x = GL(rmsnorm(x)) + x, written to the `o`
+            // buffer (sized like x in this configuration: a graph-linear may not write its own
+            // input, sibling column tiles still read it) and copied back as x
+            a = gl_args(p, p->qkv[l], w.x, 1, nullptr, nullptr, w.x, w.o, rows);
             lay(a, 1, 1, 1);
             SD_LAUNCH(prof, 0, sd::launch_graph_linear(a, true, s));
+            const int64_t rp = B ? (rows + 31) / 32 * 32 : rows;
+            SD_LAUNCH(prof, 0, sd::launch_copy_rows(w.x, (int64_t)p->J * H, w.o, (int64_t)p->J * H, rp, (int64_t)p->J * H, s));
         }
+        if ((rc = record(w.x))) return rc;
     }
     // final_res_block on cat(x, r) (generator.py:104-106)
     const float* film = p->film + ((size_t)L * p->T + t) * 2 * H;
@@ -360,6 +421,7 @@ int run_denoiser(const sd_plan* p, const float* x_t, const float* x_cond, int64_
     lay(a, 1, 1, 1);
     a.act = 1;
     SD_LAUNCH(prof, 0, sd::launch_graph_linear(a, false, s));
+    if ((rc = record(w.res))) return rc;
     // final_glin (generator.py:107)
     a = gl_args(p, p->fglin, w.res, 1, nullptr, nullptr, nullptr, x0_out, rows);
     lay(a, 1, 1, 0);
@@ -395,6 +457,9 @@ int run_update(const sd_plan* p, const float* x0, const float* xt, const float* 
     u.B = rows;
     u.J = p->J;
     u.D = p->D;
+#ifdef SD_DEBUG_LDS
+    u.dbg = sd::debug_counters();
+#endif
     if (p->d.isotropic) {
         u.c1s = p->iso_c1[t];
         u.c2s = p->iso_c2[t];
@@ -444,6 +509,13 @@ int sd_plan_create(sd_plan** out, const sd_plan_desc* desc) {
     int rc = check_dims(desc);
     if (rc) return rc;
     std::unique_ptr<sd_plan> p(new sd_plan());
+    p->variant = sd::graph_linear_variant();
+    p->gl4_cfg = sd::gl4_tile_default();
+    p->gl4_stage = sd::gl4_stage_default();
+    p->chains = g_chains;
+#ifdef SD_DEBUG_LDS
+    (void)sd::debug_counters();  // allocated here, never during a stream capture
+#endif
     p->d = *desc;
     p->J = desc->num_nodes;
     p->D = desc->latent_dim;
@@ -684,7 +756,37 @@ int sd_denoiser_forward(const sd_plan* p, const float* x_t, const float* x_cond,
     if (!x_t || !x0_out) return fail(SD_E_INVALID, "null tensor");
     if (p->C > 0 && !x_cond) return fail(SD_E_INVALID, "x_cond is required (diffusion_conditioning)");
     if (cond_repeat < 1) return fail(SD_E_INVALID, "cond_repeat must be >= 1");
+    SD_HIP(hipMemsetAsync(ws_status(w), 0, sizeof(unsigned), (hipStream_t)stream));
     return run_denoiser(p, x_t, x_cond, cond_repeat, t, x0_out, rows, w, (hipStream_t)stream);
+}
+
+int sd_workspace_status(const sd_plan* p, const void* workspace, size_t ws_bytes, uint32_t* flags, void* stream) {
+    if (!flags) return fail(SD_E_INVALID, "null flags");
+    WS w;
+    int rc = ws_setup(p, 0, const_cast<void*>(workspace), ws_bytes, &w);
+    if (rc) return rc;
+    unsigned v = 0;
+    SD_HIP(hipMemcpyAsync(&v, ws_status(w), sizeof(unsigned), hipMemcpyDeviceToHost, (hipStream_t)stream));
+    SD_HIP(hipStreamSynchronize((hipStream_t)stream));
+    *flags = v;
+    return SD_OK;
+}
+
+int sd_denoiser_trace(const sd_plan* p, const float* x_t, const float* x_cond, int64_t cond_repeat, int32_t t,
+                      float* x0_out, int64_t rows, void* workspace, size_t ws_bytes, float* const* acts,
+                      int32_t nacts, void* stream) {
+    WS w;
+    int rc = ws_setup(p, rows, workspace, ws_bytes, &w);
+    if (rc) return rc;
+    if (t < 0 || t >= p->T) return fail(SD_E_INVALID, "t out of range");
+    if (!x_t || !x0_out || !acts) return fail(SD_E_INVALID, "null tensor");
+    if (nacts != 2 + 4 * p->depth) return fail(SD_E_INVALID, "nacts must be 2 + 4 * depth");
+    for (int i = 0; i < nacts; ++i)
+        if (!acts[i]) return fail(SD_E_INVALID, "null activation buffer");
+    if (p->C > 0 && !x_cond) return fail(SD_E_INVALID, "x_cond is required (diffusion_conditioning)");
+    if (cond_repeat < 1) return fail(SD_E_INVALID, "cond_repeat must be >= 1");
+    SD_HIP(hipMemsetAsync(ws_status(w), 0, sizeof(unsigned), (hipStream_t)stream));
+    return run_denoiser(p, x_t, x_cond, cond_repeat, t, x0_out, rows, w, (hipStream_t)stream, nullptr, 0, 0, acts);
 }
 
 int sd_p_sample_update(const sd_plan* p, const float* x0_raw, const float* x_t, const float* eps,
@@ -701,18 +803,6 @@ int sd_p_sample_update(const sd_plan* p, const float* x0_raw, const float* x_t, 
                       noise_out ? noise_rs : JD, rows, (hipStream_t)stream);
 }
 
-// Row chains.  Rows never interact inside the Denoiser or the posterior update, so the T-step
-// chain of rows [r0, r1) is independent of every other row range: record_loop splits the batch
-// into `chains` row ranges (multiples of 32 rows) and records each range's
-// T steps on its own stream, forked from and joined back into the caller's stream.  Kernels of
-// different chains then run concurrently, so one chain's idle CUs (a 200-workgroup graph linear
-// on 256 CUs, the last wave of a 800-workgroup attention launch) take the other chain's
-// workgroups instead of waiting for the next kernel boundary.
-static int g_chains = [] {
-    const char* e = getenv("SKELDIFF_CHAINS");
-    return e ? atoi(e) : 3;  // 3 chains + the caller's stream fit HIP's default 4 hardware queues
-}();
-
 static WS shift_ws(const sd_plan* p, const WS& w, int64_t r0) {
     WS o = w;
     const int64_t J = p->J;
@@ -721,7 +811,7 @@ static WS shift_ws(const sd_plan* p, const WS& w, int64_t r0) {
     o.h += r0 * J * p->H;
     o.res += r0 * J * p->H;
     o.qkv += r0 * J * (p->d.use_attention ? 3 * p->hid : p->H);
-    o.o += r0 * J * (p->d.use_attention ? p->hid : 1);
+    o.o += r0 * J * (p->d.use_attention ? p->hid : p->H);
     o.x0 += r0 * J * p->D;
     o.img0 += r0 * J * p->D;
     o.img1 += r0 * J * p->D;
@@ -733,7 +823,7 @@ static int chain_count(const sd_plan* p, int64_t rows, int64_t cond_repeat, int6
     const int64_t g = 32;  // a chain starts on a row block; x_cond rows via x1_row0
     *unit = g;
     const int64_t units = rows / g;
-    int n = std::max(1, std::min(g_chains, (int)sd_plan::kMaxChains));
+    int n = std::max(1, std::min(p->chains, (int)sd_plan::kMaxChains));
     if (units < n) n = (int)std::max<int64_t>(1, units);
     return n;
 }
@@ -843,6 +933,7 @@ int sd_sample_loop(const sd_plan* p, const float* x_T, const float* x_cond, int6
     if (rows == 0) return SD_OK;
     hipStream_t s = (hipStream_t)stream;
     sd_plan* mp = const_cast<sd_plan*>(p);
+    SD_HIP(hipMemsetAsync(ws_status(w), 0, sizeof(unsigned), s));
     int64_t unit = 32;
     const int nch = chain_count(p, rows, cond_repeat, &unit);
     std::unique_lock<std::mutex> lk(mp->cmu, std::defer_lock);  // fork/join objects are shared
@@ -855,8 +946,6 @@ int sd_sample_loop(const sd_plan* p, const float* x_T, const float* x_cond, int6
     }
     if (!(flags & SD_FLAG_GRAPH)) {
         if ((rc = fork_chains(mp, s, nch, cs))) return rc;
-        if (getenv("SKELDIFF_CHAIN_SERIAL"))  // diagnostic: same row split, one stream
-            for (int i = 1; i < nch; ++i) cs[i] = s;
         rc = record_loop(p, x_T, x_cond, cond_repeat, eps_all, seed, row0, out, means_out, noise_out, timages_out,
                          start_out, rows, w, flags, false, cs, nch, unit, -1);
         if (rc) return rc;
@@ -876,15 +965,20 @@ int sd_sample_loop(const sd_plan* p, const float* x_T, const float* x_cond, int6
     key.flags = flags;
     key.chains = nch;
     key.prec = p->prec;
+    key.variant = p->variant;
+    key.gl4_cfg = p->gl4_cfg;
+    key.gl4_stage = p->gl4_stage;
     key.stream = stream;
     SD_HIP(sd::launch_set_rng(w.rng, seed, row0, s));
-    std::vector<hipGraphExec_t> execs;
+    std::shared_ptr<GraphSet> set;
     {
         std::lock_guard<std::mutex> g(mp->gmu);
         auto it = p->graphs.find(key);
-        if (it != p->graphs.end()) execs = it->second;
+        if (it != p->graphs.end()) set = it->second;
     }
-    if (execs.empty()) {
+    if (!set) {
+        set = std::make_shared<GraphSet>();
+        std::vector<hipGraphExec_t>& execs = set->execs;
         for (int i = 0; i < nch; ++i) {
             hipGraph_t graph = nullptr;
             hipGraphExec_t exec = nullptr;
@@ -897,23 +991,25 @@ int sd_sample_loop(const sd_plan* p, const float* x_T, const float* x_cond, int6
                 if (graph) (void)hipGraphDestroy(graph);
             }
             if (rc || e != hipSuccess) {
-                for (auto x : execs) (void)hipGraphExecDestroy(x);
+                if (exec) (void)hipGraphExecDestroy(exec);
                 if (rc) return rc;
                 return fail(SD_E_HIP, std::string("graph capture: ") + hipGetErrorString(e));
             }
             execs.push_back(exec);
         }
-        std::lock_guard<std::mutex> g(mp->gmu);
-        auto& cache = mp->graphs;
-        if (cache.size() >= 8) {  // bounded cache: callers that reuse buffers hit it every call
-            for (auto& kv : cache)
-                for (auto x : kv.second) (void)hipGraphExecDestroy(x);
-            cache.clear();
+        std::shared_ptr<GraphSet> evicted;  // destroyed (after a device drain) outside the lock
+        {
+            std::lock_guard<std::mutex> g(mp->gmu);
+            auto& cache = mp->graphs;
+            if (cache.size() >= 8) {  // bounded cache: callers that reuse buffers hit it every call
+                evicted = cache.begin()->second;
+                cache.erase(cache.begin());
+            }
+            cache[key] = set;
         }
-        cache[key] = execs;
     }
     if ((rc = fork_chains(mp, s, nch, cs))) return rc;
-    for (int i = 0; i < nch; ++i) SD_HIP(hipGraphLaunch(execs[i], cs[i]));
+    for (int i = 0; i < nch; ++i) SD_HIP(hipGraphLaunch(set->execs[i], cs[i]));
     return join_chains(mp, s, nch, cs);
 }
 
@@ -1001,6 +1097,43 @@ int sd_set_kernel_variant(int32_t gl_variant, int32_t gl4_tile) {
     return old;
 }
 
+int sd_plan_set_option(sd_plan* p, int32_t option, int64_t value) {
+    if (!p) return fail(SD_E_INVALID, "null plan");
+    switch (option) {
+        case SD_OPT_KERNEL_VARIANT:
+            if (value < 0 || value > 5) return fail(SD_E_INVALID, "kernel variant must be in [0, 5]");
+            p->variant = (int)value;
+            return SD_OK;
+        case SD_OPT_GL4_TILE:
+            if (value < 0) return fail(SD_E_INVALID, "gl4 tile must be >= 0");
+            p->gl4_cfg = (int)value;
+            return SD_OK;
+        case SD_OPT_ROW_CHAINS:
+            if (value < 1 || value > sd_plan::kMaxChains) return fail(SD_E_INVALID, "row chains must be in [1, 8]");
+            p->chains = (int)value;
+            return SD_OK;
+        case SD_OPT_PRECISION: return sd_plan_set_precision(p, (int32_t)value);
+        case SD_OPT_GL4_STAGING:
+            if (value < 0 || value > 2)
+                return fail(SD_E_INVALID, "gl4 staging must be 0 (LDS-DMA), 1 (registers) or 2 (diagnostic)");
+            p->gl4_stage = (int)value;
+            return SD_OK;
+        default: return fail(SD_E_INVALID, "unknown option " + std::to_string(option));
+    }
+}
+
+int sd_plan_get_option(const sd_plan* p, int32_t option, int64_t* value) {
+    if (!p || !value) return fail(SD_E_INVALID, "null argument");
+    switch (option) {
+        case SD_OPT_KERNEL_VARIANT: *value = p->variant; return SD_OK;
+        case SD_OPT_GL4_TILE: *value = p->gl4_cfg; return SD_OK;
+        case SD_OPT_ROW_CHAINS: *value = p->chains; return SD_OK;
+        case SD_OPT_PRECISION: *value = p->prec; return SD_OK;
+        case SD_OPT_GL4_STAGING: *value = p->gl4_stage; return SD_OK;
+        default: return fail(SD_E_INVALID, "unknown option " + std::to_string(option));
+    }
+}
+
 int sd_plan_set_precision(sd_plan* p, int32_t mode) {
     if (!p) return fail(SD_E_INVALID, "null plan");
     if (mode != 0 && mode != 1) return fail(SD_E_INVALID, "precision mode must be 0 (f32) or 1 (half)");
@@ -1069,8 +1202,11 @@ int sd_test_graph_linear_layout(const float* x1, int32_t K1, int64_t x1_div, con
     a.x2_blk = (layout >> 1) & 1;
     a.res_blk = (layout >> 2) & 1;
     a.out_blk = (layout >> 3) & 1;
+    a.variant = sd::graph_linear_variant();
+    a.gl4_cfg = sd::gl4_tile_default();
+    a.gl4_stage = sd::gl4_stage_default();
     sd::SplitW sw;
-    if (sd::graph_linear_variant() == 0 || sd::graph_linear_variant() == 4) {
+    if (a.variant == 0 || a.variant == 4) {
         const auto key = std::make_tuple(W, a.ntypes, N, K1 + a.K2);
         auto it = cache ? cached.find(key) : cached.end();
         if (it != cached.end()) {
@@ -1118,6 +1254,9 @@ int sd_test_qkv_attention(const float* x, int32_t K, const float* W, const int64
     }
     a.attn_heads = heads;
     a.attn_scale = (float)std::pow(32.0, -0.5);
+    a.variant = sd::graph_linear_variant();
+    a.gl4_cfg = sd::gl4_tile_default();
+    a.gl4_stage = sd::gl4_stage_default();
     a.x1_blk = layout & 1;
     a.out_blk = (layout >> 3) & 1;
     sd::SplitW sw;
@@ -1141,6 +1280,16 @@ int sd_test_attention(const float* qkv, float* out, int64_t rows, int32_t J, int
     SD_HIP(sd::launch_attention(aa, (hipStream_t)stream));
     return SD_OK;
 }
+
+#ifdef SD_DEBUG_LDS
+// diagnostic build only: copy the LDS integrity counters to out[8] (host), then zero them
+int sd_debug_lds_counters(uint32_t* out) {
+    SD_HIP(hipDeviceSynchronize());
+    SD_HIP(hipMemcpy(out, sd::debug_counters(), 8 * sizeof(unsigned), hipMemcpyDeviceToHost));
+    SD_HIP(hipMemset(sd::debug_counters(), 0, 8 * sizeof(unsigned)));
+    return SD_OK;
+}
+#endif
 
 int sd_noise_fill(float* out, int64_t rows, int64_t n_per_row, uint64_t seed, int64_t row0, int32_t step,
                   void* stream) {

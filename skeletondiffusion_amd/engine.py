@@ -31,6 +31,7 @@ class SamplingEngine:
         self._ws = {}
         self._graph = False
         self._precision = 0
+        self._options = {}  # sd_plan_set_option values, re-applied when the plan is rebuilt
 
     # ---------------------------------------------------------------------------------------
     def __del__(self):
@@ -105,6 +106,25 @@ class SamplingEngine:
         if self._plan is not None:
             check(_lib.lib().sd_plan_set_precision(self._plan, self._precision))
 
+    OPTIONS = {"kernel_variant": _lib.SD_OPT_KERNEL_VARIANT, "gl4_tile": _lib.SD_OPT_GL4_TILE,
+               "row_chains": _lib.SD_OPT_ROW_CHAINS, "gl4_staging": _lib.SD_OPT_GL4_STAGING}
+
+    def set_option(self, name: str, value: int) -> None:
+        """Per-plan kernel option (sd_plan_set_option): "kernel_variant" (0 auto, 1..5),
+        "gl4_tile" (<waves><row tiles><col tiles>, 0 auto), "row_chains" (1..8), "gl4_staging"
+        (0 LDS-DMA with the CU held exclusively, 1 register-staged).  Kept across plan rebuilds;
+        other engines (plans) in the process are unaffected."""
+        if name not in self.OPTIONS:
+            raise SkelDiffError(f"unknown option {name!r}; one of {sorted(self.OPTIONS)}")
+        if self._plan is not None:
+            check(_lib.lib().sd_plan_set_option(self._plan, self.OPTIONS[name], int(value)))
+        self._options[name] = int(value)
+
+    def get_option(self, name: str) -> int:
+        v = ctypes.c_int64()
+        check(_lib.lib().sd_plan_get_option(self.plan(), self.OPTIONS[name], ctypes.byref(v)))
+        return int(v.value)
+
     @property
     def precision(self) -> str:
         return {v: k for k, v in self.PRECISIONS.items()}[self._precision]
@@ -136,6 +156,8 @@ class SamplingEngine:
                     check(L.sd_plan_set_tensor(handle, name.encode(), ptr(t), t.numel(), stream))
                 check(L.sd_plan_finalize(handle, stream))
                 check(L.sd_plan_set_precision(handle, self._precision))
+                for name, value in self._options.items():
+                    check(L.sd_plan_set_option(handle, self.OPTIONS[name], value))
             except Exception:
                 L.sd_plan_destroy(handle)
                 raise
@@ -187,6 +209,24 @@ class SamplingEngine:
         check(_lib.lib().sd_denoiser_forward(plan, ptr(x), ptr(xc), rep, int(t), ptr(out), rows, ptr(ws), nb,
                                              _stream(self._device)))
         return out
+
+    def denoiser_trace(self, x: torch.Tensor, t: int, x_cond=None):
+        """-> (x0, [block outputs]) -- sd_denoiser_trace: init_lin, per layer the ResnetBlock and
+        attention (Identity for the last) outputs, final_res_block; each (B, J, D + cond_dim)."""
+        plan = self.plan()
+        J, D = self.diff.channels, self.diff.seq_length
+        x = self._f32(x)
+        rows = x.shape[0]
+        xc, rep = self._cond(x_cond, rows)
+        m = self.diff.model
+        H = m.dim + m.cond_dim
+        acts = [torch.empty((rows, J, H), device=self._device) for _ in range(2 + 4 * m.depth)]
+        arr = (ctypes.c_void_p * len(acts))(*[a.data_ptr() for a in acts])
+        out = torch.empty((rows, J, m.out_dim), device=self._device, dtype=torch.float32)
+        ws, nb = self.workspace(rows)
+        check(_lib.lib().sd_denoiser_trace(plan, ptr(x), ptr(xc), rep, int(t), ptr(out), rows, ptr(ws), nb, arr,
+                                           len(acts), _stream(self._device)))
+        return out, acts
 
     def p_sample(self, x, t: int, x_cond=None, eps=None):
         plan = self.plan()
@@ -256,6 +296,15 @@ class SamplingEngine:
             check(_lib.lib().sd_sample_loop(*args, cur.cuda_stream))
         start_ret = start.clone() if start is not None else start_out
         return out, start_ret, noise_t, mean_t, imgs
+
+    def status(self, rows: int) -> int:
+        """Flags of the last sample_loop / denoiser_forward on the `rows`-row workspace
+        (sd_workspace_status; synchronises the current stream): SD_STATUS_F16_RANGE = an
+        activation left the f16 range of the split-f16 products."""
+        ws, nb = self.workspace(rows)
+        v = ctypes.c_uint32()
+        check(_lib.lib().sd_workspace_status(self.plan(), ptr(ws), nb, ctypes.byref(v), _stream(self._device)))
+        return int(v.value)
 
     def enable_graph(self, on: bool = True):
         """Capture whole sample() chains in hipGraphs (cached per shape/pointer set)."""

@@ -74,12 +74,17 @@ def sample_sharded(sample_fn: Callable[..., torch.Tensor], x_cond: torch.Tensor,
     rank, world = _world()
     nseq = x_cond.shape[0]
     s0, s1 = shard_range(nseq, rank, world)
-    mine = sample_fn(batch_size=(s1 - s0) * futures, x_cond=x_cond[s0:s1], seed=seed, row0=s0 * futures)
+    if s1 > s0:
+        mine = sample_fn(batch_size=(s1 - s0) * futures, x_cond=x_cond[s0:s1], seed=seed, row0=s0 * futures)
+    else:  # more ranks than sequences: an empty shard still joins the all_gather below
+        mine = x_cond.new_empty((0,) + tuple(x_cond.shape[1:]))
     if not gather or world == 1:
         return mine, s0
     # ragged shards: pad to the largest shard, all_gather, then drop the padding
     per = [shard_range(nseq, r, world) for r in range(world)]
     rows_max = max(b - a for a, b in per) * futures
+    if rows_max == 0:
+        return mine, s0
     buf = mine.new_zeros((rows_max,) + tuple(mine.shape[1:]))
     buf[:mine.shape[0]] = mine
     parts = [torch.empty_like(buf) for _ in range(world)]

@@ -35,6 +35,27 @@ def hip_training_enabled() -> bool:
     return _ENABLED
 
 
+MAX_NODES = 64  # sd_gl_train_forward / _backward: 1 <= J <= 64
+
+
+def hip_shapes_ok(x, weight, ghat, node_types) -> bool:
+    """Whether a StaticGraphLinear call fits the HIP training kernels (else the torch path
+    runs): J <= 64, a (J, J) mixing matrix, and a node_types vector of length J whose values
+    index the weight's type axis.  Mismatches raise the torch path's own shape errors instead of
+    becoming out-of-bounds device reads."""
+    if x.dim() < 2:
+        return False
+    J = x.shape[-2]
+    if not (1 <= J <= MAX_NODES) or tuple(ghat.shape) != (J, J) or weight.dim() not in (2, 3):
+        return False
+    if node_types is None:
+        return weight.dim() == 2
+    if weight.dim() != 3 or node_types.numel() != J:
+        return False
+    nt = node_types.detach()
+    return bool((nt >= 0).all()) and int(nt.max()) < weight.shape[0]
+
+
 def _stream(dev: torch.device) -> int:
     return torch.cuda.current_stream(dev).cuda_stream
 

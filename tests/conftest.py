@@ -30,7 +30,9 @@ def golden(name):
 
 
 RELEASE_FIXTURES = ["release_h36m16_T10", "release_h36m16_T100", "release_amass21_T10",
-                    "release_freeman17_T10", "release_mano51_T10"]
+                    "release_freeman17_T10", "release_mano51_T10",
+                    # BASELINE config 3 (MANO J=51) at T=100 and config 4 (H36M J=16) at T=1000
+                    "release_mano51_T100", "release_h36m16_T1000"]
 
 
 _SKEL_BY_J = {16: "h36m16", 21: "amass21", 17: "freeman17", 51: "mano51"}
@@ -48,7 +50,7 @@ def pinned_cov(J):
     return tuple(torch.from_numpy(z[k]) for k in ("Sigma_N", "Lambda_N", "U"))
 
 
-def build_release_diffusion(z, device="cpu", T=None):
+def build_release_diffusion(z, device="cpu", T=None, use_attention=True, final_scale=None, **diff_kw):
     """Product NonisotropicGaussianDiffusion + Denoiser (release architecture) with the fixture's
     synthetic weights (gen_golden.py:build_release)."""
     from skeletondiffusion_amd import synthetic
@@ -58,10 +60,10 @@ def build_release_diffusion(z, device="cpu", T=None):
     J = z["corr"].shape[0]
     T = int(z["T"]) if T is None else T
     m = Denoiser(dim=96, cond_dim=96, out_dim=96, channels=J, num_nodes=J,
-                 node_types=torch.from_numpy(z["node_types"]), use_attention=True, self_condition=False,
+                 node_types=torch.from_numpy(z["node_types"]), use_attention=use_attention, self_condition=False,
                  norm_type="none", depth=4, attn_dim_head=32, attn_heads=8, learn_influence=True)
     synthetic.fill_module_(m, WEIGHT_SEED)
-    fs = float(z["final_scale"]) if "final_scale" in z else 1.0
+    fs = final_scale if final_scale is not None else float(z["final_scale"]) if "final_scale" in z else 1.0
     if fs != 1.0:
         with torch.no_grad():
             m.final_glin.weight.mul_(fs)
@@ -69,8 +71,29 @@ def build_release_diffusion(z, device="cpu", T=None):
     S, L, U = pinned_cov(J)
     d = NonisotropicGaussianDiffusion(Sigma_N=S, Lambda_N=L, U=U, model=m, latent_size=96,
                                       diffusion_timesteps=T, diffusion_objective="pred_x0",
-                                      diffusion_conditioning=True, beta_schedule="cosine")
+                                      diffusion_conditioning=True, beta_schedule="cosine", **diff_kw)
     return d.to(device).eval()
+
+
+# tests/golden/variants_h36m16_T10.npz (gen_golden.py:gen_variants): interpolate_funct restated
+INTERP_W = (0.25, 0.75)
+
+
+def interpolate_funct(n1, n2):
+    return INTERP_W[0] * n1 + INTERP_W[1] * n2
+
+
+def variant_inputs(z):
+    """(x_cond per row, start, sampling noise, noise2interpolate) of the variants fixture."""
+    from skeletondiffusion_amd import synthetic
+
+    bs, fu, T = int(z["B_seq"]), int(z["futures"]), int(z["T"])
+    B = bs * fu
+    xc = torch.from_numpy(synthetic.uniform((bs, 16, 96), 21)).repeat_interleave(fu, 0)
+    start = torch.from_numpy(synthetic.normal((B, 16, 96), 22))
+    samp = torch.from_numpy(synthetic.normal((B, T - 1, 16, 96), 23))
+    noise2 = torch.from_numpy(synthetic.normal((B, T - 1, 16, 96), 26))
+    return xc, start, samp, noise2
 
 
 def release_inputs(z, T=None):

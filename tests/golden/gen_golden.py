@@ -117,13 +117,13 @@ def diffusion_buffers(diff) -> dict:
     return {f"buf_{k}": v for k, v in diff.state_dict().items() if not k.startswith("model.")}
 
 
-def build_release(skel_key, T, seed=WEIGHT_SEED, final_scale=1.0):
+def build_release(skel_key, T, seed=WEIGHT_SEED, final_scale=1.0, arch=None, **diff_kw):
     sk = SKELETONS[skel_key]()
     J = sk.num_nodes
     node_types = sk.nodes_type_id
     corr = sk.adj_matrix
     model = Denoiser(dim=96, cond_dim=96, out_dim=96, channels=J, num_nodes=J,
-                     node_types=node_types, **RELEASE_ARCH)
+                     node_types=node_types, **dict(RELEASE_ARCH, **(arch or {})))
     synthetic.fill_module_(model, seed)
     if final_scale != 1.0:  # push x0 past +-1 so the clamp (base.py:318-319) is exercised
         with torch.no_grad():
@@ -136,7 +136,7 @@ def build_release(skel_key, T, seed=WEIGHT_SEED, final_scale=1.0):
                                          diffusion_objective="pred_x0",
                                          diffusion_conditioning=True, beta_schedule="cosine",
                                          diffusion_covariance_type="skeleton-diffusion",
-                                         gamma_scheduler="cosine", loss_reduction_type="l1")
+                                         gamma_scheduler="cosine", loss_reduction_type="l1", **diff_kw)
     diff.eval()
     return sk, corr, node_types, diff
 
@@ -254,6 +254,57 @@ def gen_release(skel_key, T, B_seq, futures, with_acts, steps_to_keep=None, tag=
     _save(tag or f"release_{skel_key}_T{T}", **out)
 
 
+INTERP_W = (0.25, 0.75)  # interpolate_funct(n1, n2) = 0.25 n1 + 0.75 n2 (consumers restate it)
+
+
+def gen_variants():
+    """Optional sample() surface on the release H36M J=16 Denoiser, T=10, 1 sequence x 3 futures:
+    Denoiser(use_attention=False) (generator.py:65: Residual(PreNorm(StaticGraphLinear))),
+    diffusion_activation='tanh' (base.py:78-79, 254), return_timages (base.py:371-389) and noise
+    interpolation (base.py:335-338, nonisotropic.py:218-227) with a fixed interpolate_funct."""
+    T, B_seq, futures = 10, 1, 3
+    B = B_seq * futures
+    out = {"B_seq": B_seq, "futures": futures, "T": T}
+    x_cond = torch.from_numpy(synthetic.uniform((B_seq, 16, 96), seed=21)).repeat_interleave(futures, 0)
+    start = torch.from_numpy(synthetic.normal((B, 16, 96), seed=22))
+    samp = torch.from_numpy(synthetic.normal((B, T - 1, 16, 96), seed=23))
+    noise2 = torch.from_numpy(synthetic.normal((B, T - 1, 16, 96), seed=26))
+    cases = {
+        "noattn": dict(arch=dict(use_attention=False)),
+        "tanh": dict(final_scale=8.0, diffusion_activation="tanh"),
+        "base": {},
+    }
+    for name, kw in cases.items():
+        _, corr, node_types, diff = build_release("h36m16", T, **kw)
+        out["node_types"], out["corr"] = node_types, corr
+        with torch.no_grad():
+            img, (_, _, mean_t) = diff.sample(batch_size=B, x_cond=x_cond, start_noise=start.clone(),
+                                              sampling_noise=samp.clone(), return_sampling_noise=True)
+            out[f"{name}_img"], out[f"{name}_mean_t"] = img, mean_t
+            if name == "base":
+                img2, (_, timgs) = diff.sample(batch_size=B, x_cond=x_cond, start_noise=start.clone(),
+                                               sampling_noise=samp.clone(), return_timages=True)
+                out["timages_img"], out["timages"] = img2, timgs
+                a, b = INTERP_W
+                img3, _ = diff.sample(batch_size=B, x_cond=x_cond, start_noise=start.clone(),
+                                      sampling_noise=samp.clone(), if_interpolate=True,
+                                      noise2interpolate=noise2.clone(),
+                                      interpolation_kwargs={"interpolate_funct": lambda n1, n2: a * n1 + b * n2})
+                out["interp_img"] = img3
+        if name == "noattn":
+            out["noattn_keys"] = np.array(sorted(diff.state_dict().keys()))
+    _save("variants_h36m16_T10", **out)
+
+
+def gen_new_r02():
+    """Round-2 fixtures: BASELINE config 3 at T=100 (MANO J=51) and config 4 at T=1000 (H36M
+    J=16), plus the optional sample() surface (gen_variants)."""
+    gen_variants()
+    gen_release("mano51", 100, B_seq=2, futures=2, with_acts=False, steps_to_keep=[0, 9, 49, 98])
+    gen_release("h36m16", 1000, B_seq=1, futures=2, with_acts=False,
+                steps_to_keep=[0, 1, 2, 3, 4, 499, 994, 995, 996, 997, 998])
+
+
 def gen_metrics():
     """The reference's multimodal metrics (src/metrics/multimodal.py) on synthetic samples: latent
     APD (L1) and APD (L2) over 50 futures of (J=16, 96) latents, and ADE / FDE of (frames, J*3)
@@ -321,6 +372,9 @@ def main():
     if sys.argv[1:] == ["decoder"]:
         gen_decoder()
         return
+    if sys.argv[1:] == ["r02"]:
+        gen_new_r02()
+        return
     gen_metrics()
     gen_decoder()
     gen_covariances()
@@ -330,6 +384,7 @@ def main():
     gen_release("amass21", 10, B_seq=1, futures=4, with_acts=True, final_scale=8.0)
     gen_release("freeman17", 10, B_seq=1, futures=4, with_acts=False)
     gen_release("mano51", 10, B_seq=1, futures=2, with_acts=False)
+    gen_new_r02()
 
 
 if __name__ == "__main__":

@@ -156,3 +156,46 @@ def test_three_rank_sharded_eval_equals_single_process():
     np.testing.assert_allclose(full, single.numpy(), atol=1e-6, rtol=0)
     ref_mean = single.reshape(NSEQ3, FUT3, J * 96).abs().mean((1, 2)).double().mean().item()
     assert abs(mean - ref_mean) < 1e-6
+
+
+def _empty_shard_worker(rank, world, port, q):
+    """3 ranks, 2 sequences: rank 2 owns no sequence.  Its sample_fn must not be called (the HIP
+    engine rejects x_cond with 0 rows, base.py:246-248 semantics), yet it joins the all_gather."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from skeletondiffusion_amd import sharded, synthetic
+
+    xc = torch.from_numpy(np.stack([synthetic.uniform((J, 96), 10_000 + s) for s in range(2)]))
+    calls = []
+
+    def fn(batch_size, x_cond, seed, row0):
+        if x_cond.shape[0] == 0 or batch_size == 0:
+            raise ValueError("x_cond rows (0) must divide the batch")  # what the engine raises
+        calls.append(batch_size)
+        return _oracle_sample_fn(x_cond, batch_size, seed, row0)
+
+    full, s0 = sharded.sample_sharded(fn, xc, FUT3, SEED)
+    q.put((rank, full.numpy(), s0, calls))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_more_ranks_than_sequences():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_empty_shard_worker, args=(r, 3, port, q)) for r in range(3)]
+    for p in procs:
+        p.start()
+    got = sorted([q.get(timeout=300) for _ in range(3)], key=lambda g: g[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert [g[3] for g in got] == [[FUT3], [FUT3], []]
+    from skeletondiffusion_amd import synthetic
+
+    xc = torch.from_numpy(np.stack([synthetic.uniform((J, 96), 10_000 + s) for s in range(2)]))
+    single = _oracle_sample_fn(xc, 2 * FUT3, SEED, 0).numpy()
+    for g in got:
+        assert g[1].shape == single.shape
+        np.testing.assert_allclose(g[1], single, atol=1e-6, rtol=0)

@@ -1,0 +1,263 @@
+"""GPU parity on the BASELINE configurations as they are benched, and on the optional sample()
+surface (VERDICT r01 "what's missing" 1-3):
+
+* config 4 (Human3.6M J=16, one sequence x 50 futures, T=1000, hipGraph, device noise): the
+  first 5 and the last 5 reverse steps against the oracle fed the same Philox normals, plus
+  graph == eager bitwise, finiteness, determinism and the t = 0 clamp; the reference's own T=1000
+  chain is in test_gpu_parity.py::test_release_sample_matches_reference[release_h36m16_T1000];
+* config 2 exactly as bench.py times it (J=16, B=3200, T=100, 3 row chains, 32x64 tiles,
+  hipGraph, reused output buffer, device noise): every per-step record bitwise equal to one chain
+  run eagerly, and the first 3 steps against the oracle on the rows at the chain boundaries;
+* per-layer activations of the Denoiser (sd_denoiser_trace) against the reference's forward hooks;
+* Denoiser(use_attention=False), diffusion_activation='tanh', return_timages and noise
+  interpolation against the reference's outputs (tests/golden/variants_h36m16_T10.npz);
+* two plans with different kernel options sampling concurrently in one process.
+
+Tolerance: 1e-4 absolute on generated latents (north star); the per-layer activations 1e-5."""
+import threading
+
+import numpy as np
+import pytest
+import torch
+
+import oracle as O
+from conftest import (WEIGHT_SEED, build_release_diffusion, golden, interpolate_funct, release_inputs,
+                      variant_inputs)
+from skeletondiffusion_amd import _lib
+
+pytestmark = pytest.mark.gpu
+TOL = 1e-4
+
+
+def _max_err(a, b):
+    a = a.detach().float().cpu().numpy() if torch.is_tensor(a) else np.asarray(a)
+    b = b.detach().float().cpu().numpy() if torch.is_tensor(b) else np.asarray(b)
+    return float(np.abs(a - b).max()) if a.size else 0.0
+
+
+def _oracle_setup(d):
+    J = d.channels
+    sd = {k: v.detach().cpu() for k, v in d.state_dict().items()}
+    cfg = O.release_config(J, d.model.node_types)
+    bufs = {k: v for k, v in sd.items() if not k.startswith("model.")}
+    return sd, cfg, bufs
+
+
+def _device_normals(seed, rows, step, J, D):
+    return torch.from_numpy(O.philox_normal(seed, np.asarray(rows), step, J * D).reshape(len(rows), J, D))
+
+
+def test_config4_t1000_graph_first_and_last_steps(cuda):
+    """BASELINE config 4: H36M J=16, 1 sequence x 50 futures, T=1000, hipGraph-captured chain."""
+    from bench import build_config
+
+    d, x_cond, rows = build_config("h36m_t1000", cuda)
+    J, D, T = d.channels, d.seq_length, d.num_timesteps
+    assert (rows, J, T) == (50, 16, 1000)
+    seed, eng = 4711, d.engine
+    out = torch.empty((rows, J, D), device=cuda)
+    g = eng.sample_loop(rows, x_cond=x_cond, seed=seed, graph=True, out=out, record=(False, True))
+    img_g, start, imgs = g[0].clone(), g[1].clone(), g[4]
+    g2 = eng.sample_loop(rows, x_cond=x_cond, seed=seed, graph=True, out=out, keep_start=False)[0].clone()
+    e = eng.sample_loop(rows, x_cond=x_cond, seed=seed, graph=False)[0]
+    torch.cuda.synchronize()
+    assert torch.isfinite(img_g).all() and img_g.abs().max() <= 1.0 + 1e-6  # t = 0: clamp(x0)
+    assert torch.equal(img_g, g2) and torch.equal(img_g, e)
+    sd, cfg, bufs = _oracle_setup(d)
+    xc = x_cond.cpu()
+    r = np.arange(rows)
+    # first 5 steps from the device start noise (Philox step index T)
+    st = _device_normals(seed, r, T, J, D)
+    assert _max_err(start, st) < 2e-5
+    x = st
+    for k in range(5):
+        t = T - 1 - k
+        x, _ = O.p_sample_step(sd, cfg, bufs, x, t, _device_normals(seed, r, t, J, D), x_cond=xc)
+        assert _max_err(imgs[:, k], x) < TOL, (k, _max_err(imgs[:, k], x))
+    # last 5 steps (t = 4 .. 0) from the GPU's x_5 (the output of the step at t = 5)
+    x = imgs[:, T - 1 - 5].cpu()
+    for t in range(4, -1, -1):
+        noise = _device_normals(seed, r, t, J, D) if t > 0 else 0.0
+        x, _ = O.p_sample_step(sd, cfg, bufs, x, t, noise, x_cond=xc)
+        ref = imgs[:, T - 1 - t] if t > 0 else img_g
+        assert _max_err(ref, x) < TOL, (t, _max_err(ref, x))
+
+
+def test_config2_as_benched(cuda):
+    """BASELINE config 2 with the bench's exact launch configuration: 3 row chains (32 x 64
+    graph-linear tiles), hipGraph, device noise, reused output buffer; every per-step record of
+    the whole T = 100 chain bitwise equal to one chain run eagerly; first 3 steps vs the oracle on
+    the rows either side of each chain boundary."""
+    from bench import build_config
+
+    d, x_cond, rows = build_config("amass16", cuda, T=100)
+    J, D, T = d.channels, d.seq_length, d.num_timesteps
+    eng, seed = d.engine, 20251015
+    eng.set_option("row_chains", 3)
+    out = torch.empty((rows, J, D), device=cuda)
+    a = eng.sample_loop(rows, x_cond=x_cond, seed=seed, graph=True, out=out, record=(True, True))
+    a = [t.clone() for t in (a[0], a[1], a[2], a[4])]  # img, start, noise_t, imgs
+    eng.set_option("row_chains", 1)
+    b = eng.sample_loop(rows, x_cond=x_cond, seed=seed, graph=False, record=(True, True))
+    b = [b[0], b[1], b[2], b[4]]
+    # the exact bench.py call (no records, output buffer reused, start not kept)
+    eng.set_option("row_chains", 3)
+    c = eng.sample_loop(rows, x_cond=x_cond, seed=seed, graph=True, out=out, keep_start=False)[0]
+    torch.cuda.synchronize()
+    for x, y in zip(a, b):
+        assert torch.equal(x, y)
+    assert torch.equal(c, a[0])
+    img, start, imgs = a[0], a[1], a[3]
+    assert torch.isfinite(img).all() and img.abs().max() <= 1.0 + 1e-6
+    # the chain starts of a 3200-row, 3-chain split: rows 0, 1056, 2112 (multiples of 32)
+    sel = np.concatenate([np.arange(0, 16), np.arange(1040, 1072), np.arange(2096, 2128), np.arange(3184, 3200)])
+    sd, cfg, bufs = _oracle_setup(d)
+    xc = x_cond.cpu().repeat_interleave(rows // x_cond.shape[0], 0)[sel]
+    x = _device_normals(seed, sel, T, J, D)
+    assert _max_err(start[sel], x) < 2e-5
+    for k in range(3):
+        t = T - 1 - k
+        x, _ = O.p_sample_step(sd, cfg, bufs, x, t, _device_normals(seed, sel, t, J, D), x_cond=xc)
+        assert _max_err(imgs[sel, k], x) < TOL, (k, _max_err(imgs[sel, k], x))
+
+
+def test_register_staging_shares_cus_bitwise(cuda):
+    """SD_OPT_GL4_STAGING = 1 (register-staged weight stages, no whole-CU LDS reservation): the
+    co-residency that corrupts the LDS-DMA stages is bitwise safe here, and the
+    arithmetic is the default path's (same products, same order)."""
+    from bench import build_config
+
+    d, x_cond, rows = build_config("amass16", cuda, T=10)
+    eng = d.engine
+    ref = eng.sample_loop(rows, x_cond=x_cond, seed=3)[0].clone()
+    eng.set_option("gl4_staging", 1)
+    for n in (3, 2):
+        eng.set_option("row_chains", n)
+        for graph in (False, True):
+            x = eng.sample_loop(rows, x_cond=x_cond, seed=3, graph=graph)[0]
+            torch.cuda.synchronize()
+            assert torch.equal(x, ref), (n, graph)
+    assert eng.get_option("gl4_staging") == 1
+
+
+@pytest.mark.parametrize("name", ["release_h36m16_T10", "release_amass21_T10"])
+def test_denoiser_per_layer_activations(name, cuda):
+    """Every block output of one Denoiser forward (init_lin, 8 ResnetBlocks, 7 attention blocks +
+    the final Identity, final_res_block) against the reference's forward hooks."""
+    z = golden(name)
+    d = build_release_diffusion(z, cuda)
+    xcs, fu, start, _ = release_inputs(z)
+    x0, acts = d.engine.denoiser_trace(start.to(cuda), int(z["T"]) - 1, xcs.to(cuda))
+    names = ["init_lin"] + [f"layer{i}_{k}" for i in range(8) for k in ("res", "attn")] + ["final_res"]
+    assert len(acts) == len(names)
+    for n, a in zip(names, acts):
+        assert _max_err(a, z["act_" + n]) < 1e-5, n
+    assert _max_err(x0, z["fwd_x0"]) < 1e-5
+
+
+@pytest.mark.parametrize("case", ["noattn", "tanh", "timages", "interp"])
+def test_sample_surface_variants(case, cuda):
+    z = golden("variants_h36m16_T10")
+    kw = {}
+    if case == "noattn":
+        kw = dict(use_attention=False)
+    elif case == "tanh":
+        kw = dict(final_scale=8.0, diffusion_activation="tanh")
+    d = build_release_diffusion(z, cuda, **kw)
+    xc, start, samp, noise2 = (t.to(cuda) for t in variant_inputs(z))
+    B = start.shape[0]
+    if case == "timages":
+        img, (_, timgs) = d.sample(batch_size=B, x_cond=xc, start_noise=start, sampling_noise=samp,
+                                   return_timages=True)
+        assert _max_err(img, z["timages_img"]) < TOL and _max_err(timgs, z["timages"]) < TOL
+        img2, (_, nt, timgs2) = d.sample(batch_size=B, x_cond=xc, start_noise=start, sampling_noise=samp,
+                                         return_sampling_noise=True, return_timages=True)
+        assert torch.equal(img, img2) and torch.equal(timgs, timgs2) and torch.equal(nt, samp)
+        return
+    if case == "interp":
+        img, _ = d.sample(batch_size=B, x_cond=xc, start_noise=start, sampling_noise=samp, if_interpolate=True,
+                          noise2interpolate=noise2, interpolation_kwargs={"interpolate_funct": interpolate_funct})
+        assert _max_err(img, z["interp_img"]) < TOL
+        return
+    img, (_, _, mean_t) = d.sample(batch_size=B, x_cond=xc, start_noise=start, sampling_noise=samp,
+                                   return_sampling_noise=True)
+    assert _max_err(img, z[f"{case}_img"]) < TOL and _max_err(mean_t, z[f"{case}_mean_t"]) < TOL
+    if case == "noattn":
+        assert sorted(d.state_dict().keys()) == sorted(z["noattn_keys"].tolist())
+
+
+def test_two_plans_with_different_options_concurrently(cuda):
+    """Kernel options are plan state (sd_plan_set_option), not process globals: plan A (auto
+    kernels, 3 row chains) and plan B (exact-f32 v3, 1 chain, register staging) sample at the same
+    time on two streams from two threads; each equals its own solo result bitwise, and the two
+    agree within the split-f16 vs exact-f32 difference."""
+    z = golden("release_h36m16_T100")
+    da = build_release_diffusion(z, cuda)
+    db = build_release_diffusion(z, cuda)
+    db.engine.set_option("kernel_variant", 3)
+    db.engine.set_option("gl4_staging", 1)
+    db.engine.set_option("row_chains", 1)
+    da.engine.set_option("row_chains", 3)
+    xcs = torch.from_numpy(np.repeat(release_inputs(z)[0].numpy(), 64, 0)).to(cuda)[:64]  # 64 sequences
+    rows = 64 * 4
+    solo_a = da.sample(batch_size=rows, x_cond=xcs, seed=8)[0].clone()
+    solo_b = db.sample(batch_size=rows, x_cond=xcs, seed=8)[0].clone()
+    torch.cuda.synchronize()
+    again_b = db.sample(batch_size=rows, x_cond=xcs, seed=8)[0].clone()
+    torch.cuda.synchronize()
+    assert torch.equal(again_b, solo_b), (_max_err(again_b, solo_b), _max_err(solo_a, solo_b), _max_err(again_b, solo_a))
+    res = {}
+
+    def run(name, d):
+        s = torch.cuda.Stream(cuda)
+        with torch.cuda.stream(s):
+            for _ in range(3):
+                res[name] = d.sample(batch_size=rows, x_cond=xcs, seed=8)[0]
+        s.synchronize()
+
+    th = [threading.Thread(target=run, args=("a", da)), threading.Thread(target=run, args=("b", db))]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    torch.cuda.synchronize()
+    assert torch.equal(res["a"], solo_a) and torch.equal(res["b"], solo_b)
+    assert _max_err(solo_a, solo_b) < TOL
+    assert da.engine.get_option("kernel_variant") == 0 and db.engine.get_option("kernel_variant") == 3
+
+
+def test_graph_linear_rejects_aliased_output(cuda):
+    """A graph-linear launch whose input is its output would race between column tiles (ADVICE
+    r01): the library refuses it instead of computing garbage."""
+    L = _lib.lib()
+    J, K, N, B = 16, 192, 192, 64
+    x = torch.randn((B, J, K), device=cuda)
+    W = torch.randn((1, N, K), device=cuda) * 0.05
+    gh = torch.eye(J, device=cuda)
+    types = (torch.zeros(J, dtype=torch.int64)).numpy()
+    import ctypes
+
+    tarr = (ctypes.c_int64 * J)(*types.tolist())
+    rc = L.sd_test_graph_linear(x.data_ptr(), K, 1, None, 0, W.data_ptr(), None, tarr, gh.data_ptr(), None, 0, None,
+                                x.data_ptr(), B, J, N, 0, torch.cuda.current_stream().cuda_stream)
+    assert rc != 0 and b"invalid" in L.sd_last_error().lower()
+
+
+def test_f16_range_guard_falls_back_to_exact_f32(cuda):
+    """Activations the split-f16 products cannot represent (|x| >= 65504) set the workspace status
+    (sd_workspace_status); sample() then re-runs the chain on the exact-f32 kernels, so the
+    result equals an exact-f32 plan's."""
+    z = golden("release_h36m16_T10")
+    d = build_release_diffusion(z, cuda)
+    xcs, fu, start, samp = release_inputs(z)
+    kw = dict(batch_size=start.shape[0], start_noise=start.to(cuda), sampling_noise=samp.to(cuda))
+    d.sample(x_cond=xcs.to(cuda), **kw)
+    assert d.engine.status(start.shape[0]) == 0
+    big = xcs.to(cuda) * 1e5
+    with pytest.warns(UserWarning, match="f16 range"):
+        img = d.sample(x_cond=big, **kw)[0]
+    assert d.engine.get_option("kernel_variant") == 0  # restored after the fallback
+    ref = build_release_diffusion(z, cuda)
+    ref.engine.set_option("kernel_variant", 3)
+    img_ref = ref.sample(x_cond=big, **kw)[0]
+    assert torch.equal(img, img_ref)

@@ -46,18 +46,14 @@ def test_release_sample_matches_reference(name, cuda):
 def test_exact_f32_generations_match_reference(name, variant, cuda):
     """The exact-f32 graph-linear generations (row-major activations, separate k_attention) on
     the whole sampler, against the same reference outputs as the default split-f16 v4 path."""
-    L = _lib.lib()
-    old = L.sd_set_kernel_variant(variant, -1)
-    assert old >= 0
-    try:
-        z = golden(name)
-        d = build_release_diffusion(z, cuda)
-        xcs, fu, start, samp = release_inputs(z)
-        img, _ = d.sample(batch_size=start.shape[0], x_cond=xcs.to(cuda), start_noise=start.to(cuda),
-                          sampling_noise=samp.to(cuda))
-        assert _max_err(img, z["img"]) < TOL
-    finally:
-        L.sd_set_kernel_variant(old, -1)
+    z = golden(name)
+    d = build_release_diffusion(z, cuda)
+    d.engine.set_option("kernel_variant", variant)
+    xcs, fu, start, samp = release_inputs(z)
+    img, _ = d.sample(batch_size=start.shape[0], x_cond=xcs.to(cuda), start_noise=start.to(cuda),
+                      sampling_noise=samp.to(cuda))
+    assert _max_err(img, z["img"]) < TOL
+    assert d.engine.get_option("kernel_variant") == variant
 
 
 @pytest.mark.parametrize("name", ["release_h36m16_T10", "release_amass21_T10"])
@@ -254,23 +250,20 @@ def test_row_chains_bitwise_invariant(graph, cuda):
     start = torch.randn((rows, J, 96), generator=g).to(cuda)
     samp = torch.randn((rows, T - 1, J, 96), generator=g).to(cuda)
     L = _lib.lib()
-    old = L.sd_set_row_chains(1)
-    assert old >= 1
-    try:
-        res = {}
-        for n in (1, 2, 3, 8):
-            assert L.sd_set_row_chains(n) >= 1
-            a = d.engine.sample_loop(rows, x_cond=xc, seed=21, row0=7, record=(True, False), graph=graph)
-            b = d.engine.sample_loop(rows, x_cond=xc, start_noise=start, sampling_noise=samp, record=(False, True),
-                                     graph=graph)
-            torch.cuda.synchronize()
-            res[n] = [t.clone() for t in (a[0], a[1], a[2], a[3], b[0], b[4])]
-        for n in (2, 3, 8):
-            for x, y in zip(res[1], res[n]):
-                assert torch.equal(x, y), n
-        assert L.sd_set_row_chains(0) < 0 and L.sd_set_row_chains(9) < 0
-    finally:
-        L.sd_set_row_chains(old)
+    res = {}
+    for n in (1, 2, 3, 8):
+        d.engine.set_option("row_chains", n)
+        a = d.engine.sample_loop(rows, x_cond=xc, seed=21, row0=7, record=(True, False), graph=graph)
+        b = d.engine.sample_loop(rows, x_cond=xc, start_noise=start, sampling_noise=samp, record=(False, True),
+                                 graph=graph)
+        torch.cuda.synchronize()
+        res[n] = [t.clone() for t in (a[0], a[1], a[2], a[3], b[0], b[4])]
+    for n in (2, 3, 8):
+        for x, y in zip(res[1], res[n]):
+            assert torch.equal(x, y), n
+    assert L.sd_set_row_chains(0) < 0 and L.sd_set_row_chains(9) < 0
+    with pytest.raises(_lib.SkelDiffError):
+        d.engine.set_option("row_chains", 9)
 
 
 def test_sharded_eval_single_rank(cuda):

@@ -118,3 +118,21 @@ def test_isotropic_covariance_type_fails_like_reference():
     with pytest.raises(RuntimeError):
         NonisotropicGaussianDiffusion(Sigma_N=S, Lambda_N=L, U=U, diffusion_covariance_type="isotropic",
                                       model=Denoiser(dim=96, out_dim=96, channels=4, num_nodes=4))
+
+
+def test_hip_training_route_validates_shapes():
+    """StaticGraphLinear routes to the HIP training kernels only for shapes they support (J <= 64,
+    a (J, J) mixing matrix, node types indexing the weight): anything else stays on the torch
+    path and fails with torch's own shape errors instead of out-of-bounds device reads."""
+    from skeletondiffusion_amd.training import hip_shapes_ok
+
+    x = torch.zeros(2, 16, 8)
+    W3, W2 = torch.zeros(3, 4, 8), torch.zeros(4, 8)
+    types = torch.tensor([0, 1, 2] * 5 + [0])
+    assert hip_shapes_ok(x, W3, torch.eye(16), types)
+    assert hip_shapes_ok(x, W2, torch.eye(16), None)
+    assert not hip_shapes_ok(torch.zeros(2, 65, 8), W2, torch.eye(65), None)      # J > 64
+    assert not hip_shapes_ok(x, W3, torch.eye(15), types)                           # ghat not (J, J)
+    assert not hip_shapes_ok(x, W3, torch.eye(16), types[:15])                      # len(types) != J
+    assert not hip_shapes_ok(x, W3, torch.eye(16), torch.full((16,), 3))            # type >= n_types
+    assert not hip_shapes_ok(x, W3, torch.eye(16), None)                            # 3-D weight, no types
