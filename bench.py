@@ -2,26 +2,31 @@
 """Headline benchmark: generated futures/sec of NonisotropicGaussianDiffusion.sample() on the
 MI355X HIP engine (BASELINE.json metric), one process per GPU.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config amass16]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config amass16] [--scaling weak|strong]
     torchrun --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N ...
 
 A "step" is one full sample() call: the T-step reverse chain over one batch of
 `batch` sequences x `futures` futures (B rows), with the release Denoiser and device Philox
-noise, inputs resident in HBM.  Ranks shard whole sequences (row0 = rank * B, so the device
-noise and the outputs do not depend on the GPU count); there is no collective in the data path
-and per-GPU work is fixed as N grows (weak scaling).  Weights are the repo's deterministic
-synthetic filler (no checkpoint can be fetched); conditioning latents are synthetic U(-1, 1).
+noise, inputs resident in HBM.  Ranks shard whole sequences (row0 = the rank's first global row,
+so the device noise and the outputs do not depend on the GPU count); there is no collective in
+the data path.  --scaling weak (default): every rank samples `batch` sequences (per-GPU work
+fixed as N grows); --scaling strong: the `batch` sequences are split over the N ranks
+(sharded.shard_range), total work fixed.  Weights are the repo's deterministic synthetic filler
+(no checkpoint can be fetched); conditioning latents are synthetic U(-1, 1).
 
 Rank 0 prints one JSON line.  It also carries:
-  roofline      the dominant kernel class (the graph-linear launches of a denoise step, incl. the
-                fused to_qkv + attention ones) measured live with HIP events on the launch stream
-                (sd_profile_step): algorithmic f32 FLOPs / kernel time.  The default kernels (v4)
-                compute every f32 product as three f16 MFMA products (x_hi W_hi + x_hi W_lo +
-                x_lo W_hi, f32 accumulate), so their ceiling is the f16 dense MFMA peak / 3
-                (2500 / 3 TFLOP/s of f32 work); the exact-f32 generations (SKELDIFF_GL_VARIANT=1..3)
-                are priced against the 157.3 TFLOP/s f32 peak.  "hbm_view" prices the same
-                launches by their algorithmic HBM bytes (activations in and out once, weights once)
-                against 8 TB/s;
+  roofline      the graph-linear launches (incl. the fused to_qkv + attention ones) -- the
+                dominant kernel class, >= 98 % of a denoise step's kernel time.  achieved / frac =
+                their algorithmic f32 FLOPs of the TIMED region / ms_per_step (the whole timed
+                step: row chains, hipGraphs, update kernels and gaps included).  The default
+                kernels (v4) compute every f32 product as three f16 MFMA products (x_hi W_hi +
+                x_hi W_lo + x_lo W_hi, f32 accumulate), so the ceiling is the f16 dense MFMA
+                peak / 3 (2500 / 3 TFLOP/s of f32 work); the exact-f32 generations are priced
+                against the 157.3 TFLOP/s f32 peak.  "per_launch" has the same launches measured
+                one by one with HIP events on their stream (sd_profile_step, one row chain: the
+                numbers rocprofv3 --kernel-trace reports, profiles/); "hbm_view" prices them by
+                their algorithmic HBM bytes (activations in and out once, weights once) vs 8 TB/s;
+  exact_f32     (N = 1) the same workload on the exact-f32 kernels (kernel_variant 3);
   cpu_baseline  the oracle (torch-CPU restatement of the reference path) on this host, bounded
                 sample: a few of the T steps on the same B rows, per-step time x T.
 """
@@ -31,6 +36,7 @@ import argparse
 import ctypes
 import json
 import os
+import subprocess
 import sys
 import time
 
@@ -66,7 +72,11 @@ CONFIGS = {
     # GPU), T=10 (release), reduced precision (here: the half mode, one f16 product per MAC)
     "freeman17_half": dict(skel="freeman17", T=10, batch=1377, futures=50, precision="half",
                            workload="FreeMan J=17, T=10, 50 futures, 1,377 sequences per GPU, half precision "
-                                    "(config 5)"),
+                                    "(f16 products, f32 activations)"),
+    # config 5 as stated: bf16 latents + fp32 Sigma_N projection
+    "freeman17_bf16": dict(skel="freeman17", T=10, batch=1377, futures=50, precision="bf16",
+                           workload="FreeMan J=17, T=10, 50 futures, 1,377 sequences per GPU (11,015 over 8 GPUs), "
+                                    "bf16 latents + fp32 Sigma_N projection (config 5)"),
 }
 
 RELEASE_ARCH = dict(use_attention=True, self_condition=False, norm_type="none", depth=4, attn_dim_head=32,
@@ -106,10 +116,16 @@ def build_config(name, device, T=None, batch=None, futures=None, seed=1234, seq0
     return d, torch.from_numpy(xc).to(device), batch * futures
 
 
-def shard(rank: int, batch: int, futures: int):
-    """Weak-scaling shard of rank `rank`: sequences [rank*batch, (rank+1)*batch), all futures of a
-    sequence on one rank (eval_prepare_model.py:96 repeat_interleave order).
+def shard(rank: int, batch: int, futures: int, world: int = 1, scaling: str = "weak"):
+    """Shard of rank `rank`, all futures of a sequence on one rank (eval_prepare_model.py:96
+    repeat_interleave order).  weak: sequences [rank*batch, (rank+1)*batch); strong: rank's
+    balanced part of the `batch` sequences (sharded.shard_range).
     Returns (seq0, row0, rows); row0 keys the device noise so outputs are GPU-count invariant."""
+    if scaling == "strong":
+        from skeletondiffusion_amd.sharded import shard_range
+
+        s0, s1 = shard_range(batch, rank, world)
+        return s0, s0 * futures, (s1 - s0) * futures
     return rank * batch, rank * batch * futures, batch * futures
 
 
@@ -153,6 +169,21 @@ def profile_kernels(d, x_cond, rows, reps=5):
     return list(ms), list(cnt), list(fl)
 
 
+def host_cpu():
+    """lscpu-style description of this host's CPU (model, sockets x cores x threads)."""
+    info = {}
+    try:
+        out = subprocess.run(["lscpu"], capture_output=True, text=True, timeout=10).stdout
+        for line in out.splitlines():
+            k, _, v = line.partition(":")
+            info[k.strip()] = v.strip()
+    except Exception:
+        pass
+    return {"model": info.get("Model name", "unknown"), "sockets": info.get("Socket(s)"),
+            "cores_per_socket": info.get("Core(s) per socket"), "threads_per_core": info.get("Thread(s) per core"),
+            "logical_cpus": os.cpu_count()}
+
+
 def cpu_baseline(d, x_cond, rows, steps, threads):
     """The oracle (torch-CPU restatement of the reference path) on a bounded sample."""
     import oracle as O
@@ -170,8 +201,14 @@ def cpu_baseline(d, x_cond, rows, steps, threads):
     O.p_sample_loop(sd, cfg, bufs, start, None, x_cond=xc, steps=steps)
     per_step = (time.perf_counter() - t0) / steps
     return {"value": rows / (per_step * T), "unit": "futures/s", "cores": threads, "kind": "port",
+            "host_cpu": host_cpu(),
             "sample": f"oracle/skeldiff_oracle.py p_sample_loop, {steps} of the T={T} reverse steps on the same "
                       f"{rows} rows (J={J}), per-step time x T; torch-CPU fp32, {threads} threads"}
+
+
+def world_rows(world: int, rows: int, scaling: str, batch: int, futures: int) -> int:
+    """Rows all ranks process per step: weak = world x this rank's rows; strong = the batch."""
+    return batch * futures if scaling == "strong" else world * rows
 
 
 def main():
@@ -184,12 +221,16 @@ def main():
     ap.add_argument("--batch", type=int, default=None, help="sequences per GPU")
     ap.add_argument("--futures", type=int, default=None)
     ap.add_argument("--no-graph", action="store_true")
-    ap.add_argument("--precision", choices=["f32", "half"], default=None,
+    ap.add_argument("--precision", choices=["f32", "half", "bf16"], default=None,
                     help="graph-linear arithmetic (default: the config's; f32 for the BASELINE metric)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-steps", type=int, default=4)
     ap.add_argument("--cpu-threads", type=int, default=min(16, os.cpu_count() or 1))
     ap.add_argument("--profile-reps", type=int, default=5)
+    ap.add_argument("--scaling", choices=["weak", "strong"], default="weak",
+                    help="weak: `batch` sequences per GPU; strong: `batch` sequences split over the GPUs")
+    ap.add_argument("--kernel-variant", type=int, default=0, help="0 auto (split-f16 v4), 3 exact f32, ...")
+    ap.add_argument("--no-exact-line", action="store_true", help="skip the exact-f32 comparison (N=1)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -211,14 +252,16 @@ def main():
     c = CONFIGS[args.config]
     batch = args.batch or c["batch"]
     futures = args.futures or c["futures"]
-    seq0, row0, rows = shard(rank, batch, futures)
-    d, x_cond, rows = build_config(args.config, dev, T=args.T, batch=batch, futures=futures, seq0=seq0)
+    seq0, row0, rows = shard(rank, batch, futures, world, args.scaling)
+    nseq_local = rows // futures
+    d, x_cond, rows = build_config(args.config, dev, T=args.T, batch=nseq_local, futures=futures, seq0=seq0)
     J, D, T = d.channels, d.seq_length, d.num_timesteps
     if dist:  # every rank samples with rank 0's parameters (RCCL broadcast over xGMI, untimed setup)
         from skeletondiffusion_amd.sharded import broadcast_state
         broadcast_state(d)
     eng = d.engine
     eng.set_precision(args.precision or c.get("precision", "f32"))
+    eng.set_option("kernel_variant", args.kernel_variant)
     eng.plan()
     graph = not args.no_graph
     stream = torch.cuda.Stream(dev)
@@ -250,12 +293,28 @@ def main():
             dist.all_reduce(tt, op=dist.ReduceOp.MAX)
             elapsed = float(tt.item())
         ms, cnt, fl = profile_kernels(d, x_cond, rows, args.profile_reps)
+        exact = None
+        if world == 1 and not args.no_exact_line and args.kernel_variant == 0 and J in (16, 17, 21):
+            # the same workload on the exact-f32 kernels: a second plan, same inputs
+            eng.set_option("kernel_variant", 3)
+            for i in range(args.warmup):
+                step(20_000 + i)
+            torch.cuda.synchronize(dev)
+            t1 = time.perf_counter()
+            for i in range(args.steps):
+                step(i)
+            torch.cuda.synchronize(dev)
+            el3 = time.perf_counter() - t1
+            eng.set_option("kernel_variant", args.kernel_variant)
+            exact = {"value": rows * args.steps / el3, "unit": "futures/s", "ms_per_step": el3 / args.steps * 1e3,
+                     "kernels": "exact f32 (kernel_variant 3: k_gl3 / k_gl2 on v_mfma_f32_32x32x2_f32, "
+                                "separate k_attention)",
+                     "graph_linear_tflops_timed": None}
 
-    value = world * rows * args.steps / elapsed
-    L = _lib.lib()
-    variant = L.sd_set_kernel_variant(-1, -1)
+    value = world_rows(world, rows, args.scaling, batch, futures) * args.steps / elapsed
+    variant = eng.get_option("kernel_variant")
     split = variant in (0, 4) and J in (16, 17, 21)
-    half = split and eng.precision == "half"
+    half = split and eng.precision in ("half", "bf16")
     fused_attn = ms[1] == 0.0 and cnt[1] == 0   # attention ran inside the graph-linear launches
     gl_flops = fl[0] + (fl[1] if fused_attn else 0.0)
     gl_tflops = gl_flops / (ms[0] * 1e-3) / 1e12
@@ -265,6 +324,12 @@ def main():
     upd_bytes = 3.0 * rows * J * D * 4        # x0, x_t in, x_{t-1} out (device Philox noise)
     upd_gbs = upd_bytes / (ms[2] * 1e-3) / 1e9
     step_flops = sum(fl)
+    ms_step = elapsed / args.steps * 1e3
+    # graph-linear work of the timed region: T denoise steps per bench step, on this rank's rows
+    timed_tflops = (fl[0] + fl[1]) * T / (ms_step * 1e-3) / 1e12
+    if exact is not None:
+        exact["graph_linear_tflops_timed"] = (fl[0] + fl[1]) * T / (exact["ms_per_step"] * 1e-3) / 1e12
+        exact["frac_of_f32_peak"] = exact["graph_linear_tflops_timed"] / FP32_PEAK_TFLOPS
     rec = {
         "metric": METRIC,
         "value": value,
@@ -272,37 +337,52 @@ def main():
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
-        "ms_per_step": elapsed / args.steps * 1e3,
+        "ms_per_step": ms_step,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": args.scaling,
         "vs_baseline": None,
-        "dtype": "f16" if half else "f32",
-        "arithmetic": ("half: one f16 product per multiply-add on v_mfma_f32_32x32x16_f16, f32 accumulate, f32 "
-                       "activations in HBM (latent ADE/APD within 1 % of the f32 mode, tests/test_precision.py)")
+        "dtype": ("bf16" if eng.precision == "bf16" else "f16") if half else
+                 "f32 (emulated: 3 x f16 split products)" if split else "f32",
+        "arithmetic": ("bf16: one bf16 product per multiply-add on v_mfma_f32_32x32x16_bf16, f32 accumulate; "
+                       "bf16 latents and residual-stream activations in HBM; f32 posterior update (Sigma_N / U "
+                       "projections); latent ADE/APD within 1 % of the oracle (tests/test_precision.py)")
+        if half and eng.precision == "bf16" else
+        ("half: one f16 product per multiply-add on v_mfma_f32_32x32x16_f16, f32 accumulate, f32 "
+         "activations in HBM (latent ADE/APD within 1 % of the f32 mode, tests/test_precision.py)")
         if half else ("f32-accurate: 3 x f16 split products on v_mfma_f32_32x32x16_f16, f32 accumulate "
                        "(end-to-end error within the f32-vs-f64 drift, tools/sim_split_f16.py); "
                        "exact-f32 kernels via SKELDIFF_GL_VARIANT=3") if split else "exact f32 (f32 MFMA)",
         "data": "synthetic (deterministic synthetic weights of the release Denoiser; U(-1,1) conditioning "
                 "latents; device Philox noise)",
-        "config": {"workload": c["workload"], "J": J, "T": T, "sequences_per_gpu": batch,
-                   "futures": rows // batch, "rows_per_gpu": rows, "latent_dim": D, "hipgraph": graph,
+        "config": {"workload": c["workload"], "J": J, "T": T, "sequences_per_gpu": rows // futures,
+                   "sequences_total": world_rows(world, rows, args.scaling, batch, futures) // futures,
+                   "futures": futures, "rows_per_gpu": rows, "latent_dim": D, "hipgraph": graph,
                    "parallelism": f"dp{world} (sequence-sharded, no data-path collective)",
-                   "row_chains": min(L.sd_set_row_chains(-1), max(1, rows // 32))},
+                   "row_chains": min(eng.get_option("row_chains"), max(1, rows // 32)),
+                   "kernel_variant": variant},
         "roofline": {
             "bound": "mfma",
             "kernel": ("k_gl4 graph-linear (3xf16 split MFMA, fused bias/RMS/G-hat/FiLM/tanh/residual; "
                        "to_qkv launches fused with attention)") if split else
-                      "k_gl3/k_gl2 graph-linear (exact f32 MFMA, fused epilogue)",
-            "achieved": gl_tflops, "peak": peak, "unit": "TFLOP/s", "frac": gl_tflops / peak,
-            "peak_basis": "f16 dense MFMA 2500 TFLOP/s (one product per multiply-add)" if half else
+                      "k_gl3/k_gl2/k_gl5 graph-linear (exact f32 MFMA, fused epilogue)",
+            "achieved": timed_tflops, "peak": peak, "unit": "TFLOP/s", "frac": timed_tflops / peak,
+            "measured_on": ("the timed region: graph-linear + attention algorithmic FLOPs of T denoise steps "
+                            "over this rank's rows / ms_per_step (row chains, hipGraphs, update kernels and "
+                            "launch gaps all inside)"),
+            "peak_basis": "f16 / bf16 dense MFMA 2500 TFLOP/s (one product per multiply-add)" if half else
                           "f16 dense MFMA 2500 TFLOP/s / 3 products per f32 product" if split else
                           "f32 dense 157.3 TFLOP/s",
             "traffic": None,
-            "flops_per_launch": gl_flops / max(cnt[0], 1), "launches_per_denoise_step": cnt[0],
-            "avg_launch_ms": ms[0] / max(cnt[0], 1),
-            "measured_on": ("one denoise step at the full batch on one stream (sd_profile_step: HIP events "
-                            "around each launch, kernels alone on the GPU); the timed region runs the same "
-                            "kernels as concurrent row chains (config.row_chains) with 32x64 graph-linear tiles"),
+            "flops_per_denoise_step": fl[0] + fl[1],
+            "per_launch": {
+                "achieved": gl_tflops, "frac": gl_tflops / peak, "unit": "TFLOP/s",
+                "flops_per_launch": gl_flops / max(cnt[0], 1), "launches_per_denoise_step": cnt[0],
+                "avg_launch_ms": ms[0] / max(cnt[0], 1),
+                "kernel_ms_per_bench_step": ms[0] * T,
+                "measured_on": ("one denoise step at the full batch on ONE stream (sd_profile_step: HIP events "
+                                "around each launch, kernels alone on the GPU, 32x96 tiles) -- the view "
+                                "rocprofv3 --kernel-trace gives; the timed region overlaps 3 row chains of "
+                                "32x64-tile launches, so its step is shorter than this kernel sum")},
             "hbm_view": {"achieved": gl_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": gl_gbs / HBM_PEAK_GBS,
                          "algorithmic_bytes_per_launch": gl_bytes / max(cnt[0], 1)},
         },
@@ -312,6 +392,8 @@ def main():
                           "frac": upd_gbs / HBM_PEAK_GBS, "bytes_per_launch": upd_bytes},
         "step_algorithmic_tflops_per_gpu": step_flops * T * args.steps / elapsed / 1e12,
     }
+    if exact is not None:
+        rec["exact_f32"] = exact
     traffic_file = os.path.join(HERE, "profiles", "pmc_traffic.json")
     if os.path.exists(traffic_file):
         try:

@@ -289,8 +289,13 @@ int sd_set_row_chains(int32_t n);
  * f32-accurate -- 3 split f16 products per f32 product, within the f32-vs-f64 drift.  mode 1:
  * half -- one f16 product (x and W rounded to f16), f32 accumulate, f32 activations in HBM; the
  * latent ADE / APD stay within 1 % of mode 0 (tests/test_precision.py).  Applies to the split-f16
- * (v4) kernels (J in 16, 17, 21); plans on the exact-f32 kernels stay exact.  Affects launches
- * recorded after the call; SD_E_INVALID for another mode. */
+ * (v4) kernels (J in 16, 17, 21); plans on the exact-f32 kernels stay exact.  mode 2: bf16 --
+ * "bf16 latents + fp32 Sigma_N projection" (BASELINE config 5): one bf16 product per
+ * multiply-add (v_mfma_f32_32x32x16_bf16), f32 accumulate and epilogue; the latents between
+ * steps (x_t, x0) and the residual-stream activations are bf16 in HBM; the posterior update
+ * (C1 x0 + C2 x_t + U (sigma eps)) computes in f32; start noise, records and the final latents
+ * are f32 at the ABI.  J in 16, 17, 21 only (SD_E_INVALID otherwise).  Affects launches recorded
+ * after the call; SD_E_INVALID for another mode. */
 int sd_plan_set_precision(sd_plan* plan, int32_t mode);
 
 /* Training-side StaticGraphLinear (SURVEY.md §8f "next" #4): replaces GraphLinear.forward

@@ -38,6 +38,8 @@ typedef float floatx4 __attribute__((ext_vector_type(4)));
 typedef float floatx8 __attribute__((ext_vector_type(8)));
 typedef float floatx16 __attribute__((ext_vector_type(16)));
 typedef _Float16 halfx8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 
 namespace {
 
@@ -110,6 +112,28 @@ __global__ void k_split_w(const float* __restrict__ W, int ntypes, int N, int K,
     }
 }
 
+// bf16 copy in the B-fragment layout of k_split_w: hi slots = bf16(W) (RNE), lo slots zero
+__global__ void k_bf16_w(const float* __restrict__ W, int ntypes, int N, int K, int nct, __bf16* __restrict__ out) {
+    const int nchunk = K >> 4;
+    const int64_t total = (int64_t)ntypes * nchunk * nct * 64;
+    for (int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; g < total; g += (int64_t)gridDim.x * blockDim.x) {
+        const int lane = (int)(g & 63);
+        int64_t r = g >> 6;
+        const int ct = (int)(r % nct);
+        r /= nct;
+        const int c = (int)(r % nchunk);
+        const int t = (int)(r / nchunk);
+        const int n = 32 * ct + (lane & 31);
+        const int k0 = 16 * c + 8 * (lane >> 5);
+        __bf16* hi = out + ((((int64_t)t * nchunk + c) * nct + ct) * 2) * 512 + lane * 8;
+        __bf16* lo = hi + 512;
+        for (int e = 0; e < 8; ++e) {
+            hi[e] = (__bf16)(n < N ? W[((int64_t)t * N + n) * K + k0 + e] : 0.f);
+            lo[e] = (__bf16)0.f;
+        }
+    }
+}
+
 }  // namespace
 
 // row-blocked (blk_off) -> row-major (rows, J, F) copy (sd_denoiser_trace)
@@ -129,6 +153,19 @@ hipError_t launch_unblock(float* out, const float* in, int64_t rows, int J, int 
     if (n4 <= 0) return hipSuccess;
     if (F % 4) return hipErrorInvalidValue;
     hipLaunchKernelGGL(k_unblock, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, s, out, in, rows, J, F);
+    return hipGetLastError();
+}
+
+hipError_t make_bf16_weights(const float* W, int ntypes, int N, int K, SplitW* out, hipStream_t s) {
+    out->nct = ((N + 31) / 32 + 5) / 6 * 6;
+    out->scale = out->unscale = 1.0f;
+    const size_t halves = (size_t)ntypes * (K / 16) * out->nct * 1024;
+    hipError_t e = hipMalloc(&out->w, halves * sizeof(_Float16));
+    if (e != hipSuccess) return e;
+    const int64_t total = (int64_t)ntypes * (K / 16) * out->nct * 64;
+    const int blocks = (int)std::min<int64_t>((total + 255) / 256, 4096);
+    hipLaunchKernelGGL(k_bf16_w, dim3(blocks), dim3(256), 0, s, W, ntypes, N, K, out->nct,
+                       reinterpret_cast<__bf16*>(out->w));
     return hipGetLastError();
 }
 
@@ -274,6 +311,10 @@ __device__ __forceinline__ void attention_epilogue(const GLArgs& p, floatx16 (&a
 // PREC 1 ("half" precision mode): one product x_hi W'_hi per k step, so
 //   only the hi halves of the weight fragments are streamed (half the weight bytes, a third of
 //   the MFMAs); f32 accumulate, f32 activations in HBM, same epilogue.
+// PREC 2 ("bf16" mode, config 5 as stated): one bf16 product per k step on
+//   v_mfma_f32_32x32x16_bf16 (a.wsp = make_bf16_weights), f32 accumulate and epilogue; operands
+//   and result may be stored as bf16 (GLArgs::x1_bf16 / x2_bf16 / res_bf16 / out_bf16,
+//   row-major): a bf16 operand is its own A fragment (one 16-B load per 8 k).
 // STG 0: weight stages filled by LDS-DMA (global_load_lds_dwordx4); STG 1: register-staged
 //   (global_load_dwordx4 a chunk ahead, ds_write_b128 after the chunk's MFMAs).
 template <int J, int NW, int RT, int CT, bool RMS, int DBG = 0, int MODE = 0, int XP = 0, int PREC = 0, int STG = 0>
@@ -292,6 +333,7 @@ __global__ __launch_bounds__(NW * 64, 1) void k_gl4(const GLArgs p) {
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int l32 = lane & 31, h = lane >> 5, lr = lane & 15, lg = lane >> 4;
     constexpr int TILE_H = PREC ? 512 : 1024;   // halves of one 32-column tile per k chunk (hi | hi+lo)
+    static_assert(PREC != 2 || XP == 0, "bf16 mode: one-chunk-ahead x loads");
     const int stage_h = p.ntypes * CT * TILE_H;  // halves per weight stage
     const int wfl = stage_h;                   // two stages of halves = stage_h floats
     const int yfl = MODE == 1 ? J * (8 * COLS + 16) + 8 * 16 * 100 : J * YS;  // Y slab (+ Z rows)
@@ -370,6 +412,12 @@ __global__ __launch_bounds__(NW * 64, 1) void k_gl4(const GLArgs p) {
                 if constexpr (XP == 1) {
                     g4_async(xb.a[m][rt], src);
                     g4_async(xb.b[m][rt], src + step4);
+                } else if (PREC == 2 && (k0 < p.K1 ? p.x1_bf16 : p.x2_bf16)) {
+                    // 8 bf16 k values (16 B): the A fragment itself, kept bit-exact in `a`; the
+                    // element offset of src is that of the f32 layout (row-major)
+                    const float* base = k0 < p.K1 ? p.x1 : p.x2;
+                    const __bf16* bs = reinterpret_cast<const __bf16*>(base) + (src - base);
+                    xb.a[m][rt] = *reinterpret_cast<const floatx4*>(bs);
                 } else {
                     xb.a[m][rt] = g4(src);
                     xb.b[m][rt] = g4(src + step4);
@@ -418,6 +466,32 @@ __global__ __launch_bounds__(NW * 64, 1) void k_gl4(const GLArgs p) {
         for (int m = 0; m < NPW; ++m) {
             if (wave + NW * m >= J) continue;  // wave-uniform
             const _Float16* wt = cur + toff[m] + lane * 8;
+            if constexpr (PREC == 2) {
+                const bool bsrc = (c << 4) < p.K1 ? p.x1_bf16 : p.x2_bf16;  // wave-uniform
+#pragma unroll
+                for (int rt = 0; rt < RT; ++rt) {
+                    bf16x8 xb16;
+                    floatx8 f;
+                    if (bsrc) {
+                        xb16 = __builtin_bit_cast(bf16x8, xb.a[m][rt]);
+                        f = __builtin_convertvector(xb16, floatx8);
+                    } else {
+                        f = floatx8{xb.a[m][rt].x, xb.a[m][rt].y, xb.a[m][rt].z, xb.a[m][rt].w,
+                                    xb.b[m][rt].x, xb.b[m][rt].y, xb.b[m][rt].z, xb.b[m][rt].w};
+                        xb16 = __builtin_convertvector(f, bf16x8);
+                    }
+                    if (rms_chunk) {
+                        const floatx8 q = f * f;
+                        ss[m][rt] += ((q[0] + q[1]) + (q[2] + q[3])) + ((q[4] + q[5]) + (q[6] + q[7]));
+                    }
+#pragma unroll
+                    for (int ct = 0; ct < CT; ++ct) {
+                        const bf16x8 wb = *reinterpret_cast<const bf16x8*>(wt + ct * TILE_H);
+                        acc[m][rt][ct] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(xb16, wb, acc[m][rt][ct], 0, 0, 0);
+                    }
+                }
+                continue;
+            }
             halfx8 xh[RT], xl[RT];
 #pragma unroll
             for (int rt = 0; rt < RT; ++rt) {
@@ -695,8 +769,13 @@ __global__ __launch_bounds__(NW * 64, 1) void k_gl4(const GLArgs p) {
 #pragma unroll
             for (int ib = 0; ib < IB; ++ib) {
                 const int i = ib * 16 + lr;
-                const float* src = p.res_blk ? p.res + blk_off(row, i, n, J, p.N) : p.res + row * p.res_rs + (int64_t)i * p.N + n;
-                rv[kk][ib] = (ok && i < J) ? g4(src) : floatx4{0.f, 0.f, 0.f, 0.f};
+                const int64_t ro = p.res_blk ? blk_off(row, i, n, J, p.N) : row * p.res_rs + (int64_t)i * p.N + n;
+                if (PREC == 2 && p.res_bf16)
+                    rv[kk][ib] = (ok && i < J) ? __builtin_convertvector(
+                                                     *reinterpret_cast<const bf16x4*>(reinterpret_cast<const __bf16*>(p.res) + ro), floatx4)
+                                               : floatx4{0.f, 0.f, 0.f, 0.f};
+                else
+                    rv[kk][ib] = (ok && i < J) ? g4(p.res + ro) : floatx4{0.f, 0.f, 0.f, 0.f};
             }
         }
     };
@@ -771,8 +850,11 @@ __global__ __launch_bounds__(NW * 64, 1) void k_gl4(const GLArgs p) {
                     }
                     if (p.res) v += rv[RES_EARLY ? k : kk][ib];
                     if (ok && i < J) {
-                        float* dst = p.out_blk ? p.out + blk_off(row, i, n, J, p.N) : p.out + row * p.out_rs + (int64_t)i * p.N + n;
-                        *reinterpret_cast<floatx4*>(dst) = v;
+                        const int64_t oo = p.out_blk ? blk_off(row, i, n, J, p.N) : row * p.out_rs + (int64_t)i * p.N + n;
+                        if (PREC == 2 && p.out_bf16)
+                            *reinterpret_cast<bf16x4*>(reinterpret_cast<__bf16*>(p.out) + oo) = __builtin_convertvector(v, bf16x4);
+                        else
+                            *reinterpret_cast<floatx4*>(p.out + oo) = v;
                     }
                 }
             }
@@ -872,6 +954,15 @@ hipError_t launch_graph_linear_v4(const GLArgs& a, bool rms, hipStream_t s) {
         return hipErrorNotSupported;
     if (!a.wsp || (a.K1 + a.K2) % 32 || a.K1 % 16 || (a.x1_blk && a.x1_div != 1)) return hipErrorNotSupported;
     const int cfg = a.gl4_cfg ? a.gl4_cfg : a.tile_hint;
+    if (a.prec == 2) {  // bf16 mode: row-major operands, the default tiles only
+        if (a.x1_blk || a.x2_blk || a.res_blk || a.out_blk) return hipErrorNotSupported;
+        switch (a.J) {
+            case 16: return gl4_launch<16, 8, 1, 3, 0, 0, 0, 2>(a, rms, s);
+            case 17: return gl4_launch<17, 8, 1, 2, 0, 0, 0, 2>(a, rms, s);
+            case 21: return gl4_launch<21, 8, 1, 2, 0, 0, 0, 2>(a, rms, s);
+            default: return hipErrorNotSupported;
+        }
+    }
     if (a.prec == 1) {  // half precision mode: the default tiles only
         switch (a.J) {
             case 16:
@@ -922,7 +1013,9 @@ hipError_t launch_qkv_attention_v4(const GLArgs& a, bool rms, hipStream_t s) {
     GLArgs b = a;
     b.attn_order = a.gl4_cfg == 100 ? 1 : 0;
     switch (a.J) {
-        case 16: return a.prec == 1 ? gl4_launch<16, 8, 1, 3, 0, 1, 0, 1>(b, rms, s) : gl4_launch<16, 8, 1, 3, 0, 1>(b, rms, s);
+        case 16:
+            if (a.prec == 2) return gl4_launch<16, 8, 1, 3, 0, 1, 0, 2>(b, rms, s);
+            return a.prec == 1 ? gl4_launch<16, 8, 1, 3, 0, 1, 0, 1>(b, rms, s) : gl4_launch<16, 8, 1, 3, 0, 1>(b, rms, s);
         default: return hipErrorNotSupported;
     }
 }

@@ -59,6 +59,9 @@ struct GLArgs {
     // v4: bit 0 set (atomicOr) when an activation is outside the f16 range of the split
     // (|x| >= 65504: x_hi would be inf); null = not checked
     unsigned* status;
+    // bf16 storage of operands / result (precision mode 2): the tensor
+    // holds bf16 elements at the same element offsets (row-major only)
+    int x1_bf16, x2_bf16, res_bf16, out_bf16;
 };
 
 // f16 hi/lo split of a (types, N, K) f32 weight in MFMA B-fragment order (sd_graph_linear_v4.hip)
@@ -69,6 +72,8 @@ struct SplitW {
     float unscale = 1.f;    // 1 / scale
 };
 hipError_t make_split_weights(const float* W, int ntypes, int N, int K, SplitW* out, hipStream_t s);
+// bf16 copy of W in the same B-fragment layout (the hi slots hold bf16(W), unscaled; precision 2)
+hipError_t make_bf16_weights(const float* W, int ntypes, int N, int K, SplitW* out, hipStream_t s);
 
 // Multi-head attention over joints (attention.py:122-136) from a (B, J, 3*heads*dh) qkv buffer.
 struct AttnArgs {
@@ -88,6 +93,7 @@ struct UpdArgs {
     float* mean_out; int64_t mean_rs; float* noise_out; int64_t noise_rs;
     int64_t B; int J; int D;
     unsigned* dbg;  // SD_DEBUG_LDS builds only
+    int x0_bf16, xt_bf16, out_bf16;  // bf16 latents (precision mode 2); out2 / records stay f32
 };
 
 hipError_t launch_graph_linear(const GLArgs& a, bool rms, hipStream_t s);     // dispatches v1..v5
@@ -109,7 +115,11 @@ hipError_t launch_attention(const AttnArgs& a, hipStream_t s);
 hipError_t launch_update(const UpdArgs& a, hipStream_t s);
 hipError_t launch_noise_fill(float* out, int64_t rows, int64_t n_per_row, uint64_t seed,
                              int64_t row0, int step, const uint64_t* rng_dev, hipStream_t s,
-                             int64_t row_shift = 0);  // row_shift: added to row0 (either source)
+                             int64_t row_shift = 0,   // row_shift: added to row0 (either source)
+                             int out_bf16 = 0);       // out holds bf16 elements
+// dst[r * dst_rs + i] = src[r * src_rs + i] (i < n; n % 4 == 0) with f32 <-> bf16 conversion
+hipError_t launch_convert_rows(void* dst, int dst_bf16, int64_t dst_rs, const void* src, int src_bf16,
+                               int64_t src_rs, int64_t rows, int64_t n, hipStream_t s);
 hipError_t launch_philox_raw(uint32_t* out, int64_t rows, int64_t quads, uint64_t seed,
                              int64_t row0, int step, hipStream_t s);
 hipError_t launch_set_rng(uint64_t* rng_dev, uint64_t seed, int64_t row0, hipStream_t s);

@@ -22,10 +22,21 @@ namespace sd {
 
 typedef float floatx4 __attribute__((ext_vector_type(4)));
 typedef float floatx2 __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ floatx4 ld4(const float* p) { return *reinterpret_cast<const floatx4*>(p); }
 __device__ __forceinline__ floatx2 ld2(const float* p) { return *reinterpret_cast<const floatx2*>(p); }
 __device__ __forceinline__ void st2(float* p, floatx2 v) { *reinterpret_cast<floatx2*>(p) = v; }
+// a latent pair at element offset `o` of a buffer holding f32 or (bf16 mode) bf16 elements
+__device__ __forceinline__ floatx2 ld2x(const float* p, int64_t o, int bf) {
+    return bf ? __builtin_convertvector(*reinterpret_cast<const bf16x2*>(reinterpret_cast<const __bf16*>(p) + o), floatx2)
+              : *reinterpret_cast<const floatx2*>(p + o);
+}
+__device__ __forceinline__ void st2x(float* p, int64_t o, int bf, floatx2 v) {
+    if (bf) *reinterpret_cast<bf16x2*>(reinterpret_cast<__bf16*>(p) + o) = __builtin_convertvector(v, bf16x2);
+    else *reinterpret_cast<floatx2*>(p + o) = v;
+}
 
 __device__ __forceinline__ floatx4 mfma4(float a, float b, floatx4 c) {
     return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
@@ -221,6 +232,8 @@ hipError_t launch_graph_linear(const GLArgs& a, bool rms, hipStream_t s) {
         const hipError_t e = launch_graph_linear_v4(a, rms, s);
         if (e != hipErrorNotSupported) return e;
     }
+    // bf16 operands (precision mode 2) exist only in the v4 tiles: no exact-f32 fallback
+    if (a.prec == 2 || a.x1_bf16 || a.x2_bf16 || a.res_bf16 || a.out_bf16) return hipErrorNotSupported;
     // the exact-f32 generations read and write row-major activations only
     if (a.x1_blk || a.x2_blk || a.res_blk || a.out_blk) return hipErrorNotSupported;
     // large skeletons (J > 21, MANO J = 51: 43 node types): node-batched GEMM + mixing pass
@@ -407,7 +420,7 @@ __device__ __forceinline__ floatx2 noise_pair(uint64_t seed, uint64_t row, int s
 
 __global__ __launch_bounds__(256) void k_noise_fill(float* out, int64_t rows, int64_t quads,
                                                     uint64_t seed, int64_t row0, int step,
-                                                    const uint64_t* rng_dev, int64_t row_shift) {
+                                                    const uint64_t* rng_dev, int64_t row_shift, int bf) {
     const int64_t g = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (g >= rows * quads) return;
     if (rng_dev) {
@@ -419,17 +432,19 @@ __global__ __launch_bounds__(256) void k_noise_fill(float* out, int64_t rows, in
     const uint32_t q = (uint32_t)(g % quads);
     const uint4 x = philox_at(seed, (uint64_t)(row0 + r), step, q);
     const floatx2 z0 = box_muller(x.x, x.y), z1 = box_muller(x.z, x.w);
-    *reinterpret_cast<floatx4*>(out + 4 * g) = floatx4{z0.x, z0.y, z1.x, z1.y};
+    const floatx4 v = {z0.x, z0.y, z1.x, z1.y};
+    if (bf) *reinterpret_cast<bf16x4*>(reinterpret_cast<__bf16*>(out) + 4 * g) = __builtin_convertvector(v, bf16x4);
+    else *reinterpret_cast<floatx4*>(out + 4 * g) = v;
 }
 
 hipError_t launch_noise_fill(float* out, int64_t rows, int64_t n_per_row, uint64_t seed,
                              int64_t row0, int step, const uint64_t* rng_dev, hipStream_t s,
-                             int64_t row_shift) {
+                             int64_t row_shift, int out_bf16) {
     const int64_t quads = n_per_row / 4;
     const int64_t n = rows * quads;
     if (n <= 0) return hipSuccess;
     hipLaunchKernelGGL(k_noise_fill, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, out, rows,
-                       quads, seed, row0, step, rng_dev, row_shift);
+                       quads, seed, row0, step, rng_dev, row_shift, out_bf16);
     return hipGetLastError();
 }
 
@@ -469,6 +484,29 @@ __global__ __launch_bounds__(256) void k_copy_rows(float* dst, int64_t dst_rs, c
     if (g >= rows * n4) return;
     const int64_t r = g / n4, c = g % n4;
     *reinterpret_cast<floatx4*>(dst + r * dst_rs + 4 * c) = ld4(src + r * src_rs + 4 * c);
+}
+
+__global__ __launch_bounds__(256) void k_convert_rows(void* dst, int dbf, int64_t dst_rs, const void* src, int sbf,
+                                                      int64_t src_rs, int64_t rows, int64_t n) {
+    const int64_t g = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    const int64_t n4 = n / 4;
+    if (g >= rows * n4) return;
+    const int64_t r = g / n4, c = 4 * (g % n4);
+    const int64_t so = r * src_rs + c, d0 = r * dst_rs + c;
+    const floatx4 v = sbf ? __builtin_convertvector(*reinterpret_cast<const bf16x4*>(reinterpret_cast<const __bf16*>(src) + so), floatx4)
+                          : *reinterpret_cast<const floatx4*>(reinterpret_cast<const float*>(src) + so);
+    if (dbf) *reinterpret_cast<bf16x4*>(reinterpret_cast<__bf16*>(dst) + d0) = __builtin_convertvector(v, bf16x4);
+    else *reinterpret_cast<floatx4*>(reinterpret_cast<float*>(dst) + d0) = v;
+}
+
+hipError_t launch_convert_rows(void* dst, int dst_bf16, int64_t dst_rs, const void* src, int src_bf16,
+                               int64_t src_rs, int64_t rows, int64_t n, hipStream_t s) {
+    const int64_t tot = rows * (n / 4);
+    if (tot <= 0) return hipSuccess;
+    if (n % 4) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_convert_rows, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, s, dst, dst_bf16, dst_rs, src,
+                       src_bf16, src_rs, rows, n);
+    return hipGetLastError();
 }
 
 hipError_t launch_copy_rows(float* dst, int64_t dst_rs, const float* src, int64_t src_rs,
@@ -519,13 +557,13 @@ __global__ __launch_bounds__(256) void k_update(const UpdArgs p) {
 #pragma unroll
     for (int j = 0; j < JM; ++j) {
         if (!EXACT && j >= J) continue;
-        floatx2 a = ld2(p.x0 + rb + j * D + d);
+        floatx2 a = ld2x(p.x0, rb + j * D + d, p.x0_bf16);
         if (p.act == 1) {
             a.x = tanhf(a.x);
             a.y = tanhf(a.y);
         }
         x0v[j] = floatx2{fminf(fmaxf(a.x, -1.f), 1.f), fminf(fmaxf(a.y, -1.f), 1.f)};
-        xtv[j] = ld2(p.xt + rb + j * D + d);
+        xtv[j] = ld2x(p.xt, rb + j * D + d, p.xt_bf16);
         if (p.noise_mode == 1)
             ev[j] = ld2(p.eps + row * p.eps_rs + j * D + d);
         else if (p.noise_mode == 2)
@@ -541,8 +579,8 @@ __global__ __launch_bounds__(256) void k_update(const UpdArgs p) {
             if (!EXACT && j >= J) continue;
             const floatx2 mean = p.c1s * x0v[j] + p.c2s * xtv[j];
             const floatx2 v = (p.noise_mode != 0) ? mean + p.sigs * ev[j] : mean;
-            st2(p.out + rb + j * D + d, v);
-            if (p.out2) st2(p.out2 + row * p.out2_rs + j * D + d, v);
+            st2x(p.out, rb + j * D + d, p.out_bf16, v);
+            if (p.out2) st2(p.out2 + row * p.out2_rs + j * D + d, p.out_bf16 ? __builtin_convertvector(__builtin_convertvector(v, bf16x2), floatx2) : v);
             if (p.mean_out) st2(p.mean_out + row * p.mean_rs + j * D + d, mean);
         }
         return;
@@ -565,8 +603,9 @@ __global__ __launch_bounds__(256) void k_update(const UpdArgs p) {
         }
         const floatx2 mean = m1 + m2;
         const floatx2 v = (p.noise_mode != 0) ? mean + nz : mean;
-        st2(p.out + rb + i * D + d, v);
-        if (p.out2) st2(p.out2 + row * p.out2_rs + i * D + d, v);
+        st2x(p.out, rb + i * D + d, p.out_bf16, v);
+        // the timages record holds the latent as stored (bf16-rounded in bf16 mode)
+        if (p.out2) st2(p.out2 + row * p.out2_rs + i * D + d, p.out_bf16 ? __builtin_convertvector(__builtin_convertvector(v, bf16x2), floatx2) : v);
         if (p.mean_out) st2(p.mean_out + row * p.mean_rs + i * D + d, mean);
     }
 #if defined(SD_DEBUG_LDS) && !defined(SD_DEBUG_NO_UPD)

@@ -65,6 +65,7 @@ struct GL {
     bool rms = false;
     int gain = -1;               // RMSNorm gain slot folded into this layer
     sd::SplitW split;            // f16 hi/lo B fragments of wuse for the v4 kernel
+    sd::SplitW split_bf;         // bf16 fragments of wuse (precision mode 2)
 };
 
 struct GraphKey {
@@ -119,7 +120,7 @@ struct sd_plan {
     // kernel options (sd_plan_set_option), initialised from the process defaults at creation
     int variant = 0, gl4_cfg = 0, gl4_stage = 0, chains = 3;
     bool fuse_attention_now() const { return fuse_ok && (variant == 0 || variant == 4); }
-    bool blocked_now() const { return blk_ok && fuse_attention_now(); }
+    bool blocked_now() const { return blk_ok && fuse_attention_now() && prec != 2; }
     std::vector<void*> allocs;
 
     GL init_lin;
@@ -268,9 +269,10 @@ sd::GLArgs gl_args(const sd_plan* p, const GL& g, const float* x1, int x1_div, c
         a.wrow[j] = p->types[j] * g.N;
         a.ntype[j] = p->types[j];
     }
-    a.wsp = g.split.w;
-    a.wsp_nct = g.split.nct;
-    a.wsp_unscale = g.split.unscale;
+    const sd::SplitW& sw = p->prec == 2 ? g.split_bf : g.split;  // bf16 mode: the bf16 fragments
+    a.wsp = sw.w;
+    a.wsp_nct = sw.nct;
+    a.wsp_unscale = sw.unscale;
     a.prec = p->prec;
     a.variant = p->variant;
     a.gl4_cfg = p->gl4_cfg;
@@ -311,24 +313,36 @@ struct Prof {
 // cond_phase: row 0 of this call is row cond_phase of a cond_repeat group (row chains)
 int run_denoiser(const sd_plan* p, const float* x_t, const float* x_cond, int64_t cond_repeat,
                  int t, float* x0_out, int64_t rows, const WS& w, hipStream_t s, Prof* prof = nullptr,
-                 int64_t cond_phase = 0, int tile_hint = 0, float* const* trace = nullptr) {
+                 int64_t cond_phase = 0, int tile_hint = 0, float* const* trace = nullptr,
+                 int xt_bf16 = 0, int x0_bf16 = 0) {
     const int H = p->H;
     // v4 path: every intermediate activation in the row-blocked layout (coalesced x fragments);
     // the denoiser's inputs (x_t, x_cond) and output (x0) stay row-major
     const int B = p->blocked_now() ? 1 : 0;
+    // bf16 mode (precision 2): the residual-stream activations (r, x, h, res; o without
+    // attention) are bf16 in HBM, x_t / x0 as the caller says; x_cond, qkv and the attention
+    // output stay f32
+    const bool bf = p->prec == 2;
+    auto bfl = [&](const float* q) -> int {
+        if (!q) return 0;
+        if (q == x_t) return xt_bf16;
+        if (q == x0_out) return x0_bf16;
+        return bf && (q == w.r || q == w.x || q == w.h || q == w.res || (!p->d.use_attention && q == w.o));
+    };
     // sd_denoiser_trace: block outputs (rows, J, H) row-major, in the reference's module order
     int ntr = 0;
     auto record = [&](const float* buf) -> int {
         if (!trace) return SD_OK;
         float* dst = trace[ntr++];
         if (B) SD_HIP(sd::launch_unblock(dst, buf, rows, p->J, H, s));
-        else SD_HIP(sd::launch_copy_rows(dst, (int64_t)p->J * H, buf, (int64_t)p->J * H, rows, (int64_t)p->J * H, s));
+        else SD_HIP(sd::launch_convert_rows(dst, 0, (int64_t)p->J * H, buf, bfl(buf), (int64_t)p->J * H, rows,
+                                            (int64_t)p->J * H, s));
         return SD_OK;
     };
     // v5 scratch (pre-mix activations of layers whose residual aliases their output): the qkv
     // buffer, dead outside the attention block (>= rows * J * H floats)
     const int64_t zs_cap = rows * p->J * (int64_t)(p->d.use_attention ? 3 * p->hid : p->H);
-    auto lay = [B, tile_hint, &w, zs_cap](sd::GLArgs& g, int in, int res, int out) {
+    auto lay = [B, tile_hint, &w, zs_cap, &bfl](sd::GLArgs& g, int in, int res, int out) {
         g.status = ws_status(w);
         g.zs = w.qkv;
         g.zs_cap = zs_cap;
@@ -336,6 +350,10 @@ int run_denoiser(const sd_plan* p, const float* x_t, const float* x_cond, int64_
         g.x1_blk = g.x2_blk = B & in;
         g.res_blk = B & res;
         g.out_blk = B & out;
+        g.x1_bf16 = bfl(g.x1);
+        g.x2_bf16 = bfl(g.x2);
+        g.res_bf16 = bfl(g.res);
+        g.out_bf16 = bfl(g.out);
     };
     // init_lin on cat([x_cond, x]) (generator.py:91-94)
     sd::GLArgs a;
@@ -389,6 +407,7 @@ int run_denoiser(const sd_plan* p, const float* x_t, const float* x_cond, int64_
             if (fused == hipErrorNotSupported) {
                 if (B) return fail(SD_E_INTERNAL, "row-blocked plan without the fused attention kernel");
                 a = gl_args(p, p->qkv[l], w.x, 1, nullptr, nullptr, nullptr, w.qkv, rows);
+                lay(a, 0, 0, 0);
                 SD_LAUNCH(prof, 0, sd::launch_graph_linear(a, true, s));
                 sd::AttnArgs aa{w.qkv, w.o, rows, p->J, p->d.attn_heads, p->d.attn_dim_head, qscale};
                 SD_LAUNCH(prof, 1, sd::launch_attention(aa, s));
@@ -404,7 +423,8 @@ int run_denoiser(const sd_plan* p, const float* x_t, const float* x_cond, int64_
             lay(a, 1, 1, 1);
             SD_LAUNCH(prof, 0, sd::launch_graph_linear(a, true, s));
             const int64_t rp = B ? (rows + 31) / 32 * 32 : rows;
-            SD_LAUNCH(prof, 0, sd::launch_copy_rows(w.x, (int64_t)p->J * H, w.o, (int64_t)p->J * H, rp, (int64_t)p->J * H, s));
+            SD_LAUNCH(prof, 0, sd::launch_convert_rows(w.x, bfl(w.x), (int64_t)p->J * H, w.o, bfl(w.o), (int64_t)p->J * H, rp,
+                                                       (int64_t)p->J * H, s));
         }
         if ((rc = record(w.x))) return rc;
     }
@@ -433,8 +453,12 @@ int run_update(const sd_plan* p, const float* x0, const float* xt, const float* 
                int64_t eps_rs, int noise_mode, uint64_t seed, int64_t row0,
                const uint64_t* rng_dev, int t, float* out, float* out2, int64_t out2_rs,
                float* mean_out, int64_t mean_rs, float* noise_out, int64_t noise_rs, int64_t rows,
-               hipStream_t s, Prof* prof = nullptr, int64_t row_shift = 0) {
+               hipStream_t s, Prof* prof = nullptr, int64_t row_shift = 0, int x0_bf16 = 0, int xt_bf16 = 0,
+               int out_bf16 = 0) {
     sd::UpdArgs u{};
+    u.x0_bf16 = x0_bf16;
+    u.xt_bf16 = xt_bf16;
+    u.out_bf16 = out_bf16;
     u.x0 = x0;
     u.xt = xt;
     u.eps = eps;
@@ -650,6 +674,8 @@ int sd_plan_finalize(sd_plan* p, void* stream_) {
         if ((g.K1 + g.K2) % 16 == 0 && g.K1 % 16 == 0) {
             SD_HIP(sd::make_split_weights(g.wuse, p->ntypes, g.N, g.K1 + g.K2, &g.split, s));
             p->allocs.push_back(g.split.w);
+            SD_HIP(sd::make_bf16_weights(g.wuse, p->ntypes, g.N, g.K1 + g.K2, &g.split_bf, s));
+            p->allocs.push_back(g.split_bf.w);
         }
         return SD_OK;
     };
@@ -855,6 +881,7 @@ static int record_loop(const sd_plan* p, const float* x_T, const float* x_cond, 
     const uint64_t* rng = use_rng_dev ? w.rng : nullptr;
     const bool dev_start = (flags & SD_FLAG_DEVICE_START) != 0;
     const bool dev_noise = (flags & SD_FLAG_DEVICE_NOISE) != 0;
+    const int bf = p->prec == 2;  // bf16 latents (x_t, x0 between steps); records and `out` f32
     struct Chain {
         int64_t r0, n;
         WS w;
@@ -866,9 +893,11 @@ static int record_loop(const sd_plan* p, const float* x_T, const float* x_cond, 
         c.r0 = chain_row(i, nch, rows, unit);
         c.n = chain_row(i + 1, nch, rows, unit) - c.r0;
         c.w = shift_ws(p, w, c.r0);
-        c.cur = dev_start ? c.w.img1 : x_T + c.r0 * JD;
-        if (dev_start) SD_HIP(sd::launch_noise_fill(c.w.img1, c.n, JD, seed, row0, T, rng, cs[i], c.r0));
-        if (start_out) SD_HIP(sd::launch_copy_rows(start_out + c.r0 * JD, JD, c.cur, JD, c.n, JD, cs[i]));
+        c.cur = (dev_start || bf) ? c.w.img1 : x_T + c.r0 * JD;
+        if (dev_start) SD_HIP(sd::launch_noise_fill(c.w.img1, c.n, JD, seed, row0, T, rng, cs[i], c.r0, bf));
+        else if (bf)  // bf16 latents: the caller's f32 start noise rounded once
+            SD_HIP(sd::launch_convert_rows(c.w.img1, 1, JD, x_T + c.r0 * JD, 0, JD, c.n, JD, cs[i]));
+        if (start_out) SD_HIP(sd::launch_convert_rows(start_out + c.r0 * JD, 0, JD, c.cur, bf, JD, c.n, JD, cs[i]));
     }
     for (int t = T - 1; t >= 0; --t) {
         const int64_t k = T - 1 - t;  // index into the (B, T-1, ...) records
@@ -881,7 +910,7 @@ static int record_loop(const sd_plan* p, const float* x_T, const float* x_cond, 
             // 5 % faster than the single-chain 32 x 96 choice at B = 3200, 3 chains
             const int64_t wg813 = (c.n + 31) / 32 * 2;  // 32 x 96 workgroups of an N = 192 layer
             int rc = run_denoiser(p, c.cur, xc, cond_repeat, t, c.w.x0, c.n, c.w, cs[i], nullptr, r0 % cond_repeat,
-                                  (nch > 1 && wg813 >= 32) ? 812 : 0);
+                                  (nch > 1 && wg813 >= 32) ? 812 : 0, nullptr, bf, bf);
             if (rc) return rc;
             float* nxt = (t == 0) ? out + r0 * JD : (((T - 1 - t) & 1) ? c.w.img1 : c.w.img0);
             const float* eps = (!dev_noise && t > 0) ? eps_all + r0 * step_rs + k * JD : nullptr;
@@ -889,7 +918,7 @@ static int record_loop(const sd_plan* p, const float* x_T, const float* x_cond, 
                             (rec && timages) ? timages + r0 * step_rs + k * JD : nullptr, step_rs,
                             (rec && means) ? means + r0 * step_rs + k * JD : nullptr, step_rs,
                             (rec && noise_out) ? noise_out + r0 * step_rs + k * JD : nullptr, step_rs, c.n,
-                            cs[i], nullptr, r0);
+                            cs[i], nullptr, r0, bf, bf, t > 0 ? bf : 0);
             if (rc) return rc;
             c.cur = nxt;
         }
@@ -1102,6 +1131,8 @@ int sd_plan_set_option(sd_plan* p, int32_t option, int64_t value) {
     switch (option) {
         case SD_OPT_KERNEL_VARIANT:
             if (value < 0 || value > 5) return fail(SD_E_INVALID, "kernel variant must be in [0, 5]");
+            if (p->prec == 2 && value != 0 && value != 4)
+                return fail(SD_E_INVALID, "bf16 mode runs on the v4 kernels only (variant 0 or 4)");
             p->variant = (int)value;
             return SD_OK;
         case SD_OPT_GL4_TILE:
@@ -1136,7 +1167,21 @@ int sd_plan_get_option(const sd_plan* p, int32_t option, int64_t* value) {
 
 int sd_plan_set_precision(sd_plan* p, int32_t mode) {
     if (!p) return fail(SD_E_INVALID, "null plan");
-    if (mode != 0 && mode != 1) return fail(SD_E_INVALID, "precision mode must be 0 (f32) or 1 (half)");
+    if (mode < 0 || mode > 2) return fail(SD_E_INVALID, "precision mode must be 0 (f32), 1 (half) or 2 (bf16)");
+    if (mode == 2) {  // the bf16 operands exist only in the v4 tiles (J 16 / 17 / 21, row-major)
+        if (p->J != 16 && p->J != 17 && p->J != 21)
+            return fail(SD_E_INVALID, "bf16 mode needs the split-f16 (v4) tiles: num_nodes 16, 17 or 21");
+        if (p->variant != 0 && p->variant != 4) return fail(SD_E_INVALID, "bf16 mode needs kernel variant 0 or 4");
+        if (p->finalized) {
+            auto v4ok = [](const GL& g) { return g.split_bf.w && (g.K1 + g.K2) % 32 == 0; };
+            bool ok = v4ok(p->init_lin) && v4ok(p->fres_res) && v4ok(p->fglin);
+            for (auto& g : p->r1) ok = ok && v4ok(g);
+            for (auto& g : p->r2) ok = ok && v4ok(g);
+            for (size_t l = 0; l < p->qkv.size(); ++l)
+                if (p->has_attn[l]) ok = ok && v4ok(p->qkv[l]) && (!p->d.use_attention || v4ok(p->outp[l]));
+            if (!ok) return fail(SD_E_INVALID, "bf16 mode needs every graph-linear on the v4 kernels (K % 32 == 0)");
+        }
+    }
     p->prec = mode;
     return SD_OK;
 }

@@ -10,6 +10,7 @@
 from __future__ import annotations
 
 import ctypes
+import threading
 from typing import Optional, Tuple
 
 import torch
@@ -28,7 +29,8 @@ class SamplingEngine:
         self._plan = None
         self._key = None
         self._device = None
-        self._ws = {}
+        self._ws = {}  # (device, rows, stream) -> workspace
+        self._ws_lock = threading.Lock()
         self._graph = False
         self._precision = 0
         self._options = {}  # sd_plan_set_option values, re-applied when the plan is rebuilt
@@ -94,17 +96,19 @@ class SamplingEngine:
         d.sinusoidal_theta = float(m.sinusoidal_pos_emb_theta)
         return d
 
-    PRECISIONS = {"f32": 0, "half": 1}
+    PRECISIONS = {"f32": 0, "half": 1, "bf16": 2}
 
     def set_precision(self, precision: str) -> None:
         """Arithmetic of the graph-linear launches: "f32" (default; f32-accurate split-f16
-        products) or "half" (one f16 product per multiply-add, f32 accumulate; SURVEY.md §8d
-        config 5).  See sd_plan_set_precision."""
+        products), "half" (one f16 product per multiply-add, f32 accumulate) or "bf16" (bf16
+        products, bf16 latents and residual-stream activations in HBM, f32 posterior update;
+        BASELINE config 5).  See sd_plan_set_precision."""
         if precision not in self.PRECISIONS:
             raise SkelDiffError(f"precision must be one of {sorted(self.PRECISIONS)}, got {precision!r}")
-        self._precision = self.PRECISIONS[precision]
-        if self._plan is not None:
-            check(_lib.lib().sd_plan_set_precision(self._plan, self._precision))
+        mode = self.PRECISIONS[precision]
+        if self.diff.betas.device.type == "cuda":  # validate now (builds the plan if needed)
+            check(_lib.lib().sd_plan_set_precision(self.plan(), mode))
+        self._precision = mode
 
     OPTIONS = {"kernel_variant": _lib.SD_OPT_KERNEL_VARIANT, "gl4_tile": _lib.SD_OPT_GL4_TILE,
                "row_chains": _lib.SD_OPT_ROW_CHAINS, "gl4_staging": _lib.SD_OPT_GL4_STAGING}
@@ -165,14 +169,20 @@ class SamplingEngine:
         return handle
 
     def workspace(self, rows: int) -> Tuple[torch.Tensor, int]:
+        """The workspace of `rows` rows for torch's current stream.  A workspace belongs to one
+        stream at a time (include/skeldiff.h), so concurrent callers on different streams each
+        get their own; it is allocated on that stream (caching-allocator ordering)."""
         plan = self.plan()
         nbytes = int(_lib.lib().sd_workspace_bytes(plan, rows))
-        k = (self._device, rows)
-        ws = self._ws.get(k)
-        if ws is None or ws.numel() < nbytes:
-            self._ws.clear()
-            ws = torch.empty(nbytes, dtype=torch.uint8, device=self._device)
-            self._ws[k] = ws
+        stream = _stream(self._device)
+        k = (self._device, rows, stream)
+        with self._ws_lock:
+            ws = self._ws.get(k)
+            if ws is None or ws.numel() < nbytes:
+                if len(self._ws) >= 8:  # bounded: drop the oldest
+                    self._ws.pop(next(iter(self._ws)))
+                ws = torch.empty(nbytes, dtype=torch.uint8, device=self._device)
+                self._ws[k] = ws
         return ws, nbytes
 
     # ---------------------------------------------------------------------------------------

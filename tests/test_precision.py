@@ -54,5 +54,64 @@ def test_precision_mode_validation(cuda):
     d = build_release_diffusion(z, cuda)
     with pytest.raises(SkelDiffError):
         d.engine.set_precision("bf8")
-    assert _lib.lib().sd_plan_set_precision(d.engine.plan(), 2) < 0
+    assert _lib.lib().sd_plan_set_precision(d.engine.plan(), 3) < 0
     assert d.engine.precision == "f32"
+
+
+def test_bf16_mode_config5_quality_gate_vs_oracle(cuda):
+    """BASELINE config 5 as stated: FreeMan J=17, bf16 latents + fp32 Sigma_N projection, one GPU's
+    shard of the 11,015 x 50 test set (1,377 sequences x 50 futures = 68,850 rows), T = 10.  The
+    quality gate ("ADE/APD within 1 % of reference") against the CPU oracle (f32, the reference's
+    arithmetic) fed the same Philox normals, on the first 24 sequences of the shard: latent APD
+    (multimodal.py:137-151) and latent ADE against a fixed synthetic target (multimodal.py:44-57)."""
+    import oracle as O
+    from bench import build_config
+
+    d, x_cond, rows = build_config("freeman17_bf16", cuda)
+    J, D, T = d.channels, d.seq_length, d.num_timesteps
+    assert (J, T, rows) == (17, 10, 1377 * 50)
+    eng = d.engine
+    eng.set_precision("bf16")
+    seed = 31
+    img = eng.sample_loop(rows, x_cond=x_cond, seed=seed, graph=True)[0]
+    torch.cuda.synchronize()
+    assert torch.isfinite(img).all() and img.abs().max() <= 1.0 + 1e-6
+    eng.set_precision("f32")
+    img32 = eng.sample_loop(rows, x_cond=x_cond, seed=seed)[0]
+    nseq, S = 24, 50
+    sub = img[: nseq * S].cpu()
+    sub32 = img32[: nseq * S].cpu()
+    sd = {k: v.detach().cpu() for k, v in d.state_dict().items()}
+    cfg = O.release_config(J, d.model.node_types)
+    bufs = {k: v for k, v in sd.items() if not k.startswith("model.")}
+    start, samp = O.device_noise(seed, 0, nseq * S, T, J, D)
+    torch.set_num_threads(min(16, torch.get_num_threads()))
+    ref, _ = O.p_sample_loop(sd, cfg, bufs, start, samp, x_cond=x_cond[:nseq].cpu())
+    assert float((sub32 - ref).abs().max()) < 1e-4  # the f32 mode is the oracle within the parity bar
+    g = torch.Generator().manual_seed(3)
+    target = torch.rand((nseq, 1, J * D), generator=g) * 2 - 1
+
+    def stats(x):
+        lat = x.reshape(nseq, S, J, D)
+        apd = O.metric_lat_apd(lat)
+        ade = O.metric_ade(target, lat.reshape(nseq, S, 1, J * D))
+        return float(apd.mean()), float(ade.mean())
+
+    apd_b, ade_b = stats(sub)
+    apd_r, ade_r = stats(ref)
+    assert abs(apd_b - apd_r) / apd_r < 0.01, (apd_b, apd_r)
+    assert abs(ade_b - ade_r) / ade_r < 0.01, (ade_b, ade_r)
+    assert not torch.equal(sub, sub32)  # the bf16 launches really ran
+
+
+def test_bf16_mode_validation(cuda):
+    from bench import build_config
+
+    d, _, _ = build_config("mano51", cuda, T=10, batch=1, futures=2)
+    with pytest.raises(SkelDiffError):
+        d.engine.set_precision("bf16")  # J = 51 runs on the exact-f32 v5 kernels
+    z = golden("release_h36m16_T10")
+    d = build_release_diffusion(z, cuda)
+    d.engine.set_precision("bf16")
+    with pytest.raises(SkelDiffError):
+        d.engine.set_option("kernel_variant", 3)
