@@ -241,10 +241,14 @@ enum {
     SD_OPT_GL4_TILE = 2,        /* v4 tile <waves><row tiles><col tiles>, 0 = per shape */
     SD_OPT_ROW_CHAINS = 3,      /* 1..8 concurrent row chains in sd_sample_loop */
     SD_OPT_PRECISION = 4,       /* as sd_plan_set_precision */
-    SD_OPT_GL4_STAGING = 5      /* v4 weight stages: 0 LDS-DMA, workgroup holds its CU's whole
+    SD_OPT_GL4_STAGING = 5,     /* v4 weight stages: 0 LDS-DMA, workgroup holds its CU's whole
                                    LDS (default); 1 register-staged, CU shareable;
                                    2 DIAGNOSTIC ONLY: LDS-DMA with the CU shareable -- reproduces the
                                    §4c co-residency corruption, never for production use */
+    SD_OPT_SPLIT_ROUTE = 6      /* v4 split route for small launches (GEMM phase per (tile, node)
+                                   + mixing phase; bitwise identical results):
+                                   0 auto (rows per launch <= SKELDIFF_SPLIT_ROWS, default 1024),
+                                   1 never, 2 always */
 };
 int sd_plan_set_option(sd_plan* plan, int32_t option, int64_t value);
 int sd_plan_get_option(const sd_plan* plan, int32_t option, int64_t* value);

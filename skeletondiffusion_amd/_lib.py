@@ -34,7 +34,8 @@ EXPORTED = (
 )
 
 # sd_plan_set_option keys (include/skeldiff.h)
-SD_OPT_KERNEL_VARIANT, SD_OPT_GL4_TILE, SD_OPT_ROW_CHAINS, SD_OPT_PRECISION, SD_OPT_GL4_STAGING = 1, 2, 3, 4, 5
+(SD_OPT_KERNEL_VARIANT, SD_OPT_GL4_TILE, SD_OPT_ROW_CHAINS, SD_OPT_PRECISION, SD_OPT_GL4_STAGING,
+ SD_OPT_SPLIT_ROUTE) = 1, 2, 3, 4, 5, 6
 SD_STATUS_F16_RANGE = 1
 
 

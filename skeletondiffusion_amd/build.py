@@ -31,14 +31,15 @@ def _stale() -> bool:
 def build_library(force: bool = False, verbose: bool = False, debug_lds: bool = False, extra=(), tag="_dbg") -> str:
     """debug_lds: the diagnostic variant libskeldiff_dbg.so (-DSD_DEBUG_LDS: LDS integrity
     counters in k_gl4 / k_update, sd_debug_lds_counters); load it with SKELDIFF_LIB."""
-    out = OUT.replace(".so", tag + ".so") if debug_lds else OUT
-    if not force and not debug_lds and not _stale():
+    variant = debug_lds or bool(extra)  # a diagnostic variant: libskeldiff{tag}.so, never the product
+    out = OUT.replace(".so", tag + ".so") if variant else OUT
+    if not force and not variant and not _stale():
         return OUT
     objs, procs = [], []
     for src in SOURCES:  # one hipcc per translation unit, in parallel
-        obj = os.path.join(CSRC, src.replace(".hip", tag + ".o" if debug_lds else ".o"))
+        obj = os.path.join(CSRC, src.replace(".hip", tag + ".o" if variant else ".o"))
         cmd = [_hipcc(), "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-c",
-               "-Wno-pass-failed"] + (["-DSD_DEBUG_LDS"] + list(extra) if debug_lds else []) + [os.path.join(CSRC, src), "-o", obj]
+               "-Wno-pass-failed"] + (["-DSD_DEBUG_LDS"] if debug_lds else []) + list(extra) + [os.path.join(CSRC, src), "-o", obj]
         if verbose:
             print(" ".join(cmd))
         procs.append((src, subprocess.Popen(cmd)))

@@ -197,13 +197,118 @@ hipError_t make_split_weights(const float* W, int ntypes, int N, int K, SplitW* 
     return hipGetLastError();
 }
 
+// ---- split route, phase 1 (small grids) -----------------------------------------------------
+// One wave per (32-row tile, node j, 32-column tile) walks the whole K extent with its x and
+// weight fragments loaded straight into registers, PF chunks ahead (no LDS, no barriers), and
+// stores Y = unscale * rms * acc + bias to ys[((tile * J + j) * 32 + r) * N + col].  Every
+// accumulator element sees the same MFMA sequence (x_hi W'_hi, x_hi W'_lo, x_lo W'_hi per 16-deep
+// chunk), RMS sum, range guard and scale arithmetic as in k_gl4, so phase 2 (k_gl4 MODE 2 / 3)
+// reproduces the one-kernel results bit for bit.  Workgroup = 4 waves = 4 column tiles of one
+// (row tile, node): the x fragments are shared through L1.
+template <bool RMS, int PREC, int PF = 8>  // PF: chunks in flight
+__global__ __launch_bounds__(256) void k_gl4y(const GLArgs p, int ntile_c, int64_t ntile_r) {
+    const int lane = threadIdx.x & 63, l32 = lane & 31, h = lane >> 5;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int64_t u = (int64_t)blockIdx.x * 4 + wave;
+    const int tc = (int)(u % ntile_c);
+    const int64_t rj = u / ntile_c;
+    const int J = p.J;
+    const int j = (int)(rj % J);
+    const int64_t tr = rj / J;
+    if (tr >= ntile_r) return;  // wave-uniform
+    const int64_t row0 = tr * 32;
+    const int K = p.K1 + p.K2;
+    const int nchunk = K >> 4;
+    const int64_t arow = row0 + l32;
+    const int64_t ac = arow < p.B ? arow : 0;
+    const float* x1r = p.x1_blk ? p.x1 + blk_off(arow, j, 8 * h, J, p.K1)
+                                : p.x1 + ((ac + p.x1_row0) / p.x1_div) * p.x1_rs + (int64_t)j * p.K1 + 8 * h;
+    const float* x2r = !p.K2 ? nullptr
+                             : p.x2_blk ? p.x2 + blk_off(arow, j, 8 * h, J, p.K2) : p.x2 + ac * p.x2_rs + (int64_t)j * p.K2 + 8 * h;
+    const _Float16* wbase = p.wsp + ((int64_t)p.ntype[j] * nchunk * p.wsp_nct + tc) * 1024 + lane * 8;
+    const int64_t wcs = (int64_t)p.wsp_nct * 1024;  // halves per chunk
+
+    floatx4 xa[PF], xb[PF];
+    halfx8 wh[PF], wl[PF];
+    auto issue = [&](int c, int sl) {
+        const int k0 = c << 4;
+        const float* src;
+        int step4;
+        if (k0 < p.K1) {
+            src = p.x1_blk ? x1r + (k0 << 5) : x1r + k0;
+            step4 = p.x1_blk ? 128 : 4;
+        } else {
+            src = p.x2_blk ? x2r + ((k0 - p.K1) << 5) : x2r + (k0 - p.K1);
+            step4 = p.x2_blk ? 128 : 4;
+        }
+        xa[sl] = g4(src);
+        xb[sl] = g4(src + step4);
+        const _Float16* w = wbase + c * wcs;
+        wh[sl] = *reinterpret_cast<const halfx8*>(w);
+        if constexpr (!PREC) wl[sl] = *reinterpret_cast<const halfx8*>(w + 512);
+    };
+    floatx16 acc;
+#pragma unroll
+    for (int e = 0; e < 16; ++e) acc[e] = 0.f;
+    float ss = 0.f, amx = 0.f;
+    auto compute = [&](int c, int sl) {
+        const floatx8 f = {xa[sl].x, xa[sl].y, xa[sl].z, xa[sl].w, xb[sl].x, xb[sl].y, xb[sl].z, xb[sl].w};
+        if (RMS && (c << 4) < p.K1) {
+            const floatx8 q = f * f;
+            ss += ((q[0] + q[1]) + (q[2] + q[3])) + ((q[4] + q[5]) + (q[6] + q[7]));
+        }
+        const floatx8 a = __builtin_elementwise_abs(f);
+        amx = fmaxf(amx, fmaxf(fmaxf(fmaxf(a[0], a[1]), fmaxf(a[2], a[3])), fmaxf(fmaxf(a[4], a[5]), fmaxf(a[6], a[7]))));
+        const halfx8 xh = __builtin_convertvector(f, halfx8);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(xh, wh[sl], acc, 0, 0, 0);
+        if constexpr (!PREC) {
+            const halfx8 xl = __builtin_convertvector(f - __builtin_convertvector(xh, floatx8), halfx8);
+            acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(xh, wl[sl], acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(xl, wh[sl], acc, 0, 0, 0);
+        }
+    };
+#pragma unroll
+    for (int i = 0; i < PF; ++i)
+        if (i < nchunk) issue(i, i);
+    for (int c0 = 0; c0 < nchunk; c0 += PF) {
+#pragma unroll
+        for (int i = 0; i < PF; ++i) {
+            const int c = c0 + i;
+            if (c < nchunk) {
+                compute(c, i);
+                if (c + PF < nchunk) issue(c + PF, i);
+            }
+        }
+    }
+    if (p.status && __builtin_amdgcn_ballot_w64(amx >= 65504.0f) != 0 && lane == 0) atomicOr(p.status, 1u);
+    float sc[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) sc[r] = p.wsp_unscale;
+    if (RMS) {
+        const float t = ss + __shfl_xor(ss, 32);
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const float n2 = __shfl(t, (r & 3) + 8 * (r >> 2) + 4 * h);
+            sc[r] *= 1.0f / fmaxf(sqrtf(n2), 1e-12f);
+        }
+    }
+    const int ncol = tc * 32 + l32;
+    const float bv = (p.bias && ncol < p.N) ? p.bias[p.wrow[j] + ncol] : 0.f;
+    float* y = p.zs + ((tr * J + j) * 32) * (int64_t)p.N + ncol;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) y[(int64_t)((r & 3) + 8 * (r >> 2) + 4 * h) * p.N] = acc[r] * sc[r] + bv;
+}
+
 // Epilogue of the fused to_qkv + Attention kernel (MODE 1), J <= 16, dh = 32, 8 waves, a
 // 32-row tile.  Per 8-row slab: the mixed-in q|k|v (Z = G-hat Y) goes to LDS as [row][node][96],
 // then wave w runs the attention of row 8*slab + w exactly as k_attention does (same f32 MFMA
 // order, expf softmax), writing out[row][n][head*32 + d].
-template <int J, int NW, int NPW>
+// FROM_YS (MODE 3, split route phase 2): the Y slab q8only comes from phase 1's scratch p.zs
+// instead of the accumulators.
+template <int J, int NW, int NPW, bool FROM_YS = false>
 __device__ __forceinline__ void attention_epilogue(const GLArgs& p, floatx16 (&acc)[NPW][1][3], float* smem,
-                                                   const float* sG, int64_t row0, int head, int wave, int lane) {
+                                                   const float* sG, int64_t row0, int head, int wave, int lane,
+                                                   int q8only = 0) {
     constexpr int COLS = 96;
     constexpr int YS8 = 8 * COLS + 16;  // floats per node in an 8-row Y slab (+16: bank shift)
     constexpr int ZN = 100;             // floats per node in a Z row (+4: bank shift)
@@ -220,17 +325,20 @@ __device__ __forceinline__ void attention_epilogue(const GLArgs& p, floatx16 (&a
     }
 #pragma unroll
     for (int q8 = 0; q8 < 4; ++q8) {  // rows 8 q8 .. 8 q8 + 7 = accumulator registers 4 q8 .. 4 q8 + 3
-        __syncthreads();              // K loop / previous slab done with this LDS
+        if (FROM_YS && q8 != q8only) continue;
+        if constexpr (!FROM_YS) {  // FROM_YS: k_gl4 MODE 3 has put the slab in sY
+            __syncthreads();       // K loop / previous slab done with this LDS
 #pragma unroll
-        for (int m = 0; m < NPW; ++m) {
-            const int j = wave + NW * m;
-            if (j >= J) continue;
+            for (int m = 0; m < NPW; ++m) {
+                const int j = wave + NW * m;
+                if (j >= J) continue;
 #pragma unroll
-            for (int ct = 0; ct < 3; ++ct)
+                for (int ct = 0; ct < 3; ++ct)
 #pragma unroll
-                for (int e = 0; e < 4; ++e) sY[j * YS8 + (e + 4 * h) * COLS + 32 * ct + l32] = acc[m][0][ct][4 * q8 + e];
+                    for (int e = 0; e < 4; ++e) sY[j * YS8 + (e + 4 * h) * COLS + 32 * ct + l32] = acc[m][0][ct][4 * q8 + e];
+            }
+            __syncthreads();
         }
-        __syncthreads();
         // node mixing: 48 blocks of 16 (row, column) positions, 6 per wave
 #pragma unroll
         for (int k = 0; k < 48 / NW; ++k) {
@@ -319,7 +427,8 @@ __device__ __forceinline__ void attention_epilogue(const GLArgs& p, floatx16 (&a
 //   (global_load_dwordx4 a chunk ahead, ds_write_b128 after the chunk's MFMAs).
 template <int J, int NW, int RT, int CT, bool RMS, int DBG = 0, int MODE = 0, int XP = 0, int PREC = 0, int STG = 0>
 __global__ __launch_bounds__(NW * 64, 1) void k_gl4(const GLArgs p) {
-    static_assert(MODE == 0 || (CT == 3 && RT == 1 && J <= 16 && NW == 8), "attention mode: 32 x (q|k|v)");
+    static_assert(MODE == 0 || MODE == 2 || (CT == 3 && RT == 1 && J <= 16 && NW == 8), "attention mode: 32 x (q|k|v)");
+    static_assert(MODE < 2 || (RT == 1 && XP == 0 && STG == 0 && DBG == 0), "split-route phase 2: one 32-row tile");
     constexpr int NPW = (J + NW - 1) / NW;  // nodes per wave
     constexpr int KS = (J + 3) / 4;         // 4-deep k steps of the mixing GEMM (K = J padded)
     constexpr int IB = (J + 15) / 16;       // 16-row i blocks of the mixing GEMM
@@ -334,23 +443,28 @@ __global__ __launch_bounds__(NW * 64, 1) void k_gl4(const GLArgs p) {
     const int l32 = lane & 31, h = lane >> 5, lr = lane & 15, lg = lane >> 4;
     constexpr int TILE_H = PREC ? 512 : 1024;   // halves of one 32-column tile per k chunk (hi | hi+lo)
     static_assert(PREC != 2 || XP == 0, "bf16 mode: one-chunk-ahead x loads");
-    const int stage_h = p.ntypes * CT * TILE_H;  // halves per weight stage
+    const int stage_h = MODE >= 2 ? 0 : p.ntypes * CT * TILE_H;  // halves per weight stage
     const int wfl = stage_h;                   // two stages of halves = stage_h floats
-    const int yfl = MODE == 1 ? J * (8 * COLS + 16) + 8 * 16 * 100 : J * YS;  // Y slab (+ Z rows)
+    constexpr bool ATT = MODE == 1 || MODE == 3;
+    const int yfl = ATT ? J * (8 * COLS + 16) + 8 * 16 * 100 : J * YS;  // Y slab (+ Z rows)
     _Float16* sW0 = reinterpret_cast<_Float16*>(smem);
     _Float16* sW1 = sW0 + stage_h;
     float* sY = smem;  // aliases the weight stages after the K loop
     float* sG = smem + (wfl > yfl ? wfl : yfl);
     float* sF = sG + J * J;  // FiLM (scale + 1 | shift) for this workgroup's columns
 
-    const int ntile_c = MODE == 1 ? p.attn_heads : (p.N + COLS - 1) / COLS;
+    const int ntile_c = ATT ? p.attn_heads : (p.N + COLS - 1) / COLS;
     const int nwg = gridDim.x, xcd = blockIdx.x & 7, q8 = nwg >> 3, r8 = nwg & 7;
     // XCD-aware order: consecutive L (the column tiles of one row tile) on one XCD, so x is
     // fetched into that XCD's L2 once.  attn_order 1 (fused attention): L = blockIdx, i.e. head
     // h = blockIdx % heads runs on XCD h % 8 and each XCD's L2 keeps only its heads' weights.
-    const int L = (MODE == 1 && p.attn_order == 1)
+    // Split-route phase 2: workgroup = (tile, 16-row slab) in MODE 2, (tile, 8-row slab) in MODE 3.
+    const int L = MODE == 2   ? (int)(blockIdx.x >> 1)
+                  : MODE == 3 ? (int)(blockIdx.x >> 2)
+                  : (MODE == 1 && p.attn_order == 1)
                       ? (int)blockIdx.x
                       : (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (blockIdx.x >> 3);
+    const int slab = MODE == 2 ? (int)(blockIdx.x & 1) : MODE == 3 ? (int)(blockIdx.x & 3) : 0;
     const int ctile = L % ntile_c;
     const int64_t row0 = (int64_t)(L / ntile_c) * (32 * RT);
     const int c0 = ctile * COLS;
@@ -376,6 +490,62 @@ __global__ __launch_bounds__(NW * 64, 1) void k_gl4(const GLArgs p) {
     }
 
     floatx16 acc[NPW][RT][CT];
+    uint64_t ts[8];  // DBG 6: phase stamps (s_memrealtime, 100 MHz) + shader clock around the K loop
+    uint64_t cs[5];  // DBG 6: shader-clock stamps inside chunk 5
+    if constexpr (MODE >= 2) {
+        // split-route phase 2: the slab's Y (from phase 1's p.zs), G-hat and FiLM all loaded to
+        // registers first (one memory round trip), then to LDS, one barrier
+        constexpr int C4 = COLS / 4;
+        constexpr int YQ = MODE == 2 ? J * 16 * C4 : J * 8 * 24;  // 16-B pieces of the slab
+        constexpr int NYL = (YQ + NTH - 1) / NTH, NGL = (J * J + NTH - 1) / NTH;
+        constexpr int YS8 = 8 * COLS + 16;  // MODE 3: attention_epilogue's slab layout
+        const int64_t tb = (row0 >> 5) * J;
+        auto ysrc = [&](int q, float*& dst) -> const float* {
+            if constexpr (MODE == 2) {
+                const int cc = (q % C4) * 4, r = (q / C4) & 15, j = q / (16 * C4);
+                dst = sY + j * YS + r * YR + cc;
+                return p.zs + ((tb + j) * 32 + 16 * slab + r) * (int64_t)p.N + c0 + cc;
+            } else {
+                const int c4 = q % 24, rr = (q / 24) & 7, j = q / 192;
+                const int ct = c4 >> 3, cc = (c4 & 7) * 4;
+                dst = sY + j * YS8 + rr * COLS + 32 * ct + cc;
+                return p.zs + ((tb + j) * 32 + 8 * slab + rr) * (int64_t)p.N + (ctile + ct * p.attn_heads) * 32 + cc;
+            }
+        };
+        floatx4 yv[NYL];
+        float gv[NGL];
+        float f0 = 1.0f, f1 = 0.0f;
+#pragma unroll
+        for (int k = 0; k < NYL; ++k) {
+            const int q = tid + k * NTH;
+            float* d;
+            if (q < YQ) yv[k] = g4(ysrc(q, d));
+        }
+#pragma unroll
+        for (int k = 0; k < NGL; ++k)
+            if (tid + k * NTH < J * J) gv[k] = p.G[tid + k * NTH];
+        if (tid < COLS && p.film && c0 + tid < p.N) {
+            f0 = p.film[c0 + tid] + 1.0f;
+            f1 = p.film[p.N + c0 + tid];
+        }
+#pragma unroll
+        for (int k = 0; k < NYL; ++k) {
+            const int q = tid + k * NTH;
+            float* d;
+            if (q < YQ) {
+                (void)ysrc(q, d);
+                *reinterpret_cast<floatx4*>(d) = yv[k];
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < NGL; ++k)
+            if (tid + k * NTH < J * J) sG[tid + k * NTH] = gv[k];
+        if (tid < COLS) {
+            sF[tid] = f0;
+            sF[COLS + tid] = f1;
+        }
+        __syncthreads();
+    } else {
     float ss[NPW][RT];
     float amx = 0.f;  // max |x| this lane split to f16 (range guard, GLArgs::status)
 #pragma unroll
@@ -531,7 +701,6 @@ __global__ __launch_bounds__(NW * 64, 1) void k_gl4(const GLArgs p) {
     // issue chunk c+1 into the other stage / register buffer -> MFMAs on chunk c.  The waitcnt
     // is a builtin (not inline asm) so the compiler knows x(c) is complete and inserts no
     // further vmcnt waits before the MFMAs.
-    uint64_t cs[5];  // DBG 6: shader-clock stamps inside chunk 5
     auto step = [&](int c, const XBuf& cur, XBuf& nxt) {
         if (DBG == 6 && c == 5) cs[0] = clock64();
         __builtin_amdgcn_s_waitcnt(VmCnt4<0>::imm);
@@ -553,7 +722,6 @@ __global__ __launch_bounds__(NW * 64, 1) void k_gl4(const GLArgs p) {
 #endif
     };
 
-    uint64_t ts[8];  // DBG 6: phase stamps (s_memrealtime, 100 MHz) + shader clock around the K loop
     if (DBG == 6) ts[0] = wall_clock64();
     // G-hat and FiLM (scale + 1 | shift) for this workgroup's columns -> LDS, bias -> registers:
     // all read by the epilogue only, after the K loop's barriers
@@ -706,6 +874,7 @@ __global__ __launch_bounds__(NW * 64, 1) void k_gl4(const GLArgs p) {
                 for (int r = 0; r < 16; ++r) acc[m][rt][ct][r] = acc[m][rt][ct][r] * sc[r] + bv[m][ct];
         }
     }
+    }  // MODE < 2: K loop
     if (DBG == 6) ts[3] = wall_clock64();
 #if defined(SD_DEBUG_LDS) && !defined(SD_DEBUG_NO_G)
     {
@@ -716,6 +885,9 @@ __global__ __launch_bounds__(NW * 64, 1) void k_gl4(const GLArgs p) {
 #endif
     if constexpr (MODE == 1) {
         attention_epilogue<J, NW, NPW>(p, acc, smem, sG, row0, ctile, wave, lane);
+        return;
+    } else if constexpr (MODE == 3) {
+        attention_epilogue<J, NW, NPW, true>(p, acc, smem, sG, row0, ctile, wave, lane, slab);
         return;
     }
     // ---- mixing + epilogue, one 16-row slab at a time.  Z^T = Y^T G-hat^T on 16x16x4 f32 MFMA
@@ -781,23 +953,26 @@ __global__ __launch_bounds__(NW * 64, 1) void k_gl4(const GLArgs p) {
     };
 
 #pragma unroll
-    for (int hc = 0; hc < 2 * RT; ++hc) {
+    for (int hc0 = 0; hc0 < (MODE == 2 ? 1 : 2 * RT); ++hc0) {
+        const int hc = MODE == 2 ? slab : hc0;
         const int rt = hc >> 1, hf = hc & 1;
         if (RES_EARLY && p.res) load_res(hc, 0, BPW);  // latency hides under the Y exchange below
-        __syncthreads();          // K loop / previous slab done with the LDS that sY aliases
+        if constexpr (MODE != 2) {  // MODE 2: the slab is in sY already
+            __syncthreads();        // K loop / previous slab done with the LDS that sY aliases
 #pragma unroll
-        for (int m = 0; m < NPW; ++m) {
-            const int j = wave + NW * m;
-            if (j >= J) continue;
+            for (int m = 0; m < NPW; ++m) {
+                const int j = wave + NW * m;
+                if (j >= J) continue;
 #pragma unroll
-            for (int ct = 0; ct < CT; ++ct)
+                for (int ct = 0; ct < CT; ++ct)
 #pragma unroll
-                for (int q = 0; q < 8; ++q) {
-                    const int r = (q & 3) + 8 * (q >> 2) + 4 * h;
-                    sY[j * YS + r * YR + 32 * ct + l32] = acc[m][rt][ct][8 * hf + q];
-                }
+                    for (int q = 0; q < 8; ++q) {
+                        const int r = (q & 3) + 8 * (q >> 2) + 4 * h;
+                        sY[j * YS + r * YR + 32 * ct + l32] = acc[m][rt][ct][8 * hf + q];
+                    }
+            }
+            __syncthreads();
         }
-        __syncthreads();
         // per group of PG blocks: phase 1 every LDS read, phase 2 the mixing MFMAs, phase 3
         // FiLM / tanh / residual / 16-B stores -- no dependent chain per block
         constexpr int PG = (IB == 1 && BPW <= 8) ? BPW : (BPW < 4 ? BPW : 4);
@@ -899,19 +1074,20 @@ static hipError_t gl4_launch_t(const GLArgs& a, bool rms, hipStream_t s);
 template <int J, int NW, int RT, int CT, int DBG = 0, int MODE = 0, int XP = 0, int PREC = 0>
 static hipError_t gl4_launch(const GLArgs& a, bool rms, hipStream_t s) {
     constexpr int TILE_H = PREC ? 512 : 1024;
-    if (a.gl4_stage == 1 && XP == 0 && DBG == 0 && a.ntypes * CT * (TILE_H / 8) <= 8 * NW * 64)
-        return gl4_launch_t<J, NW, RT, CT, DBG, MODE, XP, PREC, 1>(a, rms, s);
+    if (MODE < 2 && a.gl4_stage == 1 && XP == 0 && DBG == 0 && a.ntypes * CT * (TILE_H / 8) <= 8 * NW * 64)
+        return gl4_launch_t<J, NW, RT, CT, DBG, MODE, XP, PREC, MODE < 2 ? 1 : 0>(a, rms, s);
     return gl4_launch_t<J, NW, RT, CT, DBG, MODE, XP, PREC, 0>(a, rms, s);
 }
 
 template <int J, int NW, int RT, int CT, int DBG, int MODE, int XP, int PREC, int STG>
 static hipError_t gl4_launch_t(const GLArgs& a, bool rms, hipStream_t s) {
     constexpr int COLS = 32 * CT;
-    const int ntile_c = MODE == 1 ? a.attn_heads : (a.N + COLS - 1) / COLS;
+    constexpr bool ATT = MODE == 1 || MODE == 3;
+    const int ntile_c = ATT ? a.attn_heads : (a.N + COLS - 1) / COLS;
     const int64_t ntile_r = (a.B + 32 * RT - 1) / (32 * RT);
-    const dim3 grid((unsigned)(ntile_c * ntile_r));
-    const size_t wfl = (size_t)a.ntypes * CT * (PREC ? 512 : 1024);  // two stages of halves, in floats
-    const size_t yfl = MODE == 1 ? (size_t)J * (8 * COLS + 16) + 8 * 16 * 100 : (size_t)J * (16 * (COLS + 4) + 16);
+    const dim3 grid((unsigned)(ntile_c * ntile_r * (MODE == 2 ? 2 : MODE == 3 ? 4 : 1)));
+    const size_t wfl = MODE >= 2 ? 0 : (size_t)a.ntypes * CT * (PREC ? 512 : 1024);  // two stages of halves, in floats
+    const size_t yfl = ATT ? (size_t)J * (8 * COLS + 16) + 8 * 16 * 100 : (size_t)J * (16 * (COLS + 4) + 16);
     size_t lds = ((wfl > yfl ? wfl : yfl) + (size_t)J * J + 2 * COLS) * sizeof(float);
     if (lds > 160 * 1024) return hipErrorNotSupported;
     // LDS-DMA staging (STG 0): the workgroup takes its CU's whole LDS, so no other kernel's
@@ -923,7 +1099,8 @@ static hipError_t gl4_launch_t(const GLArgs& a, bool rms, hipStream_t s) {
     // placement and the vmcnt / barrier ordering of the K loop.
     // gl4_stage 2 (diagnostic only): LDS-DMA stages at their exact size, so the hazard can be
     // reproduced (tools/lds_hazard.py)
-    if (STG == 0 && a.gl4_stage != 2) lds = 160 * 1024;
+    // Split-route phase 2 (MODE 2 / 3) has no weight stages: exact size.
+    if (MODE < 2 && STG == 0 && a.gl4_stage != 2) lds = 160 * 1024;
     auto kt = rms ? k_gl4<J, NW, RT, CT, true, DBG, MODE, XP, PREC, STG> : k_gl4<J, NW, RT, CT, false, DBG, MODE, XP, PREC, STG>;
     if (lds > 64 * 1024) {
         hipError_t e = hipFuncSetAttribute((const void*)kt, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
@@ -946,6 +1123,62 @@ int set_gl4_tile(int cfg) {
     return old;
 }
 
+// ---- split route (small grids) -------------------------------------------------
+// A one-kernel launch is one workgroup's K-loop latency however few workgroups it has: at 50
+// rows an N = 192 layer is 12 workgroups on 256 CUs.  The split route runs phase 1 (k_gl4y, one
+// wave per (32-row tile, node, 32-column tile): J x more parallel work, no LDS) into the zs
+// scratch and phase 2 (k_gl4 MODE 2: mixing + FiLM / tanh / residual per 16-row slab, or MODE 3:
+// the attention epilogue per 8-row slab).  Same arithmetic in the same order as the one-kernel
+// route, so the results are bitwise identical and the route can follow the shard size.
+// Auto threshold on the rows of the whole sampling call (all row chains; GLArgs::route_rows):
+// process default SKELDIFF_SPLIT_ROWS = 1024.  Measured (B = 400 / 800 / 1600 at T = 100, three
+// chains): split 5,764 / 9,018 / 11,389 futures/s vs one-kernel 4,440 / 8,666 / 12,594.
+static int64_t g_split_rows = [] {
+    const char* e = getenv("SKELDIFF_SPLIT_ROWS");
+    return e ? (int64_t)atoll(e) : (int64_t)640;
+}();
+int64_t split_rows_default() { return g_split_rows; }
+
+static bool split_route(const GLArgs& a, bool attn) {
+    if (a.split == 1 || !a.zs || a.prec == 2 || (a.N & 31) || a.J > 32) return false;
+    const int64_t tiles = (a.B + 31) / 32;
+    if (tiles * 32 * a.J * (int64_t)a.N > a.zs_cap) return false;
+    if (a.zs == a.out || a.zs == a.x1 || a.zs == a.x2 || a.zs == a.res) return false;
+    if (attn && (a.attn_heads * 96 != a.N)) return false;
+    if (a.split == 2) return true;
+    return a.gl4_cfg == 0 && (a.route_rows > 0 ? a.route_rows : a.B) <= g_split_rows;
+}
+
+template <int J>
+static hipError_t gl4_split(const GLArgs& a, bool rms, bool attn, hipStream_t s) {
+    const int64_t ntile_r = (a.B + 31) / 32;
+    const int ntc = a.N / 32;
+    const int64_t units = ntile_r * J * ntc;
+    const dim3 grid((unsigned)((units + 3) / 4));
+    if (a.prec == 1) {
+        if (rms) hipLaunchKernelGGL((k_gl4y<true, 1>), grid, dim3(256), 0, s, a, ntc, ntile_r);
+        else hipLaunchKernelGGL((k_gl4y<false, 1>), grid, dim3(256), 0, s, a, ntc, ntile_r);
+    } else {
+        if (rms) hipLaunchKernelGGL((k_gl4y<true, 0>), grid, dim3(256), 0, s, a, ntc, ntile_r);
+        else hipLaunchKernelGGL((k_gl4y<false, 0>), grid, dim3(256), 0, s, a, ntc, ntile_r);
+    }
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    if constexpr (J <= 16) {
+        if (attn) return gl4_launch_t<J, 8, 1, 3, 0, 3, 0, 0, 0>(a, false, s);
+    }
+    return gl4_launch_t<J, 8, 1, 1, 0, 2, 0, 0, 0>(a, false, s);
+}
+
+static hipError_t gl4_split_dispatch(const GLArgs& a, bool rms, bool attn, hipStream_t s) {
+    switch (a.J) {
+        case 16: return gl4_split<16>(a, rms, attn, s);
+        case 17: return gl4_split<17>(a, rms, attn, s);
+        case 21: return gl4_split<21>(a, rms, attn, s);
+        default: return hipErrorNotSupported;
+    }
+}
+
 hipError_t launch_graph_linear_v4(const GLArgs& a, bool rms, hipStream_t s) {
     if (a.B <= 0) return hipSuccess;
     // K1, K2 multiples of 16 and an even number of 16-deep chunks (the K loop is unrolled by 2)
@@ -953,6 +1186,7 @@ hipError_t launch_graph_linear_v4(const GLArgs& a, bool rms, hipStream_t s) {
     if ((a.N & 3) || ((uintptr_t)a.out & 15) || ((uintptr_t)a.res & 15) || (a.res && (a.res_rs & 3)) || (a.out_rs & 3))
         return hipErrorNotSupported;
     if (!a.wsp || (a.K1 + a.K2) % 32 || a.K1 % 16 || (a.x1_blk && a.x1_div != 1)) return hipErrorNotSupported;
+    if ((a.J == 16 || a.J == 17 || a.J == 21) && split_route(a, false)) return gl4_split_dispatch(a, rms, false, s);
     const int cfg = a.gl4_cfg ? a.gl4_cfg : a.tile_hint;
     if (a.prec == 2) {  // bf16 mode: row-major operands, the default tiles only
         if (a.x1_blk || a.x2_blk || a.res_blk || a.out_blk) return hipErrorNotSupported;
@@ -1012,6 +1246,7 @@ hipError_t launch_qkv_attention_v4(const GLArgs& a, bool rms, hipStream_t s) {
         return hipErrorNotSupported;
     GLArgs b = a;
     b.attn_order = a.gl4_cfg == 100 ? 1 : 0;
+    if (a.J == 16 && a.prec != 2 && split_route(a, true)) return gl4_split_dispatch(b, rms, true, s);
     switch (a.J) {
         case 16:
             if (a.prec == 2) return gl4_launch<16, 8, 1, 3, 0, 1, 0, 2>(b, rms, s);

@@ -31,6 +31,10 @@ struct GLArgs {
     // the test entry points): generation 0 auto / 1..5 forced, v4 tile <NW><RT><CT> (0 auto),
     // v4 weight staging 0 LDS-DMA (CU held exclusively) / 1 register-staged (CU shareable)
     int variant, gl4_cfg, gl4_stage;
+    // v4 split route for small grids (phase 1 GEMM per (tile, node) into the zs scratch, phase 2
+    // mixing epilogue; bitwise identical to the one-kernel route): 0 auto, 1 never, 2 always
+    int split;
+    int64_t route_rows;  // rows of the whole sampling call on this device (row chains: all chains); 0 = B
     const float* x2; int64_t x2_rs; int K2;               // optional second input (cat along K)
     const float* W;                                       // (types, N, K1+K2), K contiguous
     const float* bias;                                    // (types, N) or null
@@ -53,7 +57,8 @@ struct GLArgs {
     // v4 only: operand / result layouts, 0 = row-major (B, J, F), 1 = row-blocked (blk_off in
     // sd_graph_linear_v4.hip; rows padded to 32)
     int x1_blk, x2_blk, res_blk, out_blk;
-    // v5 only: scratch for the pre-mix activations when res aliases out (zs_cap floats), or null
+    // v5: scratch for the pre-mix activations when res aliases out (zs_cap floats), or null;
+    // v4 split route: the pre-mix Y of phase 1
     float* zs; int64_t zs_cap;
     unsigned* dbg;  // SD_DEBUG_LDS builds only: integrity counters (else unused)
     // v4: bit 0 set (atomicOr) when an activation is outside the f16 range of the split
@@ -110,6 +115,7 @@ int set_graph_linear_variant(int v);  // returns the previous value, -1 if v is 
 int gl4_tile_default();
 int set_gl4_tile(int cfg);            // returns the previous value
 int gl4_stage_default();
+int64_t split_rows_default();         // SKELDIFF_SPLIT_ROWS: auto split route at or below this many rows
 int set_gl4_stage(int stage);         // returns the previous value, -1 if out of range
 hipError_t launch_attention(const AttnArgs& a, hipStream_t s);
 hipError_t launch_update(const UpdArgs& a, hipStream_t s);

@@ -617,8 +617,96 @@ __global__ __launch_bounds__(256) void k_update(const UpdArgs p) {
 #endif
 }
 
+// Small batches: k_update's thread owns a (row, feature pair) and walks all J nodes serially
+// (J Philox draws + 3 J^2 FMAs, ~16 us of dependent work whatever the batch).  Here one
+// workgroup per row spreads the same work over (node, feature pair) items in two phases:
+//   A: item (j, d): x0 (act, clamp), x_t and sigma_j eps_j of one node -> LDS;
+//   B: item (i, d): the C1 / C2 / U sums over j from LDS, in k_update's order and expressions.
+__global__ __launch_bounds__(256) void k_update_row(const UpdArgs p) {
+    extern __shared__ __attribute__((aligned(16))) float sm[];
+    const int J = p.J, D = p.D, DP = D >> 1, JD = J * D;
+    const int nt = p.iso ? 0 : 3 * J * J + J;
+    float* sC1 = sm;
+    float* sC2 = sC1 + J * J;
+    float* sU = sC2 + J * J;
+    float* sS = sU + J * J;
+    float* sx0 = sm + ((nt + 3) & ~3);
+    float* sxt = sx0 + JD;
+    float* sev = sxt + JD;
+    if (!p.iso) {
+        for (int i = threadIdx.x; i < J * J; i += 256) {
+            sC1[i] = p.C1[i];
+            sC2[i] = p.C2[i];
+            sU[i] = p.U[i];
+        }
+        for (int i = threadIdx.x; i < J; i += 256) sS[i] = p.sig[i];
+    }
+    const int64_t row = blockIdx.x;
+    const int64_t rb = row * (int64_t)JD;
+    uint64_t seed = p.seed;
+    int64_t row0 = p.row0;
+    if (p.noise_mode == 2 && p.rng_dev) {
+        seed = p.rng_dev[0];
+        row0 = (int64_t)p.rng_dev[1];
+    }
+    row0 += p.row_shift;
+    __syncthreads();  // sS
+    for (int q = threadIdx.x; q < J * DP; q += 256) {
+        const int j = q / DP, d = 2 * (q - j * DP), o = j * D + d;
+        floatx2 a = ld2x(p.x0, rb + o, p.x0_bf16);
+        if (p.act == 1) {
+            a.x = tanhf(a.x);
+            a.y = tanhf(a.y);
+        }
+        st2(sx0 + o, floatx2{fminf(fmaxf(a.x, -1.f), 1.f), fminf(fmaxf(a.y, -1.f), 1.f)});
+        st2(sxt + o, ld2x(p.xt, rb + o, p.xt_bf16));
+        floatx2 e;
+        if (p.noise_mode == 1) e = ld2(p.eps + row * p.eps_rs + o);
+        else if (p.noise_mode == 2) e = noise_pair(seed, (uint64_t)(row0 + row), p.step, (uint32_t)o);
+        else e = floatx2{0.f, 0.f};
+        if (p.noise_out) st2(p.noise_out + row * p.noise_rs + o, e);
+        if (!p.iso && p.noise_mode != 0) e *= sS[j];
+        st2(sev + o, e);
+    }
+    __syncthreads();
+    for (int q = threadIdx.x; q < J * DP; q += 256) {
+        const int i = q / DP, d = 2 * (q - i * DP), o = i * D + d;
+        floatx2 mean, v;
+        if (p.iso) {
+            mean = p.c1s * ld2(sx0 + o) + p.c2s * ld2(sxt + o);
+            v = (p.noise_mode != 0) ? mean + p.sigs * ld2(sev + o) : mean;
+        } else {
+            floatx2 m1 = {0.f, 0.f}, m2 = {0.f, 0.f}, nz = {0.f, 0.f};
+            for (int j = 0; j < J; ++j) {
+                m1 += sC1[i * J + j] * ld2(sx0 + j * D + d);
+                m2 += sC2[i * J + j] * ld2(sxt + j * D + d);
+                nz += sU[i * J + j] * ld2(sev + j * D + d);
+            }
+            mean = m1 + m2;
+            v = (p.noise_mode != 0) ? mean + nz : mean;
+        }
+        st2x(p.out, rb + o, p.out_bf16, v);
+        if (p.out2) st2(p.out2 + row * p.out2_rs + o, p.out_bf16 ? __builtin_convertvector(__builtin_convertvector(v, bf16x2), floatx2) : v);
+        if (p.mean_out) st2(p.mean_out + row * p.mean_rs + o, mean);
+    }
+}
+
+// rows at or below which launch_update runs k_update_row (process default SKELDIFF_UPDATE_ROWS)
+static int64_t g_update_rows = [] {
+    const char* e = getenv("SKELDIFF_UPDATE_ROWS");
+    return e ? (int64_t)atoll(e) : (int64_t)1024;
+}();
+
 hipError_t launch_update(const UpdArgs& a, hipStream_t s) {
     if (a.B <= 0) return hipSuccess;
+    if (a.B <= g_update_rows && a.D % 2 == 0) {
+        const size_t nt = a.iso ? 0 : 3 * (size_t)a.J * a.J + a.J;
+        const size_t lds = (((nt + 3) & ~(size_t)3) + 3 * (size_t)a.J * a.D) * sizeof(float);
+        if (lds <= 64 * 1024) {
+            hipLaunchKernelGGL(k_update_row, dim3((unsigned)a.B), dim3(256), lds, s, a);
+            return hipGetLastError();
+        }
+    }
     const int64_t n = a.B * (a.D / 2);
     const dim3 grid((unsigned)((n + 255) / 256));
     switch (a.J) {

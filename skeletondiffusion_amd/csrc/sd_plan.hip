@@ -75,7 +75,7 @@ struct GraphKey {
     int32_t flags;
     int32_t chains;
     int32_t prec;
-    int32_t variant, gl4_cfg, gl4_stage;  // the plan's kernel options at capture time
+    int32_t variant, gl4_cfg, gl4_stage, split;  // the plan's kernel options at capture time
     void* stream;
     bool operator<(const GraphKey& o) const { return std::memcmp(this, &o, sizeof(GraphKey)) < 0; }
 };
@@ -118,7 +118,7 @@ struct sd_plan {
     bool blk_ok = false;   // every layer on v4 with row-blocked intermediate activations
     int prec = 0;          // sd_plan_set_precision: 0 f32-accurate, 1 half (f16 products)
     // kernel options (sd_plan_set_option), initialised from the process defaults at creation
-    int variant = 0, gl4_cfg = 0, gl4_stage = 0, chains = 3;
+    int variant = 0, gl4_cfg = 0, gl4_stage = 0, split = 0, chains = 3;
     bool fuse_attention_now() const { return fuse_ok && (variant == 0 || variant == 4); }
     bool blocked_now() const { return blk_ok && fuse_attention_now() && prec != 2; }
     std::vector<void*> allocs;
@@ -277,6 +277,7 @@ sd::GLArgs gl_args(const sd_plan* p, const GL& g, const float* x1, int x1_div, c
     a.variant = p->variant;
     a.gl4_cfg = p->gl4_cfg;
     a.gl4_stage = p->gl4_stage;
+    a.split = p->split;
 #ifdef SD_DEBUG_LDS
     a.dbg = sd::debug_counters();
 #endif
@@ -314,7 +315,7 @@ struct Prof {
 int run_denoiser(const sd_plan* p, const float* x_t, const float* x_cond, int64_t cond_repeat,
                  int t, float* x0_out, int64_t rows, const WS& w, hipStream_t s, Prof* prof = nullptr,
                  int64_t cond_phase = 0, int tile_hint = 0, float* const* trace = nullptr,
-                 int xt_bf16 = 0, int x0_bf16 = 0) {
+                 int xt_bf16 = 0, int x0_bf16 = 0, int64_t route_rows = 0) {
     const int H = p->H;
     // v4 path: every intermediate activation in the row-blocked layout (coalesced x fragments);
     // the denoiser's inputs (x_t, x_cond) and output (x0) stay row-major
@@ -341,9 +342,10 @@ int run_denoiser(const sd_plan* p, const float* x_t, const float* x_cond, int64_
     };
     // v5 scratch (pre-mix activations of layers whose residual aliases their output): the qkv
     // buffer, dead outside the attention block (>= rows * J * H floats)
-    const int64_t zs_cap = rows * p->J * (int64_t)(p->d.use_attention ? 3 * p->hid : p->H);
-    auto lay = [B, tile_hint, &w, zs_cap, &bfl](sd::GLArgs& g, int in, int res, int out) {
+    const int64_t zs_cap = (rows + 31) / 32 * 32 * p->J * (int64_t)(p->d.use_attention ? 3 * p->hid : p->H);
+    auto lay = [B, tile_hint, &w, zs_cap, &bfl, route_rows](sd::GLArgs& g, int in, int res, int out) {
         g.status = ws_status(w);
+        g.route_rows = route_rows;
         g.zs = w.qkv;
         g.zs_cap = zs_cap;
         g.tile_hint = tile_hint;
@@ -851,6 +853,10 @@ static int chain_count(const sd_plan* p, int64_t rows, int64_t cond_repeat, int6
     const int64_t units = rows / g;
     int n = std::max(1, std::min(p->chains, (int)sd_plan::kMaxChains));
     if (units < n) n = (int)std::max<int64_t>(1, units);
+    // the split route (small batches) runs on one stream: its kernels gave run-to-run different
+    // rows when two chains' launches shared CUs, and the single chain is as fast
+    // there (one 400-row chain 5,565 vs three 5,764 futures/s)
+    if (p->split == 2 || (p->split == 0 && rows <= sd::split_rows_default())) n = 1;
     return n;
 }
 static int64_t chain_row(int i, int n, int64_t rows, int64_t unit) {
@@ -910,7 +916,7 @@ static int record_loop(const sd_plan* p, const float* x_T, const float* x_cond, 
             // 5 % faster than the single-chain 32 x 96 choice at B = 3200, 3 chains
             const int64_t wg813 = (c.n + 31) / 32 * 2;  // 32 x 96 workgroups of an N = 192 layer
             int rc = run_denoiser(p, c.cur, xc, cond_repeat, t, c.w.x0, c.n, c.w, cs[i], nullptr, r0 % cond_repeat,
-                                  (nch > 1 && wg813 >= 32) ? 812 : 0, nullptr, bf, bf);
+                                  (nch > 1 && wg813 >= 32) ? 812 : 0, nullptr, bf, bf, rows);
             if (rc) return rc;
             float* nxt = (t == 0) ? out + r0 * JD : (((T - 1 - t) & 1) ? c.w.img1 : c.w.img0);
             const float* eps = (!dev_noise && t > 0) ? eps_all + r0 * step_rs + k * JD : nullptr;
@@ -997,6 +1003,7 @@ int sd_sample_loop(const sd_plan* p, const float* x_T, const float* x_cond, int6
     key.variant = p->variant;
     key.gl4_cfg = p->gl4_cfg;
     key.gl4_stage = p->gl4_stage;
+    key.split = p->split;
     key.stream = stream;
     SD_HIP(sd::launch_set_rng(w.rng, seed, row0, s));
     std::shared_ptr<GraphSet> set;
@@ -1149,6 +1156,10 @@ int sd_plan_set_option(sd_plan* p, int32_t option, int64_t value) {
                 return fail(SD_E_INVALID, "gl4 staging must be 0 (LDS-DMA), 1 (registers) or 2 (diagnostic)");
             p->gl4_stage = (int)value;
             return SD_OK;
+        case SD_OPT_SPLIT_ROUTE:
+            if (value < 0 || value > 2) return fail(SD_E_INVALID, "split route must be 0 (auto), 1 (never) or 2 (always)");
+            p->split = (int)value;
+            return SD_OK;
         default: return fail(SD_E_INVALID, "unknown option " + std::to_string(option));
     }
 }
@@ -1161,6 +1172,7 @@ int sd_plan_get_option(const sd_plan* p, int32_t option, int64_t* value) {
         case SD_OPT_ROW_CHAINS: *value = p->chains; return SD_OK;
         case SD_OPT_PRECISION: *value = p->prec; return SD_OK;
         case SD_OPT_GL4_STAGING: *value = p->gl4_stage; return SD_OK;
+        case SD_OPT_SPLIT_ROUTE: *value = p->split; return SD_OK;
         default: return fail(SD_E_INVALID, "unknown option " + std::to_string(option));
     }
 }

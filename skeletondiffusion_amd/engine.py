@@ -111,7 +111,8 @@ class SamplingEngine:
         self._precision = mode
 
     OPTIONS = {"kernel_variant": _lib.SD_OPT_KERNEL_VARIANT, "gl4_tile": _lib.SD_OPT_GL4_TILE,
-               "row_chains": _lib.SD_OPT_ROW_CHAINS, "gl4_staging": _lib.SD_OPT_GL4_STAGING}
+               "row_chains": _lib.SD_OPT_ROW_CHAINS, "gl4_staging": _lib.SD_OPT_GL4_STAGING,
+               "split_route": _lib.SD_OPT_SPLIT_ROUTE}
 
     def set_option(self, name: str, value: int) -> None:
         """Per-plan kernel option (sd_plan_set_option): "kernel_variant" (0 auto, 1..5),

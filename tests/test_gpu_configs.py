@@ -140,6 +140,82 @@ def test_register_staging_shares_cus_bitwise(cuda):
     assert eng.get_option("gl4_staging") == 1
 
 
+@pytest.mark.parametrize("cfg,batch,kw", [("h36m_t1000", 1, {}), ("amass16", 4, {}), ("amass16", 12, {}),
+                                          ("amass21", 4, {}), ("freeman17", 2, {}),
+                                          ("amass16", 4, {"precision": "half"})])
+def test_split_route_bitwise(cfg, batch, kw, cuda):
+    """SD_OPT_SPLIT_ROUTE: the small-launch route (k_gl4y GEMM phase per (tile,
+    node, column tile) + k_gl4 MODE 2 / 3 mixing or attention phase) is bitwise equal to the
+    one-kernel route, graph and eager, with the f16 range guard word untouched."""
+    from bench import build_config
+
+    d, x_cond, rows = build_config(cfg, cuda, T=10, batch=batch)
+    eng = d.engine
+    if kw.get("precision"):
+        eng.set_precision(kw["precision"])
+    eng.set_option("row_chains", 1)
+    eng.set_option("split_route", 1)
+    ref = eng.sample_loop(rows, x_cond=x_cond, seed=5, record=(False, True))
+    ref = [ref[0].clone(), ref[4].clone()]
+    eng.set_option("split_route", 2)
+    for graph in (False, True):
+        got = eng.sample_loop(rows, x_cond=x_cond, seed=5, graph=graph, record=(False, True))
+        torch.cuda.synchronize()
+        assert torch.equal(got[0], ref[0]) and torch.equal(got[4], ref[1]), (cfg, batch, graph)
+    assert eng.status(rows) == 0
+
+
+def test_split_route_shard_equals_full_batch(cuda):
+    """A shard small enough for the split route (400 rows at row0 = 1600, as one rank of an
+    8-GPU strong-scaling run of config 2) reproduces those rows of the full 3,200-row batch on
+    the one-kernel route bitwise: the route follows the shard size without changing results."""
+    from bench import build_config
+
+    d, x_cond, rows = build_config("amass16", cuda, T=10)
+    eng = d.engine
+    eng.set_option("split_route", 1)
+    full = eng.sample_loop(rows, x_cond=x_cond, seed=9)[0].clone()
+    eng.set_option("split_route", 0)
+    per = rows // x_cond.shape[0]
+    s0, n = 1600, 400
+    part = eng.sample_loop(n, x_cond=x_cond[s0 // per:(s0 + n) // per], seed=9, row0=s0)[0]
+    torch.cuda.synchronize()
+    assert torch.equal(part, full[s0:s0 + n])
+
+
+def test_exact_variant_row_chains_bitwise(cuda):
+    """The exact-f32 kernels (v3, LDS-DMA stages of <= 64 KB, CU shareable) with three concurrent
+    row chains, graph replay, equal one chain run eagerly bit for bit (config 2, T = 10)."""
+    from bench import build_config
+
+    d, x_cond, rows = build_config("amass16", cuda, T=10)
+    eng = d.engine
+    eng.set_option("kernel_variant", 3)
+    eng.set_option("row_chains", 1)
+    ref = eng.sample_loop(rows, x_cond=x_cond, seed=21)[0].clone()
+    eng.set_option("row_chains", 3)
+    for graph in (False, True, True):
+        x = eng.sample_loop(rows, x_cond=x_cond, seed=21, graph=graph)[0]
+        torch.cuda.synchronize()
+        assert torch.equal(x, ref), graph
+
+
+def test_split_route_runs_one_chain_deterministic(cuda):
+    """At or below the split-route threshold the plan runs a single row chain (DESIGN.md §4c:
+    concurrent chains on the split kernels gave run-to-run different rows); 200 rows at T = 100
+    with row_chains = 3 requested: repeated runs, eager and graph, are bitwise identical."""
+    from bench import build_config
+
+    d, x_cond, rows = build_config("amass16", cuda, T=100, batch=4)
+    eng = d.engine
+    eng.set_option("row_chains", 3)
+    ref = eng.sample_loop(rows, x_cond=x_cond, seed=5)[0].clone()
+    for graph in (False, False, True, True):
+        x = eng.sample_loop(rows, x_cond=x_cond, seed=5, graph=graph)[0]
+        torch.cuda.synchronize()
+        assert torch.equal(x, ref), graph
+
+
 @pytest.mark.parametrize("name", ["release_h36m16_T10", "release_amass21_T10"])
 def test_denoiser_per_layer_activations(name, cuda):
     """Every block output of one Denoiser forward (init_lin, 8 ResnetBlocks, 7 attention blocks +
@@ -219,7 +295,8 @@ def test_two_plans_with_different_options_concurrently(cuda):
     for t in th:
         t.join()
     torch.cuda.synchronize()
-    assert torch.equal(res["a"], solo_a) and torch.equal(res["b"], solo_b)
+    assert torch.equal(res["a"], solo_a), _max_err(res["a"], solo_a)
+    assert torch.equal(res["b"], solo_b), _max_err(res["b"], solo_b)
     assert _max_err(solo_a, solo_b) < TOL
     assert da.engine.get_option("kernel_variant") == 0 and db.engine.get_option("kernel_variant") == 3
 
