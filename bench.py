@@ -294,7 +294,8 @@ def main():
             elapsed = float(tt.item())
         ms, cnt, fl = profile_kernels(d, x_cond, rows, args.profile_reps)
         exact = None
-        if world == 1 and not args.no_exact_line and args.kernel_variant == 0 and J in (16, 17, 21):
+        if (world == 1 and not args.no_exact_line and args.kernel_variant == 0 and J in (16, 17, 21)
+                and eng.precision == "f32"):
             # the same workload on the exact-f32 kernels: a second plan, same inputs
             eng.set_option("kernel_variant", 3)
             for i in range(args.warmup):
