@@ -64,6 +64,8 @@ CONFIGS = {
                     workload="AMASS real node count J=21, T=100, 50 futures, batch=64 (config 2, secondary)"),
     "mano51": dict(skel="mano51", T=100, batch=64, futures=50,
                    workload="AMASS-MANO J=51, T=100, 50 futures, 64 sequences per GPU (config 3 per-rank shard)"),
+    "mano52": dict(skel="mano52", T=100, batch=64, futures=50,
+                   workload="AMASS-MANO hip-included J=52, T=100, 50 futures, 64 sequences per GPU (config 3 label)"),
     "h36m_t1000": dict(skel="h36m16", T=1000, batch=1, futures=50,
                        workload="Human3.6M J=16, T=1000, 50 futures, 1 sequence, hipGraph (config 4)"),
     "freeman17": dict(skel="freeman17", T=100, batch=64, futures=50,

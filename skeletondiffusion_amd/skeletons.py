@@ -58,13 +58,22 @@ SKELETONS: Dict[str, Tuple[List[str], List[Tuple[int, int]], Tuple[str, str, str
 }
 
 
+# hip-included variants (if_consider_hip=True, e.g. amass.py:81-83): the root joint is node 0 and
+# the original limbs are kept (BASELINE config 3's "J=52" label for AMASS-MANO)
+HIP_INCLUDED: Dict[str, str] = {"mano52": "mano51"}
+
+
 def skeleton(key: str):
     """-> (node_names, node_limbs, adjacency (J,J) float32, node_types (J,) int64)."""
-    names, limbs, (a, b, c) = SKELETONS[key]
-    nodes = names[1:]
-    idx = {n: i for i, n in enumerate(nodes)}
-    node_limbs = [(idx[a], idx[b]), (idx[a], idx[c]), (idx[b], idx[c])]
-    node_limbs += [(i - 1, j - 1) for i, j in limbs if i != 0 and j != 0]
+    if key in HIP_INCLUDED:
+        names, limbs, _ = SKELETONS[HIP_INCLUDED[key]]
+        nodes, node_limbs = list(names), [tuple(l) for l in limbs]
+    else:
+        names, limbs, (a, b, c) = SKELETONS[key]
+        nodes = names[1:]
+        idx = {n: i for i, n in enumerate(nodes)}
+        node_limbs = [(idx[a], idx[b]), (idx[a], idx[c]), (idx[b], idx[c])]
+        node_limbs += [(i - 1, j - 1) for i, j in limbs if i != 0 and j != 0]
     J = len(nodes)
     adj = np.zeros((J, J), dtype=np.float32)
     for i, j in node_limbs:

@@ -94,6 +94,10 @@ SKELETONS = {
     "amass21": lambda: AMASSKinematic(num_joints=22, if_consider_hip=False),
     "mano51": lambda: AMASSKinematic(num_joints=52, if_consider_hip=False),
     "freeman17": lambda: FreeManKinematic(if_consider_hip=False),
+    # hip-included AMASS-MANO (amass.py:81-83): the root joint is a node (config 3's J=52 label)
+    # (the compound skeleton class takes node_hip from motion/base.py:5, `Skeleton.node_hip`)
+    "mano52": lambda: type("AMASSKinematicHip", (AMASSKinematic,), {"node_hip": {0: "GlobalRoot"}})(
+        num_joints=52, if_consider_hip=True),
 }
 
 RELEASE_ARCH = dict(use_attention=True, self_condition=False, norm_type="none", depth=4,
@@ -162,8 +166,10 @@ def capture_forward(model, x, t, x_cond):
     return out, acts
 
 
-def gen_covariances():
+def gen_covariances(keys=None):
     for key, ctor in SKELETONS.items():
+        if keys and key not in keys:
+            continue
         sk = ctor()
         corr = sk.adj_matrix
         Sigma_N, Lambda_N, U = get_cov_from_corr(correlation_matrix=corr, if_sigma_n_scale=True,
@@ -305,6 +311,13 @@ def gen_new_r02():
                 steps_to_keep=[0, 1, 2, 3, 4, 499, 994, 995, 996, 997, 998])
 
 
+def gen_hip_included():
+    """Round 2: the hip-included MANO skeleton (J = 52, if_consider_hip=True): covariances and a
+    T = 10 release sample (1 sequence x 2 futures)."""
+    gen_covariances(["mano52"])
+    gen_release("mano52", 10, B_seq=1, futures=2, with_acts=False)
+
+
 def gen_metrics():
     """The reference's multimodal metrics (src/metrics/multimodal.py) on synthetic samples: latent
     APD (L1) and APD (L2) over 50 futures of (J=16, 96) latents, and ADE / FDE of (frames, J*3)
@@ -375,6 +388,9 @@ def main():
     if sys.argv[1:] == ["r02"]:
         gen_new_r02()
         return
+    if sys.argv[1:] == ["hip"]:
+        gen_hip_included()
+        return
     gen_metrics()
     gen_decoder()
     gen_covariances()
@@ -385,6 +401,7 @@ def main():
     gen_release("freeman17", 10, B_seq=1, futures=4, with_acts=False)
     gen_release("mano51", 10, B_seq=1, futures=2, with_acts=False)
     gen_new_r02()
+    gen_hip_included()
 
 
 if __name__ == "__main__":

@@ -32,7 +32,7 @@ def test_release_module_forward_and_loss(name):
     assert d.model.init_lin.G.grad is not None and torch.isfinite(d.model.init_lin.weight.grad).all()
 
 
-@pytest.mark.parametrize("key", ["h36m16", "amass21", "mano51", "freeman17"])
+@pytest.mark.parametrize("key", ["h36m16", "amass21", "mano51", "freeman17", "mano52"])
 def test_buffers_bit_exact(key):
     from skeletondiffusion_amd.core.diffusion import NonisotropicGaussianDiffusion, get_cov_from_corr
     from skeletondiffusion_amd.core.network import Denoiser

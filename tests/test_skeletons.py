@@ -8,7 +8,7 @@ from skeletondiffusion_amd.skeletons import skeleton
 
 
 @pytest.mark.parametrize("key,J,ntypes", [("h36m16", 16, 10), ("amass21", 21, 13), ("mano51", 51, 43),
-                                          ("freeman17", 17, 9)])
+                                          ("freeman17", 17, 9), ("mano52", 52, 44)])
 def test_skeleton_tables_match_reference(key, J, ntypes):
     z = golden("cov_" + key)
     names, limbs, adj, types = skeleton(key)
