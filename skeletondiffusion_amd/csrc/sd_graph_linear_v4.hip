@@ -205,8 +205,17 @@ hipError_t make_split_weights(const float* W, int ntypes, int N, int K, SplitW* 
 // chunk), RMS sum, range guard and scale arithmetic as in k_gl4, so phase 2 (k_gl4 MODE 2 / 3)
 // reproduces the one-kernel results bit for bit.  Workgroup = 4 waves = 4 column tiles of one
 // (row tile, node): the x fragments are shared through L1.
+// Output addressing: element (row 32 tr + r, node j, column n) at y + tr y_ts + j y_js + r y_rs + n;
+// the split route's scratch is [tile][node][32 rows][N] (y_rs = N, y_js = 32 N, y_ts = 32 J N, all
+// 32 rows stored), v5 (J > 21) writes row-major z (y_rs = J N, y_js = N, rows >= B not stored).
+struct YOut {
+    float* y;
+    int64_t y_rs, y_js, y_ts;
+    int mask_rows;
+};
+
 template <bool RMS, int PREC, int PF = 8>  // PF: chunks in flight
-__global__ __launch_bounds__(256) void k_gl4y(const GLArgs p, int ntile_c, int64_t ntile_r) {
+__global__ __launch_bounds__(256) void k_gl4y(const GLArgs p, int ntile_c, int64_t ntile_r, const YOut yo) {
     const int lane = threadIdx.x & 63, l32 = lane & 31, h = lane >> 5;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int64_t u = (int64_t)blockIdx.x * 4 + wave;
@@ -294,40 +303,47 @@ __global__ __launch_bounds__(256) void k_gl4y(const GLArgs p, int ntile_c, int64
     }
     const int ncol = tc * 32 + l32;
     const float bv = (p.bias && ncol < p.N) ? p.bias[p.wrow[j] + ncol] : 0.f;
-    float* y = p.zs + ((tr * J + j) * 32) * (int64_t)p.N + ncol;
+    if (ncol >= p.N) return;
+    float* y = yo.y + tr * yo.y_ts + j * yo.y_js + ncol;
 #pragma unroll
-    for (int r = 0; r < 16; ++r) y[(int64_t)((r & 3) + 8 * (r >> 2) + 4 * h) * p.N] = acc[r] * sc[r] + bv;
+    for (int r = 0; r < 16; ++r) {
+        const int rr = (r & 3) + 8 * (r >> 2) + 4 * h;
+        if (!yo.mask_rows || row0 + rr < p.B) y[rr * yo.y_rs] = acc[r] * sc[r] + bv;
+    }
 }
 
-// Epilogue of the fused to_qkv + Attention kernel (MODE 1), J <= 16, dh = 32, 8 waves, a
+// Epilogue of the fused to_qkv + Attention kernel (MODE 1), J <= 32, dh = 32, 8 waves, a
 // 32-row tile.  Per 8-row slab: the mixed-in q|k|v (Z = G-hat Y) goes to LDS as [row][node][96],
-// then wave w runs the attention of row 8*slab + w exactly as k_attention does (same f32 MFMA
-// order, expf softmax), writing out[row][n][head*32 + d].
-// FROM_YS (MODE 3, split route phase 2): the Y slab q8only comes from phase 1's scratch p.zs
-// instead of the accumulators.
+// then wave w runs the attention of row 8*slab + w exactly as k_attention<JT> does (same f32 MFMA
+// order over JT 16-node tiles, expf softmax), writing out[row][n][head*32 + d].
+// FROM_YS (MODE 3, split route phase 2): k_gl4 MODE 3 has put slab q8only in sY already.
 template <int J, int NW, int NPW, bool FROM_YS = false>
 __device__ __forceinline__ void attention_epilogue(const GLArgs& p, floatx16 (&acc)[NPW][1][3], float* smem,
                                                    const float* sG, int64_t row0, int head, int wave, int lane,
                                                    int q8only = 0) {
     constexpr int COLS = 96;
+    constexpr int JT = (J + 15) / 16;   // 16-node tiles (k_attention<JT>)
+    constexpr int KS = (J + 3) / 4;     // 4-deep k steps of the mixing GEMM
     constexpr int YS8 = 8 * COLS + 16;  // floats per node in an 8-row Y slab (+16: bank shift)
     constexpr int ZN = 100;             // floats per node in a Z row (+4: bank shift)
-    constexpr int ZR = 16 * ZN;         // floats per Z row
+    constexpr int ZR = J * ZN;          // floats per Z row
     const int l32 = lane & 31, h = lane >> 5, lr = lane & 15, lg = lane >> 4;
     const int hid = p.attn_heads * 32;
     float* sY = smem;
     float* sZ = smem + J * YS8;
-    float ga[4];  // G-hat^T[k = j = 4s + lg][col = i = lr]
+    float ga[JT][KS];  // G-hat^T[k = j = 4s + lg][col = i = 16 it + lr]
 #pragma unroll
-    for (int s = 0; s < 4; ++s) {
-        const int jj = 4 * s + lg;
-        ga[s] = (lr < J && jj < J) ? sG[lr * J + jj] : 0.f;
-    }
+    for (int it = 0; it < JT; ++it)
+#pragma unroll
+        for (int s = 0; s < KS; ++s) {
+            const int i = 16 * it + lr, jj = 4 * s + lg;
+            ga[it][s] = (i < J && jj < J) ? sG[i * J + jj] : 0.f;
+        }
 #pragma unroll
     for (int q8 = 0; q8 < 4; ++q8) {  // rows 8 q8 .. 8 q8 + 7 = accumulator registers 4 q8 .. 4 q8 + 3
         if (FROM_YS && q8 != q8only) continue;
-        if constexpr (!FROM_YS) {  // FROM_YS: k_gl4 MODE 3 has put the slab in sY
-            __syncthreads();       // K loop / previous slab done with this LDS
+        if constexpr (!FROM_YS) {
+            __syncthreads();  // K loop / previous slab done with this LDS
 #pragma unroll
             for (int m = 0; m < NPW; ++m) {
                 const int j = wave + NW * m;
@@ -343,69 +359,106 @@ __device__ __forceinline__ void attention_epilogue(const GLArgs& p, floatx16 (&a
 #pragma unroll
         for (int k = 0; k < 48 / NW; ++k) {
             const int rc0 = (wave + NW * k) * 16;
-            float ya[4];
+            float ya[KS];
 #pragma unroll
-            for (int s = 0; s < 4; ++s) {
+            for (int s = 0; s < KS; ++s) {
                 const int jj = 4 * s + lg;
                 ya[s] = jj < J ? sY[jj * YS8 + rc0 + lr] : 0.f;
             }
-            floatx4 z = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-            for (int s = 0; s < 4; ++s) z = __builtin_amdgcn_mfma_f32_16x16x4f32(ya[s], ga[s], z, 0, 0, 0);
             const int rc = rc0 + 4 * lg, r = rc / COLS, c = rc - r * COLS;
-            if (lr < J) *reinterpret_cast<floatx4*>(sZ + r * ZR + lr * ZN + c) = z;
+#pragma unroll
+            for (int it = 0; it < JT; ++it) {
+                floatx4 z = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                for (int s = 0; s < KS; ++s) z = __builtin_amdgcn_mfma_f32_16x16x4f32(ya[s], ga[it][s], z, 0, 0, 0);
+                const int i = 16 * it + lr;
+                if (i < J) *reinterpret_cast<floatx4*>(sZ + r * ZR + i * ZN + c) = z;
+            }
         }
         __syncthreads();
-        // attention of one row per wave (k_attention's math, one 16-node tile)
+        // attention of one row per wave (k_attention<JT>'s math)
         const int64_t row = row0 + 8 * q8 + wave;
         const float* zr = sZ + wave * ZR;
-        floatx4 S = {0.f, 0.f, 0.f, 0.f};
+        floatx4 S[JT][JT];
+#pragma unroll
+        for (int a = 0; a < JT; ++a)
+#pragma unroll
+            for (int c = 0; c < JT; ++c) S[a][c] = floatx4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int cc = 0; cc < 32; cc += 16) {
-            const floatx4 ka = lr < J ? *reinterpret_cast<const floatx4*>(zr + lr * ZN + 32 + cc + 4 * lg)
-                                      : floatx4{0.f, 0.f, 0.f, 0.f};
-            const floatx4 qv = lr < J ? *reinterpret_cast<const floatx4*>(zr + lr * ZN + cc + 4 * lg) * p.attn_scale
-                                      : floatx4{0.f, 0.f, 0.f, 0.f};
-            S = __builtin_amdgcn_mfma_f32_16x16x4f32(ka.x, qv.x, S, 0, 0, 0);
-            S = __builtin_amdgcn_mfma_f32_16x16x4f32(ka.y, qv.y, S, 0, 0, 0);
-            S = __builtin_amdgcn_mfma_f32_16x16x4f32(ka.z, qv.z, S, 0, 0, 0);
-            S = __builtin_amdgcn_mfma_f32_16x16x4f32(ka.w, qv.w, S, 0, 0, 0);
-        }
-        // softmax over j = 4 lg + e for query column n = lr
-        float mx = -INFINITY;
+            floatx4 ka[JT], qv[JT];
 #pragma unroll
-        for (int e = 0; e < 4; ++e)
-            if (4 * lg + e < J) mx = fmaxf(mx, S[e]);
-        mx = fmaxf(mx, __shfl_xor(mx, 16));
-        mx = fmaxf(mx, __shfl_xor(mx, 32));
-        float sum = 0.f;
+            for (int t = 0; t < JT; ++t) {
+                const int j = t * 16 + lr;
+                ka[t] = j < J ? *reinterpret_cast<const floatx4*>(zr + j * ZN + 32 + cc + 4 * lg) : floatx4{0.f, 0.f, 0.f, 0.f};
+                qv[t] = j < J ? *reinterpret_cast<const floatx4*>(zr + j * ZN + cc + 4 * lg) * p.attn_scale
+                              : floatx4{0.f, 0.f, 0.f, 0.f};
+            }
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-            const float ex = (4 * lg + e < J) ? expf(S[e] - mx) : 0.f;
-            S[e] = ex;
-            sum += ex;
+            for (int jt = 0; jt < JT; ++jt)
+#pragma unroll
+                for (int nt = 0; nt < JT; ++nt) {
+                    floatx4 cacc = S[jt][nt];
+                    cacc = __builtin_amdgcn_mfma_f32_16x16x4f32(ka[jt].x, qv[nt].x, cacc, 0, 0, 0);
+                    cacc = __builtin_amdgcn_mfma_f32_16x16x4f32(ka[jt].y, qv[nt].y, cacc, 0, 0, 0);
+                    cacc = __builtin_amdgcn_mfma_f32_16x16x4f32(ka[jt].z, qv[nt].z, cacc, 0, 0, 0);
+                    cacc = __builtin_amdgcn_mfma_f32_16x16x4f32(ka[jt].w, qv[nt].w, cacc, 0, 0, 0);
+                    S[jt][nt] = cacc;
+                }
         }
-        sum += __shfl_xor(sum, 16);
-        sum += __shfl_xor(sum, 32);
-        S *= 1.0f / sum;
+        // softmax over j (rows of S^T) for every query column n = nt * 16 + lr
+#pragma unroll
+        for (int nt = 0; nt < JT; ++nt) {
+            float mx = -INFINITY;
+#pragma unroll
+            for (int jt = 0; jt < JT; ++jt)
+#pragma unroll
+                for (int e = 0; e < 4; ++e)
+                    if (jt * 16 + 4 * lg + e < J) mx = fmaxf(mx, S[jt][nt][e]);
+            mx = fmaxf(mx, __shfl_xor(mx, 16));
+            mx = fmaxf(mx, __shfl_xor(mx, 32));
+            float sum = 0.f;
+#pragma unroll
+            for (int jt = 0; jt < JT; ++jt)
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const float ex = (jt * 16 + 4 * lg + e < J) ? expf(S[jt][nt][e] - mx) : 0.f;
+                    S[jt][nt][e] = ex;
+                    sum += ex;
+                }
+            sum += __shfl_xor(sum, 16);
+            sum += __shfl_xor(sum, 32);
+            const float inv = 1.0f / sum;
+#pragma unroll
+            for (int jt = 0; jt < JT; ++jt) S[jt][nt] *= inv;
+        }
         // O^T[d][n] = sum_j V[j][d] P^T[j][n]
 #pragma unroll
         for (int dc = 0; dc < 32; dc += 16) {
-            floatx4 vv;
+            floatx4 vv[JT];
 #pragma unroll
-            for (int s4 = 0; s4 < 4; ++s4) {
-                const int j = 4 * lg + s4;
-                vv[s4] = j < J ? zr[j * ZN + 64 + dc + lr] : 0.f;
-            }
-            floatx4 o = {0.f, 0.f, 0.f, 0.f};
-            o = __builtin_amdgcn_mfma_f32_16x16x4f32(vv.x, S.x, o, 0, 0, 0);
-            o = __builtin_amdgcn_mfma_f32_16x16x4f32(vv.y, S.y, o, 0, 0, 0);
-            o = __builtin_amdgcn_mfma_f32_16x16x4f32(vv.z, S.z, o, 0, 0, 0);
-            o = __builtin_amdgcn_mfma_f32_16x16x4f32(vv.w, S.w, o, 0, 0, 0);
-            if (lr < J && row < p.B) {
-                const int f = head * 32 + dc + 4 * lg;
-                float* dst = p.out_blk ? p.out + blk_off(row, lr, f, J, hid) : p.out + row * p.out_rs + (int64_t)lr * hid + f;
-                *reinterpret_cast<floatx4*>(dst) = o;
+            for (int jt = 0; jt < JT; ++jt)
+#pragma unroll
+                for (int s4 = 0; s4 < 4; ++s4) {
+                    const int j = jt * 16 + 4 * lg + s4;
+                    vv[jt][s4] = j < J ? zr[j * ZN + 64 + dc + lr] : 0.f;
+                }
+#pragma unroll
+            for (int nt = 0; nt < JT; ++nt) {
+                floatx4 o = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                for (int jt = 0; jt < JT; ++jt) {
+                    o = __builtin_amdgcn_mfma_f32_16x16x4f32(vv[jt].x, S[jt][nt].x, o, 0, 0, 0);
+                    o = __builtin_amdgcn_mfma_f32_16x16x4f32(vv[jt].y, S[jt][nt].y, o, 0, 0, 0);
+                    o = __builtin_amdgcn_mfma_f32_16x16x4f32(vv[jt].z, S[jt][nt].z, o, 0, 0, 0);
+                    o = __builtin_amdgcn_mfma_f32_16x16x4f32(vv[jt].w, S[jt][nt].w, o, 0, 0, 0);
+                }
+                const int n = nt * 16 + lr;
+                if (n < J && row < p.B) {
+                    const int f = head * 32 + dc + 4 * lg;
+                    float* dst = p.out_blk ? p.out + blk_off(row, n, f, J, hid) : p.out + row * p.out_rs + (int64_t)n * hid + f;
+                    *reinterpret_cast<floatx4*>(dst) = o;
+                }
             }
         }
     }
@@ -427,7 +480,7 @@ __device__ __forceinline__ void attention_epilogue(const GLArgs& p, floatx16 (&a
 //   (global_load_dwordx4 a chunk ahead, ds_write_b128 after the chunk's MFMAs).
 template <int J, int NW, int RT, int CT, bool RMS, int DBG = 0, int MODE = 0, int XP = 0, int PREC = 0, int STG = 0>
 __global__ __launch_bounds__(NW * 64, 1) void k_gl4(const GLArgs p) {
-    static_assert(MODE == 0 || MODE == 2 || (CT == 3 && RT == 1 && J <= 16 && NW == 8), "attention mode: 32 x (q|k|v)");
+    static_assert(MODE == 0 || MODE == 2 || (CT == 3 && RT == 1 && J <= 32 && NW == 8), "attention mode: 32 x (q|k|v)");
     static_assert(MODE < 2 || (RT == 1 && XP == 0 && STG == 0 && DBG == 0), "split-route phase 2: one 32-row tile");
     constexpr int NPW = (J + NW - 1) / NW;  // nodes per wave
     constexpr int KS = (J + 3) / 4;         // 4-deep k steps of the mixing GEMM (K = J padded)
@@ -446,7 +499,7 @@ __global__ __launch_bounds__(NW * 64, 1) void k_gl4(const GLArgs p) {
     const int stage_h = MODE >= 2 ? 0 : p.ntypes * CT * TILE_H;  // halves per weight stage
     const int wfl = stage_h;                   // two stages of halves = stage_h floats
     constexpr bool ATT = MODE == 1 || MODE == 3;
-    const int yfl = ATT ? J * (8 * COLS + 16) + 8 * 16 * 100 : J * YS;  // Y slab (+ Z rows)
+    const int yfl = ATT ? J * (8 * COLS + 16) + 8 * J * 100 : J * YS;  // Y slab (+ Z rows)
     _Float16* sW0 = reinterpret_cast<_Float16*>(smem);
     _Float16* sW1 = sW0 + stage_h;
     float* sY = smem;  // aliases the weight stages after the K loop
@@ -1074,8 +1127,11 @@ static hipError_t gl4_launch_t(const GLArgs& a, bool rms, hipStream_t s);
 template <int J, int NW, int RT, int CT, int DBG = 0, int MODE = 0, int XP = 0, int PREC = 0>
 static hipError_t gl4_launch(const GLArgs& a, bool rms, hipStream_t s) {
     constexpr int TILE_H = PREC ? 512 : 1024;
-    if (MODE < 2 && a.gl4_stage == 1 && XP == 0 && DBG == 0 && a.ntypes * CT * (TILE_H / 8) <= 8 * NW * 64)
-        return gl4_launch_t<J, NW, RT, CT, DBG, MODE, XP, PREC, MODE < 2 ? 1 : 0>(a, rms, s);
+    // register staging: not for the J > 16 fused attention tile (3 nodes per wave: it would spill)
+    if constexpr (MODE == 0 || (MODE == 1 && J <= 16)) {
+        if (a.gl4_stage == 1 && XP == 0 && DBG == 0 && a.ntypes * CT * (TILE_H / 8) <= 8 * NW * 64)
+            return gl4_launch_t<J, NW, RT, CT, DBG, MODE, XP, PREC, 1>(a, rms, s);
+    }
     return gl4_launch_t<J, NW, RT, CT, DBG, MODE, XP, PREC, 0>(a, rms, s);
 }
 
@@ -1087,7 +1143,7 @@ static hipError_t gl4_launch_t(const GLArgs& a, bool rms, hipStream_t s) {
     const int64_t ntile_r = (a.B + 32 * RT - 1) / (32 * RT);
     const dim3 grid((unsigned)(ntile_c * ntile_r * (MODE == 2 ? 2 : MODE == 3 ? 4 : 1)));
     const size_t wfl = MODE >= 2 ? 0 : (size_t)a.ntypes * CT * (PREC ? 512 : 1024);  // two stages of halves, in floats
-    const size_t yfl = ATT ? (size_t)J * (8 * COLS + 16) + 8 * 16 * 100 : (size_t)J * (16 * (COLS + 4) + 16);
+    const size_t yfl = ATT ? (size_t)J * (8 * COLS + 16) + 8 * J * 100 : (size_t)J * (16 * (COLS + 4) + 16);
     size_t lds = ((wfl > yfl ? wfl : yfl) + (size_t)J * J + 2 * COLS) * sizeof(float);
     if (lds > 160 * 1024) return hipErrorNotSupported;
     // LDS-DMA staging (STG 0): the workgroup takes its CU's whole LDS, so no other kernel's
@@ -1149,22 +1205,37 @@ static bool split_route(const GLArgs& a, bool attn) {
     return a.gl4_cfg == 0 && (a.route_rows > 0 ? a.route_rows : a.B) <= g_split_rows;
 }
 
+static hipError_t launch_gl4y(const GLArgs& a, bool rms, int ntc, int64_t ntile_r, const YOut& yo, hipStream_t s) {
+    const int64_t units = ntile_r * a.J * ntc;
+    const dim3 grid((unsigned)((units + 3) / 4));
+    if (a.prec == 1) {
+        if (rms) hipLaunchKernelGGL((k_gl4y<true, 1>), grid, dim3(256), 0, s, a, ntc, ntile_r, yo);
+        else hipLaunchKernelGGL((k_gl4y<false, 1>), grid, dim3(256), 0, s, a, ntc, ntile_r, yo);
+    } else {
+        if (rms) hipLaunchKernelGGL((k_gl4y<true, 0>), grid, dim3(256), 0, s, a, ntc, ntile_r, yo);
+        else hipLaunchKernelGGL((k_gl4y<false, 0>), grid, dim3(256), 0, s, a, ntc, ntile_r, yo);
+    }
+    return hipGetLastError();
+}
+
+// v5's GEMM phase on split-f16 products (J > 21; sd_graph_linear_v5.hip): z[b, j, n] row-major
+// with row stride z_rs, rows < B only.  hipErrorNotSupported without split weights.
+hipError_t launch_gemm_split(const GLArgs& a, bool rms, float* z, int64_t z_rs, hipStream_t s) {
+    if (!a.wsp || a.prec == 2 || (a.K1 + a.K2) % 16 || a.K1 % 16 || a.x1_blk || a.x2_blk) return hipErrorNotSupported;
+    const int64_t ntile_r = (a.B + 31) / 32;
+    const int ntc = (a.N + 31) / 32;
+    const YOut yo{z, z_rs, a.N, 32 * z_rs, 1};
+    return launch_gl4y(a, rms, ntc, ntile_r, yo, s);
+}
+
 template <int J>
 static hipError_t gl4_split(const GLArgs& a, bool rms, bool attn, hipStream_t s) {
     const int64_t ntile_r = (a.B + 31) / 32;
     const int ntc = a.N / 32;
-    const int64_t units = ntile_r * J * ntc;
-    const dim3 grid((unsigned)((units + 3) / 4));
-    if (a.prec == 1) {
-        if (rms) hipLaunchKernelGGL((k_gl4y<true, 1>), grid, dim3(256), 0, s, a, ntc, ntile_r);
-        else hipLaunchKernelGGL((k_gl4y<false, 1>), grid, dim3(256), 0, s, a, ntc, ntile_r);
-    } else {
-        if (rms) hipLaunchKernelGGL((k_gl4y<true, 0>), grid, dim3(256), 0, s, a, ntc, ntile_r);
-        else hipLaunchKernelGGL((k_gl4y<false, 0>), grid, dim3(256), 0, s, a, ntc, ntile_r);
-    }
-    hipError_t e = hipGetLastError();
+    const YOut yo{a.zs, a.N, 32LL * a.N, 32LL * J * a.N, 0};
+    hipError_t e = launch_gl4y(a, rms, ntc, ntile_r, yo, s);
     if (e != hipSuccess) return e;
-    if constexpr (J <= 16) {
+    if constexpr (J <= 17) {
         if (attn) return gl4_launch_t<J, 8, 1, 3, 0, 3, 0, 0, 0>(a, false, s);
     }
     return gl4_launch_t<J, 8, 1, 1, 0, 2, 0, 0, 0>(a, false, s);
@@ -1241,16 +1312,21 @@ hipError_t launch_graph_linear_v4(const GLArgs& a, bool rms, hipStream_t s) {
 // graph-linear + k_attention pair).
 hipError_t launch_qkv_attention_v4(const GLArgs& a, bool rms, hipStream_t s) {
     if (a.B <= 0) return hipSuccess;
-    if (!a.wsp || a.J > 16 || a.attn_heads < 1 || a.N != 3 * a.attn_heads * 32 || a.bias || a.film || a.res ||
+    if (!a.wsp || a.J > 32 || a.attn_heads < 1 || a.N != 3 * a.attn_heads * 32 || a.bias || a.film || a.res ||
         a.act || (a.K1 + a.K2) % 32 || a.K1 % 16 || ((uintptr_t)a.out & 15) || (a.out_rs & 3))
         return hipErrorNotSupported;
     GLArgs b = a;
     b.attn_order = a.gl4_cfg == 100 ? 1 : 0;
-    if (a.J == 16 && a.prec != 2 && split_route(a, true)) return gl4_split_dispatch(b, rms, true, s);
+    if ((a.J == 16 || a.J == 17) && a.prec != 2 && split_route(a, true)) return gl4_split_dispatch(b, rms, true, s);
+    // J = 17 (FreeMan): 3 nodes per wave, two 16-node tiles in the softmax; J = 21's 13 node types
+    // need 2 x 78 KB of weight stages at 96 columns (> 160 KB of LDS): unfused (NotSupported)
     switch (a.J) {
         case 16:
             if (a.prec == 2) return gl4_launch<16, 8, 1, 3, 0, 1, 0, 2>(b, rms, s);
             return a.prec == 1 ? gl4_launch<16, 8, 1, 3, 0, 1, 0, 1>(b, rms, s) : gl4_launch<16, 8, 1, 3, 0, 1>(b, rms, s);
+        case 17:
+            if (a.prec == 2) return gl4_launch<17, 8, 1, 3, 0, 1, 0, 2>(b, rms, s);
+            return a.prec == 1 ? gl4_launch<17, 8, 1, 3, 0, 1, 0, 1>(b, rms, s) : gl4_launch<17, 8, 1, 3, 0, 1>(b, rms, s);
         default: return hipErrorNotSupported;
     }
 }

@@ -215,12 +215,17 @@ hipError_t launch_graph_linear_v5(const GLArgs& a, bool rms, hipStream_t s) {
     }
     const int64_t row_tiles = (a.B + TM - 1) / TM;
     if (row_tiles > 65535 || a.B > 65535 * 1024LL) return hipErrorNotSupported;
-    const dim3 g1((unsigned)((a.N + TN - 1) / TN), (unsigned)row_tiles, (unsigned)a.J);
-    if (rms)
-        hipLaunchKernelGGL(k_gl5_gemm<true>, g1, dim3(256), 0, s, a, z, z_rs);
-    else
-        hipLaunchKernelGGL(k_gl5_gemm<false>, g1, dim3(256), 0, s, a, z, z_rs);
-    hipError_t e = hipGetLastError();
+    // GEMM phase: split-f16 products (k_gl4y: 3 x v_mfma_f32_32x32x16_f16 per 16-deep k step, the
+    // v4 arithmetic) unless the exact-f32 v5 is forced (kernel variant 5)
+    hipError_t e = a.variant == 5 ? hipErrorNotSupported : launch_gemm_split(a, rms, z, z_rs, s);
+    if (e == hipErrorNotSupported) {
+        const dim3 g1((unsigned)((a.N + TN - 1) / TN), (unsigned)row_tiles, (unsigned)a.J);
+        if (rms)
+            hipLaunchKernelGGL(k_gl5_gemm<true>, g1, dim3(256), 0, s, a, z, z_rs);
+        else
+            hipLaunchKernelGGL(k_gl5_gemm<false>, g1, dim3(256), 0, s, a, z, z_rs);
+        e = hipGetLastError();
+    }
     if (e != hipSuccess) return e;
     const dim3 g2((unsigned)a.B, (unsigned)((a.N + 63) / 64));
     const int vec = ((uintptr_t)z & 15) == 0 && (a.N & 3) == 0 && (z_rs & 3) == 0;

@@ -108,6 +108,8 @@ hipError_t launch_graph_linear_v2(const GLArgs& a, bool rms, hipStream_t s);
 hipError_t launch_graph_linear_v3(const GLArgs& a, bool rms, hipStream_t s);  // J in {16,17,21}
 hipError_t launch_graph_linear_v4(const GLArgs& a, bool rms, hipStream_t s);  // needs a.wsp
 hipError_t launch_qkv_attention_v4(const GLArgs& a, bool rms, hipStream_t s);  // J <= 16, dh 32
+// split-f16 GEMM phase (k_gl4y) into row-major z (B, J, N) with row stride z_rs (v5, J > 21)
+hipError_t launch_gemm_split(const GLArgs& a, bool rms, float* z, int64_t z_rs, hipStream_t s);
 // process defaults that new plans (and the sd_test_* hooks) start from: SKELDIFF_GL_VARIANT
 // (0 auto, 1..5), SKELDIFF_GL4_CFG (<NW><RT><CT>, 0 auto), SKELDIFF_GL4_STAGE (0 / 1), read at load
 int graph_linear_variant();

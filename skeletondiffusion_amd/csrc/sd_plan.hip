@@ -693,7 +693,7 @@ int sd_plan_finalize(sd_plan* p, void* stream_) {
     }
     if ((rc = pack_gl(p->fres_res))) return rc;
     if ((rc = pack_gl(p->fglin))) return rc;
-    p->fuse_ok = p->d.use_attention && J <= 16 && p->d.attn_dim_head == 32;
+    p->fuse_ok = p->d.use_attention && J <= 17 && p->d.attn_dim_head == 32;
     for (size_t l = 0; l < p->qkv.size(); ++l)
         if (p->has_attn[l] && !p->qkv[l].split.w) p->fuse_ok = false;
     // row-blocked activations need every graph-linear on v4 (split weights, K multiple of 32)
