@@ -1235,9 +1235,7 @@ static hipError_t gl4_split(const GLArgs& a, bool rms, bool attn, hipStream_t s)
     const YOut yo{a.zs, a.N, 32LL * a.N, 32LL * J * a.N, 0};
     hipError_t e = launch_gl4y(a, rms, ntc, ntile_r, yo, s);
     if (e != hipSuccess) return e;
-    if constexpr (J <= 17) {
-        if (attn) return gl4_launch_t<J, 8, 1, 3, 0, 3, 0, 0, 0>(a, false, s);
-    }
+    if (attn) return gl4_launch_t<J, 8, 1, 3, 0, 3, 0, 0, 0>(a, false, s);
     return gl4_launch_t<J, 8, 1, 1, 0, 2, 0, 0, 0>(a, false, s);
 }
 
@@ -1317,9 +1315,8 @@ hipError_t launch_qkv_attention_v4(const GLArgs& a, bool rms, hipStream_t s) {
         return hipErrorNotSupported;
     GLArgs b = a;
     b.attn_order = a.gl4_cfg == 100 ? 1 : 0;
-    if ((a.J == 16 || a.J == 17) && a.prec != 2 && split_route(a, true)) return gl4_split_dispatch(b, rms, true, s);
-    // J = 17 (FreeMan): 3 nodes per wave, two 16-node tiles in the softmax; J = 21's 13 node types
-    // need 2 x 78 KB of weight stages at 96 columns (> 160 KB of LDS): unfused (NotSupported)
+    if ((a.J == 16 || a.J == 17 || a.J == 21) && a.prec != 2 && split_route(a, true)) return gl4_split_dispatch(b, rms, true, s);
+    // J = 17 / 21: 3 nodes per wave, two 16-node tiles in the softmax
     switch (a.J) {
         case 16:
             if (a.prec == 2) return gl4_launch<16, 8, 1, 3, 0, 1, 0, 2>(b, rms, s);
@@ -1327,6 +1324,9 @@ hipError_t launch_qkv_attention_v4(const GLArgs& a, bool rms, hipStream_t s) {
         case 17:
             if (a.prec == 2) return gl4_launch<17, 8, 1, 3, 0, 1, 0, 2>(b, rms, s);
             return a.prec == 1 ? gl4_launch<17, 8, 1, 3, 0, 1, 0, 1>(b, rms, s) : gl4_launch<17, 8, 1, 3, 0, 1>(b, rms, s);
+        case 21:  // 13 node types: 2 x 78 KB weight stages + G-hat + FiLM = 158.5 KB of LDS
+            if (a.prec == 2) return gl4_launch<21, 8, 1, 3, 0, 1, 0, 2>(b, rms, s);
+            return a.prec == 1 ? gl4_launch<21, 8, 1, 3, 0, 1, 0, 1>(b, rms, s) : gl4_launch<21, 8, 1, 3, 0, 1>(b, rms, s);
         default: return hipErrorNotSupported;
     }
 }

@@ -114,7 +114,7 @@ struct sd_plan {
     std::vector<Slot> slots;
     std::map<std::string, int> index;
     bool finalized = false;
-    bool fuse_ok = false;  // to_qkv + attention fusable (v4 split weights, J <= 16, dim_head 32)
+    bool fuse_ok = false;  // to_qkv + attention fusable (v4 split weights, J <= 17 or 21, dim_head 32)
     bool blk_ok = false;   // every layer on v4 with row-blocked intermediate activations
     int prec = 0;          // sd_plan_set_precision: 0 f32-accurate, 1 half (f16 products)
     // kernel options (sd_plan_set_option), initialised from the process defaults at creation
@@ -693,7 +693,7 @@ int sd_plan_finalize(sd_plan* p, void* stream_) {
     }
     if ((rc = pack_gl(p->fres_res))) return rc;
     if ((rc = pack_gl(p->fglin))) return rc;
-    p->fuse_ok = p->d.use_attention && J <= 17 && p->d.attn_dim_head == 32;
+    p->fuse_ok = p->d.use_attention && (J <= 17 || J == 21) && p->d.attn_dim_head == 32;
     for (size_t l = 0; l < p->qkv.size(); ++l)
         if (p->has_attn[l] && !p->qkv[l].split.w) p->fuse_ok = false;
     // row-blocked activations need every graph-linear on v4 (split weights, K multiple of 32)

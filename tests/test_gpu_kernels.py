@@ -174,11 +174,13 @@ def test_attention_kernel(J, heads, dh, cuda):
     assert (out.cpu().double() - ref).abs().max().item() < 2e-5
 
 
-@pytest.mark.parametrize("J,nty,heads,rms", [(16, 10, 8, True), (16, 1, 4, True), (16, 10, 8, False), (16, 3, 2, True)])
-@pytest.mark.parametrize("B", [64, 67])
+@pytest.mark.parametrize("J,nty,heads,rms", [(16, 10, 8, True), (16, 1, 4, True), (16, 10, 8, False), (16, 3, 2, True),
+                                          (17, 9, 8, True), (21, 13, 8, True), (21, 13, 2, False)])
+@pytest.mark.parametrize("B", [64, 67, 704])
 @pytest.mark.parametrize("blocked", [False, True])
 def test_qkv_attention_fused(J, nty, heads, rms, B, blocked, cuda):
-    """Fused to_qkv + attention kernel vs a float64 torch restatement of the two ops."""
+    """Fused to_qkv + attention kernel vs a float64 torch restatement of the two ops (B <= 640:
+    the split route's k_gl4y + k_gl4 MODE 3; B = 704: the one-kernel k_gl4 MODE 1)."""
     g = torch.Generator().manual_seed(J * 100 + heads + B + rms)
     K, hid = 192, heads * 32
     r = lambda *s: torch.rand(*s, generator=g) * 2 - 1  # noqa: E731
@@ -206,7 +208,9 @@ def test_qkv_attention_fused(J, nty, heads, rms, B, blocked, cuda):
 
 
 def test_qkv_attention_rejects_large_J(cuda):
-    J, K, heads, B = 21, 192, 8, 8
+    """Node counts without a fused tile (J not in 16 / 17 / 21 and J > 16, here the MANO J = 51)
+    are refused; the caller runs the graph-linear + k_attention pair."""
+    J, K, heads, B = 51, 192, 8, 8
     x = torch.zeros(B, J, K, device=cuda)
     W = torch.zeros(1, 3 * heads * 32, K, device=cuda)
     out = torch.zeros(B, J, heads * 32, device=cuda)
