@@ -205,16 +205,15 @@ hipError_t make_split_weights(const float* W, int ntypes, int N, int K, SplitW* 
 // chunk), RMS sum, range guard and scale arithmetic as in k_gl4, so phase 2 (k_gl4 MODE 2 / 3)
 // reproduces the one-kernel results bit for bit.  Workgroup = 4 waves = 4 column tiles of one
 // (row tile, node): the x fragments are shared through L1.
-// Output addressing: element (row 32 tr + r, node j, column n) at y + tr y_ts + j y_js + r y_rs + n;
-// the split route's scratch is [tile][node][32 rows][N] (y_rs = N, y_js = 32 N, y_ts = 32 J N, all
-// 32 rows stored), v5 (J > 21) writes row-major z (y_rs = J N, y_js = N, rows >= B not stored).
+// Output: the split route's scratch p.zs as [tile][node][32 rows][N] (all 32 rows of a tile), or
+// (ROWMAJOR, v5 for J > 21) element (row 32 tr + r, node j, column n) at
+// y + tr y_ts + j y_js + r y_rs + n for rows < B only.
 struct YOut {
     float* y;
     int64_t y_rs, y_js, y_ts;
-    int mask_rows;
 };
 
-template <bool RMS, int PREC, int PF = 8>  // PF: chunks in flight
+template <bool RMS, int PREC, bool ROWMAJOR, int PF = 8>  // PF: chunks in flight
 __global__ __launch_bounds__(256) void k_gl4y(const GLArgs p, int ntile_c, int64_t ntile_r, const YOut yo) {
     const int lane = threadIdx.x & 63, l32 = lane & 31, h = lane >> 5;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -303,12 +302,18 @@ __global__ __launch_bounds__(256) void k_gl4y(const GLArgs p, int ntile_c, int64
     }
     const int ncol = tc * 32 + l32;
     const float bv = (p.bias && ncol < p.N) ? p.bias[p.wrow[j] + ncol] : 0.f;
-    if (ncol >= p.N) return;
-    float* y = yo.y + tr * yo.y_ts + j * yo.y_js + ncol;
+    if constexpr (ROWMAJOR) {
+        if (ncol >= p.N) return;
+        float* y = yo.y + tr * yo.y_ts + j * yo.y_js + ncol;
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-        const int rr = (r & 3) + 8 * (r >> 2) + 4 * h;
-        if (!yo.mask_rows || row0 + rr < p.B) y[rr * yo.y_rs] = acc[r] * sc[r] + bv;
+        for (int r = 0; r < 16; ++r) {
+            const int rr = (r & 3) + 8 * (r >> 2) + 4 * h;
+            if (row0 + rr < p.B) y[rr * yo.y_rs] = acc[r] * sc[r] + bv;
+        }
+    } else {  // the split route's scratch: every row of the tile, N % 32 == 0
+        float* y = p.zs + ((tr * J + j) * 32) * (int64_t)p.N + ncol;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) y[(int64_t)((r & 3) + 8 * (r >> 2) + 4 * h) * p.N] = acc[r] * sc[r] + bv;
     }
 }
 
@@ -1205,15 +1210,16 @@ static bool split_route(const GLArgs& a, bool attn) {
     return a.gl4_cfg == 0 && (a.route_rows > 0 ? a.route_rows : a.B) <= g_split_rows;
 }
 
+template <bool ROWMAJOR>
 static hipError_t launch_gl4y(const GLArgs& a, bool rms, int ntc, int64_t ntile_r, const YOut& yo, hipStream_t s) {
     const int64_t units = ntile_r * a.J * ntc;
-    const dim3 grid((unsigned)((units + 3) / 4));
+    const dim3 grid((unsigned)((units + 3) / 4)), block(256);
     if (a.prec == 1) {
-        if (rms) hipLaunchKernelGGL((k_gl4y<true, 1>), grid, dim3(256), 0, s, a, ntc, ntile_r, yo);
-        else hipLaunchKernelGGL((k_gl4y<false, 1>), grid, dim3(256), 0, s, a, ntc, ntile_r, yo);
+        if (rms) hipLaunchKernelGGL((k_gl4y<true, 1, ROWMAJOR>), grid, block, 0, s, a, ntc, ntile_r, yo);
+        else hipLaunchKernelGGL((k_gl4y<false, 1, ROWMAJOR>), grid, block, 0, s, a, ntc, ntile_r, yo);
     } else {
-        if (rms) hipLaunchKernelGGL((k_gl4y<true, 0>), grid, dim3(256), 0, s, a, ntc, ntile_r, yo);
-        else hipLaunchKernelGGL((k_gl4y<false, 0>), grid, dim3(256), 0, s, a, ntc, ntile_r, yo);
+        if (rms) hipLaunchKernelGGL((k_gl4y<true, 0, ROWMAJOR>), grid, block, 0, s, a, ntc, ntile_r, yo);
+        else hipLaunchKernelGGL((k_gl4y<false, 0, ROWMAJOR>), grid, block, 0, s, a, ntc, ntile_r, yo);
     }
     return hipGetLastError();
 }
@@ -1224,16 +1230,16 @@ hipError_t launch_gemm_split(const GLArgs& a, bool rms, float* z, int64_t z_rs, 
     if (!a.wsp || a.prec == 2 || (a.K1 + a.K2) % 16 || a.K1 % 16 || a.x1_blk || a.x2_blk) return hipErrorNotSupported;
     const int64_t ntile_r = (a.B + 31) / 32;
     const int ntc = (a.N + 31) / 32;
-    const YOut yo{z, z_rs, a.N, 32 * z_rs, 1};
-    return launch_gl4y(a, rms, ntc, ntile_r, yo, s);
+    const YOut yo{z, z_rs, a.N, 32 * z_rs};
+    return launch_gl4y<true>(a, rms, ntc, ntile_r, yo, s);
 }
 
 template <int J>
 static hipError_t gl4_split(const GLArgs& a, bool rms, bool attn, hipStream_t s) {
     const int64_t ntile_r = (a.B + 31) / 32;
     const int ntc = a.N / 32;
-    const YOut yo{a.zs, a.N, 32LL * a.N, 32LL * J * a.N, 0};
-    hipError_t e = launch_gl4y(a, rms, ntc, ntile_r, yo, s);
+    const YOut yo{a.zs, a.N, 32LL * a.N, 32LL * J * a.N};
+    hipError_t e = launch_gl4y<false>(a, rms, ntc, ntile_r, yo, s);
     if (e != hipSuccess) return e;
     if (attn) return gl4_launch_t<J, 8, 1, 3, 0, 3, 0, 0, 0>(a, false, s);
     return gl4_launch_t<J, 8, 1, 1, 0, 2, 0, 0, 0>(a, false, s);
@@ -1299,8 +1305,11 @@ hipError_t launch_graph_linear_v4(const GLArgs& a, bool rms, hipStream_t s) {
         // J > 16 needs two 16-node blocks in the mixing epilogue: 96 columns spill there
         case 17:
             if (cfg == 821) return gl4_launch<17, 8, 2, 1>(a, rms, s);
+            if (cfg == 813) return gl4_launch<17, 8, 1, 3>(a, rms, s);
             return gl4_launch<17, 8, 1, 2>(a, rms, s);
-        case 21: return gl4_launch<21, 8, 1, 2>(a, rms, s);
+        case 21:
+            if (cfg == 813) return gl4_launch<21, 8, 1, 3>(a, rms, s);
+            return gl4_launch<21, 8, 1, 2>(a, rms, s);
         default: return hipErrorNotSupported;
     }
 }
