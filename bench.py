@@ -233,6 +233,8 @@ def main():
                     help="weak: `batch` sequences per GPU; strong: `batch` sequences split over the GPUs")
     ap.add_argument("--kernel-variant", type=int, default=0, help="0 auto (split-f16 v4), 3 exact f32, ...")
     ap.add_argument("--no-exact-line", action="store_true", help="skip the exact-f32 comparison (N=1)")
+    ap.add_argument("--option", action="append", default=[], metavar="NAME=VALUE",
+                    help="per-plan kernel option (engine.set_option), e.g. split_route=3, row_chains=1")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -264,6 +266,9 @@ def main():
     eng = d.engine
     eng.set_precision(args.precision or c.get("precision", "f32"))
     eng.set_option("kernel_variant", args.kernel_variant)
+    for o in args.option:
+        name, value = o.split("=", 1)
+        eng.set_option(name, int(value))
     eng.plan()
     graph = not args.no_graph
     stream = torch.cuda.Stream(dev)

@@ -248,7 +248,9 @@ enum {
     SD_OPT_SPLIT_ROUTE = 6      /* v4 split route for small launches (GEMM phase per (tile, node)
                                    + mixing phase; bitwise identical results):
                                    0 auto (rows per launch <= SKELDIFF_SPLIT_ROWS, default 1024),
-                                   1 never, 2 always */
+                                   1 never, 2 always, 3 always with the tiled GEMM phase
+                                   (k_gl4t: 128 rows x up to 192 columns of one node per
+                                   workgroup, for full batches) */
 };
 int sd_plan_set_option(sd_plan* plan, int32_t option, int64_t value);
 int sd_plan_get_option(const sd_plan* plan, int32_t option, int64_t* value);

@@ -317,6 +317,184 @@ __global__ __launch_bounds__(256) void k_gl4y(const GLArgs p, int ntile_c, int64
     }
 }
 
+// ---- split route, phase 1 for full batches (tiled GEMM) --------------------------------------
+// k_gl4y gives every (32-row tile, node, 32-column tile) its own wave and its own operand loads:
+// 4 B of operands per output per k chunk, fine for latency at 50 rows, ingest-bound at 3,200.
+// k_gl4t: one workgroup = 4 waves = 4 consecutive 32-row tiles of ONE node x CT 32-column tiles.
+// The node's weight slice for the CT tiles (CT x 2 KiB per 16-deep chunk) is staged once per
+// workgroup in LDS (register-staged, double-buffered: no LDS-DMA) and shared by the 4 waves; each
+// wave streams its own x fragments PF chunks ahead and reuses them over CT tiles.  Per chunk a
+// workgroup pulls 8 KiB of x + CT x 2 KiB of weights for 128 x 32 CT outputs (0.8 B per output
+// at CT = 6 vs 2.2 B in the one-kernel k_gl4 32 x 64 tile).  Per accumulator element the MFMA
+// sequence (x_hi W'_hi, x_hi W'_lo, x_lo W'_hi per chunk), RMS sum, scale and bias arithmetic are
+// k_gl4's, so phase 2 (k_gl4 MODE 2 / 3) reproduces the one-kernel route bit for bit.
+template <bool RMS, int PREC, int CT, int NCH, int PF = 4>  // NCH: 16-deep k chunks (K / 16)
+__global__ __launch_bounds__(256, 2) void k_gl4t(const GLArgs p, int ncg, int64_t ntile_r) {
+    if (p.diag & 8) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // diagnostic (SKELDIFF_DIAG)
+    constexpr int TILE_H = PREC ? 512 : 1024;   // halves of one 32-column tile per chunk
+    constexpr int PPT = TILE_H / 8;             // 16-B pieces per tile
+    constexpr int NP = (CT * PPT + 255) / 256;  // staged pieces per thread
+    constexpr int TS = 36;                      // floats per row of a wave's 32 x 32 output transpose
+    constexpr int SB = 2 * CT * TILE_H * 2 > 4 * 32 * TS * 4 ? 2 * CT * TILE_H * 2 : 4 * 32 * TS * 4;
+    __shared__ __attribute__((aligned(16))) char smem_raw[SB];  // weight stages, then the transposes
+    _Float16(*sW)[CT * TILE_H] = reinterpret_cast<_Float16(*)[CT * TILE_H]>(smem_raw);
+    const int tid = threadIdx.x, lane = tid & 63, l32 = lane & 31, h = lane >> 5;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int J = p.J;
+    // XCD-aware order (k_gl4's): consecutive u -- the column groups of one (row group, node), which
+    // read the same x -- on one XCD (blocks b, b + 8, ... share one), so x reaches that L2 once
+    const int nwg = gridDim.x, xcd = blockIdx.x & 7, q8 = nwg >> 3, r8 = nwg & 7;
+    const int64_t u = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (blockIdx.x >> 3);
+    const int cg = (int)(u % ncg);
+    const int64_t rj = u / ncg;
+    const int j = (int)(rj % J);
+    const int64_t tr = (rj / J) * 4 + wave;
+    const bool live = tr < ntile_r;  // wave-uniform; a dead wave still stages weights and joins barriers
+    const int64_t row0 = (live ? tr : 0) * 32;
+    constexpr int nchunk = NCH;
+    const int64_t arow = row0 + l32;
+    const int64_t ac = arow < p.B ? arow : 0;
+    const float* x1r = p.x1_blk ? p.x1 + blk_off(arow, j, 8 * h, J, p.K1)
+                                : p.x1 + ((ac + p.x1_row0) / p.x1_div) * p.x1_rs + (int64_t)j * p.K1 + 8 * h;
+    const float* x2r = !p.K2 ? nullptr
+                             : p.x2_blk ? p.x2 + blk_off(arow, j, 8 * h, J, p.K2) : p.x2 + ac * p.x2_rs + (int64_t)j * p.K2 + 8 * h;
+    // staged pieces: piece q of a chunk = tile q / PPT, 16-B piece q % PPT of it
+    const _Float16* wsrc[NP];
+#pragma unroll
+    for (int k = 0; k < NP; ++k) {
+        const int q = min(tid + 256 * k, CT * PPT - 1);
+        wsrc[k] = p.wsp + ((int64_t)p.ntype[j] * nchunk * p.wsp_nct + cg * CT + q / PPT) * 1024 + (q % PPT) * 8;
+    }
+    const int64_t wcs = (int64_t)p.wsp_nct * 1024;  // halves per chunk
+    // the carried pieces as named registers, loaded unconditionally from clamped sources (an
+    // array under conditional loads was placed in scratch, with a vmcnt(0) before every store)
+    static_assert(NP <= 4, "staged pieces per thread");
+    uint4 w0, w1, w2, w3;
+    auto load_w = [&](int c) {
+        const int64_t o = c * wcs;
+        w0 = *reinterpret_cast<const uint4*>(wsrc[0] + o);
+        if constexpr (NP > 1) w1 = *reinterpret_cast<const uint4*>(wsrc[1] + o);
+        if constexpr (NP > 2) w2 = *reinterpret_cast<const uint4*>(wsrc[2] + o);
+        if constexpr (NP > 3) w3 = *reinterpret_cast<const uint4*>(wsrc[3] + o);
+    };
+    auto store_w = [&](int sl) {
+        uint4* d = reinterpret_cast<uint4*>(&sW[sl][tid * 8]);
+        constexpr bool FULL = CT * PPT % 256 == 0;
+        if (FULL || tid < CT * PPT) d[0] = w0;
+        if constexpr (NP > 1) if (FULL || tid + 256 < CT * PPT) d[256] = w1;
+        if constexpr (NP > 2) if (FULL || tid + 512 < CT * PPT) d[512] = w2;
+        if constexpr (NP > 3) if (FULL || tid + 768 < CT * PPT) d[768] = w3;
+    };
+    floatx4 xa[PF], xb[PF];
+    auto issue_x = [&](int c, int sl) {
+        const int k0 = c << 4;
+        const float* src;
+        int step4;
+        if (k0 < p.K1) {
+            src = p.x1_blk ? x1r + (k0 << 5) : x1r + k0;
+            step4 = p.x1_blk ? 128 : 4;
+        } else {
+            src = p.x2_blk ? x2r + ((k0 - p.K1) << 5) : x2r + (k0 - p.K1);
+            step4 = p.x2_blk ? 128 : 4;
+        }
+        xa[sl] = g4(src);
+        xb[sl] = g4(src + step4);
+    };
+    floatx16 acc[CT];
+#pragma unroll
+    for (int ct = 0; ct < CT; ++ct)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) acc[ct][e] = 0.f;
+    float ss = 0.f, amx = 0.f;
+    auto compute = [&](int c, int sl, int ws) {
+        const floatx8 f = {xa[sl].x, xa[sl].y, xa[sl].z, xa[sl].w, xb[sl].x, xb[sl].y, xb[sl].z, xb[sl].w};
+        if (RMS && (c << 4) < p.K1) {
+            const floatx8 q = f * f;
+            ss += ((q[0] + q[1]) + (q[2] + q[3])) + ((q[4] + q[5]) + (q[6] + q[7]));
+        }
+        const floatx8 a = __builtin_elementwise_abs(f);
+        amx = fmaxf(amx, fmaxf(fmaxf(fmaxf(a[0], a[1]), fmaxf(a[2], a[3])), fmaxf(fmaxf(a[4], a[5]), fmaxf(a[6], a[7]))));
+        const halfx8 xh = __builtin_convertvector(f, halfx8);
+        halfx8 xl;
+        if constexpr (!PREC) xl = __builtin_convertvector(f - __builtin_convertvector(xh, floatx8), halfx8);
+        const _Float16* wt = &sW[ws][lane * 8];
+#pragma unroll
+        for (int ct = 0; ct < CT; ++ct) {
+            const halfx8 wh = *reinterpret_cast<const halfx8*>(wt + ct * TILE_H);
+            floatx16 t = __builtin_amdgcn_mfma_f32_32x32x16_f16(xh, wh, acc[ct], 0, 0, 0);
+            if constexpr (!PREC) {
+                const halfx8 wl = *reinterpret_cast<const halfx8*>(wt + ct * TILE_H + 512);
+                t = __builtin_amdgcn_mfma_f32_32x32x16_f16(xh, wl, t, 0, 0, 0);
+                t = __builtin_amdgcn_mfma_f32_32x32x16_f16(xl, wh, t, 0, 0, 0);
+            }
+            acc[ct] = t;
+        }
+    };
+    load_w(0);
+#pragma unroll
+    for (int i = 0; i < PF; ++i)
+        if (i < nchunk) issue_x(i, i);
+    // chunk c: weights of c (loaded one chunk earlier, older than every x load in flight) ->
+    // stage c & 1 (free: every wave passed barrier c - 1 after its reads of chunk c - 2) ->
+    // lgkmcnt(0) + s_barrier (not __syncthreads(): its fence would drain the x loads in flight)
+    // -> weights of c + 1 to registers -> MFMAs on c -> x of c + PF into the freed ring slot
+    static_assert(NCH % PF == 0 && PF % 2 == 0, "ring slot and stage parity fixed per unrolled position");
+#pragma nounroll
+    for (int c0 = 0; c0 < nchunk; c0 += PF) {
+#pragma unroll
+        for (int i = 0; i < PF; ++i) {
+            const int c = c0 + i;
+            store_w(i & 1);
+            __builtin_amdgcn_s_waitcnt(0xC07F);
+            asm volatile("" ::: "memory");
+            __builtin_amdgcn_s_barrier();
+            asm volatile("" ::: "memory");
+            // unconditional loads (past the end: a clamped, unused chunk): a branch around them
+            // made the waitcnt pass merge both paths and drain the x ring every chunk
+            load_w(min(c + 1, nchunk - 1));
+            asm volatile("" ::: "memory");  // keep w(c + 1) older than x(c + PF): store_w(c + 1) waits for it alone
+            compute(c, i, i & 1);
+            asm volatile("" ::: "memory");
+            issue_x(min(c + PF, nchunk - 1), i);
+        }
+    }
+    __syncthreads();  // every wave past its last chunk: the stages become the output transposes
+    if (!live) return;
+    if (p.status && __builtin_amdgcn_ballot_w64(amx >= 65504.0f) != 0 && lane == 0) atomicOr(p.status, 1u);
+    float sc[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) sc[r] = p.wsp_unscale;
+    if (RMS) {
+        const float t = ss + __shfl_xor(ss, 32);
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const float n2 = __shfl(t, (r & 3) + 8 * (r >> 2) + 4 * h);
+            sc[r] *= 1.0f / fmaxf(sqrtf(n2), 1e-12f);
+        }
+    }
+    // Y = acc * sc + bias through a per-wave 32 x 32 LDS transpose (the stages are dead: every
+    // wave is past its last chunk), stored as 16-B pieces: 4 dwordx4 instead of 16 dword stores
+    // per tile.  Launch shapes: N a multiple of 32 CT (launch_gl4t), so every column is real.
+    float* sT = reinterpret_cast<float*>(smem_raw) + wave * 32 * TS;
+    float* y = p.zs + ((tr * J + j) * 32) * (int64_t)p.N + (int64_t)cg * CT * 32;
+#pragma unroll
+    for (int ct = 0; ct < CT; ++ct) {
+        const int ncol = (cg * CT + ct) * 32 + l32;
+        const float bv = p.bias ? p.bias[p.wrow[j] + ncol] : 0.f;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) sT[((r & 3) + 8 * (r >> 2) + 4 * h) * TS + l32] = acc[ct][r] * sc[r] + bv;
+        __builtin_amdgcn_wave_barrier();  // DS operations of one wave complete in order
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int row = 8 * q + (lane >> 3), c4 = (lane & 7) * 4;
+            const floatx4 v = *reinterpret_cast<const floatx4*>(sT + row * TS + c4);
+            *reinterpret_cast<floatx4*>(y + (int64_t)row * p.N + ct * 32 + c4) = v;
+        }
+        __builtin_amdgcn_wave_barrier();
+    }
+    if (p.diag & 1) __threadfence();  // diagnostic (SKELDIFF_DIAG): agent-scope release of Y
+}
+
 // Epilogue of the fused to_qkv + Attention kernel (MODE 1), J <= 32, dh = 32, 8 waves, a
 // 32-row tile.  Per 8-row slab: the mixed-in q|k|v (Z = G-hat Y) goes to LDS as [row][node][96],
 // then wave w runs the attention of row 8*slab + w exactly as k_attention<JT> does (same f32 MFMA
@@ -485,6 +663,7 @@ __device__ __forceinline__ void attention_epilogue(const GLArgs& p, floatx16 (&a
 //   (global_load_dwordx4 a chunk ahead, ds_write_b128 after the chunk's MFMAs).
 template <int J, int NW, int RT, int CT, bool RMS, int DBG = 0, int MODE = 0, int XP = 0, int PREC = 0, int STG = 0>
 __global__ __launch_bounds__(NW * 64, 1) void k_gl4(const GLArgs p) {
+    if (p.diag & 8) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // diagnostic (SKELDIFF_DIAG)
     static_assert(MODE == 0 || MODE == 2 || (CT == 3 && RT == 1 && J <= 32 && NW == 8), "attention mode: 32 x (q|k|v)");
     static_assert(MODE < 2 || (RT == 1 && XP == 0 && STG == 0 && DBG == 0), "split-route phase 2: one 32-row tile");
     constexpr int NPW = (J + NW - 1) / NW;  // nodes per wave
@@ -573,6 +752,7 @@ __global__ __launch_bounds__(NW * 64, 1) void k_gl4(const GLArgs p) {
         floatx4 yv[NYL];
         float gv[NGL];
         float f0 = 1.0f, f1 = 0.0f;
+        if (p.diag & 2) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // diagnostic (SKELDIFF_DIAG)
 #pragma unroll
         for (int k = 0; k < NYL; ++k) {
             const int q = tid + k * NTH;
@@ -1162,6 +1342,10 @@ static hipError_t gl4_launch_t(const GLArgs& a, bool rms, hipStream_t s) {
     // reproduced (tools/lds_hazard.py)
     // Split-route phase 2 (MODE 2 / 3) has no weight stages: exact size.
     if (MODE < 2 && STG == 0 && a.gl4_stage != 2) lds = 160 * 1024;
+    // Any allocation above 64 KB (MODE 3's attention slabs: 101 KB at J = 16) holds the whole CU
+    // too: the split route's phase 2 beside other chains' workgroups reproduced the hazard with no
+    // LDS-DMA anywhere (tools/gpu_diag.sh)
+    if (lds > 64 * 1024 && a.gl4_stage != 2) lds = 160 * 1024;
     auto kt = rms ? k_gl4<J, NW, RT, CT, true, DBG, MODE, XP, PREC, STG> : k_gl4<J, NW, RT, CT, false, DBG, MODE, XP, PREC, STG>;
     if (lds > 64 * 1024) {
         hipError_t e = hipFuncSetAttribute((const void*)kt, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
@@ -1200,14 +1384,18 @@ static int64_t g_split_rows = [] {
 }();
 int64_t split_rows_default() { return g_split_rows; }
 
-static bool split_route(const GLArgs& a, bool attn) {
-    if (a.split == 1 || !a.zs || a.prec == 2 || (a.N & 31) || a.J > 32) return false;
+// 0: one-kernel route; 1: split route with the per-wave phase 1 (k_gl4y, small grids); 2: split
+// route with the tiled phase 1 (k_gl4t, full batches).  GLArgs::split: 0 auto, 1 never, 2 always
+// (k_gl4y), 3 always (k_gl4t).
+static int split_route(const GLArgs& a, bool attn) {
+    if (a.split == 1 || !a.zs || a.prec == 2 || (a.N & 31) || a.J > 32) return 0;
     const int64_t tiles = (a.B + 31) / 32;
-    if (tiles * 32 * a.J * (int64_t)a.N > a.zs_cap) return false;
-    if (a.zs == a.out || a.zs == a.x1 || a.zs == a.x2 || a.zs == a.res) return false;
-    if (attn && (a.attn_heads * 96 != a.N)) return false;
-    if (a.split == 2) return true;
-    return a.gl4_cfg == 0 && (a.route_rows > 0 ? a.route_rows : a.B) <= g_split_rows;
+    if (tiles * 32 * a.J * (int64_t)a.N > a.zs_cap) return 0;
+    if (a.zs == a.out || a.zs == a.x1 || a.zs == a.x2 || a.zs == a.res) return 0;
+    if (attn && (a.attn_heads * 96 != a.N)) return 0;
+    if (a.split == 2) return 1;
+    if (a.split == 3) return 2;
+    return (a.gl4_cfg == 0 && (a.route_rows > 0 ? a.route_rows : a.B) <= g_split_rows) ? 1 : 0;
 }
 
 template <bool ROWMAJOR>
@@ -1234,22 +1422,52 @@ hipError_t launch_gemm_split(const GLArgs& a, bool rms, float* z, int64_t z_rs, 
     return launch_gl4y<true>(a, rms, ntc, ntile_r, yo, s);
 }
 
+template <int CT, int NCH>
+static hipError_t launch_gl4t_ct(const GLArgs& a, bool rms, int64_t ntile_r, hipStream_t s) {
+    const int ncg = a.N / (32 * CT);
+    const dim3 grid((unsigned)(((ntile_r + 3) / 4) * a.J * ncg)), block(256);
+    if (a.prec == 1) {
+        if (rms) hipLaunchKernelGGL((k_gl4t<true, 1, CT, NCH>), grid, block, 0, s, a, ncg, ntile_r);
+        else hipLaunchKernelGGL((k_gl4t<false, 1, CT, NCH>), grid, block, 0, s, a, ncg, ntile_r);
+    } else {
+        if (rms) hipLaunchKernelGGL((k_gl4t<true, 0, CT, NCH>), grid, block, 0, s, a, ncg, ntile_r);
+        else hipLaunchKernelGGL((k_gl4t<false, 0, CT, NCH>), grid, block, 0, s, a, ncg, ntile_r);
+    }
+    return hipGetLastError();
+}
+
+// the release Denoiser's shapes: K = 192 (12 chunks), 256 (to_out, 16) or 384 (24), N a multiple
+// of 96 (192 wide layers, 768 to_qkv, 96 final_glin); anything else takes k_gl4y
+static hipError_t launch_gl4t(const GLArgs& a, bool rms, int64_t ntile_r, hipStream_t s) {
+    const int K = a.K1 + a.K2;
+    if (a.N % 192 == 0) {
+        if (K == 192) return launch_gl4t_ct<6, 12>(a, rms, ntile_r, s);
+        if (K == 256) return launch_gl4t_ct<6, 16>(a, rms, ntile_r, s);
+        if (K == 384) return launch_gl4t_ct<6, 24>(a, rms, ntile_r, s);
+    } else if (a.N % 96 == 0) {
+        if (K == 192) return launch_gl4t_ct<3, 12>(a, rms, ntile_r, s);
+        if (K == 384) return launch_gl4t_ct<3, 24>(a, rms, ntile_r, s);
+    }
+    return hipErrorNotSupported;
+}
+
 template <int J>
-static hipError_t gl4_split(const GLArgs& a, bool rms, bool attn, hipStream_t s) {
+static hipError_t gl4_split(const GLArgs& a, bool rms, bool attn, int route, hipStream_t s) {
     const int64_t ntile_r = (a.B + 31) / 32;
     const int ntc = a.N / 32;
     const YOut yo{a.zs, a.N, 32LL * a.N, 32LL * J * a.N};
-    hipError_t e = launch_gl4y<false>(a, rms, ntc, ntile_r, yo, s);
+    hipError_t e = route == 2 ? launch_gl4t(a, rms, ntile_r, s) : hipErrorNotSupported;
+    if (e == hipErrorNotSupported) e = launch_gl4y<false>(a, rms, ntc, ntile_r, yo, s);
     if (e != hipSuccess) return e;
     if (attn) return gl4_launch_t<J, 8, 1, 3, 0, 3, 0, 0, 0>(a, false, s);
     return gl4_launch_t<J, 8, 1, 1, 0, 2, 0, 0, 0>(a, false, s);
 }
 
-static hipError_t gl4_split_dispatch(const GLArgs& a, bool rms, bool attn, hipStream_t s) {
+static hipError_t gl4_split_dispatch(const GLArgs& a, bool rms, bool attn, int route, hipStream_t s) {
     switch (a.J) {
-        case 16: return gl4_split<16>(a, rms, attn, s);
-        case 17: return gl4_split<17>(a, rms, attn, s);
-        case 21: return gl4_split<21>(a, rms, attn, s);
+        case 16: return gl4_split<16>(a, rms, attn, route, s);
+        case 17: return gl4_split<17>(a, rms, attn, route, s);
+        case 21: return gl4_split<21>(a, rms, attn, route, s);
         default: return hipErrorNotSupported;
     }
 }
@@ -1261,7 +1479,8 @@ hipError_t launch_graph_linear_v4(const GLArgs& a, bool rms, hipStream_t s) {
     if ((a.N & 3) || ((uintptr_t)a.out & 15) || ((uintptr_t)a.res & 15) || (a.res && (a.res_rs & 3)) || (a.out_rs & 3))
         return hipErrorNotSupported;
     if (!a.wsp || (a.K1 + a.K2) % 32 || a.K1 % 16 || (a.x1_blk && a.x1_div != 1)) return hipErrorNotSupported;
-    if ((a.J == 16 || a.J == 17 || a.J == 21) && split_route(a, false)) return gl4_split_dispatch(a, rms, false, s);
+    if (a.J == 16 || a.J == 17 || a.J == 21)
+        if (const int route = split_route(a, false)) return gl4_split_dispatch(a, rms, false, route, s);
     const int cfg = a.gl4_cfg ? a.gl4_cfg : a.tile_hint;
     if (a.prec == 2) {  // bf16 mode: row-major operands, the default tiles only
         if (a.x1_blk || a.x2_blk || a.res_blk || a.out_blk) return hipErrorNotSupported;
@@ -1324,7 +1543,8 @@ hipError_t launch_qkv_attention_v4(const GLArgs& a, bool rms, hipStream_t s) {
         return hipErrorNotSupported;
     GLArgs b = a;
     b.attn_order = a.gl4_cfg == 100 ? 1 : 0;
-    if ((a.J == 16 || a.J == 17 || a.J == 21) && a.prec != 2 && split_route(a, true)) return gl4_split_dispatch(b, rms, true, s);
+    if ((a.J == 16 || a.J == 17 || a.J == 21) && a.prec != 2)
+        if (const int route = split_route(a, true)) return gl4_split_dispatch(b, rms, true, route, s);
     // J = 17 / 21: 3 nodes per wave, two 16-node tiles in the softmax
     switch (a.J) {
         case 16:

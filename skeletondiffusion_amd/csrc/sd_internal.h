@@ -67,7 +67,12 @@ struct GLArgs {
     // bf16 storage of operands / result (precision mode 2): the tensor
     // holds bf16 elements at the same element offsets (row-major only)
     int x1_bf16, x2_bf16, res_bf16, out_bf16;
+    // diagnostics only (SKELDIFF_DIAG, read once per process): bit 0 agent-scope release after the
+    // split route's phase 1 stores, bit 1 agent-scope acquire before phase 2's Y loads, bit 3
+    // agent-scope acquire at the start of every v4 / update kernel
+    int diag;
 };
+int diag_flags();  // SKELDIFF_DIAG (sd_plan.hip)
 
 // f16 hi/lo split of a (types, N, K) f32 weight in MFMA B-fragment order (sd_graph_linear_v4.hip)
 struct SplitW {
@@ -99,6 +104,7 @@ struct UpdArgs {
     int64_t B; int J; int D;
     unsigned* dbg;  // SD_DEBUG_LDS builds only
     int x0_bf16, xt_bf16, out_bf16;  // bf16 latents (precision mode 2); out2 / records stay f32
+    int diag;                        // SKELDIFF_DIAG (diagnostics only, as GLArgs::diag)
 };
 
 hipError_t launch_graph_linear(const GLArgs& a, bool rms, hipStream_t s);     // dispatches v1..v5

@@ -526,6 +526,7 @@ hipError_t launch_copy_rows(float* dst, int64_t dst_rs, const float* src, int64_
 
 template <int JM, bool EXACT>
 __global__ __launch_bounds__(256) void k_update(const UpdArgs p) {
+    if (p.diag & 8) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // diagnostic (SKELDIFF_DIAG)
     __shared__ float sC1[JM * JM], sC2[JM * JM], sU[JM * JM], sS[JM];
     const int J = EXACT ? JM : p.J;
     if (!p.iso) {
@@ -623,6 +624,7 @@ __global__ __launch_bounds__(256) void k_update(const UpdArgs p) {
 //   A: item (j, d): x0 (act, clamp), x_t and sigma_j eps_j of one node -> LDS;
 //   B: item (i, d): the C1 / C2 / U sums over j from LDS, in k_update's order and expressions.
 __global__ __launch_bounds__(256) void k_update_row(const UpdArgs p) {
+    if (p.diag & 8) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // diagnostic (SKELDIFF_DIAG)
     extern __shared__ __attribute__((aligned(16))) float sm[];
     const int J = p.J, D = p.D, DP = D >> 1, JD = J * D;
     const int nt = p.iso ? 0 : 3 * J * J + J;

@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cmath>
+#include <cstdlib>
 #include <algorithm>
 #include <cstring>
 #include <map>
@@ -29,6 +30,13 @@ int fail(int code, const std::string& msg) {
 }  // namespace
 
 int sd::set_error(int code, const std::string& msg) { return fail(code, msg); }
+int sd::diag_flags() {
+    static const int v = [] {
+        const char* e = getenv("SKELDIFF_DIAG");
+        return e ? atoi(e) : 0;
+    }();
+    return v;
+}
 
 #ifdef SD_DEBUG_LDS
 unsigned* sd::debug_counters() {
@@ -345,6 +353,7 @@ int run_denoiser(const sd_plan* p, const float* x_t, const float* x_cond, int64_
     const int64_t zs_cap = (rows + 31) / 32 * 32 * p->J * (int64_t)(p->d.use_attention ? 3 * p->hid : p->H);
     auto lay = [B, tile_hint, &w, zs_cap, &bfl, route_rows](sd::GLArgs& g, int in, int res, int out) {
         g.status = ws_status(w);
+        g.diag = sd::diag_flags();
         g.route_rows = route_rows;
         g.zs = w.qkv;
         g.zs_cap = zs_cap;
@@ -483,6 +492,7 @@ int run_update(const sd_plan* p, const float* x0, const float* xt, const float* 
     u.B = rows;
     u.J = p->J;
     u.D = p->D;
+    u.diag = sd::diag_flags();
 #ifdef SD_DEBUG_LDS
     u.dbg = sd::debug_counters();
 #endif
@@ -935,6 +945,10 @@ static int record_loop(const sd_plan* p, const float* x_T, const float* x_cond, 
 // fork chains 1 .. n-1 off s (caller holds cmu, ensure_chains done)
 static int fork_chains(sd_plan* mp, hipStream_t s, int n, hipStream_t* cs) {
     cs[0] = s;
+    if (sd::diag_flags() & 4) {  // diagnostic: every chain on the caller's stream (no concurrency)
+        for (int i = 1; i < n; ++i) cs[i] = s;
+        return SD_OK;
+    }
     if (n > 1) SD_HIP(hipEventRecord(mp->ev_fork, s));
     for (int i = 1; i < n; ++i) {
         SD_HIP(hipStreamWaitEvent(mp->aux[i], mp->ev_fork, 0));
@@ -1157,7 +1171,8 @@ int sd_plan_set_option(sd_plan* p, int32_t option, int64_t value) {
             p->gl4_stage = (int)value;
             return SD_OK;
         case SD_OPT_SPLIT_ROUTE:
-            if (value < 0 || value > 2) return fail(SD_E_INVALID, "split route must be 0 (auto), 1 (never) or 2 (always)");
+            if (value < 0 || value > 3)
+                return fail(SD_E_INVALID, "split route must be 0 (auto), 1 (never), 2 (always) or 3 (always, tiled phase 1)");
             p->split = (int)value;
             return SD_OK;
         default: return fail(SD_E_INVALID, "unknown option " + std::to_string(option));
