@@ -328,9 +328,12 @@ __global__ __launch_bounds__(256) void k_gl4y(const GLArgs p, int ntile_c, int64
 // at CT = 6 vs 2.2 B in the one-kernel k_gl4 32 x 64 tile).  Per accumulator element the MFMA
 // sequence (x_hi W'_hi, x_hi W'_lo, x_lo W'_hi per chunk), RMS sum, scale and bias arithmetic are
 // k_gl4's, so phase 2 (k_gl4 MODE 2 / 3) reproduces the one-kernel route bit for bit.
-template <bool RMS, int PREC, int CT, int NCH, int PF = 4>  // NCH: 16-deep k chunks (K / 16)
-__global__ __launch_bounds__(256, 2) void k_gl4t(const GLArgs p, int ncg, int64_t ntile_r) {
+template <bool RMS, int PREC, int CT, int NCH, bool ROWMAJOR, int PF = 4>  // NCH: 16-deep k chunks (K / 16)
+__global__ __launch_bounds__(256, 2) void k_gl4t(const GLArgs p, int ncg, int64_t ntile_r, const YOut yo) {
     if (p.diag & 8) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // diagnostic (SKELDIFF_DIAG)
+    if ((p.diag & 16) && threadIdx.x == 0 && p.status &&  // diagnostic: do these arguments belong to this grid?
+        (ntile_r != (p.B + 31) / 32 || (int64_t)gridDim.x != ((ntile_r + 3) / 4) * p.J * ncg))
+        atomicOr(p.status, 4u);
     constexpr int TILE_H = PREC ? 512 : 1024;   // halves of one 32-column tile per chunk
     constexpr int PPT = TILE_H / 8;             // 16-B pieces per tile
     constexpr int NP = (CT * PPT + 255) / 256;  // staged pieces per thread
@@ -446,6 +449,7 @@ __global__ __launch_bounds__(256, 2) void k_gl4t(const GLArgs p, int ncg, int64_
             const int c = c0 + i;
             store_w(i & 1);
             __builtin_amdgcn_s_waitcnt(0xC07F);
+            if (p.diag & 512) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // diagnostic: no loads in flight at the barrier
             asm volatile("" ::: "memory");
             __builtin_amdgcn_s_barrier();
             asm volatile("" ::: "memory");
@@ -476,7 +480,7 @@ __global__ __launch_bounds__(256, 2) void k_gl4t(const GLArgs p, int ncg, int64_
     // wave is past its last chunk), stored as 16-B pieces: 4 dwordx4 instead of 16 dword stores
     // per tile.  Launch shapes: N a multiple of 32 CT (launch_gl4t), so every column is real.
     float* sT = reinterpret_cast<float*>(smem_raw) + wave * 32 * TS;
-    float* y = p.zs + ((tr * J + j) * 32) * (int64_t)p.N + (int64_t)cg * CT * 32;
+    float* y = yo.y + tr * yo.y_ts + j * yo.y_js + (int64_t)cg * CT * 32;  // YOut as k_gl4y's
 #pragma unroll
     for (int ct = 0; ct < CT; ++ct) {
         const int ncol = (cg * CT + ct) * 32 + l32;
@@ -488,7 +492,8 @@ __global__ __launch_bounds__(256, 2) void k_gl4t(const GLArgs p, int ncg, int64_
         for (int q = 0; q < 4; ++q) {
             const int row = 8 * q + (lane >> 3), c4 = (lane & 7) * 4;
             const floatx4 v = *reinterpret_cast<const floatx4*>(sT + row * TS + c4);
-            *reinterpret_cast<floatx4*>(y + (int64_t)row * p.N + ct * 32 + c4) = v;
+            if (!ROWMAJOR || row0 + row < p.B)  // row-major z holds rows < B only
+                *reinterpret_cast<floatx4*>(y + (int64_t)row * yo.y_rs + ct * 32 + c4) = v;
         }
         __builtin_amdgcn_wave_barrier();
     }
@@ -691,6 +696,9 @@ __global__ __launch_bounds__(NW * 64, 1) void k_gl4(const GLArgs p) {
     float* sF = sG + J * J;  // FiLM (scale + 1 | shift) for this workgroup's columns
 
     const int ntile_c = ATT ? p.attn_heads : (p.N + COLS - 1) / COLS;
+    if ((p.diag & 16) && tid == 0 && p.status &&  // diagnostic: do these arguments belong to this grid?
+        (int64_t)gridDim.x != ntile_c * ((p.B + 32 * RT - 1) / (32 * RT)) * (MODE == 2 ? 2 : MODE == 3 ? 4 : 1))
+        atomicOr(p.status, 4u);
     const int nwg = gridDim.x, xcd = blockIdx.x & 7, q8 = nwg >> 3, r8 = nwg & 7;
     // XCD-aware order: consecutive L (the column tiles of one row tile) on one XCD, so x is
     // fetched into that XCD's L2 once.  attn_order 1 (fused attention): L = blockIdx, i.e. head
@@ -1346,6 +1354,7 @@ static hipError_t gl4_launch_t(const GLArgs& a, bool rms, hipStream_t s) {
     // too: the split route's phase 2 beside other chains' workgroups reproduced the hazard with no
     // LDS-DMA anywhere (tools/gpu_diag.sh)
     if (lds > 64 * 1024 && a.gl4_stage != 2) lds = 160 * 1024;
+    if (MODE == 2 && (a.diag & 256)) lds = 160 * 1024;  // diagnostic (SKELDIFF_DIAG)
     auto kt = rms ? k_gl4<J, NW, RT, CT, true, DBG, MODE, XP, PREC, STG> : k_gl4<J, NW, RT, CT, false, DBG, MODE, XP, PREC, STG>;
     if (lds > 64 * 1024) {
         hipError_t e = hipFuncSetAttribute((const void*)kt, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
@@ -1412,6 +1421,9 @@ static hipError_t launch_gl4y(const GLArgs& a, bool rms, int ntc, int64_t ntile_
     return hipGetLastError();
 }
 
+template <bool ROWMAJOR>
+static hipError_t launch_gl4t(const GLArgs& a, bool rms, int64_t ntile_r, const YOut& yo, hipStream_t s);
+
 // v5's GEMM phase on split-f16 products (J > 21; sd_graph_linear_v5.hip): z[b, j, n] row-major
 // with row stride z_rs, rows < B only.  hipErrorNotSupported without split weights.
 hipError_t launch_gemm_split(const GLArgs& a, bool rms, float* z, int64_t z_rs, hipStream_t s) {
@@ -1419,34 +1431,50 @@ hipError_t launch_gemm_split(const GLArgs& a, bool rms, float* z, int64_t z_rs, 
     const int64_t ntile_r = (a.B + 31) / 32;
     const int ntc = (a.N + 31) / 32;
     const YOut yo{z, z_rs, a.N, 32 * z_rs};
+    // the tiled phase (128 rows x up to 192 columns of one node per workgroup) where the shape
+    // has one; SKELDIFF_DIAG bit 10 keeps k_gl4y (comparison runs)
+    if (!(a.diag & 1024) && ((uintptr_t)z & 15) == 0 && (z_rs & 3) == 0 && (a.N & 3) == 0) {  // 16-B Y pieces
+        const hipError_t e = launch_gl4t<true>(a, rms, ntile_r, yo, s);
+        if (e != hipErrorNotSupported) return e;
+    }
     return launch_gl4y<true>(a, rms, ntc, ntile_r, yo, s);
 }
 
-template <int CT, int NCH>
-static hipError_t launch_gl4t_ct(const GLArgs& a, bool rms, int64_t ntile_r, hipStream_t s) {
+template <int CT, int NCH, bool ROWMAJOR>
+static hipError_t launch_gl4t_ct(const GLArgs& a, bool rms, int64_t ntile_r, const YOut& yo, hipStream_t s) {
     const int ncg = a.N / (32 * CT);
     const dim3 grid((unsigned)(((ntile_r + 3) / 4) * a.J * ncg)), block(256);
-    if (a.prec == 1) {
-        if (rms) hipLaunchKernelGGL((k_gl4t<true, 1, CT, NCH>), grid, block, 0, s, a, ncg, ntile_r);
-        else hipLaunchKernelGGL((k_gl4t<false, 1, CT, NCH>), grid, block, 0, s, a, ncg, ntile_r);
-    } else {
-        if (rms) hipLaunchKernelGGL((k_gl4t<true, 0, CT, NCH>), grid, block, 0, s, a, ncg, ntile_r);
-        else hipLaunchKernelGGL((k_gl4t<false, 0, CT, NCH>), grid, block, 0, s, a, ncg, ntile_r);
+    auto kt = a.prec == 1 ? (rms ? k_gl4t<true, 1, CT, NCH, ROWMAJOR> : k_gl4t<false, 1, CT, NCH, ROWMAJOR>)
+                          : (rms ? k_gl4t<true, 0, CT, NCH, ROWMAJOR> : k_gl4t<false, 0, CT, NCH, ROWMAJOR>);
+    size_t dyn = 0;
+    // Beside other kernels' workgroups (concurrent row chains) k_gl4t gave wrong, run-to-run
+    // different rows unless its workgroup holds the CU (tools/gpu_diag*.sh): then
+    // it takes the whole LDS (one workgroup per CU).  One stream: two per CU, of this launch only.
+    if (a.concurrent || (a.diag & 128)) {
+        hipFuncAttributes fa;
+        hipError_t e = hipFuncGetAttributes(&fa, (const void*)kt);
+        if (e != hipSuccess) return e;
+        dyn = 160 * 1024 - fa.sharedSizeBytes;
+        if ((e = hipFuncSetAttribute((const void*)kt, hipFuncAttributeMaxDynamicSharedMemorySize, (int)dyn)) != hipSuccess)
+            return e;
     }
+    hipLaunchKernelGGL(kt, grid, block, dyn, s, a, ncg, ntile_r, yo);
     return hipGetLastError();
 }
 
 // the release Denoiser's shapes: K = 192 (12 chunks), 256 (to_out, 16) or 384 (24), N a multiple
-// of 96 (192 wide layers, 768 to_qkv, 96 final_glin); anything else takes k_gl4y
-static hipError_t launch_gl4t(const GLArgs& a, bool rms, int64_t ntile_r, hipStream_t s) {
+// of 96 (192 wide layers, 768 to_qkv, 96 final_glin); hipErrorNotSupported otherwise (k_gl4y)
+template <bool ROWMAJOR>
+static hipError_t launch_gl4t(const GLArgs& a, bool rms, int64_t ntile_r, const YOut& yo, hipStream_t s) {
     const int K = a.K1 + a.K2;
+    if (a.K1 % 16 || (a.x1_div != 1 && a.x1_blk)) return hipErrorNotSupported;
     if (a.N % 192 == 0) {
-        if (K == 192) return launch_gl4t_ct<6, 12>(a, rms, ntile_r, s);
-        if (K == 256) return launch_gl4t_ct<6, 16>(a, rms, ntile_r, s);
-        if (K == 384) return launch_gl4t_ct<6, 24>(a, rms, ntile_r, s);
+        if (K == 192) return launch_gl4t_ct<6, 12, ROWMAJOR>(a, rms, ntile_r, yo, s);
+        if (K == 256) return launch_gl4t_ct<6, 16, ROWMAJOR>(a, rms, ntile_r, yo, s);
+        if (K == 384) return launch_gl4t_ct<6, 24, ROWMAJOR>(a, rms, ntile_r, yo, s);
     } else if (a.N % 96 == 0) {
-        if (K == 192) return launch_gl4t_ct<3, 12>(a, rms, ntile_r, s);
-        if (K == 384) return launch_gl4t_ct<3, 24>(a, rms, ntile_r, s);
+        if (K == 192) return launch_gl4t_ct<3, 12, ROWMAJOR>(a, rms, ntile_r, yo, s);
+        if (K == 384) return launch_gl4t_ct<3, 24, ROWMAJOR>(a, rms, ntile_r, yo, s);
     }
     return hipErrorNotSupported;
 }
@@ -1456,7 +1484,7 @@ static hipError_t gl4_split(const GLArgs& a, bool rms, bool attn, int route, hip
     const int64_t ntile_r = (a.B + 31) / 32;
     const int ntc = a.N / 32;
     const YOut yo{a.zs, a.N, 32LL * a.N, 32LL * J * a.N};
-    hipError_t e = route == 2 ? launch_gl4t(a, rms, ntile_r, s) : hipErrorNotSupported;
+    hipError_t e = route == 2 ? launch_gl4t<false>(a, rms, ntile_r, yo, s) : hipErrorNotSupported;
     if (e == hipErrorNotSupported) e = launch_gl4y<false>(a, rms, ntc, ntile_r, yo, s);
     if (e != hipSuccess) return e;
     if (attn) return gl4_launch_t<J, 8, 1, 3, 0, 3, 0, 0, 0>(a, false, s);

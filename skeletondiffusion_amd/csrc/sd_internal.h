@@ -71,6 +71,7 @@ struct GLArgs {
     // split route's phase 1 stores, bit 1 agent-scope acquire before phase 2's Y loads, bit 3
     // agent-scope acquire at the start of every v4 / update kernel
     int diag;
+    int concurrent;  // other row chains of the call run on other streams (k_gl4t then holds its CU)
 };
 int diag_flags();  // SKELDIFF_DIAG (sd_plan.hip)
 

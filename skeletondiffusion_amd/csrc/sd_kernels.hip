@@ -524,20 +524,32 @@ hipError_t launch_copy_rows(float* dst, int64_t dst_rs, const float* src, int64_
 // wave-uniform broadcasts.  HBM-bound: 4 * J * D * 4 B per row (x0, x_t, eps in; x_{t-1} out).
 // =============================================================================================
 
-template <int JM, bool EXACT>
+template <int JM, bool EXACT, bool GT = false>  // GT: step tables read from global memory (no LDS)
 __global__ __launch_bounds__(256) void k_update(const UpdArgs p) {
     if (p.diag & 8) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // diagnostic (SKELDIFF_DIAG)
-    __shared__ float sC1[JM * JM], sC2[JM * JM], sU[JM * JM], sS[JM];
     const int J = EXACT ? JM : p.J;
-    if (!p.iso) {
-        for (int i = threadIdx.x; i < J * J; i += 256) {
-            sC1[i] = p.C1[i];
-            sC2[i] = p.C2[i];
-            sU[i] = p.U[i];
+    const float *sC1, *sC2, *sU, *sS;
+    if constexpr (GT) {
+        sC1 = p.C1;
+        sC2 = p.C2;
+        sU = p.U;
+        sS = p.sig;
+    } else {
+        __shared__ float tC1[JM * JM], tC2[JM * JM], tU[JM * JM], tS[JM];
+        if (!p.iso) {
+            for (int i = threadIdx.x; i < J * J; i += 256) {
+                tC1[i] = p.C1[i];
+                tC2[i] = p.C2[i];
+                tU[i] = p.U[i];
+            }
+            for (int i = threadIdx.x; i < J; i += 256) tS[i] = p.sig[i];
         }
-        for (int i = threadIdx.x; i < J; i += 256) sS[i] = p.sig[i];
+        __syncthreads();
+        sC1 = tC1;
+        sC2 = tC2;
+        sU = tU;
+        sS = tS;
     }
-    __syncthreads();
     const int D = p.D;
     const int DP = D >> 1;
     const int64_t g = (int64_t)blockIdx.x * 256 + threadIdx.x;
@@ -711,6 +723,17 @@ hipError_t launch_update(const UpdArgs& a, hipStream_t s) {
     }
     const int64_t n = a.B * (a.D / 2);
     const dim3 grid((unsigned)((n + 255) / 256));
+    if (a.J == 16 && (a.diag & 32)) {  // diagnostic (SKELDIFF_DIAG): no LDS at all
+        hipLaunchKernelGGL((k_update<16, true, true>), grid, dim3(256), 0, s, a);
+        return hipGetLastError();
+    }
+    if (a.J == 16 && (a.diag & 64)) {  // diagnostic (SKELDIFF_DIAG): the workgroup holds its CU's LDS
+        hipError_t e = hipFuncSetAttribute((const void*)k_update<16, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                           160 * 1024);
+        if (e != hipSuccess) return e;
+        hipLaunchKernelGGL((k_update<16, true>), grid, dim3(256), 160 * 1024 - 3 * 16 * 16 * 4 - 64, s, a);
+        return hipGetLastError();
+    }
     switch (a.J) {
         case 16: hipLaunchKernelGGL((k_update<16, true>), grid, dim3(256), 0, s, a); break;
         case 17: hipLaunchKernelGGL((k_update<17, true>), grid, dim3(256), 0, s, a); break;

@@ -323,7 +323,7 @@ struct Prof {
 int run_denoiser(const sd_plan* p, const float* x_t, const float* x_cond, int64_t cond_repeat,
                  int t, float* x0_out, int64_t rows, const WS& w, hipStream_t s, Prof* prof = nullptr,
                  int64_t cond_phase = 0, int tile_hint = 0, float* const* trace = nullptr,
-                 int xt_bf16 = 0, int x0_bf16 = 0, int64_t route_rows = 0) {
+                 int xt_bf16 = 0, int x0_bf16 = 0, int64_t route_rows = 0, int concurrent = 0) {
     const int H = p->H;
     // v4 path: every intermediate activation in the row-blocked layout (coalesced x fragments);
     // the denoiser's inputs (x_t, x_cond) and output (x0) stay row-major
@@ -351,9 +351,10 @@ int run_denoiser(const sd_plan* p, const float* x_t, const float* x_cond, int64_
     // v5 scratch (pre-mix activations of layers whose residual aliases their output): the qkv
     // buffer, dead outside the attention block (>= rows * J * H floats)
     const int64_t zs_cap = (rows + 31) / 32 * 32 * p->J * (int64_t)(p->d.use_attention ? 3 * p->hid : p->H);
-    auto lay = [B, tile_hint, &w, zs_cap, &bfl, route_rows](sd::GLArgs& g, int in, int res, int out) {
+    auto lay = [B, tile_hint, &w, zs_cap, &bfl, route_rows, concurrent](sd::GLArgs& g, int in, int res, int out) {
         g.status = ws_status(w);
         g.diag = sd::diag_flags();
+        g.concurrent = concurrent;
         g.route_rows = route_rows;
         g.zs = w.qkv;
         g.zs_cap = zs_cap;
@@ -926,7 +927,7 @@ static int record_loop(const sd_plan* p, const float* x_T, const float* x_cond, 
             // 5 % faster than the single-chain 32 x 96 choice at B = 3200, 3 chains
             const int64_t wg813 = (c.n + 31) / 32 * 2;  // 32 x 96 workgroups of an N = 192 layer
             int rc = run_denoiser(p, c.cur, xc, cond_repeat, t, c.w.x0, c.n, c.w, cs[i], nullptr, r0 % cond_repeat,
-                                  (nch > 1 && wg813 >= 32) ? 812 : 0, nullptr, bf, bf, rows);
+                                  (nch > 1 && wg813 >= 32) ? 812 : 0, nullptr, bf, bf, rows, nch > 1);
             if (rc) return rc;
             float* nxt = (t == 0) ? out + r0 * JD : (((T - 1 - t) & 1) ? c.w.img1 : c.w.img0);
             const float* eps = (!dev_noise && t > 0) ? eps_all + r0 * step_rs + k * JD : nullptr;

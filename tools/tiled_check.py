@@ -30,6 +30,9 @@ for name, opts in RUNS:
     for graph in (False, True):
         eng.sample_loop(rows, x_cond=xc, seed=77, row0=0, graph=graph, out=out, keep_start=False)
         torch.cuda.synchronize()
+        st = eng.status(rows)
+        if st:
+            print(f"{name} graph={graph}: workspace status word {st:#x}")
         res[(name, graph)] = out.clone()
 ref = res[("one-kernel", False)]
 ok = True
