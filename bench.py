@@ -321,7 +321,9 @@ def main():
 
     value = world_rows(world, rows, args.scaling, batch, futures) * args.steps / elapsed
     variant = eng.get_option("kernel_variant")
-    split = variant in (0, 4) and J in (16, 17, 21)
+    # J > 21 (v5): the GEMM phase on the same split-f16 products (k_gl4t), the node mixing (2 J^2 N
+    # of the 2 J K N + 2 J^2 N FLOPs per row) in exact f32 on the VALU
+    split = (variant in (0, 4) and J in (16, 17, 21)) or (variant == 0 and J > 21)
     half = split and eng.precision in ("half", "bf16")
     fused_attn = ms[1] == 0.0 and cnt[1] == 0   # attention ran inside the graph-linear launches
     gl_flops = fl[0] + (fl[1] if fused_attn else 0.0)

@@ -1,5 +1,7 @@
 // v5: StaticGraphLinear (graph_structural.py:30-43) + fused epilogue for LARGE skeletons
-// (J > 21: AMASS-MANO J = 51 with 43 node types, config 3).  Exact f32.
+// (J > 21: AMASS-MANO J = 51 with 43 node types, config 3).  The GEMM phase runs on the v4
+// split-f16 products (k_gl4t, sd_graph_linear_v4.hip: launch_gemm_split) wherever the plan holds
+// split weights; k_gl5_gemm below is the exact-f32 GEMM phase (kernel variant 5, other shapes).
 //
 // The one-kernel generations keep all J nodes of a row tile in one workgroup, so every k chunk
 // stages the weights of every node type: at J = 51 that is 43 types (v3/v4 do not fit the LDS;
@@ -138,9 +140,15 @@ __global__ __launch_bounds__(256) void k_gl5_mix(const GLArgs p, const float* z,
     const int n0 = blockIdx.y * 64;
     float* orow = p.out + b * p.out_rs;
     const float* zrow = z + b * z_rs;
-    for (int e = tid; e < J * kMaxNodes; e += 256) {
-        const int jj = e / kMaxNodes, i = e % kMaxNodes;
-        s_gt[jj][i] = i < J ? p.G[i * J + jj] : 0.f;
+    // G-hat^T staged from coalesced reads of G-hat's rows (reading its columns, one 4-B load per
+    // lane from J different rows, was ~60 % of the kernel at J = 51); the padding nodes are zero
+    for (int e = tid; e < J * J; e += 256) {
+        const int i = e / J, jj = e - i * J;
+        s_gt[jj][i] = p.G[e];
+    }
+    for (int e = tid; e < J * (kMaxNodes - J); e += 256) {
+        const int jj = e / (kMaxNodes - J), i = J + e % (kMaxNodes - J);
+        s_gt[jj][i] = 0.f;
     }
     if (vec && n0 + 64 <= N) {  // 16-B pieces (z, N and z_rs 16-B aligned: checked at launch)
         for (int e = tid; e < J * 16; e += 256) {
@@ -188,7 +196,7 @@ __global__ __launch_bounds__(256) void k_gl5_mix(const GLArgs p, const float* z,
         if (i >= J) break;
         float v = acc[q];
         if (p.film) v = v * fa + fb;
-        if (p.act == 1) v = tanhf(v);
+        if (p.act == 1) v = tanhf(v);  // (the v_exp / v_rcp form measured no faster here: 175 vs 174 us)
         orow[(int64_t)i * N + n] = v + rv[q];
     }
 }

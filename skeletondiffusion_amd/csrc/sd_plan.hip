@@ -868,6 +868,9 @@ static int chain_count(const sd_plan* p, int64_t rows, int64_t cond_repeat, int6
     // rows when two chains' launches shared CUs, and the single chain is as fast
     // there (one 400-row chain 5,565 vs three 5,764 futures/s)
     if (p->split == 2 || (p->split == 0 && rows <= sd::split_rows_default())) n = 1;
+    // v5 (J > 21): its GEMM phase (k_gl4t) holds the CU under concurrent chains,
+    // and one chain measured faster (MANO J = 51: 2,411 vs 2,338 futures/s with three)
+    if (p->J > 21 && p->variant == 0) n = 1;
     return n;
 }
 static int64_t chain_row(int i, int n, int64_t rows, int64_t unit) {

@@ -165,6 +165,29 @@ def test_split_route_bitwise(cfg, batch, kw, cuda):
     assert eng.status(rows) == 0
 
 
+@pytest.mark.parametrize("cfg,batch,T", [("amass16", 64, 4), ("amass21", 8, 10), ("freeman17", 8, 10)])
+def test_tiled_split_route_bitwise(cfg, batch, T, cuda):
+    """SD_OPT_SPLIT_ROUTE = 3 (DESIGN.md §4d''): the tiled GEMM phase k_gl4t (128 rows x 192
+    columns of one node per workgroup) + k_gl4 MODE 2 / 3 is bitwise equal to the one-kernel
+    route, graph and eager, on one row chain and on three (where k_gl4t holds its CU: §4c)."""
+    from bench import build_config
+
+    d, x_cond, rows = build_config(cfg, cuda, T=T, batch=batch)
+    eng = d.engine
+    eng.set_option("row_chains", 1)
+    eng.set_option("split_route", 1)
+    ref = eng.sample_loop(rows, x_cond=x_cond, seed=13, record=(False, True))
+    ref = [ref[0].clone(), ref[4].clone()]
+    eng.set_option("split_route", 3)
+    for chains in (1, 3):
+        eng.set_option("row_chains", chains)
+        for graph in (False, True):
+            got = eng.sample_loop(rows, x_cond=x_cond, seed=13, graph=graph, record=(False, True))
+            torch.cuda.synchronize()
+            assert torch.equal(got[0], ref[0]) and torch.equal(got[4], ref[1]), (cfg, chains, graph)
+    assert eng.status(rows) == 0
+
+
 def test_split_route_shard_equals_full_batch(cuda):
     """A shard small enough for the split route (400 rows at row0 = 1600, as one rank of an
     8-GPU strong-scaling run of config 2) reproduces those rows of the full 3,200-row batch on
