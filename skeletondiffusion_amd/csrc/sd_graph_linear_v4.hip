@@ -1404,7 +1404,13 @@ static int split_route(const GLArgs& a, bool attn) {
     if (attn && (a.attn_heads * 96 != a.N)) return 0;
     if (a.split == 2) return 1;
     if (a.split == 3) return 2;
-    return (a.gl4_cfg == 0 && (a.route_rows > 0 ? a.route_rows : a.B) <= g_split_rows) ? 1 : 0;
+    if (a.gl4_cfg != 0) return 0;
+    const int64_t rows = a.route_rows > 0 ? a.route_rows : a.B;
+    if (rows <= g_split_rows) return 1;
+    // J = 17 / 21 full batches (f32 and half): the tiled route on one chain measured faster than
+    // the one-kernel route on three (FreeMan J = 17 10,954 vs 9,547, AMASS J = 21 8,567 vs 8,371
+    // futures/s at 3,200 rows, T = 100; config 5 half 133,002 vs 92,456; DESIGN.md §4d'')
+    return ((a.J == 17 || a.J == 21) && a.prec <= 1) ? 2 : 0;
 }
 
 template <bool ROWMAJOR>
