@@ -400,8 +400,18 @@ __global__ __launch_bounds__(256, 2) void k_gl4t(const GLArgs p, int ncg, int64_
             src = p.x2_blk ? x2r + ((k0 - p.K1) << 5) : x2r + (k0 - p.K1);
             step4 = p.x2_blk ? 128 : 4;
         }
-        xa[sl] = g4(src);
-        xb[sl] = g4(src + step4);
+        if constexpr (PREC == 2) {
+            // a bf16 operand: its 8 k values (16 B) are the A fragment itself; the same two loads
+            // on both paths (selected addresses, no branch), so the waitcnt pass keeps the ring
+            const bool bsrc = k0 < p.K1 ? p.x1_bf16 : p.x2_bf16;
+            const float* base = k0 < p.K1 ? p.x1 : p.x2;
+            const float* qb = reinterpret_cast<const float*>(reinterpret_cast<const __bf16*>(base) + (src - base));
+            xa[sl] = g4(bsrc ? qb : src);
+            xb[sl] = g4(bsrc ? qb : src + step4);
+        } else {
+            xa[sl] = g4(src);
+            xb[sl] = g4(src + step4);
+        }
     };
     floatx16 acc[CT];
 #pragma unroll
@@ -410,6 +420,29 @@ __global__ __launch_bounds__(256, 2) void k_gl4t(const GLArgs p, int ncg, int64_
         for (int e = 0; e < 16; ++e) acc[ct][e] = 0.f;
     float ss = 0.f, amx = 0.f;
     auto compute = [&](int c, int sl, int ws) {
+        if constexpr (PREC == 2) {  // bf16 mode: one bf16 product per k step (k_gl4 PREC 2's arithmetic)
+            const bool bsrc = (c << 4) < p.K1 ? p.x1_bf16 : p.x2_bf16;  // wave-uniform
+            bf16x8 xb16;
+            floatx8 f;
+            if (bsrc) {
+                xb16 = __builtin_bit_cast(bf16x8, xa[sl]);
+                f = __builtin_convertvector(xb16, floatx8);
+            } else {
+                f = floatx8{xa[sl].x, xa[sl].y, xa[sl].z, xa[sl].w, xb[sl].x, xb[sl].y, xb[sl].z, xb[sl].w};
+                xb16 = __builtin_convertvector(f, bf16x8);
+            }
+            if (RMS && (c << 4) < p.K1) {
+                const floatx8 q = f * f;
+                ss += ((q[0] + q[1]) + (q[2] + q[3])) + ((q[4] + q[5]) + (q[6] + q[7]));
+            }
+            const _Float16* wt = &sW[ws][lane * 8];
+#pragma unroll
+            for (int ct = 0; ct < CT; ++ct) {
+                const bf16x8 wb = *reinterpret_cast<const bf16x8*>(wt + ct * TILE_H);
+                acc[ct] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(xb16, wb, acc[ct], 0, 0, 0);
+            }
+            return;
+        }
         const floatx8 f = {xa[sl].x, xa[sl].y, xa[sl].z, xa[sl].w, xb[sl].x, xb[sl].y, xb[sl].z, xb[sl].w};
         if (RMS && (c << 4) < p.K1) {
             const floatx8 q = f * f;
@@ -449,7 +482,6 @@ __global__ __launch_bounds__(256, 2) void k_gl4t(const GLArgs p, int ncg, int64_
             const int c = c0 + i;
             store_w(i & 1);
             __builtin_amdgcn_s_waitcnt(0xC07F);
-            if (p.diag & 512) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // diagnostic: no loads in flight at the barrier
             asm volatile("" ::: "memory");
             __builtin_amdgcn_s_barrier();
             asm volatile("" ::: "memory");
@@ -1397,20 +1429,22 @@ int64_t split_rows_default() { return g_split_rows; }
 // route with the tiled phase 1 (k_gl4t, full batches).  GLArgs::split: 0 auto, 1 never, 2 always
 // (k_gl4y), 3 always (k_gl4t).
 static int split_route(const GLArgs& a, bool attn) {
-    if (a.split == 1 || !a.zs || a.prec == 2 || (a.N & 31) || a.J > 32) return 0;
+    if (a.split == 1 || !a.zs || (a.N & 31) || a.J > 32) return 0;
+    if (a.prec == 2 && a.split != 3 && !(a.split == 0 && a.J == 17)) return 0;  // bf16: tiled only (J = 17 auto)
     const int64_t tiles = (a.B + 31) / 32;
     if (tiles * 32 * a.J * (int64_t)a.N > a.zs_cap) return 0;
     if (a.zs == a.out || a.zs == a.x1 || a.zs == a.x2 || a.zs == a.res) return 0;
     if (attn && (a.attn_heads * 96 != a.N)) return 0;
-    if (a.split == 2) return 1;
+    if (a.split == 2) return a.prec == 2 ? 0 : 1;
     if (a.split == 3) return 2;
     if (a.gl4_cfg != 0) return 0;
     const int64_t rows = a.route_rows > 0 ? a.route_rows : a.B;
-    if (rows <= g_split_rows) return 1;
-    // J = 17 / 21 full batches (f32 and half): the tiled route on one chain measured faster than
-    // the one-kernel route on three (FreeMan J = 17 10,954 vs 9,547, AMASS J = 21 8,567 vs 8,371
-    // futures/s at 3,200 rows, T = 100; config 5 half 133,002 vs 92,456; DESIGN.md §4d'')
-    return ((a.J == 17 || a.J == 21) && a.prec <= 1) ? 2 : 0;
+    if (rows <= g_split_rows) return a.prec == 2 ? 0 : 1;
+    // J = 17 / 21 full batches (f32 and half; bf16 at J = 17): the tiled route on one chain measured
+    // faster than the one-kernel route on three (FreeMan J = 17 10,954 vs 9,547, AMASS J = 21 8,567
+    // vs 8,371 futures/s at 3,200 rows, T = 100; config 5 half 133,002 vs 92,456, bf16 134,084 vs
+    // 120,821; AMASS J = 21 bf16 9,563 vs 9,946 keeps the one-kernel route; DESIGN.md §4d'')
+    return (a.J == 17 || a.J == 21) ? 2 : 0;
 }
 
 template <bool ROWMAJOR>
@@ -1452,6 +1486,9 @@ static hipError_t launch_gl4t_ct(const GLArgs& a, bool rms, int64_t ntile_r, con
     const dim3 grid((unsigned)(((ntile_r + 3) / 4) * a.J * ncg)), block(256);
     auto kt = a.prec == 1 ? (rms ? k_gl4t<true, 1, CT, NCH, ROWMAJOR> : k_gl4t<false, 1, CT, NCH, ROWMAJOR>)
                           : (rms ? k_gl4t<true, 0, CT, NCH, ROWMAJOR> : k_gl4t<false, 0, CT, NCH, ROWMAJOR>);
+    if constexpr (!ROWMAJOR) {  // bf16 mode (precision 2): the split route's scratch output only
+        if (a.prec == 2) kt = rms ? k_gl4t<true, 2, CT, NCH, false> : k_gl4t<false, 2, CT, NCH, false>;
+    }
     size_t dyn = 0;
     // Beside other kernels' workgroups (concurrent row chains) k_gl4t gave wrong, run-to-run
     // different rows unless its workgroup holds the CU (tools/gpu_diag*.sh): then
@@ -1491,8 +1528,15 @@ static hipError_t gl4_split(const GLArgs& a, bool rms, bool attn, int route, hip
     const int ntc = a.N / 32;
     const YOut yo{a.zs, a.N, 32LL * a.N, 32LL * J * a.N};
     hipError_t e = route == 2 ? launch_gl4t<false>(a, rms, ntile_r, yo, s) : hipErrorNotSupported;
-    if (e == hipErrorNotSupported) e = launch_gl4y<false>(a, rms, ntc, ntile_r, yo, s);
+    if (e == hipErrorNotSupported) {
+        if (a.prec == 2) return hipErrorNotSupported;  // k_gl4y has no bf16 form
+        e = launch_gl4y<false>(a, rms, ntc, ntile_r, yo, s);
+    }
     if (e != hipSuccess) return e;
+    if (a.prec == 2) {  // bf16 residual / output storage (PREC 2 epilogue)
+        if (attn) return gl4_launch_t<J, 8, 1, 3, 0, 3, 0, 2, 0>(a, false, s);
+        return gl4_launch_t<J, 8, 1, 1, 0, 2, 0, 2, 0>(a, false, s);
+    }
     if (attn) return gl4_launch_t<J, 8, 1, 3, 0, 3, 0, 0, 0>(a, false, s);
     return gl4_launch_t<J, 8, 1, 1, 0, 2, 0, 0, 0>(a, false, s);
 }
@@ -1514,7 +1558,10 @@ hipError_t launch_graph_linear_v4(const GLArgs& a, bool rms, hipStream_t s) {
         return hipErrorNotSupported;
     if (!a.wsp || (a.K1 + a.K2) % 32 || a.K1 % 16 || (a.x1_blk && a.x1_div != 1)) return hipErrorNotSupported;
     if (a.J == 16 || a.J == 17 || a.J == 21)
-        if (const int route = split_route(a, false)) return gl4_split_dispatch(a, rms, false, route, s);
+        if (const int route = split_route(a, false)) {
+            const hipError_t e = gl4_split_dispatch(a, rms, false, route, s);
+            if (e != hipErrorNotSupported) return e;  // else: nothing launched, the one-kernel route
+        }
     const int cfg = a.gl4_cfg ? a.gl4_cfg : a.tile_hint;
     if (a.prec == 2) {  // bf16 mode: row-major operands, the default tiles only
         if (a.x1_blk || a.x2_blk || a.res_blk || a.out_blk) return hipErrorNotSupported;
@@ -1577,8 +1624,11 @@ hipError_t launch_qkv_attention_v4(const GLArgs& a, bool rms, hipStream_t s) {
         return hipErrorNotSupported;
     GLArgs b = a;
     b.attn_order = a.gl4_cfg == 100 ? 1 : 0;
-    if ((a.J == 16 || a.J == 17 || a.J == 21) && a.prec != 2)
-        if (const int route = split_route(a, true)) return gl4_split_dispatch(b, rms, true, route, s);
+    if (a.J == 16 || a.J == 17 || a.J == 21)
+        if (const int route = split_route(a, true)) {
+            const hipError_t e = gl4_split_dispatch(b, rms, true, route, s);
+            if (e != hipErrorNotSupported) return e;
+        }
     // J = 17 / 21: 3 nodes per wave, two 16-node tiles in the softmax
     switch (a.J) {
         case 16:

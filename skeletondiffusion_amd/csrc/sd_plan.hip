@@ -871,10 +871,10 @@ static int chain_count(const sd_plan* p, int64_t rows, int64_t cond_repeat, int6
     // v5 (J > 21): its GEMM phase (k_gl4t) holds the CU under concurrent chains,
     // and one chain measured faster (MANO J = 51: 2,411 vs 2,338 futures/s with three)
     if (p->J > 21 && p->variant == 0) n = 1;
-    // J = 17 / 21, f32 or half, default options: the tiled split route, on one chain
+    // J = 17 / 21 (bf16: J = 17), default options: the tiled split route, on one chain
     // (sd_graph_linear_v4.hip split_route; its GEMM phase would hold whole CUs beside other chains)
-    if (p->split == 0 && p->gl4_cfg == 0 && (p->variant == 0 || p->variant == 4) && (p->J == 17 || p->J == 21) &&
-        p->prec <= 1)
+    if (p->split == 0 && p->gl4_cfg == 0 && (p->variant == 0 || p->variant == 4) &&
+        (p->J == 17 || (p->J == 21 && p->prec != 2)))
         n = 1;
     return n;
 }

@@ -165,8 +165,10 @@ def test_split_route_bitwise(cfg, batch, kw, cuda):
     assert eng.status(rows) == 0
 
 
-@pytest.mark.parametrize("cfg,batch,T", [("amass16", 64, 4), ("amass21", 8, 10), ("freeman17", 8, 10)])
-def test_tiled_split_route_bitwise(cfg, batch, T, cuda):
+@pytest.mark.parametrize("cfg,batch,T,prec", [("amass16", 64, 4, "f32"), ("amass21", 8, 10, "f32"),
+                                               ("freeman17", 8, 10, "f32"), ("freeman17", 16, 10, "half"),
+                                               ("freeman17", 16, 10, "bf16"), ("amass21", 16, 10, "bf16")])
+def test_tiled_split_route_bitwise(cfg, batch, T, prec, cuda):
     """SD_OPT_SPLIT_ROUTE = 3 (DESIGN.md §4d''): the tiled GEMM phase k_gl4t (128 rows x 192
     columns of one node per workgroup) + k_gl4 MODE 2 / 3 is bitwise equal to the one-kernel
     route, graph and eager, on one row chain and on three (where k_gl4t holds its CU: §4c)."""
@@ -174,6 +176,7 @@ def test_tiled_split_route_bitwise(cfg, batch, T, cuda):
 
     d, x_cond, rows = build_config(cfg, cuda, T=T, batch=batch)
     eng = d.engine
+    eng.set_precision(prec)
     eng.set_option("row_chains", 1)
     eng.set_option("split_route", 1)
     ref = eng.sample_loop(rows, x_cond=x_cond, seed=13, record=(False, True))
