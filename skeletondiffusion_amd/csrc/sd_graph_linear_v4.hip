@@ -550,7 +550,10 @@ __device__ __forceinline__ void attention_epilogue(const GLArgs& p, floatx16 (&a
     const int l32 = lane & 31, h = lane >> 5, lr = lane & 15, lg = lane >> 4;
     const int hid = p.attn_heads * 32;
     float* sY = smem;
-    float* sZ = smem + J * YS8;
+    // FROM_YS (MODE 3): Z overwrites the Y slab (mixed into registers first, one barrier between),
+    // so the workgroup needs max(Y, Z) instead of Y + Z: 52 KB at J = 16, 54 KB at J = 17 -- under
+    // 64 KB, two workgroups per CU instead of one holding the whole CU
+    float* sZ = FROM_YS ? smem : smem + J * YS8;
     float ga[JT][KS];  // G-hat^T[k = j = 4s + lg][col = i = 16 it + lr]
 #pragma unroll
     for (int it = 0; it < JT; ++it)
@@ -576,6 +579,7 @@ __device__ __forceinline__ void attention_epilogue(const GLArgs& p, floatx16 (&a
             __syncthreads();
         }
         // node mixing: 48 blocks of 16 (row, column) positions, 6 per wave
+        floatx4 zk[FROM_YS ? 48 / NW : 1][JT];  // FROM_YS: all of this wave's Z before the overwrite
 #pragma unroll
         for (int k = 0; k < 48 / NW; ++k) {
             const int rc0 = (wave + NW * k) * 16;
@@ -592,7 +596,20 @@ __device__ __forceinline__ void attention_epilogue(const GLArgs& p, floatx16 (&a
 #pragma unroll
                 for (int s = 0; s < KS; ++s) z = __builtin_amdgcn_mfma_f32_16x16x4f32(ya[s], ga[it][s], z, 0, 0, 0);
                 const int i = 16 * it + lr;
-                if (i < J) *reinterpret_cast<floatx4*>(sZ + r * ZR + i * ZN + c) = z;
+                if constexpr (FROM_YS) zk[k][it] = z;
+                else if (i < J) *reinterpret_cast<floatx4*>(sZ + r * ZR + i * ZN + c) = z;
+            }
+        }
+        if constexpr (FROM_YS) {
+            __syncthreads();  // every wave's Y reads done: Z may overwrite the slab
+#pragma unroll
+            for (int k = 0; k < 48 / NW; ++k) {
+                const int rc = (wave + NW * k) * 16 + 4 * lg, r = rc / COLS, c = rc - r * COLS;
+#pragma unroll
+                for (int it = 0; it < JT; ++it) {
+                    const int i = 16 * it + lr;
+                    if (i < J) *reinterpret_cast<floatx4*>(sZ + r * ZR + i * ZN + c) = zk[k][it];
+                }
             }
         }
         __syncthreads();
@@ -720,7 +737,8 @@ __global__ __launch_bounds__(NW * 64, 1) void k_gl4(const GLArgs p) {
     const int stage_h = MODE >= 2 ? 0 : p.ntypes * CT * TILE_H;  // halves per weight stage
     const int wfl = stage_h;                   // two stages of halves = stage_h floats
     constexpr bool ATT = MODE == 1 || MODE == 3;
-    const int yfl = ATT ? J * (8 * COLS + 16) + 8 * J * 100 : J * YS;  // Y slab (+ Z rows)
+    // Y slab (+ Z rows; MODE 3: Z overwrites Y, attention_epilogue<…, FROM_YS>)
+    const int yfl = MODE == 3 ? max(J * (8 * COLS + 16), 8 * J * 100) : ATT ? J * (8 * COLS + 16) + 8 * J * 100 : J * YS;
     _Float16* sW0 = reinterpret_cast<_Float16*>(smem);
     _Float16* sW1 = sW0 + stage_h;
     float* sY = smem;  // aliases the weight stages after the K loop
@@ -1368,7 +1386,9 @@ static hipError_t gl4_launch_t(const GLArgs& a, bool rms, hipStream_t s) {
     const int64_t ntile_r = (a.B + 32 * RT - 1) / (32 * RT);
     const dim3 grid((unsigned)(ntile_c * ntile_r * (MODE == 2 ? 2 : MODE == 3 ? 4 : 1)));
     const size_t wfl = MODE >= 2 ? 0 : (size_t)a.ntypes * CT * (PREC ? 512 : 1024);  // two stages of halves, in floats
-    const size_t yfl = ATT ? (size_t)J * (8 * COLS + 16) + 8 * J * 100 : (size_t)J * (16 * (COLS + 4) + 16);
+    const size_t yfl = MODE == 3 ? std::max((size_t)J * (8 * COLS + 16), (size_t)8 * J * 100)
+                       : ATT     ? (size_t)J * (8 * COLS + 16) + 8 * J * 100
+                                 : (size_t)J * (16 * (COLS + 4) + 16);
     size_t lds = ((wfl > yfl ? wfl : yfl) + (size_t)J * J + 2 * COLS) * sizeof(float);
     if (lds > 160 * 1024) return hipErrorNotSupported;
     // LDS-DMA staging (STG 0): the workgroup takes its CU's whole LDS, so no other kernel's
