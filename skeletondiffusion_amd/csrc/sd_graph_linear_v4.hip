@@ -1464,6 +1464,10 @@ static int split_route(const GLArgs& a, bool attn) {
     // faster than the one-kernel route on three (FreeMan J = 17 10,954 vs 9,547, AMASS J = 21 8,567
     // vs 8,371 futures/s at 3,200 rows, T = 100; config 5 half 133,002 vs 92,456, bf16 134,084 vs
     // 120,821; AMASS J = 21 bf16 9,563 vs 9,946 keeps the one-kernel route; DESIGN.md §4d'')
+    // J = 16 (f32): the tiled route (one chain) at 3,200 rows and up measured 15,135 / 15,195 vs
+    // 14,947 / 14,917 futures/s for the one-kernel route on three chains (config 2); below that, and
+    // in half / bf16 mode, the one-kernel tiles stay (1,600 rows: 10.9k vs 12.5k)
+    if (a.J == 16) return (a.prec == 0 && rows >= 3200) ? 2 : 0;
     return (a.J == 17 || a.J == 21) ? 2 : 0;
 }
 

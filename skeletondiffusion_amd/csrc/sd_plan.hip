@@ -874,7 +874,7 @@ static int chain_count(const sd_plan* p, int64_t rows, int64_t cond_repeat, int6
     // J = 17 / 21 (bf16: J = 17), default options: the tiled split route, on one chain
     // (sd_graph_linear_v4.hip split_route; its GEMM phase would hold whole CUs beside other chains)
     if (p->split == 0 && p->gl4_cfg == 0 && (p->variant == 0 || p->variant == 4) &&
-        (p->J == 17 || (p->J == 21 && p->prec != 2)))
+        (p->J == 17 || (p->J == 21 && p->prec != 2) || (p->J == 16 && p->prec == 0 && rows >= 3200)))
         n = 1;
     return n;
 }
