@@ -34,7 +34,13 @@ for r in trace:
     if "k_gl2" not in n and "k_graph_linear" not in n and "k_gl3" not in n and "k_gl4" not in n:
         continue
     wgs = int(r.get("Grid_Size") or r["Grid_Size_X"]) // 256
-    if "k_gl4" in n:  # <J, NW, RT, CT, RMS, DBG, MODE>: tile 32 RT rows x 32 CT columns, NW * 64 threads
+    if "k_gl4t" in n or "k_gl4y" in n:  # split-route phase 1: N from its template / not recoverable
+        targs = [t.strip() for t in n.split("<")[1].split(">")[0].split(",")]
+        if "k_gl4y" in n:
+            nt, NT = 0, 0
+        else:  # <RMS, PREC, CT, NCH, ROWMAJOR, PF>: 4 row tiles x CT column tiles of one node
+            nt, NT = wgs // ((((rows_b + 31) // 32 + 3) // 4) * J), 32 * int(targs[2])
+    elif "k_gl4" in n:  # <J, NW, RT, CT, RMS, DBG, MODE>: tile 32 RT rows x 32 CT columns, NW * 64 threads
         targs = [t.strip() for t in n.split("<")[1].split(">")[0].split(",")]
         nw, rt, ctl = int(targs[1]), int(targs[2]), int(targs[3])
         wgs = int(r.get("Grid_Size") or r["Grid_Size_X"]) // (nw * 64)
@@ -87,10 +93,18 @@ if traffic:
             continue
         for r in csv.DictReader(open(path)):
             n = r["Kernel_Name"]
-            if "k_gl4" not in n:
+            if "k_gl4" not in n or "k_gl4y" in n:
                 continue
             targs = [t.strip() for t in n.split("<")[1].split(">")[0].split(",")]
+            if "k_gl4t" in n:  # tiled split route: one k_gl4t dispatch per graph-linear layer
+                full["split route (k_gl4t + k_gl4 MODE 2 / 3)"][col] += float(r["Counter_Value"])
+                if col == 0:
+                    full["split route (k_gl4t + k_gl4 MODE 2 / 3)"][2] += 1
+                continue
             nw, rt, mode = int(targs[1]), int(targs[2]), int(targs[6])
+            if mode >= 2:  # the split route's phase 2: bytes of the layer its k_gl4t dispatch counted
+                full["split route (k_gl4t + k_gl4 MODE 2 / 3)"][col] += float(r["Counter_Value"])
+                continue
             wgs = int(r["Grid_Size"]) // (nw * 64)
             ntile_r = (rows_b + 32 * rt - 1) // (32 * rt)
             if wgs < ntile_r or wgs % ntile_r:
