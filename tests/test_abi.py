@@ -70,3 +70,29 @@ def test_plan_registry_uses_reference_state_dict_keys():
         assert lib.sd_plan_kernels_per_step(h) == 1 + 8 * 2 + 7 * 3 + 3 + 1 + 1
     finally:
         lib.sd_plan_destroy(h)
+
+
+def test_plan_options_validated_on_host():
+    """sd_plan_set_option / sd_plan_get_option are host-side plan state (no device call): every
+    SD_OPT_* range is checked, including the split route's tiled value 3 (DESIGN.md §4d'')."""
+    lib = _lib.lib()
+    d = _lib.SDPlanDesc(num_nodes=16, latent_dim=96, cond_dim=96, out_dim=96, depth=1, attn_heads=8,
+                        attn_dim_head=32, use_attention=1, self_condition=0, learn_influence=1,
+                        num_node_types=10, timesteps=10, isotropic=0, activation=0, sinusoidal_theta=10000.0)
+    arr = (ctypes.c_int64 * 16)(0, 1, 2, 0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 7, 8, 9)
+    d.node_types = ctypes.cast(arr, ctypes.POINTER(ctypes.c_int64))
+    h = ctypes.c_void_p()
+    assert lib.sd_plan_create(ctypes.byref(h), ctypes.byref(d)) == 0, lib.sd_last_error()
+    try:
+        v = ctypes.c_int64()
+        for value in (0, 1, 2, 3):
+            assert lib.sd_plan_set_option(h, _lib.SD_OPT_SPLIT_ROUTE, value) == 0
+            assert lib.sd_plan_get_option(h, _lib.SD_OPT_SPLIT_ROUTE, ctypes.byref(v)) == 0 and v.value == value
+        assert lib.sd_plan_set_option(h, _lib.SD_OPT_SPLIT_ROUTE, 4) == -1
+        assert b"split route" in lib.sd_last_error()
+        assert lib.sd_plan_set_option(h, _lib.SD_OPT_ROW_CHAINS, 0) == -1
+        assert lib.sd_plan_set_option(h, _lib.SD_OPT_ROW_CHAINS, 8) == 0
+        assert lib.sd_plan_set_option(h, _lib.SD_OPT_GL4_STAGING, 3) == -1
+        assert lib.sd_plan_set_option(h, 99, 0) == -1
+    finally:
+        lib.sd_plan_destroy(h)
