@@ -348,10 +348,22 @@ __global__ __launch_bounds__(256, 2) void k_gl4t(const GLArgs p, int ncg, int64_
     // read the same x -- on one XCD (blocks b, b + 8, ... share one), so x reaches that L2 once
     const int nwg = gridDim.x, xcd = blockIdx.x & 7, q8 = nwg >> 3, r8 = nwg & 7;
     const int64_t u = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (blockIdx.x >> 3);
+    // node-major order: column group fastest (the ncg workgroups sharing one x tile), then row
+    // groups, then nodes, so an XCD's contiguous share of u holds one or two nodes' weights
+    // (N = 768: 5.9 MB of split weights for all 10 types did not fit a 4 MB L2 when every XCD
+    // walked every node: 196 MB fetched per launch for ~45 MB of operands)
     const int cg = (int)(u % ncg);
-    const int64_t rj = u / ncg;
-    const int j = (int)(rj % J);
-    const int64_t tr = (rj / J) * 4 + wave;
+    const int64_t nrg = (ntile_r + 3) / 4;
+    int j;
+    int64_t rgi;
+    if (p.diag & 4096) {  // diagnostic (SKELDIFF_DIAG): the previous row-group-major order
+        j = (int)((u / ncg) % J);
+        rgi = (u / ncg) / J;
+    } else {
+        j = (int)((u / ncg) / nrg);
+        rgi = (u / ncg) % nrg;
+    }
+    const int64_t tr = rgi * 4 + wave;
     const bool live = tr < ntile_r;  // wave-uniform; a dead wave still stages weights and joins barriers
     const int64_t row0 = (live ? tr : 0) * 32;
     constexpr int nchunk = NCH;
