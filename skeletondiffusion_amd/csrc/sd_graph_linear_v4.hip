@@ -1414,10 +1414,10 @@ static hipError_t gl4_launch_t(const GLArgs& a, bool rms, hipStream_t s) {
     // reproduced (tools/lds_hazard.py)
     // Split-route phase 2 (MODE 2 / 3) has no weight stages: exact size.
     if (MODE < 2 && STG == 0 && a.gl4_stage != 2) lds = 160 * 1024;
-    // Any allocation above 64 KB (MODE 3's attention slabs: 101 KB at J = 16) holds the whole CU
-    // too: the split route's phase 2 beside other chains' workgroups reproduced the hazard with no
-    // LDS-DMA anywhere (tools/gpu_diag.sh)
-    if (lds > 64 * 1024 && a.gl4_stage != 2) lds = 160 * 1024;
+    // Any allocation above 64 KB beside other row chains holds the whole CU too.  Alone on the GPU
+    // (one chain) the split route's phase 2 shares CUs only with workgroups of its own launch, which
+    // every measurement found exact: MODE 3 at J = 21 (70 KB) then runs two per CU.
+    if (lds > 64 * 1024 && a.gl4_stage != 2 && (MODE < 2 || a.concurrent)) lds = 160 * 1024;
     if (MODE == 2 && (a.diag & 256)) lds = 160 * 1024;  // diagnostic (SKELDIFF_DIAG)
     auto kt = rms ? k_gl4<J, NW, RT, CT, true, DBG, MODE, XP, PREC, STG> : k_gl4<J, NW, RT, CT, false, DBG, MODE, XP, PREC, STG>;
     if (lds > 64 * 1024) {
