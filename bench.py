@@ -324,6 +324,19 @@ def main():
     # J > 21 (v5): the GEMM phase on the same split-f16 products (k_gl4t), the node mixing (2 J^2 N
     # of the 2 J K N + 2 J^2 N FLOPs per row) in exact f32 on the VALU
     split = (variant in (0, 4) and J in (16, 17, 21)) or (variant == 0 and J > 21)
+    # the tiled split route (sd_graph_linear_v4.hip split_route: auto at J = 17 / 21, and J = 16 f32
+    # from 3,200 rows; bf16 at J = 17 only; or forced by split_route = 3)
+    sr = eng.get_option("split_route")
+    tiled = variant in (0, 4) and J in (16, 17, 21) and (
+        sr == 3 or (sr == 0 and eng.get_option("gl4_tile") == 0 and rows > 640 and (
+            J == 17 or (J == 21 and eng.precision != "bf16") or (J == 16 and eng.precision == "f32" and rows >= 3200))))
+    row_chains = min(eng.get_option("row_chains"), max(1, rows // 32))
+    small = split and J <= 21 and eng.precision != "bf16" and (sr == 2 or (sr == 0 and rows <= 640))
+    route = ("tiled split (k_gl4t + k_gl4 MODE 2/3)" if tiled else
+             "small-batch split (k_gl4y + k_gl4 MODE 2/3)" if small else
+             "one-kernel (k_gl4)" if split and J <= 21 else "v5 (k_gl4t + k_gl5_mix)" if split else "exact f32")
+    if small or (J > 21 and variant == 0):  # one chain on these routes (sd_plan.hip chain_count)
+        row_chains = 1
     half = split and eng.precision in ("half", "bf16")
     fused_attn = ms[1] == 0.0 and cnt[1] == 0   # attention ran inside the graph-linear launches
     gl_flops = fl[0] + (fl[1] if fused_attn else 0.0)
@@ -368,12 +381,18 @@ def main():
                    "sequences_total": world_rows(world, rows, args.scaling, batch, futures) // futures,
                    "futures": futures, "rows_per_gpu": rows, "latent_dim": D, "hipgraph": graph,
                    "parallelism": f"dp{world} (sequence-sharded, no data-path collective)",
-                   "row_chains": min(eng.get_option("row_chains"), max(1, rows // 32)),
+                   "row_chains": 1 if tiled and sr == 0 else row_chains, "route": route,
                    "kernel_variant": variant},
         "roofline": {
             "bound": "mfma",
-            "kernel": ("k_gl4 graph-linear (3xf16 split MFMA, fused bias/RMS/G-hat/FiLM/tanh/residual; "
-                       "to_qkv launches fused with attention)") if split else
+            "kernel": ("tiled split route: k_gl4t GEMM phase (3xf16 split MFMA, 128 rows x 192 columns of one "
+                       "node per workgroup, pre-mix Y to HBM) + k_gl4 MODE 2 / 3 phase (G-hat mixing, "
+                       "FiLM/tanh/residual or attention)") if tiled else
+                      ("small-batch split route: k_gl4y GEMM phase (one wave per 32-row tile, node, 32 "
+                       "columns) + k_gl4 MODE 2 / 3 phase") if small else
+                      ("k_gl4 graph-linear (3xf16 split MFMA, fused bias/RMS/G-hat/FiLM/tanh/residual; "
+                       "to_qkv launches fused with attention)") if split and J <= 21 else
+                      ("v5: k_gl4t split-f16 GEMM phase + k_gl5_mix mixing pass") if split else
                       "k_gl3/k_gl2/k_gl5 graph-linear (exact f32 MFMA, fused epilogue)",
             "achieved": timed_tflops, "peak": peak, "unit": "TFLOP/s", "frac": timed_tflops / peak,
             "measured_on": ("the timed region: graph-linear + attention algorithmic FLOPs of T denoise steps "
@@ -390,9 +409,10 @@ def main():
                 "avg_launch_ms": ms[0] / max(cnt[0], 1),
                 "kernel_ms_per_bench_step": ms[0] * T,
                 "measured_on": ("one denoise step at the full batch on ONE stream (sd_profile_step: HIP events "
-                                "around each launch, kernels alone on the GPU, 32x96 tiles) -- the view "
-                                "rocprofv3 --kernel-trace gives; the timed region overlaps 3 row chains of "
-                                "32x64-tile launches, so its step is shorter than this kernel sum")},
+                                "around each launch (a split-route layer = its two kernels), kernels alone on the "
+                                "GPU) -- the view rocprofv3 --kernel-trace gives" +
+                                ("" if tiled or row_chains == 1 else
+                                 "; the timed region overlaps row chains, so its step is shorter than this kernel sum"))},
             "hbm_view": {"achieved": gl_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": gl_gbs / HBM_PEAK_GBS,
                          "algorithmic_bytes_per_launch": gl_bytes / max(cnt[0], 1)},
         },
