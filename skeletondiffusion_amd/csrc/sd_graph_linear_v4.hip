@@ -339,7 +339,11 @@ __global__ __launch_bounds__(256, 2) void k_gl4t(const GLArgs p, int ncg, int64_
     constexpr int NP = (CT * PPT + 255) / 256;  // staged pieces per thread
     constexpr int TS = 36;                      // floats per row of a wave's 32 x 32 output transpose
     constexpr int SB = 2 * CT * TILE_H * 2 > 4 * 32 * TS * 4 ? 2 * CT * TILE_H * 2 : 4 * 32 * TS * 4;
+#ifdef SD_DIAG_GL4T_DYNLDS  // diagnostic build: the same bytes as dynamic LDS
+    extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+#else
     __shared__ __attribute__((aligned(16))) char smem_raw[SB];  // weight stages, then the transposes
+#endif
     _Float16(*sW)[CT * TILE_H] = reinterpret_cast<_Float16(*)[CT * TILE_H]>(smem_raw);
     const int tid = threadIdx.x, lane = tid & 63, l32 = lane & 31, h = lane >> 5;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -493,10 +497,14 @@ __global__ __launch_bounds__(256, 2) void k_gl4t(const GLArgs p, int ncg, int64_
         for (int i = 0; i < PF; ++i) {
             const int c = c0 + i;
             store_w(i & 1);
+#ifdef SD_DIAG_GL4T_SYNCTHREADS  // diagnostic build: a full __syncthreads()
+            __syncthreads();
+#else
             __builtin_amdgcn_s_waitcnt(0xC07F);
             asm volatile("" ::: "memory");
             __builtin_amdgcn_s_barrier();
             asm volatile("" ::: "memory");
+#endif
             // unconditional loads (past the end: a clamped, unused chunk): a branch around them
             // made the waitcnt pass merge both paths and drain the x ring every chunk
             load_w(min(c + 1, nchunk - 1));
@@ -1529,7 +1537,14 @@ static hipError_t launch_gl4t_ct(const GLArgs& a, bool rms, int64_t ntile_r, con
     // Beside other kernels' workgroups (concurrent row chains) k_gl4t gave wrong, run-to-run
     // different rows unless its workgroup holds the CU (tools/gpu_diag*.sh): then
     // it takes the whole LDS (one workgroup per CU).  One stream: two per CU, of this launch only.
+#ifdef SD_DIAG_GL4T_DYNLDS
+    dyn = 2 * CT * 1024 * 2 > 4 * 32 * 36 * 4 ? 2 * CT * 1024 * 2 : 4 * 32 * 36 * 4;  // k_gl4t's SB
+#endif
+#ifdef SD_DIAG_GL4T_SHARE  // diagnostic build: k_gl4t shares CUs under row chains
+    if (a.diag & 128) {
+#else
     if (a.concurrent || (a.diag & 128)) {
+#endif
         hipFuncAttributes fa;
         hipError_t e = hipFuncGetAttributes(&fa, (const void*)kt);
         if (e != hipSuccess) return e;
