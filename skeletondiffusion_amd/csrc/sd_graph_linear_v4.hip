@@ -215,6 +215,7 @@ struct YOut {
 
 template <bool RMS, int PREC, bool ROWMAJOR, int PF = 8>  // PF: chunks in flight
 __global__ __launch_bounds__(256) void k_gl4y(const GLArgs p, int ntile_c, int64_t ntile_r, const YOut yo) {
+    if ((p.diag & kDiagArgsHash) && threadIdx.x == 0 && p.status && !kernel_args_intact()) atomicOr(p.status, 0x800u);
     const int lane = threadIdx.x & 63, l32 = lane & 31, h = lane >> 5;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int64_t u = (int64_t)blockIdx.x * 4 + wave;
@@ -334,6 +335,8 @@ __global__ __launch_bounds__(256, 2) void k_gl4t(const GLArgs p, int ncg, int64_
     if ((p.diag & 16) && threadIdx.x == 0 && p.status &&  // diagnostic: do these arguments belong to this grid?
         (ntile_r != (p.B + 31) / 32 || (int64_t)gridDim.x != ((ntile_r + 3) / 4) * p.J * ncg))
         atomicOr(p.status, 4u);
+    if ((p.diag & kDiagArgsHash) && threadIdx.x == 0 && p.status && !kernel_args_intact()) atomicOr(p.status, 0x100u);
+    const uint64_t dt0 = (p.diag & kDiagSelfCheck) ? __builtin_amdgcn_s_memrealtime() : 0;
     constexpr int TILE_H = PREC ? 512 : 1024;   // halves of one 32-column tile per chunk
     constexpr int PPT = TILE_H / 8;             // 16-B pieces per tile
     constexpr int NP = (CT * PPT + 255) / 256;  // staged pieces per thread
@@ -515,7 +518,7 @@ __global__ __launch_bounds__(256, 2) void k_gl4t(const GLArgs p, int ncg, int64_
         }
     }
     __syncthreads();  // every wave past its last chunk: the stages become the output transposes
-    if (!live) return;
+    if (!live) return;  // (no stores)
     if (p.status && __builtin_amdgcn_ballot_w64(amx >= 65504.0f) != 0 && lane == 0) atomicOr(p.status, 1u);
     float sc[16];
 #pragma unroll
@@ -549,6 +552,9 @@ __global__ __launch_bounds__(256, 2) void k_gl4t(const GLArgs p, int ncg, int64_
         }
         __builtin_amdgcn_wave_barrier();
     }
+    if ((p.diag & kDiagArgsHash) && tid == 0 && p.status && !kernel_args_intact()) atomicOr(p.status, 0x200u);
+    if ((p.diag & kDiagSelfCheck) && tid == 0 && p.dbg) diag_wg_log(p.dbg, 1, dt0);
+    if (p.diag & kDiagRelease) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
     if (p.diag & 1) __threadfence();  // diagnostic (SKELDIFF_DIAG): agent-scope release of Y
 }
 
@@ -738,6 +744,8 @@ __device__ __forceinline__ void attention_epilogue(const GLArgs& p, floatx16 (&a
 template <int J, int NW, int RT, int CT, bool RMS, int DBG = 0, int MODE = 0, int XP = 0, int PREC = 0, int STG = 0>
 __global__ __launch_bounds__(NW * 64, 1) void k_gl4(const GLArgs p) {
     if (p.diag & 8) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // diagnostic (SKELDIFF_DIAG)
+    if ((p.diag & kDiagArgsHash) && threadIdx.x == 0 && p.status && !kernel_args_intact()) atomicOr(p.status, 0x400u);
+    const uint64_t dt0 = (p.diag & kDiagSelfCheck) ? __builtin_amdgcn_s_memrealtime() : 0;
     static_assert(MODE == 0 || MODE == 2 || (CT == 3 && RT == 1 && J <= 32 && NW == 8), "attention mode: 32 x (q|k|v)");
     static_assert(MODE < 2 || (RT == 1 && XP == 0 && STG == 0 && DBG == 0), "split-route phase 2: one 32-row tile");
     constexpr int NPW = (J + NW - 1) / NW;  // nodes per wave
@@ -1201,9 +1209,13 @@ __global__ __launch_bounds__(NW * 64, 1) void k_gl4(const GLArgs p) {
 #endif
     if constexpr (MODE == 1) {
         attention_epilogue<J, NW, NPW>(p, acc, smem, sG, row0, ctile, wave, lane);
+        if ((p.diag & kDiagSelfCheck) && tid == 0 && p.dbg) diag_wg_log(p.dbg, 2 + MODE, dt0);
+        if (p.diag & kDiagRelease) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
         return;
     } else if constexpr (MODE == 3) {
         attention_epilogue<J, NW, NPW, true>(p, acc, smem, sG, row0, ctile, wave, lane, slab);
+        if ((p.diag & kDiagSelfCheck) && tid == 0 && p.dbg) diag_wg_log(p.dbg, 2 + MODE, dt0);
+        if (p.diag & kDiagRelease) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
         return;
     }
     // ---- mixing + epilogue, one 16-row slab at a time.  Z^T = Y^T G-hat^T on 16x16x4 f32 MFMA
@@ -1366,6 +1378,8 @@ __global__ __launch_bounds__(NW * 64, 1) void k_gl4(const GLArgs p) {
             o[7] = (unsigned)(ts[7] - ts[6]);  // shader-clock cycles of chunks 2 .. end
         }
     }
+    if ((p.diag & kDiagSelfCheck) && tid == 0 && p.dbg) diag_wg_log(p.dbg, 2 + MODE, dt0);
+    if (p.diag & kDiagRelease) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
 }
 
 // v4 weight staging (GLArgs::gl4_stage): 0 = LDS-DMA stages, the workgroup holds
@@ -1432,7 +1446,7 @@ static hipError_t gl4_launch_t(const GLArgs& a, bool rms, hipStream_t s) {
         hipError_t e = hipFuncSetAttribute((const void*)kt, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         if (e != hipSuccess) return e;
     }
-    hipLaunchKernelGGL(kt, grid, dim3(NW * 64), lds, s, a);
+    hipLaunchKernelGGL(kt, grid, dim3(NW * 64), lds, s, sealed(a));
     return hipGetLastError();
 }
 
@@ -1496,11 +1510,11 @@ static hipError_t launch_gl4y(const GLArgs& a, bool rms, int ntc, int64_t ntile_
     const int64_t units = ntile_r * a.J * ntc;
     const dim3 grid((unsigned)((units + 3) / 4)), block(256);
     if (a.prec == 1) {
-        if (rms) hipLaunchKernelGGL((k_gl4y<true, 1, ROWMAJOR>), grid, block, 0, s, a, ntc, ntile_r, yo);
-        else hipLaunchKernelGGL((k_gl4y<false, 1, ROWMAJOR>), grid, block, 0, s, a, ntc, ntile_r, yo);
+        if (rms) hipLaunchKernelGGL((k_gl4y<true, 1, ROWMAJOR>), grid, block, 0, s, sealed(a), ntc, ntile_r, yo);
+        else hipLaunchKernelGGL((k_gl4y<false, 1, ROWMAJOR>), grid, block, 0, s, sealed(a), ntc, ntile_r, yo);
     } else {
-        if (rms) hipLaunchKernelGGL((k_gl4y<true, 0, ROWMAJOR>), grid, block, 0, s, a, ntc, ntile_r, yo);
-        else hipLaunchKernelGGL((k_gl4y<false, 0, ROWMAJOR>), grid, block, 0, s, a, ntc, ntile_r, yo);
+        if (rms) hipLaunchKernelGGL((k_gl4y<true, 0, ROWMAJOR>), grid, block, 0, s, sealed(a), ntc, ntile_r, yo);
+        else hipLaunchKernelGGL((k_gl4y<false, 0, ROWMAJOR>), grid, block, 0, s, sealed(a), ntc, ntile_r, yo);
     }
     return hipGetLastError();
 }
@@ -1552,7 +1566,7 @@ static hipError_t launch_gl4t_ct(const GLArgs& a, bool rms, int64_t ntile_r, con
         if ((e = hipFuncSetAttribute((const void*)kt, hipFuncAttributeMaxDynamicSharedMemorySize, (int)dyn)) != hipSuccess)
             return e;
     }
-    hipLaunchKernelGGL(kt, grid, block, dyn, s, a, ncg, ntile_r, yo);
+    hipLaunchKernelGGL(kt, grid, block, dyn, s, sealed(a), ncg, ntile_r, yo);
     return hipGetLastError();
 }
 

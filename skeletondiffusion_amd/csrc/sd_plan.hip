@@ -1,6 +1,7 @@
 // Host side of libskeldiff: plan construction (state_dict-keyed tensor registry), one-time
 // packing, the per-step launch sequence of the Denoiser + posterior update, and the hipGraph
 // capture of the whole T-step chain.  Implements include/skeldiff.h.
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
 #include <cmath>
@@ -36,6 +37,17 @@ int sd::diag_flags() {
         return e ? atoi(e) : 0;
     }();
     return v;
+}
+
+unsigned* sd::diag_buffer() {
+    static unsigned* buf = [] {
+        unsigned* b = nullptr;
+        if (hipMalloc(&b, sd::kDiagWords * sizeof(unsigned)) != hipSuccess ||
+            hipMemset(b, 0, sd::kDiagWords * sizeof(unsigned)) != hipSuccess || hipDeviceSynchronize() != hipSuccess)
+            abort();
+        return b;
+    }();
+    return buf;
 }
 
 #ifdef SD_DEBUG_LDS
@@ -100,6 +112,27 @@ struct GraphSet {
     }
 };
 
+}  // namespace
+
+// Diagnostics (tools/hazard_snap.py): when an arena is set (sd_debug_snapshot),
+// every graph-linear call of run_denoiser copies its phase-1 scratch Y (zs) and its output rows
+// into slot (step, call) of the arena at the chain's row offset, and the posterior update its
+// output into call slot kSnapCalls - 1, so a run with row chains can be compared slot by slot
+// with a one-chain run.  Never set on the product path.
+namespace {
+constexpr int kSnapCalls = 40;
+struct Snap {
+    float* arena = nullptr;
+    int64_t slot = 0, half = 0;  // floats per slot; the Y region is [0, half), the output region the rest
+    int nslots = 0;
+    std::vector<int> meta;  // per slot: N, output floats per row, Y floats per row
+};
+Snap g_snap;
+// diagnostics (sd_debug_update_dump): the first update of a sampling call dumps its inputs
+struct UpdDump {
+    float *x0 = nullptr, *xt = nullptr, *ev = nullptr;
+};
+UpdDump g_dump;
 }  // namespace
 
 // Row chains.  Rows never interact inside the Denoiser or the posterior update, so the T-step
@@ -289,6 +322,7 @@ sd::GLArgs gl_args(const sd_plan* p, const GL& g, const float* x1, int x1_div, c
 #ifdef SD_DEBUG_LDS
     a.dbg = sd::debug_counters();
 #endif
+    if (sd::diag_flags() & sd::kDiagSelfCheck) a.dbg = sd::diag_buffer();  // diagnostics only
     return a;
 }
 
@@ -323,8 +357,27 @@ struct Prof {
 int run_denoiser(const sd_plan* p, const float* x_t, const float* x_cond, int64_t cond_repeat,
                  int t, float* x0_out, int64_t rows, const WS& w, hipStream_t s, Prof* prof = nullptr,
                  int64_t cond_phase = 0, int tile_hint = 0, float* const* trace = nullptr,
-                 int xt_bf16 = 0, int x0_bf16 = 0, int64_t route_rows = 0, int concurrent = 0) {
+                 int xt_bf16 = 0, int x0_bf16 = 0, int64_t route_rows = 0, int concurrent = 0,
+                 int64_t snap_r0 = -1, int snap_step = 0) {
     const int H = p->H;
+    int snap_call = 0;
+    auto snap = [&](const sd::GLArgs& g) -> int {
+        const int call = snap_call++;
+        if (!g_snap.arena || snap_r0 < 0) return SD_OK;
+        const int64_t sl = (int64_t)snap_step * kSnapCalls + call;
+        if (sl >= g_snap.nslots) return SD_OK;
+        float* base = g_snap.arena + sl * g_snap.slot;
+        const int64_t yrow = (int64_t)p->J * g.N;
+        g_snap.meta[3 * sl] = g.N;
+        g_snap.meta[3 * sl + 1] = (int)g.out_rs;
+        g_snap.meta[3 * sl + 2] = (int)yrow;
+        if (g.zs && (snap_r0 + rows) * yrow <= g_snap.half)
+            SD_HIP(hipMemcpyAsync(base + snap_r0 * yrow, g.zs, rows * yrow * sizeof(float), hipMemcpyDeviceToDevice, s));
+        if ((snap_r0 + rows) * g.out_rs <= g_snap.slot - g_snap.half)
+            SD_HIP(hipMemcpyAsync(base + g_snap.half + snap_r0 * g.out_rs, g.out, rows * g.out_rs * sizeof(float),
+                                  hipMemcpyDeviceToDevice, s));
+        return SD_OK;
+    };
     // v4 path: every intermediate activation in the row-blocked layout (coalesced x fragments);
     // the denoiser's inputs (x_t, x_cond) and output (x0) stay row-major
     const int B = p->blocked_now() ? 1 : 0;
@@ -379,7 +432,9 @@ int run_denoiser(const sd_plan* p, const float* x_t, const float* x_cond, int64_
     }
     lay(a, 0, 0, 1);
     SD_LAUNCH(prof, 0, sd::launch_graph_linear(a, false, s));
-    int rc = record(w.r);
+    int rc = snap(a);
+    if (rc) return rc;
+    rc = record(w.r);
     if (rc) return rc;
 
     const int L = 2 * p->depth;
@@ -391,10 +446,12 @@ int run_denoiser(const sd_plan* p, const float* x_t, const float* x_cond, int64_
         lay(a, 1, 1, 1);
         a.act = 1;
         SD_LAUNCH(prof, 0, sd::launch_graph_linear(a, false, s));
+        if ((rc = snap(a))) return rc;
         a = gl_args(p, p->r2[l], w.h, 1, nullptr, nullptr, xin, w.x, rows);
         lay(a, 1, 1, 1);
         a.act = 1;
         SD_LAUNCH(prof, 0, sd::launch_graph_linear(a, false, s));
+        if ((rc = snap(a))) return rc;
         if ((rc = record(w.x))) return rc;
         if (!p->has_attn[l]) {
             if ((rc = record(w.x))) return rc;  // nn.Identity in place of the last attention
@@ -415,18 +472,21 @@ int run_denoiser(const sd_plan* p, const float* x_t, const float* x_cond, int64_
                 fused = sd::launch_qkv_attention_v4(a, true, s);
                 if (fused != hipSuccess && fused != hipErrorNotSupported) SD_HIP(fused);
                 if (prof && prof->post(s)) return fail(SD_E_HIP, "hipEventRecord failed");
+                if (fused == hipSuccess && (rc = snap(a))) return rc;
             }
             if (fused == hipErrorNotSupported) {
                 if (B) return fail(SD_E_INTERNAL, "row-blocked plan without the fused attention kernel");
                 a = gl_args(p, p->qkv[l], w.x, 1, nullptr, nullptr, nullptr, w.qkv, rows);
                 lay(a, 0, 0, 0);
                 SD_LAUNCH(prof, 0, sd::launch_graph_linear(a, true, s));
+                if ((rc = snap(a))) return rc;
                 sd::AttnArgs aa{w.qkv, w.o, rows, p->J, p->d.attn_heads, p->d.attn_dim_head, qscale};
                 SD_LAUNCH(prof, 1, sd::launch_attention(aa, s));
             }
             a = gl_args(p, p->outp[l], w.o, 1, nullptr, nullptr, w.x, w.x, rows);
             lay(a, 1, 1, 1);
             SD_LAUNCH(prof, 0, sd::launch_graph_linear(a, false, s));
+            if ((rc = snap(a))) return rc;
         } else {
             // Residual(PreNorm(StaticGraphLinear)): x = GL(rmsnorm(x)) + x, written to the `o`
             // buffer (sized like x in this configuration: a graph-linear may not write its own
@@ -434,6 +494,7 @@ int run_denoiser(const sd_plan* p, const float* x_t, const float* x_cond, int64_
             a = gl_args(p, p->qkv[l], w.x, 1, nullptr, nullptr, w.x, w.o, rows);
             lay(a, 1, 1, 1);
             SD_LAUNCH(prof, 0, sd::launch_graph_linear(a, true, s));
+            if ((rc = snap(a))) return rc;
             const int64_t rp = B ? (rows + 31) / 32 * 32 : rows;
             SD_LAUNCH(prof, 0, sd::launch_convert_rows(w.x, bfl(w.x), (int64_t)p->J * H, w.o, bfl(w.o), (int64_t)p->J * H, rp,
                                                        (int64_t)p->J * H, s));
@@ -445,19 +506,23 @@ int run_denoiser(const sd_plan* p, const float* x_t, const float* x_cond, int64_
     a = gl_args(p, p->fres_res, w.x, 1, w.r, nullptr, nullptr, w.res, rows);
     lay(a, 1, 1, 1);
     SD_LAUNCH(prof, 0, sd::launch_graph_linear(a, false, s));
+    if ((rc = snap(a))) return rc;
     a = gl_args(p, p->r1[L], w.x, 1, w.r, film, nullptr, w.h, rows);
     lay(a, 1, 1, 1);
     a.act = 1;
     SD_LAUNCH(prof, 0, sd::launch_graph_linear(a, false, s));
+    if ((rc = snap(a))) return rc;
     a = gl_args(p, p->r2[L], w.h, 1, nullptr, nullptr, w.res, w.res, rows);
     lay(a, 1, 1, 1);
     a.act = 1;
     SD_LAUNCH(prof, 0, sd::launch_graph_linear(a, false, s));
+    if ((rc = snap(a))) return rc;
     if ((rc = record(w.res))) return rc;
     // final_glin (generator.py:107)
     a = gl_args(p, p->fglin, w.res, 1, nullptr, nullptr, nullptr, x0_out, rows);
     lay(a, 1, 1, 0);
     SD_LAUNCH(prof, 0, sd::launch_graph_linear(a, false, s));
+    if ((rc = snap(a))) return rc;
     return SD_OK;
 }
 
@@ -497,6 +562,10 @@ int run_update(const sd_plan* p, const float* x0, const float* xt, const float* 
 #ifdef SD_DEBUG_LDS
     u.dbg = sd::debug_counters();
 #endif
+    if (sd::diag_flags() & sd::kDiagSelfCheck) u.dbg = sd::diag_buffer();  // diagnostics only
+    u.dump_x0 = g_dump.x0;
+    u.dump_xt = g_dump.xt;
+    u.dump_ev = g_dump.ev;
     if (p->d.isotropic) {
         u.c1s = p->iso_c1[t];
         u.c2s = p->iso_c2[t];
@@ -537,6 +606,41 @@ void step_flops(const sd_plan* p, int64_t rows, double* f) {
 extern "C" {
 
 int32_t sd_abi_version(void) { return SD_ABI_VERSION; }
+
+// Diagnostics only (tools/hazard_snap.py; not in include/skeldiff.h): set (arena != null) or clear
+// the snapshot arena of run_denoiser / record_loop.  slot_floats per slot, the first y_floats of
+// it for the phase-1 scratch Y.  Not thread-safe; never used by the product path.
+int sd_debug_snapshot(float* arena, int64_t slot_floats, int64_t y_floats, int32_t nslots) {
+    g_snap.arena = arena;
+    g_snap.slot = slot_floats;
+    g_snap.half = y_floats;
+    g_snap.nslots = arena ? nslots : 0;
+    g_snap.meta.assign(3 * (size_t)std::max(nslots, 0), 0);
+    return SD_OK;
+}
+// Diagnostics only: copy (and with reset != 0, then zero) the SKELDIFF_DIAG bit-15 buffer
+// (sd_internal.h, kDiagWords words)
+int sd_debug_diag_buffer(uint32_t* host, int64_t words, int32_t reset) {
+    unsigned* b = sd::diag_buffer();
+    const int64_t n = std::min<int64_t>(words, sd::kDiagWords);
+    SD_HIP(hipDeviceSynchronize());
+    if (host && n > 0) SD_HIP(hipMemcpy(host, b, n * sizeof(unsigned), hipMemcpyDeviceToHost));
+    if (reset) SD_HIP(hipMemset(b, 0, sd::kDiagWords * sizeof(unsigned)));
+    SD_HIP(hipDeviceSynchronize());
+    return SD_OK;
+}
+// Diagnostics only: the first posterior update of the next sampling calls stores its inputs
+// (x0 after activation and clamp, x_t, sigma eps; (rows, J, D) each) to these buffers; nulls = off
+int sd_debug_update_dump(float* x0, float* xt, float* ev) {
+    g_dump = UpdDump{x0, xt, ev};
+    if (!x0 || !xt || !ev) g_dump = UpdDump{};
+    return SD_OK;
+}
+int sd_debug_snapshot_meta(int32_t slot, int32_t* out3) {
+    if (slot < 0 || 3 * (size_t)slot + 2 >= g_snap.meta.size()) return SD_E_INVALID;
+    for (int i = 0; i < 3; ++i) out3[i] = g_snap.meta[3 * (size_t)slot + i];
+    return SD_OK;
+}
 
 const char* sd_last_error(void) { return g_err.c_str(); }
 
@@ -883,10 +987,29 @@ static int64_t chain_row(int i, int n, int64_t rows, int64_t unit) {
 }
 
 // Creates the auxiliary streams / fork-join events chains 1 .. n-1 use (caller holds cmu).
+// Diagnostics (SKELDIFF_DIAG bit 13): every chain, the first included, on a stream
+// of its own whose CU mask is a disjoint 1/n of the device's CUs (no two chains share a CU).
+constexpr int kDiagCuMask = 1 << 13;
 static int ensure_chains(sd_plan* mp, int n) {
+    const bool masked = sd::diag_flags() & kDiagCuMask;
     if (!mp->ev_fork) SD_HIP(hipEventCreateWithFlags(&mp->ev_fork, hipEventDisableTiming));
-    for (int i = 1; i < n; ++i) {
-        if (!mp->aux[i]) SD_HIP(hipStreamCreateWithFlags(&mp->aux[i], hipStreamNonBlocking));
+    for (int i = masked ? 0 : 1; i < n; ++i) {
+        if (!mp->aux[i]) {
+            if (masked) {
+                int dev = 0;
+                hipDeviceProp_t pr;
+                SD_HIP(hipGetDevice(&dev));
+                SD_HIP(hipGetDeviceProperties(&pr, dev));
+                const int ncu = pr.multiProcessorCount;
+                std::vector<uint32_t> m((ncu + 31) / 32, 0u);
+                const bool inter = sd::diag_flags() & (1 << 17);  // bit 17: interleaved (cu % n == i)
+                for (int c = 0; c < ncu; ++c)
+                    if (inter ? c % n == i : c * n / ncu == i) m[c / 32] |= 1u << (c % 32);
+                SD_HIP(hipExtStreamCreateWithCUMask(&mp->aux[i], (uint32_t)m.size(), m.data()));
+            } else {
+                SD_HIP(hipStreamCreateWithFlags(&mp->aux[i], hipStreamNonBlocking));
+            }
+        }
         if (!mp->ev_join[i]) SD_HIP(hipEventCreateWithFlags(&mp->ev_join[i], hipEventDisableTiming));
     }
     return SD_OK;
@@ -935,16 +1058,24 @@ static int record_loop(const sd_plan* p, const float* x_T, const float* x_cond, 
             // 5 % faster than the single-chain 32 x 96 choice at B = 3200, 3 chains
             const int64_t wg813 = (c.n + 31) / 32 * 2;  // 32 x 96 workgroups of an N = 192 layer
             int rc = run_denoiser(p, c.cur, xc, cond_repeat, t, c.w.x0, c.n, c.w, cs[i], nullptr, r0 % cond_repeat,
-                                  (nch > 1 && wg813 >= 32) ? 812 : 0, nullptr, bf, bf, rows, nch > 1);
+                                  (nch > 1 && wg813 >= 32) ? 812 : 0, nullptr, bf, bf, rows, nch > 1, r0, (int)k);
             if (rc) return rc;
             float* nxt = (t == 0) ? out + r0 * JD : (((T - 1 - t) & 1) ? c.w.img1 : c.w.img0);
             const float* eps = (!dev_noise && t > 0) ? eps_all + r0 * step_rs + k * JD : nullptr;
+            const UpdDump saved = g_dump;
+            if (k != 0 || !g_dump.x0) g_dump = UpdDump{};
+            else g_dump = UpdDump{g_dump.x0 + r0 * JD, g_dump.xt + r0 * JD, g_dump.ev + r0 * JD};
             rc = run_update(p, c.w.x0, c.cur, eps, step_rs, dev_noise ? 2 : 1, seed, row0, rng, t, nxt,
                             (rec && timages) ? timages + r0 * step_rs + k * JD : nullptr, step_rs,
                             (rec && means) ? means + r0 * step_rs + k * JD : nullptr, step_rs,
                             (rec && noise_out) ? noise_out + r0 * step_rs + k * JD : nullptr, step_rs, c.n,
                             cs[i], nullptr, r0, bf, bf, t > 0 ? bf : 0);
+            g_dump = saved;
             if (rc) return rc;
+            const int64_t sl = k * kSnapCalls + kSnapCalls - 1;  // diagnostics: the update's output
+            if (g_snap.arena && sl < g_snap.nslots && (r0 + c.n) * JD <= g_snap.slot - g_snap.half)
+                SD_HIP(hipMemcpyAsync(g_snap.arena + sl * g_snap.slot + g_snap.half + r0 * JD, nxt, c.n * JD * sizeof(float),
+                                      hipMemcpyDeviceToDevice, cs[i]));
             c.cur = nxt;
         }
     }
@@ -959,14 +1090,14 @@ static int fork_chains(sd_plan* mp, hipStream_t s, int n, hipStream_t* cs) {
         return SD_OK;
     }
     if (n > 1) SD_HIP(hipEventRecord(mp->ev_fork, s));
-    for (int i = 1; i < n; ++i) {
+    for (int i = (n > 1 && (sd::diag_flags() & kDiagCuMask)) ? 0 : 1; i < n; ++i) {
         SD_HIP(hipStreamWaitEvent(mp->aux[i], mp->ev_fork, 0));
         cs[i] = mp->aux[i];
     }
     return SD_OK;
 }
 static int join_chains(sd_plan* mp, hipStream_t s, int n, const hipStream_t* cs) {
-    for (int i = 1; i < n; ++i) {
+    for (int i = (n > 1 && (sd::diag_flags() & kDiagCuMask)) ? 0 : 1; i < n; ++i) {
         SD_HIP(hipEventRecord(mp->ev_join[i], cs[i]));
         SD_HIP(hipStreamWaitEvent(s, mp->ev_join[i], 0));
     }
@@ -1001,6 +1132,7 @@ int sd_sample_loop(const sd_plan* p, const float* x_T, const float* x_cond, int6
         lk.lock();
         if ((rc = ensure_chains(mp, nch))) return rc;
         for (int i = 1; i < nch; ++i) cs[i] = mp->aux[i];
+        if (sd::diag_flags() & kDiagCuMask) cs[0] = mp->aux[0];
     }
     if (!(flags & SD_FLAG_GRAPH)) {
         if ((rc = fork_chains(mp, s, nch, cs))) return rc;
