@@ -15,20 +15,23 @@ fixed as N grows); --scaling strong: the `batch` sequences are split over the N 
 (no checkpoint can be fetched); conditioning latents are synthetic U(-1, 1).
 
 Rank 0 prints one JSON line.  It also carries:
-  roofline      the graph-linear launches (incl. the fused to_qkv + attention ones) -- the
-                dominant kernel class, >= 98 % of a denoise step's kernel time.  achieved / frac =
-                their algorithmic f32 FLOPs of the TIMED region / ms_per_step (the whole timed
-                step: row chains, hipGraphs, update kernels and gaps included).  The default
-                kernels (v4) compute every f32 product as three f16 MFMA products (x_hi W_hi +
-                x_hi W_lo + x_lo W_hi, f32 accumulate), so the ceiling is the f16 dense MFMA
-                peak / 3 (2500 / 3 TFLOP/s of f32 work); the exact-f32 generations are priced
-                against the 157.3 TFLOP/s f32 peak.  "per_launch" has the same launches measured
-                one by one with HIP events on their stream (sd_profile_step, one row chain: the
-                numbers rocprofv3 --kernel-trace reports, profiles/); "hbm_view" prices them by
-                their algorithmic HBM bytes (activations in and out once, weights once) vs 8 TB/s;
+  roofline      the dominant kernel class: one graph-linear layer (on the split routes its GEMM
+                phase + mixing / attention phase; fused to_qkv + attention launches included),
+                >= 97 % of a denoise step's kernel time.  Bound "hbm": achieved = the layer's
+                algorithmic HBM bytes (activations in and out once, residual in, weights once)
+                per launch / its average duration, timed with HIP events on the launch stream
+                (sd_profile_step, one denoise step at the full batch; rocprofv3 --kernel-trace of
+                the same command under profiles/ gives the per-kernel durations) vs 8 TB/s;
+                traffic = PMC HBM bytes per layer launch (FETCH_SIZE x 2 + WRITE_SIZE, separate
+                passes, profiles/pmc_traffic.json keyed by config and the kernels the call
+                launched).  "mfma_view" prices the same launches by their f32 FLOPs against the
+                f16 MFMA peak / 3 (2500 / 3 TFLOP/s: every f32 product is three f16 products);
+                "timed_region" by the FLOPs of the whole timed step (row chains, hipGraphs, the
+                update kernels and launch gaps inside) / ms_per_step;
   exact_f32     (N = 1) the same workload on the exact-f32 kernels (kernel_variant 3);
-  cpu_baseline  the oracle (torch-CPU restatement of the reference path) on this host, bounded
-                sample: a few of the T steps on the same B rows, per-step time x T.
+  cpu_baseline  the oracle (torch-CPU restatement of the reference path) on this host's physical
+                cores (those this process may use: affinity and cgroup quota), median of 3 runs
+                of a few of the T steps on the same B rows, per-step time x T.
 """
 from __future__ import annotations
 
@@ -186,8 +189,32 @@ def host_cpu():
             "logical_cpus": os.cpu_count()}
 
 
-def cpu_baseline(d, x_cond, rows, steps, threads):
-    """The oracle (torch-CPU restatement of the reference path) on a bounded sample."""
+def physical_cores():
+    """Physical cores this process may run on: lscpu's sockets x cores per socket, capped by the
+    CPU affinity mask (logical CPUs / threads per core) and the cgroup CPU quota (cpu.max)."""
+    h = host_cpu()
+    try:
+        phys = int(h["sockets"]) * int(h["cores_per_socket"])
+        tpc = max(1, int(h["threads_per_core"]))
+    except (TypeError, ValueError):
+        phys, tpc = os.cpu_count() or 1, 1
+    avail = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    quota = None
+    try:
+        q, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = max(1, int(float(q) / float(period)))
+    except Exception:
+        pass
+    n = min(phys, max(1, avail // tpc) if avail < (os.cpu_count() or avail) else phys)
+    if quota:
+        n = min(n, quota)
+    return max(1, n), {"physical_cores": phys, "threads_per_core": tpc, "affinity_cpus": avail, "cgroup_cpu_quota": quota}
+
+
+def cpu_baseline(d, x_cond, rows, steps, threads, repeats=3):
+    """The oracle (torch-CPU restatement of the reference path) on a bounded sample: one warm-up
+    step, then the median of `repeats` timed runs of `steps` reverse steps."""
     import oracle as O
 
     torch.set_num_threads(threads)
@@ -199,13 +226,17 @@ def cpu_baseline(d, x_cond, rows, steps, threads):
     g = torch.Generator().manual_seed(0)
     start = torch.randn((rows, J, D), generator=g)
     O.p_sample_loop(sd, cfg, bufs, start, None, x_cond=xc, steps=1)   # warm-up step
-    t0 = time.perf_counter()
-    O.p_sample_loop(sd, cfg, bufs, start, None, x_cond=xc, steps=steps)
-    per_step = (time.perf_counter() - t0) / steps
+    runs = []
+    for _ in range(repeats):
+        t0 = time.perf_counter()
+        O.p_sample_loop(sd, cfg, bufs, start, None, x_cond=xc, steps=steps)
+        runs.append((time.perf_counter() - t0) / steps)
+    per_step = float(np.median(runs))
     return {"value": rows / (per_step * T), "unit": "futures/s", "cores": threads, "kind": "port",
-            "host_cpu": host_cpu(),
-            "sample": f"oracle/skeldiff_oracle.py p_sample_loop, {steps} of the T={T} reverse steps on the same "
-                      f"{rows} rows (J={J}), per-step time x T; torch-CPU fp32, {threads} threads"}
+            "host_cpu": host_cpu(), "runs_futures_per_s": [rows / (r * T) for r in runs],
+            "sample": f"oracle/skeldiff_oracle.py p_sample_loop, median of {repeats} runs of {steps} of the T={T} "
+                      f"reverse steps on the same {rows} rows (J={J}), per-step time x T; torch-CPU fp32, "
+                      f"{threads} threads (torch.set_num_threads)"}
 
 
 def world_rows(world: int, rows: int, scaling: str, batch: int, futures: int) -> int:
@@ -227,7 +258,7 @@ def main():
                     help="graph-linear arithmetic (default: the config's; f32 for the BASELINE metric)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-steps", type=int, default=4)
-    ap.add_argument("--cpu-threads", type=int, default=min(16, os.cpu_count() or 1))
+    ap.add_argument("--cpu-threads", type=int, default=0, help="0: every physical core this process may use")
     ap.add_argument("--profile-reps", type=int, default=5)
     ap.add_argument("--scaling", choices=["weak", "strong"], default="weak",
                     help="weak: `batch` sequences per GPU; strong: `batch` sequences split over the GPUs")
@@ -321,22 +352,17 @@ def main():
 
     value = world_rows(world, rows, args.scaling, batch, futures) * args.steps / elapsed
     variant = eng.get_option("kernel_variant")
-    # J > 21 (v5): the GEMM phase on the same split-f16 products (k_gl4t), the node mixing (2 J^2 N
-    # of the 2 J K N + 2 J^2 N FLOPs per row) in exact f32 on the VALU
-    split = (variant in (0, 4) and J in (16, 17, 21)) or (variant == 0 and J > 21)
-    # the tiled split route (sd_graph_linear_v4.hip split_route: auto at J = 17 / 21, and J = 16 f32
-    # from 3,200 rows; bf16 at J = 17 only; or forced by split_route = 3)
-    sr = eng.get_option("split_route")
-    tiled = variant in (0, 4) and J in (16, 17, 21) and (
-        sr == 3 or (sr == 0 and eng.get_option("gl4_tile") == 0 and rows > 640 and (
-            J == 17 or (J == 21 and eng.precision != "bf16") or (J == 16 and eng.precision == "f32" and rows >= 3200))))
-    row_chains = min(eng.get_option("row_chains"), max(1, rows // 32))
-    small = split and J <= 21 and eng.precision != "bf16" and (sr == 2 or (sr == 0 and rows <= 640))
-    route = ("tiled split (k_gl4t + k_gl4 MODE 2/3)" if tiled else
+    row_chains = eng.get_option("last_chains")
+    route_bits = eng.get_option("last_route")
+    kernels = [name for bit, name in sorted(_lib.ROUTE_BITS.items()) if route_bits & bit]
+    split = bool(route_bits & (1 | 2 | 4 | 8)) and not (route_bits & 64)  # split-f16 products (v4 / v5 GEMM phase)
+    tiled = bool(route_bits & 8) and J <= 21
+    small = bool(route_bits & 4)
+    route = ("tiled split (k_gl4t + k_gl4 MODE 2/3)" if tiled and not route_bits & (1 | 2) else
+             "tiled split + one-kernel fused attention" if tiled else
              "small-batch split (k_gl4y + k_gl4 MODE 2/3)" if small else
-             "one-kernel (k_gl4)" if split and J <= 21 else "v5 (k_gl4t + k_gl5_mix)" if split else "exact f32")
-    if small or (J > 21 and variant == 0):  # one chain on these routes (sd_plan.hip chain_count)
-        row_chains = 1
+             "v5 (k_gl4t + k_gl5_mix)" if route_bits & 32 and split else
+             "one-kernel (k_gl4)" if split else "exact f32")
     half = split and eng.precision in ("half", "bf16")
     fused_attn = ms[1] == 0.0 and cnt[1] == 0   # attention ran inside the graph-linear launches
     gl_flops = fl[0] + (fl[1] if fused_attn else 0.0)
@@ -344,6 +370,7 @@ def main():
     peak = F16_MFMA_PEAK_TFLOPS if half else F16_MFMA_PEAK_TFLOPS / 3.0 if split else FP32_PEAK_TFLOPS
     gl_bytes = graph_linear_bytes(d, rows, fused_attn)
     gl_gbs = gl_bytes / (ms[0] * 1e-3) / 1e9
+    launches = max(cnt[0], 1)
     upd_bytes = 3.0 * rows * J * D * 4        # x0, x_t in, x_{t-1} out (device Philox noise)
     upd_gbs = upd_bytes / (ms[2] * 1e-3) / 1e9
     step_flops = sum(fl)
@@ -353,6 +380,17 @@ def main():
     if exact is not None:
         exact["graph_linear_tflops_timed"] = (fl[0] + fl[1]) * T / (exact["ms_per_step"] * 1e-3) / 1e12
         exact["frac_of_f32_peak"] = exact["graph_linear_tflops_timed"] / FP32_PEAK_TFLOPS
+    traffic, traffic_note = None, "no PMC pass on record for this config and kernel set"
+    traffic_file = os.path.join(HERE, "profiles", "pmc_traffic.json")
+    traffic_key = f"{args.config}|{route_bits}"
+    if os.path.exists(traffic_file):
+        try:
+            tr = json.load(open(traffic_file)).get(traffic_key)
+            if tr and tr.get("rows") == rows:
+                traffic = tr.get("hbm_bytes_per_layer_launch")
+                traffic_note = tr.get("source")
+        except Exception:
+            pass
     rec = {
         "metric": METRIC,
         "value": value,
@@ -381,58 +419,42 @@ def main():
                    "sequences_total": world_rows(world, rows, args.scaling, batch, futures) // futures,
                    "futures": futures, "rows_per_gpu": rows, "latent_dim": D, "hipgraph": graph,
                    "parallelism": f"dp{world} (sequence-sharded, no data-path collective)",
-                   "row_chains": 1 if tiled and sr == 0 else row_chains, "route": route,
+                   "row_chains": row_chains, "route": route, "kernels": kernels, "route_bits": route_bits,
                    "kernel_variant": variant},
         "roofline": {
-            "bound": "mfma",
-            "kernel": ("tiled split route: k_gl4t GEMM phase (3xf16 split MFMA, 128 rows x 192 columns of one "
-                       "node per workgroup, pre-mix Y to HBM) + k_gl4 MODE 2 / 3 phase (G-hat mixing, "
-                       "FiLM/tanh/residual or attention)") if tiled else
-                      ("small-batch split route: k_gl4y GEMM phase (one wave per 32-row tile, node, 32 "
-                       "columns) + k_gl4 MODE 2 / 3 phase") if small else
-                      ("k_gl4 graph-linear (3xf16 split MFMA, fused bias/RMS/G-hat/FiLM/tanh/residual; "
-                       "to_qkv launches fused with attention)") if split and J <= 21 else
-                      ("v5: k_gl4t split-f16 GEMM phase + k_gl5_mix mixing pass") if split else
-                      "k_gl3/k_gl2/k_gl5 graph-linear (exact f32 MFMA, fused epilogue)",
-            "achieved": timed_tflops, "peak": peak, "unit": "TFLOP/s", "frac": timed_tflops / peak,
-            "measured_on": ("the timed region: graph-linear + attention algorithmic FLOPs of T denoise steps "
-                            "over this rank's rows / ms_per_step (row chains, hipGraphs, update kernels and "
-                            "launch gaps all inside)"),
-            "peak_basis": "f16 / bf16 dense MFMA 2500 TFLOP/s (one product per multiply-add)" if half else
-                          "f16 dense MFMA 2500 TFLOP/s / 3 products per f32 product" if split else
-                          "f32 dense 157.3 TFLOP/s",
-            "traffic": None,
-            "flops_per_denoise_step": fl[0] + fl[1],
-            "per_launch": {
-                "achieved": gl_tflops, "frac": gl_tflops / peak, "unit": "TFLOP/s",
-                "flops_per_launch": gl_flops / max(cnt[0], 1), "launches_per_denoise_step": cnt[0],
-                "avg_launch_ms": ms[0] / max(cnt[0], 1),
-                "kernel_ms_per_bench_step": ms[0] * T,
-                "measured_on": ("one denoise step at the full batch on ONE stream (sd_profile_step: HIP events "
-                                "around each launch (a split-route layer = its two kernels), kernels alone on the "
-                                "GPU) -- the view rocprofv3 --kernel-trace gives" +
-                                ("" if tiled or row_chains == 1 else
-                                 "; the timed region overlaps row chains, so its step is shorter than this kernel sum"))},
-            "hbm_view": {"achieved": gl_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": gl_gbs / HBM_PEAK_GBS,
-                         "algorithmic_bytes_per_launch": gl_bytes / max(cnt[0], 1)},
+            "bound": "hbm",
+            "kernel": "one graph-linear layer: " + route + " (the launches of one StaticGraphLinear, to_qkv + "
+                      "attention fused); per-launch average over the layers of one denoise step",
+            "achieved": gl_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": gl_gbs / HBM_PEAK_GBS,
+            "traffic": traffic, "traffic_source": traffic_note,
+            "algorithmic_bytes_per_launch": gl_bytes / launches, "avg_launch_ms": ms[0] / launches,
+            "launches_per_denoise_step": cnt[0],
+            "measured_on": ("HIP events on the launch stream around each layer, one denoise step at the full "
+                            "batch on one stream (sd_profile_step, kernels alone on the GPU), "
+                            f"{args.profile_reps} repetitions"),
+            "mfma_view": {"achieved": gl_tflops, "peak": peak, "unit": "TFLOP/s", "frac": gl_tflops / peak,
+                          "flops_per_launch": gl_flops / launches,
+                          "peak_basis": "f16 / bf16 dense MFMA 2500 TFLOP/s (one product per multiply-add)" if half
+                          else "f16 dense MFMA 2500 TFLOP/s / 3 products per f32 product" if split
+                          else "f32 dense 157.3 TFLOP/s"},
+            "timed_region": {"achieved": timed_tflops, "peak": peak, "unit": "TFLOP/s", "frac": timed_tflops / peak,
+                             "flops_per_denoise_step": fl[0] + fl[1],
+                             "measured_on": "graph-linear + attention FLOPs of T denoise steps over this rank's rows "
+                                            "/ ms_per_step (row chains, hipGraphs, update kernels, gaps inside)"},
         },
         "kernels_per_denoise_step_ms": {"graph_linear": ms[0], "attention": ms[1], "update": ms[2],
                                         "step_first_to_last_event": ms[3]},
         "update_kernel": {"bound": "hbm", "achieved": upd_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                          "frac": upd_gbs / HBM_PEAK_GBS, "bytes_per_launch": upd_bytes},
+                          "frac": upd_gbs / HBM_PEAK_GBS, "bytes_per_launch": upd_bytes,
+                          "avg_launch_ms": ms[2] / max(cnt[2], 1)},
         "step_algorithmic_tflops_per_gpu": step_flops * T * args.steps / elapsed / 1e12,
     }
     if exact is not None:
         rec["exact_f32"] = exact
-    traffic_file = os.path.join(HERE, "profiles", "pmc_traffic.json")
-    if os.path.exists(traffic_file):
-        try:
-            tr = json.load(open(traffic_file)).get(args.config, {})
-            rec["roofline"]["traffic"] = tr.get("graph_linear_bytes_per_launch")
-        except Exception:
-            pass
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        rec["cpu_baseline"] = cpu_baseline(d, x_cond, rows, args.cpu_steps, args.cpu_threads)
+        threads, cores = physical_cores()
+        rec["cpu_baseline"] = cpu_baseline(d, x_cond, rows, args.cpu_steps, args.cpu_threads or threads)
+        rec["cpu_baseline"]["host_cores"] = cores
         rec["speedup_vs_cpu_baseline"] = value / rec["cpu_baseline"]["value"]
     if dist:
         dist.destroy_process_group()

@@ -239,18 +239,26 @@ int sd_set_kernel_variant(int32_t gl_variant, int32_t gl4_tile);
 enum {
     SD_OPT_KERNEL_VARIANT = 1,  /* 0 auto, 1..5 force a graph-linear generation */
     SD_OPT_GL4_TILE = 2,        /* v4 tile <waves><row tiles><col tiles>, 0 = per shape */
-    SD_OPT_ROW_CHAINS = 3,      /* 1..8 concurrent row chains in sd_sample_loop */
+    SD_OPT_ROW_CHAINS = 3,      /* 1..8 concurrent row chains in sd_sample_loop; 0 = auto
+                                   (3, or 2 at <= SKELDIFF_SPLIT_ROWS rows) */
     SD_OPT_PRECISION = 4,       /* as sd_plan_set_precision */
-    SD_OPT_GL4_STAGING = 5,     /* v4 weight stages: 0 LDS-DMA, workgroup holds its CU's whole
-                                   LDS (default); 1 register-staged, CU shareable;
-                                   2 DIAGNOSTIC ONLY: LDS-DMA with the CU shareable -- reproduces the
-                                   §4c co-residency corruption, never for production use */
-    SD_OPT_SPLIT_ROUTE = 6      /* v4 split route for small launches (GEMM phase per (tile, node)
-                                   + mixing phase; bitwise identical results):
-                                   0 auto (rows per launch <= SKELDIFF_SPLIT_ROWS, default 1024),
-                                   1 never, 2 always, 3 always with the tiled GEMM phase
-                                   (k_gl4t: 128 rows x up to 192 columns of one node per
-                                   workgroup, for full batches) */
+    SD_OPT_GL4_STAGING = 5,     /* v4 weight stages: 0 LDS-DMA (default), 1 register-staged;
+                                   2 = 0 (a round-2 diagnostic setting, kept for compatibility) */
+    SD_OPT_SPLIT_ROUTE = 6,     /* v4 split route (GEMM phase per (tile, node) + mixing phase,
+                                   DESIGN.md §4d'; bitwise identical results): 0 auto (k_gl4y at
+                                   <= SKELDIFF_SPLIT_ROWS rows of the call, default 640; k_gl4t
+                                   for full batches where measured faster), 1 never, 2 always
+                                   (k_gl4y), 3 always with the tiled GEMM phase (k_gl4t: 128 rows
+                                   x up to 192 columns of one node per workgroup), 4 the tiled
+                                   GEMM phase except for to_qkv + attention (one-kernel fused
+                                   tile) */
+    SD_OPT_LAST_CHAINS = 7,     /* read-only: row chains the plan's last sd_sample_loop ran (the
+                                   SD_OPT_ROW_CHAINS value, fewer for batches under 32 x n rows);
+                                   0 before the first call */
+    SD_OPT_LAST_ROUTE = 8       /* read-only: kernels the plan's last sd_sample_loop launched, bits
+                                   1 one-kernel k_gl4, 2 fused to_qkv + attention k_gl4, 4 k_gl4y
+                                   GEMM phase, 8 k_gl4t GEMM phase, 16 split-route mixing /
+                                   attention phase, 32 v5 (J > 21), 64 exact-f32 kernels */
 };
 int sd_plan_set_option(sd_plan* plan, int32_t option, int64_t value);
 int sd_plan_get_option(const sd_plan* plan, int32_t option, int64_t* value);
@@ -285,11 +293,11 @@ size_t sd_gru_encode_workspace_bytes(const sd_gru_decoder_desc* desc, int64_t ro
 int sd_gru_encode(const sd_gru_decoder_desc* desc, const float* x, int64_t rows, int32_t frames, float* z,
                   void* workspace, size_t workspace_bytes, void* stream);
 /* Process DEFAULT of the row chains of sd_sample_loop for plans created afterwards (a plan keeps
- * its own: SD_OPT_ROW_CHAINS; SKELDIFF_CHAINS at load, default 3): the batch is split into
+ * its own: SD_OPT_ROW_CHAINS; SKELDIFF_CHAINS at load, default 0 = auto): the batch is split into
  * n row ranges (multiples of 32 rows; fewer when the batch is small) whose
  * T-step chains run on forked streams and overlap on the GPU.  Rows are independent, so the
  * results do not depend on n.  Returns the previous n; n = -1 only queries; SD_E_INVALID
- * outside [1, 8]. */
+ * outside [0, 8]. */
 int sd_set_row_chains(int32_t n);
 /* Arithmetic of the plan's graph-linear launches.  mode 0 (default):
  * f32-accurate -- 3 split f16 products per f32 product, within the f32-vs-f64 drift.  mode 1:

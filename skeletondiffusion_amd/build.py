@@ -5,6 +5,7 @@ from __future__ import annotations
 import os
 import shutil
 import subprocess
+import sys
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
@@ -28,7 +29,18 @@ def _stale() -> bool:
     return any(os.path.getmtime(os.path.join(CSRC, f)) > t for f in SOURCES + HEADERS)
 
 
-def build_library(force: bool = False, verbose: bool = False, debug_lds: bool = False, extra=(), tag="_dbg") -> str:
+# Device code is compiled WITHOUT packed-FP32 instructions (v_pk_fma/mul/add_f32).  Measured on
+# MI355X: a packed-FP32 instruction reading a register just written by an LDS load
+# returned zeros in lanes 48-63 whenever a workgroup of another kernel shared the CU (row chains,
+# concurrent plans), so the posterior update drew sigma * eps = 0 for some latents; with the
+# feature off every row-chain configuration is bitwise equal to one chain, at unchanged speed.
+# (The host pass of each hipcc call ignores the feature, with a one-line note that build filters.)
+DEVICE_FLAGS = ["-Xclang", "-target-feature", "-Xclang", "-packed-fp32-ops"]
+_FEATURE_NOTE = b"'-packed-fp32-ops' is not a recognized feature for this target"
+
+
+def build_library(force: bool = False, verbose: bool = False, debug_lds: bool = False, extra=(), tag="_dbg",
+                  packed_fp32: bool = False) -> str:
     """debug_lds: the diagnostic variant libskeldiff_dbg.so (-DSD_DEBUG_LDS: LDS integrity
     counters in k_gl4 / k_update, sd_debug_lds_counters); load it with SKELDIFF_LIB."""
     variant = debug_lds or bool(extra)  # a diagnostic variant: libskeldiff{tag}.so, never the product
@@ -39,12 +51,20 @@ def build_library(force: bool = False, verbose: bool = False, debug_lds: bool = 
     for src in SOURCES:  # one hipcc per translation unit, in parallel
         obj = os.path.join(CSRC, src.replace(".hip", tag + ".o" if variant else ".o"))
         cmd = [_hipcc(), "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-c",
-               "-Wno-pass-failed"] + (["-DSD_DEBUG_LDS"] if debug_lds else []) + list(extra) + [os.path.join(CSRC, src), "-o", obj]
+               "-Wno-pass-failed"] + ([] if packed_fp32 else DEVICE_FLAGS) + (["-DSD_DEBUG_LDS"] if debug_lds else []) + \
+            list(extra) + [os.path.join(CSRC, src), "-o", obj]
         if verbose:
             print(" ".join(cmd))
-        procs.append((src, subprocess.Popen(cmd)))
+        procs.append((src, subprocess.Popen(cmd, stderr=subprocess.PIPE)))
         objs.append(obj)
-    failed = [src for src, pr in procs if pr.wait() != 0]
+    failed = []
+    for src, pr in procs:
+        _, err = pr.communicate()
+        msg = b"\n".join(l for l in err.splitlines() if _FEATURE_NOTE not in l)
+        if msg.strip():
+            sys.stderr.write(msg.decode(errors="replace") + "\n")
+        if pr.returncode != 0:
+            failed.append(src)
     if failed:
         raise RuntimeError("hipcc failed: " + ", ".join(failed))
     tmp = out + ".tmp"
@@ -56,6 +76,4 @@ def build_library(force: bool = False, verbose: bool = False, debug_lds: bool = 
 
 
 if __name__ == "__main__":
-    import sys
-
     print(build_library(force=True, verbose=True, debug_lds="--debug-lds" in sys.argv))

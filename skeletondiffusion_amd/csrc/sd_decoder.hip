@@ -245,7 +245,6 @@ int sd_gru_decode(const sd_gru_decoder_desc* d, const float* x, const float* h, 
     DHIP(sd::launch_graph_linear(sd::gl(d, w.xprev, sd::KF, h, L, w.winit, d->init_bias, w.ghat_init, H, w.h0, JH, rows, 0), false, s));
     DHIP(sd::launch_graph_linear(sd::gl(d, w.xlast, sd::KF, h, L, w.wih, d->bias_ih, w.ident, 3 * H, w.xres, JH3, rows, 0), false, s));
     size_t gate_lds = ((size_t)J * 3 * H + (size_t)J * J) * sizeof(float);
-    if (gate_lds > 64 * 1024) gate_lds = 160 * 1024;  // > 64 KB holds the CU
     if (gate_lds > 64 * 1024)
         DHIP(hipFuncSetAttribute((const void*)sd::k_gru_gate, hipFuncAttributeMaxDynamicSharedMemorySize, (int)gate_lds));
     float* hx = w.h0;
@@ -307,7 +306,6 @@ int sd_gru_encode(const sd_gru_decoder_desc* d, const float* x, int64_t rows, in
     DHIP(sd::launch_ghat(d->fc_G, w.ghat_fc, J, 1, s));
     const int64_t JH = (int64_t)J * H, JH3 = 3 * JH;
     size_t gate_lds = ((size_t)J * 3 * H + (size_t)J * J) * sizeof(float);
-    if (gate_lds > 64 * 1024) gate_lds = 160 * 1024;  // > 64 KB holds the CU
     if (gate_lds > 64 * 1024)
         DHIP(hipFuncSetAttribute((const void*)sd::k_gru_gate, hipFuncAttributeMaxDynamicSharedMemorySize, (int)gate_lds));
     // x (rows, frames, J, F): frame t -> xprev via k_pad_frame's (rows, 2, J, F) view at stride

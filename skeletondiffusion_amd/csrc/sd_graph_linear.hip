@@ -249,13 +249,12 @@ static hipError_t gl2_launch(const GLArgs& a, bool rms, hipStream_t s) {
     const dim3 grid((unsigned)(ntile_c * ntile_r));
     size_t lds = (size_t)(2 * a.ntypes * NT * 16 + a.J * a.J) * sizeof(float);
     if (lds > 160 * 1024) return hipErrorInvalidValue;
-    // LDS-DMA weight stages above 64 KB: hold the whole CU, as k_gl4 does
-    if (lds > 64 * 1024) lds = 160 * 1024;
     auto kt = rms ? k_gl2<JM, EXACT, NCB, true, PREF, MINW> : k_gl2<JM, EXACT, NCB, false, PREF, MINW>;
     if (lds > 64 * 1024) {
         hipError_t e = hipFuncSetAttribute((const void*)kt, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         if (e != hipSuccess) return e;
     }
+    g_route_bits |= kRouteExact;
     hipLaunchKernelGGL(kt, grid, dim3(256), lds, s, a);
     return hipGetLastError();
 }

@@ -269,13 +269,12 @@ static hipError_t gl3_launch(const GLArgs& a, bool rms, hipStream_t s) {
     const size_t wfl = (size_t)2 * a.ntypes * 512, yfl = (size_t)J * YSTRIDE;
     size_t lds = ((wfl > yfl ? wfl : yfl) + (size_t)J * J) * sizeof(float);
     if (lds > 160 * 1024) return hipErrorInvalidValue;
-    // LDS-DMA weight stages above 64 KB: hold the whole CU, as k_gl4 does
-    if (lds > 64 * 1024) lds = 160 * 1024;
     auto kt = rms ? k_gl3<J, true> : k_gl3<J, false>;
     if (lds > 64 * 1024) {
         hipError_t e = hipFuncSetAttribute((const void*)kt, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         if (e != hipSuccess) return e;
     }
+    g_route_bits |= kRouteExact;
     hipLaunchKernelGGL(kt, grid, dim3(256), lds, s, a);
     return hipGetLastError();
 }

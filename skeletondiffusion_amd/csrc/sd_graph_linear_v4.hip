@@ -215,7 +215,6 @@ struct YOut {
 
 template <bool RMS, int PREC, bool ROWMAJOR, int PF = 8>  // PF: chunks in flight
 __global__ __launch_bounds__(256) void k_gl4y(const GLArgs p, int ntile_c, int64_t ntile_r, const YOut yo) {
-    if ((p.diag & kDiagArgsHash) && threadIdx.x == 0 && p.status && !kernel_args_intact()) atomicOr(p.status, 0x800u);
     const int lane = threadIdx.x & 63, l32 = lane & 31, h = lane >> 5;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int64_t u = (int64_t)blockIdx.x * 4 + wave;
@@ -331,22 +330,12 @@ __global__ __launch_bounds__(256) void k_gl4y(const GLArgs p, int ntile_c, int64
 // k_gl4's, so phase 2 (k_gl4 MODE 2 / 3) reproduces the one-kernel route bit for bit.
 template <bool RMS, int PREC, int CT, int NCH, bool ROWMAJOR, int PF = 4>  // NCH: 16-deep k chunks (K / 16)
 __global__ __launch_bounds__(256, 2) void k_gl4t(const GLArgs p, int ncg, int64_t ntile_r, const YOut yo) {
-    if (p.diag & 8) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // diagnostic (SKELDIFF_DIAG)
-    if ((p.diag & 16) && threadIdx.x == 0 && p.status &&  // diagnostic: do these arguments belong to this grid?
-        (ntile_r != (p.B + 31) / 32 || (int64_t)gridDim.x != ((ntile_r + 3) / 4) * p.J * ncg))
-        atomicOr(p.status, 4u);
-    if ((p.diag & kDiagArgsHash) && threadIdx.x == 0 && p.status && !kernel_args_intact()) atomicOr(p.status, 0x100u);
-    const uint64_t dt0 = (p.diag & kDiagSelfCheck) ? __builtin_amdgcn_s_memrealtime() : 0;
     constexpr int TILE_H = PREC ? 512 : 1024;   // halves of one 32-column tile per chunk
     constexpr int PPT = TILE_H / 8;             // 16-B pieces per tile
     constexpr int NP = (CT * PPT + 255) / 256;  // staged pieces per thread
     constexpr int TS = 36;                      // floats per row of a wave's 32 x 32 output transpose
     constexpr int SB = 2 * CT * TILE_H * 2 > 4 * 32 * TS * 4 ? 2 * CT * TILE_H * 2 : 4 * 32 * TS * 4;
-#ifdef SD_DIAG_GL4T_DYNLDS  // diagnostic build: the same bytes as dynamic LDS
-    extern __shared__ __attribute__((aligned(16))) char smem_raw[];
-#else
     __shared__ __attribute__((aligned(16))) char smem_raw[SB];  // weight stages, then the transposes
-#endif
     _Float16(*sW)[CT * TILE_H] = reinterpret_cast<_Float16(*)[CT * TILE_H]>(smem_raw);
     const int tid = threadIdx.x, lane = tid & 63, l32 = lane & 31, h = lane >> 5;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -361,15 +350,8 @@ __global__ __launch_bounds__(256, 2) void k_gl4t(const GLArgs p, int ncg, int64_
     // walked every node: 196 MB fetched per launch for ~45 MB of operands)
     const int cg = (int)(u % ncg);
     const int64_t nrg = (ntile_r + 3) / 4;
-    int j;
-    int64_t rgi;
-    if (p.diag & 4096) {  // diagnostic (SKELDIFF_DIAG): the previous row-group-major order
-        j = (int)((u / ncg) % J);
-        rgi = (u / ncg) / J;
-    } else {
-        j = (int)((u / ncg) / nrg);
-        rgi = (u / ncg) % nrg;
-    }
+    const int j = (int)((u / ncg) / nrg);
+    const int64_t rgi = (u / ncg) % nrg;
     const int64_t tr = rgi * 4 + wave;
     const bool live = tr < ntile_r;  // wave-uniform; a dead wave still stages weights and joins barriers
     const int64_t row0 = (live ? tr : 0) * 32;
@@ -500,14 +482,10 @@ __global__ __launch_bounds__(256, 2) void k_gl4t(const GLArgs p, int ncg, int64_
         for (int i = 0; i < PF; ++i) {
             const int c = c0 + i;
             store_w(i & 1);
-#ifdef SD_DIAG_GL4T_SYNCTHREADS  // diagnostic build: a full __syncthreads()
-            __syncthreads();
-#else
             __builtin_amdgcn_s_waitcnt(0xC07F);
             asm volatile("" ::: "memory");
             __builtin_amdgcn_s_barrier();
             asm volatile("" ::: "memory");
-#endif
             // unconditional loads (past the end: a clamped, unused chunk): a branch around them
             // made the waitcnt pass merge both paths and drain the x ring every chunk
             load_w(min(c + 1, nchunk - 1));
@@ -518,7 +496,7 @@ __global__ __launch_bounds__(256, 2) void k_gl4t(const GLArgs p, int ncg, int64_
         }
     }
     __syncthreads();  // every wave past its last chunk: the stages become the output transposes
-    if (!live) return;  // (no stores)
+    if (!live) return;
     if (p.status && __builtin_amdgcn_ballot_w64(amx >= 65504.0f) != 0 && lane == 0) atomicOr(p.status, 1u);
     float sc[16];
 #pragma unroll
@@ -552,10 +530,6 @@ __global__ __launch_bounds__(256, 2) void k_gl4t(const GLArgs p, int ncg, int64_
         }
         __builtin_amdgcn_wave_barrier();
     }
-    if ((p.diag & kDiagArgsHash) && tid == 0 && p.status && !kernel_args_intact()) atomicOr(p.status, 0x200u);
-    if ((p.diag & kDiagSelfCheck) && tid == 0 && p.dbg) diag_wg_log(p.dbg, 1, dt0);
-    if (p.diag & kDiagRelease) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    if (p.diag & 1) __threadfence();  // diagnostic (SKELDIFF_DIAG): agent-scope release of Y
 }
 
 // Epilogue of the fused to_qkv + Attention kernel (MODE 1), J <= 32, dh = 32, 8 waves, a
@@ -743,9 +717,6 @@ __device__ __forceinline__ void attention_epilogue(const GLArgs& p, floatx16 (&a
 //   (global_load_dwordx4 a chunk ahead, ds_write_b128 after the chunk's MFMAs).
 template <int J, int NW, int RT, int CT, bool RMS, int DBG = 0, int MODE = 0, int XP = 0, int PREC = 0, int STG = 0>
 __global__ __launch_bounds__(NW * 64, 1) void k_gl4(const GLArgs p) {
-    if (p.diag & 8) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // diagnostic (SKELDIFF_DIAG)
-    if ((p.diag & kDiagArgsHash) && threadIdx.x == 0 && p.status && !kernel_args_intact()) atomicOr(p.status, 0x400u);
-    const uint64_t dt0 = (p.diag & kDiagSelfCheck) ? __builtin_amdgcn_s_memrealtime() : 0;
     static_assert(MODE == 0 || MODE == 2 || (CT == 3 && RT == 1 && J <= 32 && NW == 8), "attention mode: 32 x (q|k|v)");
     static_assert(MODE < 2 || (RT == 1 && XP == 0 && STG == 0 && DBG == 0), "split-route phase 2: one 32-row tile");
     constexpr int NPW = (J + NW - 1) / NW;  // nodes per wave
@@ -774,9 +745,6 @@ __global__ __launch_bounds__(NW * 64, 1) void k_gl4(const GLArgs p) {
     float* sF = sG + J * J;  // FiLM (scale + 1 | shift) for this workgroup's columns
 
     const int ntile_c = ATT ? p.attn_heads : (p.N + COLS - 1) / COLS;
-    if ((p.diag & 16) && tid == 0 && p.status &&  // diagnostic: do these arguments belong to this grid?
-        (int64_t)gridDim.x != ntile_c * ((p.B + 32 * RT - 1) / (32 * RT)) * (MODE == 2 ? 2 : MODE == 3 ? 4 : 1))
-        atomicOr(p.status, 4u);
     const int nwg = gridDim.x, xcd = blockIdx.x & 7, q8 = nwg >> 3, r8 = nwg & 7;
     // XCD-aware order: consecutive L (the column tiles of one row tile) on one XCD, so x is
     // fetched into that XCD's L2 once.  attn_order 1 (fused attention): L = blockIdx, i.e. head
@@ -838,7 +806,6 @@ __global__ __launch_bounds__(NW * 64, 1) void k_gl4(const GLArgs p) {
         floatx4 yv[NYL];
         float gv[NGL];
         float f0 = 1.0f, f1 = 0.0f;
-        if (p.diag & 2) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // diagnostic (SKELDIFF_DIAG)
 #pragma unroll
         for (int k = 0; k < NYL; ++k) {
             const int q = tid + k * NTH;
@@ -1209,13 +1176,9 @@ __global__ __launch_bounds__(NW * 64, 1) void k_gl4(const GLArgs p) {
 #endif
     if constexpr (MODE == 1) {
         attention_epilogue<J, NW, NPW>(p, acc, smem, sG, row0, ctile, wave, lane);
-        if ((p.diag & kDiagSelfCheck) && tid == 0 && p.dbg) diag_wg_log(p.dbg, 2 + MODE, dt0);
-        if (p.diag & kDiagRelease) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
         return;
     } else if constexpr (MODE == 3) {
         attention_epilogue<J, NW, NPW, true>(p, acc, smem, sG, row0, ctile, wave, lane, slab);
-        if ((p.diag & kDiagSelfCheck) && tid == 0 && p.dbg) diag_wg_log(p.dbg, 2 + MODE, dt0);
-        if (p.diag & kDiagRelease) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
         return;
     }
     // ---- mixing + epilogue, one 16-row slab at a time.  Z^T = Y^T G-hat^T on 16x16x4 f32 MFMA
@@ -1378,13 +1341,11 @@ __global__ __launch_bounds__(NW * 64, 1) void k_gl4(const GLArgs p) {
             o[7] = (unsigned)(ts[7] - ts[6]);  // shader-clock cycles of chunks 2 .. end
         }
     }
-    if ((p.diag & kDiagSelfCheck) && tid == 0 && p.dbg) diag_wg_log(p.dbg, 2 + MODE, dt0);
-    if (p.diag & kDiagRelease) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
 }
 
-// v4 weight staging (GLArgs::gl4_stage): 0 = LDS-DMA stages, the workgroup holds
-// its CU's whole LDS; 1 = register-staged stages, exact LDS size (CU shareable).  Process default
-// SKELDIFF_GL4_STAGE for new plans.
+// v4 weight staging (GLArgs::gl4_stage): 0 = LDS-DMA stages, 1 = register-staged stages (2, a
+// round-2 diagnostic setting, is now the same as 0: every launch takes its exact LDS).  Process
+// default SKELDIFF_GL4_STAGE for new plans.
 static int g_gl4_stage = [] {
     const char* e = getenv("SKELDIFF_GL4_STAGE");
     const int v = e ? atoi(e) : 0;
@@ -1425,28 +1386,16 @@ static hipError_t gl4_launch_t(const GLArgs& a, bool rms, hipStream_t s) {
                                  : (size_t)J * (16 * (COLS + 4) + 16);
     size_t lds = ((wfl > yfl ? wfl : yfl) + (size_t)J * J + 2 * COLS) * sizeof(float);
     if (lds > 160 * 1024) return hipErrorNotSupported;
-    // LDS-DMA staging (STG 0): the workgroup takes its CU's whole LDS, so no other kernel's
-    // workgroup shares the CU (these tiles run one workgroup per CU anyway, by registers).  With
-    // concurrent row chains, STG-0 workgroups co-resident with another kernel's LDS-holding
-    // workgroups (k_update's tables) gave wrong, run-to-run different elements; the same
-    // co-residency with register-staged stages (STG 1) is bitwise correct, as is STG 0 alone on
-    // its CU.  DESIGN.md §4c has the measurements and the probes that rule out LDS-DMA addressing,
-    // placement and the vmcnt / barrier ordering of the K loop.
-    // gl4_stage 2 (diagnostic only): LDS-DMA stages at their exact size, so the hazard can be
-    // reproduced (tools/lds_hazard.py)
-    // Split-route phase 2 (MODE 2 / 3) has no weight stages: exact size.
-    if (MODE < 2 && STG == 0 && a.gl4_stage != 2) lds = 160 * 1024;
-    // Any allocation above 64 KB beside other row chains holds the whole CU too.  Alone on the GPU
-    // (one chain) the split route's phase 2 shares CUs only with workgroups of its own launch, which
-    // every measurement found exact: MODE 3 at J = 21 (70 KB) then runs two per CU.
-    if (lds > 64 * 1024 && a.gl4_stage != 2 && (MODE < 2 || a.concurrent)) lds = 160 * 1024;
-    if (MODE == 2 && (a.diag & 256)) lds = 160 * 1024;  // diagnostic (SKELDIFF_DIAG)
+    // Every launch takes exactly the LDS it uses and may share its CU with other kernels' workgroups
+    // (row chains, concurrent plans): the co-residency hazard of rounds 1-2 was the packed-FP32
+    // instructions of the co-resident update kernel, not these tiles (build.py).
     auto kt = rms ? k_gl4<J, NW, RT, CT, true, DBG, MODE, XP, PREC, STG> : k_gl4<J, NW, RT, CT, false, DBG, MODE, XP, PREC, STG>;
     if (lds > 64 * 1024) {
         hipError_t e = hipFuncSetAttribute((const void*)kt, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         if (e != hipSuccess) return e;
     }
-    hipLaunchKernelGGL(kt, grid, dim3(NW * 64), lds, s, sealed(a));
+    g_route_bits |= MODE >= 2 ? kRouteMixPhase : MODE == 1 ? kRouteFusedAttn : kRouteOneKernel;
+    hipLaunchKernelGGL(kt, grid, dim3(NW * 64), lds, s, a);
     return hipGetLastError();
 }
 
@@ -1471,7 +1420,7 @@ int set_gl4_tile(int cfg) {
 // the attention epilogue per 8-row slab).  Same arithmetic in the same order as the one-kernel
 // route, so the results are bitwise identical and the route can follow the shard size.
 // Auto threshold on the rows of the whole sampling call (all row chains; GLArgs::route_rows):
-// process default SKELDIFF_SPLIT_ROWS = 1024.  Measured (B = 400 / 800 / 1600 at T = 100, three
+// process default SKELDIFF_SPLIT_ROWS = 640.  Measured (B = 400 / 800 / 1600 at T = 100, three
 // chains): split 5,764 / 9,018 / 11,389 futures/s vs one-kernel 4,440 / 8,666 / 12,594.
 static int64_t g_split_rows = [] {
     const char* e = getenv("SKELDIFF_SPLIT_ROWS");
@@ -1484,13 +1433,14 @@ int64_t split_rows_default() { return g_split_rows; }
 // (k_gl4y), 3 always (k_gl4t).
 static int split_route(const GLArgs& a, bool attn) {
     if (a.split == 1 || !a.zs || (a.N & 31) || a.J > 32) return 0;
-    if (a.prec == 2 && a.split != 3 && !(a.split == 0 && a.J == 17)) return 0;  // bf16: tiled only (J = 17 auto)
+    if (a.prec == 2 && a.split < 3 && !(a.split == 0 && a.J == 17)) return 0;  // bf16: tiled only (J = 17 auto)
     const int64_t tiles = (a.B + 31) / 32;
     if (tiles * 32 * a.J * (int64_t)a.N > a.zs_cap) return 0;
     if (a.zs == a.out || a.zs == a.x1 || a.zs == a.x2 || a.zs == a.res) return 0;
     if (attn && (a.attn_heads * 96 != a.N)) return 0;
     if (a.split == 2) return a.prec == 2 ? 0 : 1;
     if (a.split == 3) return 2;
+    if (a.split == 4) return attn ? 0 : 2;  // tiled GEMM phase; to_qkv + attention on the one-kernel tile
     if (a.gl4_cfg != 0) return 0;
     const int64_t rows = a.route_rows > 0 ? a.route_rows : a.B;
     if (rows <= g_split_rows) return a.prec == 2 ? 0 : 1;
@@ -1509,12 +1459,13 @@ template <bool ROWMAJOR>
 static hipError_t launch_gl4y(const GLArgs& a, bool rms, int ntc, int64_t ntile_r, const YOut& yo, hipStream_t s) {
     const int64_t units = ntile_r * a.J * ntc;
     const dim3 grid((unsigned)((units + 3) / 4)), block(256);
+    g_route_bits |= kRouteGemmWave;
     if (a.prec == 1) {
-        if (rms) hipLaunchKernelGGL((k_gl4y<true, 1, ROWMAJOR>), grid, block, 0, s, sealed(a), ntc, ntile_r, yo);
-        else hipLaunchKernelGGL((k_gl4y<false, 1, ROWMAJOR>), grid, block, 0, s, sealed(a), ntc, ntile_r, yo);
+        if (rms) hipLaunchKernelGGL((k_gl4y<true, 1, ROWMAJOR>), grid, block, 0, s, a, ntc, ntile_r, yo);
+        else hipLaunchKernelGGL((k_gl4y<false, 1, ROWMAJOR>), grid, block, 0, s, a, ntc, ntile_r, yo);
     } else {
-        if (rms) hipLaunchKernelGGL((k_gl4y<true, 0, ROWMAJOR>), grid, block, 0, s, sealed(a), ntc, ntile_r, yo);
-        else hipLaunchKernelGGL((k_gl4y<false, 0, ROWMAJOR>), grid, block, 0, s, sealed(a), ntc, ntile_r, yo);
+        if (rms) hipLaunchKernelGGL((k_gl4y<true, 0, ROWMAJOR>), grid, block, 0, s, a, ntc, ntile_r, yo);
+        else hipLaunchKernelGGL((k_gl4y<false, 0, ROWMAJOR>), grid, block, 0, s, a, ntc, ntile_r, yo);
     }
     return hipGetLastError();
 }
@@ -1530,8 +1481,8 @@ hipError_t launch_gemm_split(const GLArgs& a, bool rms, float* z, int64_t z_rs, 
     const int ntc = (a.N + 31) / 32;
     const YOut yo{z, z_rs, a.N, 32 * z_rs};
     // the tiled phase (128 rows x up to 192 columns of one node per workgroup) where the shape
-    // has one; SKELDIFF_DIAG bit 10 keeps k_gl4y (comparison runs)
-    if (!(a.diag & 1024) && ((uintptr_t)z & 15) == 0 && (z_rs & 3) == 0 && (a.N & 3) == 0) {  // 16-B Y pieces
+    // has one
+    if (((uintptr_t)z & 15) == 0 && (z_rs & 3) == 0 && (a.N & 3) == 0) {  // 16-B Y pieces
         const hipError_t e = launch_gl4t<true>(a, rms, ntile_r, yo, s);
         if (e != hipErrorNotSupported) return e;
     }
@@ -1547,26 +1498,8 @@ static hipError_t launch_gl4t_ct(const GLArgs& a, bool rms, int64_t ntile_r, con
     if constexpr (!ROWMAJOR) {  // bf16 mode (precision 2): the split route's scratch output only
         if (a.prec == 2) kt = rms ? k_gl4t<true, 2, CT, NCH, false> : k_gl4t<false, 2, CT, NCH, false>;
     }
-    size_t dyn = 0;
-    // Beside other kernels' workgroups (concurrent row chains) k_gl4t gave wrong, run-to-run
-    // different rows unless its workgroup holds the CU (tools/gpu_diag*.sh): then
-    // it takes the whole LDS (one workgroup per CU).  One stream: two per CU, of this launch only.
-#ifdef SD_DIAG_GL4T_DYNLDS
-    dyn = 2 * CT * 1024 * 2 > 4 * 32 * 36 * 4 ? 2 * CT * 1024 * 2 : 4 * 32 * 36 * 4;  // k_gl4t's SB
-#endif
-#ifdef SD_DIAG_GL4T_SHARE  // diagnostic build: k_gl4t shares CUs under row chains
-    if (a.diag & 128) {
-#else
-    if (a.concurrent || (a.diag & 128)) {
-#endif
-        hipFuncAttributes fa;
-        hipError_t e = hipFuncGetAttributes(&fa, (const void*)kt);
-        if (e != hipSuccess) return e;
-        dyn = 160 * 1024 - fa.sharedSizeBytes;
-        if ((e = hipFuncSetAttribute((const void*)kt, hipFuncAttributeMaxDynamicSharedMemorySize, (int)dyn)) != hipSuccess)
-            return e;
-    }
-    hipLaunchKernelGGL(kt, grid, block, dyn, s, sealed(a), ncg, ntile_r, yo);
+    g_route_bits |= kRouteGemmTiled;
+    hipLaunchKernelGGL(kt, grid, block, 0, s, a, ncg, ntile_r, yo);
     return hipGetLastError();
 }
 

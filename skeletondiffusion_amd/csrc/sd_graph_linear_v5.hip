@@ -228,6 +228,7 @@ hipError_t launch_graph_linear_v5(const GLArgs& a, bool rms, hipStream_t s) {
     hipError_t e = a.variant == 5 ? hipErrorNotSupported : launch_gemm_split(a, rms, z, z_rs, s);
     if (e == hipErrorNotSupported) {
         const dim3 g1((unsigned)((a.N + TN - 1) / TN), (unsigned)row_tiles, (unsigned)a.J);
+        g_route_bits |= kRouteV5Mix;
         if (rms)
             hipLaunchKernelGGL(k_gl5_gemm<true>, g1, dim3(256), 0, s, a, z, z_rs);
         else
@@ -237,6 +238,7 @@ hipError_t launch_graph_linear_v5(const GLArgs& a, bool rms, hipStream_t s) {
     if (e != hipSuccess) return e;
     const dim3 g2((unsigned)a.B, (unsigned)((a.N + 63) / 64));
     const int vec = ((uintptr_t)z & 15) == 0 && (a.N & 3) == 0 && (z_rs & 3) == 0;
+    g_route_bits |= kRouteV5Mix;
     hipLaunchKernelGGL(k_gl5_mix, g2, dim3(256), 0, s, a, (const float*)z, z_rs, vec);
     return hipGetLastError();
 }

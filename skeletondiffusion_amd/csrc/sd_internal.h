@@ -3,8 +3,6 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
-#include <cstddef>
-#include <cstring>
 #include <string>
 #include <stdint.h>
 
@@ -69,77 +67,21 @@ struct GLArgs {
     // bf16 storage of operands / result (precision mode 2): the tensor
     // holds bf16 elements at the same element offsets (row-major only)
     int x1_bf16, x2_bf16, res_bf16, out_bf16;
-    // diagnostics only (SKELDIFF_DIAG, read once per process): bit 0 agent-scope release after the
-    // split route's phase 1 stores, bit 1 agent-scope acquire before phase 2's Y loads, bit 3
-    // agent-scope acquire at the start of every v4 / update kernel
-    int diag;
-    int concurrent;  // other row chains of the call run on other streams (k_gl4t then holds its CU)
-    unsigned args_hash;  // diagnostics (diag bit 14): FNV-1a of this block with args_hash = 0 (sealed)
-    unsigned pad_;
 };
 int diag_flags();  // SKELDIFF_DIAG (sd_plan.hip)
 
-// Diagnostics, SKELDIFF_DIAG bit 14: the launch site seals the argument block
-// (FNV-1a over its 32-bit words, args_hash counted as 0; GLArgs is zero-initialised, so padding
-// is 0) and one thread per workgroup recomputes the hash from the kernarg segment itself
-// (kernel_args_intact), at entry and (k_gl4t) after the stores: a torn, stale or foreign
-// argument block shows as a mismatch (status bits 0x100 at entry, 0x200 at exit).
-constexpr int kDiagArgsHash = 1 << 14;
-constexpr int kArgsWords = (int)(sizeof(GLArgs) / 4);
-constexpr int kArgsHashWord = (int)(offsetof(GLArgs, args_hash) / 4);
-__host__ __device__ inline unsigned fnv_words(const unsigned* w) {
-    unsigned h = 2166136261u;
-    for (int i = 0; i < kArgsWords; ++i) h = (h ^ (i == kArgsHashWord ? 0u : w[i])) * 16777619u;
-    return h;
-}
-inline GLArgs sealed(const GLArgs& a) {
-    GLArgs b = a;
-    if (a.diag & kDiagArgsHash) {
-        unsigned w[kArgsWords];
-        b.args_hash = 0;
-        std::memcpy(w, &b, sizeof(GLArgs));
-        b.args_hash = fnv_words(w);
-    }
-    return b;
-}
-// GLArgs is the kernel's first parameter: kernarg offset 0
-__device__ __forceinline__ bool kernel_args_intact() {
-    typedef const volatile __attribute__((address_space(4))) unsigned kword;
-    kword* k = (kword*)__builtin_amdgcn_kernarg_segment_ptr();
-    unsigned h = 2166136261u;
-#pragma nounroll
-    for (int i = 0; i < kArgsWords; ++i) h = (h ^ (i == kArgsHashWord ? 0u : k[i])) * 16777619u;
-    return h == k[kArgsHashWord];
-}
-
-// Diagnostics, SKELDIFF_DIAG bit 15: k_update's self-check (k_update_chk) and a
-// per-workgroup log of the split-route kernels, into one device buffer (diag_buffer(), passed as
-// GLArgs::dbg / UpdArgs::dbg): word 0 failing update threads, word 1 logged workgroups; update
-// records (16 words) from kDiagUpdBase, workgroup records {tag, blockIdx, HW_ID, XCC_ID,
-// s_memrealtime at entry (2 words), at exit (2 words)} from kDiagWgBase.
-constexpr int kDiagSelfCheck = 1 << 15;
-constexpr int kDiagRelease = 1 << 16;    // every wave of k_gl4t / k_gl4 / k_update ends with an agent-scope release
-constexpr unsigned kDiagWords = 1u << 22;
-constexpr unsigned kDiagUpdBase = 16, kDiagUpdMax = 1u << 15;  // 16-word update records
-constexpr unsigned kDiagWgBase = kDiagUpdBase + 16 * kDiagUpdMax;
-constexpr unsigned kDiagWgMax = (kDiagWords - kDiagWgBase) / 8;
-constexpr int kHwRegHwId = (31 << 11) | 4;    // s_getreg: HW_REG_HW_ID, 32 bits
-constexpr int kHwRegXccId = (31 << 11) | 20;  // s_getreg: HW_REG_XCC_ID, 32 bits
-unsigned* diag_buffer();  // allocated (zeroed) on first use, never during a capture
-__device__ __forceinline__ void diag_wg_log(unsigned* dbg, unsigned tag, uint64_t t0) {
-    const unsigned i = atomicAdd(&dbg[1], 1u);
-    if (i >= kDiagWgMax) return;
-    unsigned* r = dbg + kDiagWgBase + 8 * (size_t)i;
-    const uint64_t t1 = __builtin_amdgcn_s_memrealtime();
-    r[0] = tag;
-    r[1] = blockIdx.x;
-    r[2] = __builtin_amdgcn_s_getreg(kHwRegHwId);
-    r[3] = __builtin_amdgcn_s_getreg(kHwRegXccId);
-    r[4] = (unsigned)t0;
-    r[5] = (unsigned)(t0 >> 32);
-    r[6] = (unsigned)t1;
-    r[7] = (unsigned)(t1 >> 32);
-}
+// Kernels a sampling call launched (SD_OPT_LAST_ROUTE): every graph-linear / attention launch site
+// ORs its bit into this host thread's word while run_denoiser records (eager) or captures (graph).
+enum RouteBits : unsigned {
+    kRouteOneKernel = 1,   // k_gl4 MODE 0: one-kernel graph-linear tile
+    kRouteFusedAttn = 2,   // k_gl4 MODE 1: one-kernel to_qkv + attention
+    kRouteGemmWave = 4,    // k_gl4y: small-batch split route, GEMM phase
+    kRouteGemmTiled = 8,   // k_gl4t: tiled split route (and v5) GEMM phase
+    kRouteMixPhase = 16,   // k_gl4 MODE 2 / 3: split-route mixing / attention phase
+    kRouteV5Mix = 32,      // k_gl5_gemm / k_gl5_mix (J > 21)
+    kRouteExact = 64       // exact-f32 generations v1-v3 and k_attention
+};
+extern thread_local unsigned g_route_bits;
 
 // f16 hi/lo split of a (types, N, K) f32 weight in MFMA B-fragment order (sd_graph_linear_v4.hip)
 struct SplitW {
@@ -171,7 +113,6 @@ struct UpdArgs {
     int64_t B; int J; int D;
     unsigned* dbg;  // SD_DEBUG_LDS builds only
     int x0_bf16, xt_bf16, out_bf16;  // bf16 latents (precision mode 2); out2 / records stay f32
-    int diag;                        // SKELDIFF_DIAG (diagnostics only, as GLArgs::diag)
     // diagnostics only (sd_debug_update_dump): the J values of x0 (activation + clamp applied),
     // x_t and sigma eps each thread computed from, stored after its outputs; null = off
     float* dump_x0; float* dump_xt; float* dump_ev;

@@ -20,6 +20,8 @@
 
 namespace sd {
 
+thread_local unsigned g_route_bits = 0;
+
 typedef float floatx4 __attribute__((ext_vector_type(4)));
 typedef float floatx2 __attribute__((ext_vector_type(2)));
 typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
@@ -194,6 +196,7 @@ static hipError_t gl_dispatch_rms(const GLArgs& a, bool rms, hipStream_t s) {
     const int ntile_c = (a.N + 16 * NCB - 1) / (16 * NCB);
     const int64_t ntile_r = (a.B + 63) / 64;
     const dim3 grid((unsigned)(ntile_c * ntile_r));
+    g_route_bits |= kRouteExact;
     if (rms)
         hipLaunchKernelGGL((k_graph_linear<JM, EXACT, NCB, true>), grid, dim3(256), 0, s, a);
     else
@@ -372,6 +375,7 @@ hipError_t launch_attention(const AttnArgs& a, hipStream_t s) {
     if (a.B <= 0) return hipSuccess;
     const int64_t waves = a.B * a.heads;
     const dim3 grid((unsigned)((waves + 3) / 4));
+    g_route_bits |= kRouteExact;
     if (a.J <= 16) hipLaunchKernelGGL((k_attention<1>), grid, dim3(256), 0, s, a);
     else if (a.J <= 32) hipLaunchKernelGGL((k_attention<2>), grid, dim3(256), 0, s, a);
     else if (a.J <= 48) hipLaunchKernelGGL((k_attention<3>), grid, dim3(256), 0, s, a);
@@ -524,32 +528,19 @@ hipError_t launch_copy_rows(float* dst, int64_t dst_rs, const float* src, int64_
 // wave-uniform broadcasts.  HBM-bound: 4 * J * D * 4 B per row (x0, x_t, eps in; x_{t-1} out).
 // =============================================================================================
 
-template <int JM, bool EXACT, bool GT = false>  // GT: step tables read from global memory (no LDS)
+template <int JM, bool EXACT>
 __global__ __launch_bounds__(256) void k_update(const UpdArgs p) {
-    if (p.diag & 8) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // diagnostic (SKELDIFF_DIAG)
     const int J = EXACT ? JM : p.J;
-    const float *sC1, *sC2, *sU, *sS;
-    if constexpr (GT) {
-        sC1 = p.C1;
-        sC2 = p.C2;
-        sU = p.U;
-        sS = p.sig;
-    } else {
-        __shared__ float tC1[JM * JM], tC2[JM * JM], tU[JM * JM], tS[JM];
-        if (!p.iso) {
-            for (int i = threadIdx.x; i < J * J; i += 256) {
-                tC1[i] = p.C1[i];
-                tC2[i] = p.C2[i];
-                tU[i] = p.U[i];
-            }
-            for (int i = threadIdx.x; i < J; i += 256) tS[i] = p.sig[i];
+    __shared__ float sC1[JM * JM], sC2[JM * JM], sU[JM * JM], sS[JM];
+    if (!p.iso) {
+        for (int i = threadIdx.x; i < J * J; i += 256) {
+            sC1[i] = p.C1[i];
+            sC2[i] = p.C2[i];
+            sU[i] = p.U[i];
         }
-        __syncthreads();
-        sC1 = tC1;
-        sC2 = tC2;
-        sU = tU;
-        sS = tS;
+        for (int i = threadIdx.x; i < J; i += 256) sS[i] = p.sig[i];
     }
+    __syncthreads();
     const int D = p.D;
     const int DP = D >> 1;
     const int64_t g = (int64_t)blockIdx.x * 256 + threadIdx.x;
@@ -637,120 +628,6 @@ __global__ __launch_bounds__(256) void k_update(const UpdArgs p) {
         if (bad) atomicAdd(&p.dbg[1], bad);
     }
 #endif
-    if (p.diag & kDiagRelease) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");  // diagnostic (SKELDIFF_DIAG)
-}
-
-// Diagnostics (SKELDIFF_DIAG bit 15, DESIGN.md §4c, tools/hazard_snap.py): k_update<16> with a
-// self-check.  After the stores every thread reloads its inputs (x0 with act/clamp, x_t, the
-// Philox normals), compares them bitwise with the values it computed from (still in registers),
-// recomputes its outputs from the reloaded values and the global tables and compares those with
-// the outputs it stored; a failing thread appends {row, d, failed checks, HW_ID, XCC_ID, its
-// workgroup's s_memrealtime at entry and at the check} to p.dbg (sd_diag_buffer layout).
-__global__ __launch_bounds__(256) void k_update_chk(const UpdArgs p) {
-    constexpr int JM = 16;
-    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-    __shared__ float tC1[JM * JM], tC2[JM * JM], tU[JM * JM], tS[JM];
-    for (int i = threadIdx.x; i < JM * JM; i += 256) {
-        tC1[i] = p.C1[i];
-        tC2[i] = p.C2[i];
-        tU[i] = p.U[i];
-    }
-    for (int i = threadIdx.x; i < JM; i += 256) tS[i] = p.sig[i];
-    __syncthreads();
-    const int D = p.D, DP = D >> 1;
-    const int64_t g = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    const int64_t row = g / DP;
-    if (row >= p.B) return;
-    const int d = 2 * (int)(g % DP);
-    const int64_t rb = row * (int64_t)JM * D;
-    uint64_t seed = p.seed;
-    int64_t row0 = p.row0;
-    if (p.noise_mode == 2 && p.rng_dev) {
-        seed = p.rng_dev[0];
-        row0 = (int64_t)p.rng_dev[1];
-    }
-    row0 += p.row_shift;
-    auto load = [&](floatx2 (&x0v)[JM], floatx2 (&xtv)[JM], floatx2 (&ev)[JM], const float* sS) {
-#pragma unroll
-        for (int j = 0; j < JM; ++j) {
-            floatx2 a = ld2(p.x0 + rb + j * D + d);
-            if (p.act == 1) {
-                a.x = tanhf(a.x);
-                a.y = tanhf(a.y);
-            }
-            x0v[j] = floatx2{fminf(fmaxf(a.x, -1.f), 1.f), fminf(fmaxf(a.y, -1.f), 1.f)};
-            xtv[j] = ld2(p.xt + rb + j * D + d);
-            ev[j] = p.noise_mode == 2 ? noise_pair(seed, (uint64_t)(row0 + row), p.step, (uint32_t)(j * D + d))
-                                      : floatx2{0.f, 0.f};
-            if (p.noise_mode != 0) ev[j] *= sS[j];
-        }
-    };
-    auto compute = [&](const floatx2 (&x0v)[JM], const floatx2 (&xtv)[JM], const floatx2 (&ev)[JM], const float* C1,
-                       const float* C2, const float* U, floatx2 (&ov)[JM]) {
-        for (int i = 0; i < JM; ++i) {
-            floatx2 m1 = {0.f, 0.f}, m2 = {0.f, 0.f}, nz = {0.f, 0.f};
-#pragma unroll
-            for (int j = 0; j < JM; ++j) {
-                m1 += C1[i * JM + j] * x0v[j];
-                m2 += C2[i * JM + j] * xtv[j];
-                nz += U[i * JM + j] * ev[j];
-            }
-            const floatx2 mean = m1 + m2;
-            ov[i] = (p.noise_mode != 0) ? mean + nz : mean;
-        }
-    };
-    floatx2 x0v[JM], xtv[JM], ev[JM], ov[JM];
-    load(x0v, xtv, ev, tS);
-    compute(x0v, xtv, ev, tC1, tC2, tU, ov);
-#pragma unroll
-    for (int i = 0; i < JM; ++i) st2(p.out + rb + i * D + d, ov[i]);
-    // self-check
-    floatx2 x0r[JM], xtr[JM], er[JM], orr[JM];
-    load(x0r, xtr, er, p.sig);
-    compute(x0r, xtr, er, p.C1, p.C2, p.U, orr);
-    auto ne = [](floatx2 a, floatx2 b) {
-        return __float_as_uint(a.x) != __float_as_uint(b.x) || __float_as_uint(a.y) != __float_as_uint(b.y);
-    };
-    unsigned bad = 0, jb = 0xFFFFu;
-    floatx2 rv = {0.f, 0.f}, lv = {0.f, 0.f};  // first failing pair: register value, reloaded value
-#pragma unroll
-    for (int j = 0; j < JM; ++j) {
-        unsigned b = 0;
-        b |= ne(x0v[j], x0r[j]) ? 1u : 0u;
-        b |= ne(xtv[j], xtr[j]) ? 2u : 0u;
-        b |= ne(ev[j], er[j]) ? 4u : 0u;
-        b |= ne(ov[j], orr[j]) ? 8u : 0u;
-        const floatx2 st = ld2(p.out + rb + j * D + d);
-        b |= ne(ov[j], st) ? 16u : 0u;
-        if (b && !bad) {
-            jb = (unsigned)j | (b << 8);
-            rv = (b & 1) ? x0v[j] : (b & 2) ? xtv[j] : (b & 4) ? ev[j] : ov[j];
-            lv = (b & 1) ? x0r[j] : (b & 2) ? xtr[j] : (b & 4) ? er[j] : (b & 8) ? orr[j] : st;
-        }
-        bad |= b;
-    }
-    if (threadIdx.x == 0 && p.dbg) diag_wg_log(p.dbg, 10, t0);
-    if (bad && p.dbg) {
-        const unsigned i = atomicAdd(&p.dbg[0], 1u);
-        if (i < kDiagUpdMax) {
-            unsigned* r = p.dbg + kDiagUpdBase + 16 * (size_t)i;
-            const uint64_t t1 = __builtin_amdgcn_s_memrealtime();
-            r[0] = (unsigned)row;
-            r[1] = (unsigned)d | (bad << 16);
-            r[2] = __builtin_amdgcn_s_getreg(kHwRegHwId);
-            r[3] = __builtin_amdgcn_s_getreg(kHwRegXccId);
-            r[4] = (unsigned)t0;
-            r[5] = (unsigned)(t0 >> 32);
-            r[6] = (unsigned)t1;
-            r[7] = (unsigned)(t1 >> 32);
-            r[8] = jb;
-            r[9] = __float_as_uint(rv.x);
-            r[10] = __float_as_uint(rv.y);
-            r[11] = __float_as_uint(lv.x);
-            r[12] = __float_as_uint(lv.y);
-            r[13] = blockIdx.x;
-        }
-    }
 }
 
 // Small batches: k_update's thread owns a (row, feature pair) and walks all J nodes serially
@@ -759,7 +636,6 @@ __global__ __launch_bounds__(256) void k_update_chk(const UpdArgs p) {
 //   A: item (j, d): x0 (act, clamp), x_t and sigma_j eps_j of one node -> LDS;
 //   B: item (i, d): the C1 / C2 / U sums over j from LDS, in k_update's order and expressions.
 __global__ __launch_bounds__(256) void k_update_row(const UpdArgs p) {
-    if (p.diag & 8) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // diagnostic (SKELDIFF_DIAG)
     extern __shared__ __attribute__((aligned(16))) float sm[];
     const int J = p.J, D = p.D, DP = D >> 1, JD = J * D;
     const int nt = p.iso ? 0 : 3 * J * J + J;
@@ -846,22 +722,6 @@ hipError_t launch_update(const UpdArgs& a, hipStream_t s) {
     }
     const int64_t n = a.B * (a.D / 2);
     const dim3 grid((unsigned)((n + 255) / 256));
-    if (a.J == 16 && (a.diag & kDiagSelfCheck) && !a.iso && a.noise_mode != 1 && !a.x0_bf16 && !a.xt_bf16 && !a.out_bf16 &&
-        !a.out2 && !a.mean_out && !a.noise_out) {  // diagnostic (SKELDIFF_DIAG bit 15)
-        hipLaunchKernelGGL(k_update_chk, grid, dim3(256), 0, s, a);
-        return hipGetLastError();
-    }
-    if (a.J == 16 && (a.diag & 32)) {  // diagnostic (SKELDIFF_DIAG): no LDS at all
-        hipLaunchKernelGGL((k_update<16, true, true>), grid, dim3(256), 0, s, a);
-        return hipGetLastError();
-    }
-    if (a.J == 16 && (a.diag & 64)) {  // diagnostic (SKELDIFF_DIAG): the workgroup holds its CU's LDS
-        hipError_t e = hipFuncSetAttribute((const void*)k_update<16, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                           160 * 1024);
-        if (e != hipSuccess) return e;
-        hipLaunchKernelGGL((k_update<16, true>), grid, dim3(256), 160 * 1024 - 3 * 16 * 16 * 4 - 64, s, a);
-        return hipGetLastError();
-    }
     switch (a.J) {
         case 16: hipLaunchKernelGGL((k_update<16, true>), grid, dim3(256), 0, s, a); break;
         case 17: hipLaunchKernelGGL((k_update<17, true>), grid, dim3(256), 0, s, a); break;

@@ -7,6 +7,7 @@
 #include <cmath>
 #include <cstdlib>
 #include <algorithm>
+#include <atomic>
 #include <cstring>
 #include <map>
 #include <memory>
@@ -37,17 +38,6 @@ int sd::diag_flags() {
         return e ? atoi(e) : 0;
     }();
     return v;
-}
-
-unsigned* sd::diag_buffer() {
-    static unsigned* buf = [] {
-        unsigned* b = nullptr;
-        if (hipMalloc(&b, sd::kDiagWords * sizeof(unsigned)) != hipSuccess ||
-            hipMemset(b, 0, sd::kDiagWords * sizeof(unsigned)) != hipSuccess || hipDeviceSynchronize() != hipSuccess)
-            abort();
-        return b;
-    }();
-    return buf;
 }
 
 #ifdef SD_DEBUG_LDS
@@ -102,12 +92,17 @@ struct GraphKey {
 
 // The captured graphs of one sd_sample_loop shape (one per row chain).  Shared by the cache and
 // every caller that is about to launch them, so an eviction by another thread never destroys an
-// exec a caller still holds; the last holder destroys them after the device has drained.
+// exec a caller still holds; the last holder destroys them after their own last launches are done
+// (an event recorded behind each launch: no device-wide drain, other streams are not waited for).
 struct GraphSet {
     std::vector<hipGraphExec_t> execs;
+    std::vector<hipEvent_t> done;  // one per exec, recorded on the exec's stream after each launch
+    unsigned route_bits = 0;       // sd::RouteBits the captured chains launch
     ~GraphSet() {
-        if (execs.empty()) return;
-        (void)hipDeviceSynchronize();  // an exec may still be running on a caller's stream
+        for (auto e : done) {
+            (void)hipEventSynchronize(e);
+            (void)hipEventDestroy(e);
+        }
         for (auto x : execs) (void)hipGraphExecDestroy(x);
     }
 };
@@ -144,7 +139,8 @@ UpdDump g_dump;
 // workgroups instead of waiting for the next kernel boundary.
 static int g_chains = [] {
     const char* e = getenv("SKELDIFF_CHAINS");
-    return e ? atoi(e) : 3;  // 3 chains + the caller's stream fit HIP's default 4 hardware queues
+    const int v = e ? atoi(e) : 0;
+    return (v >= 0 && v <= 8) ? v : 0;  // 0: per batch size (chain_count)
 }();
 
 
@@ -159,7 +155,7 @@ struct sd_plan {
     bool blk_ok = false;   // every layer on v4 with row-blocked intermediate activations
     int prec = 0;          // sd_plan_set_precision: 0 f32-accurate, 1 half (f16 products)
     // kernel options (sd_plan_set_option), initialised from the process defaults at creation
-    int variant = 0, gl4_cfg = 0, gl4_stage = 0, split = 0, chains = 3;
+    int variant = 0, gl4_cfg = 0, gl4_stage = 0, split = 0, chains = 0;
     bool fuse_attention_now() const { return fuse_ok && (variant == 0 || variant == 4); }
     bool blocked_now() const { return blk_ok && fuse_attention_now() && prec != 2; }
     std::vector<void*> allocs;
@@ -182,6 +178,8 @@ struct sd_plan {
     // row chains (record_loop): auxiliary streams + fork/join events, created on first use
     static constexpr int kMaxChains = 8;
     std::mutex cmu;
+    std::atomic<int> last_chains{0};  // SD_OPT_LAST_CHAINS
+    std::atomic<unsigned> last_route{0};  // SD_OPT_LAST_ROUTE
     hipStream_t aux[kMaxChains] = {};
     hipEvent_t ev_fork = nullptr, ev_join[kMaxChains] = {};
 
@@ -322,7 +320,6 @@ sd::GLArgs gl_args(const sd_plan* p, const GL& g, const float* x1, int x1_div, c
 #ifdef SD_DEBUG_LDS
     a.dbg = sd::debug_counters();
 #endif
-    if (sd::diag_flags() & sd::kDiagSelfCheck) a.dbg = sd::diag_buffer();  // diagnostics only
     return a;
 }
 
@@ -357,8 +354,8 @@ struct Prof {
 int run_denoiser(const sd_plan* p, const float* x_t, const float* x_cond, int64_t cond_repeat,
                  int t, float* x0_out, int64_t rows, const WS& w, hipStream_t s, Prof* prof = nullptr,
                  int64_t cond_phase = 0, int tile_hint = 0, float* const* trace = nullptr,
-                 int xt_bf16 = 0, int x0_bf16 = 0, int64_t route_rows = 0, int concurrent = 0,
-                 int64_t snap_r0 = -1, int snap_step = 0) {
+                 int xt_bf16 = 0, int x0_bf16 = 0, int64_t route_rows = 0, int64_t snap_r0 = -1,
+                 int snap_step = 0) {
     const int H = p->H;
     int snap_call = 0;
     auto snap = [&](const sd::GLArgs& g) -> int {
@@ -404,10 +401,8 @@ int run_denoiser(const sd_plan* p, const float* x_t, const float* x_cond, int64_
     // v5 scratch (pre-mix activations of layers whose residual aliases their output): the qkv
     // buffer, dead outside the attention block (>= rows * J * H floats)
     const int64_t zs_cap = (rows + 31) / 32 * 32 * p->J * (int64_t)(p->d.use_attention ? 3 * p->hid : p->H);
-    auto lay = [B, tile_hint, &w, zs_cap, &bfl, route_rows, concurrent](sd::GLArgs& g, int in, int res, int out) {
+    auto lay = [B, tile_hint, &w, zs_cap, &bfl, route_rows](sd::GLArgs& g, int in, int res, int out) {
         g.status = ws_status(w);
-        g.diag = sd::diag_flags();
-        g.concurrent = concurrent;
         g.route_rows = route_rows;
         g.zs = w.qkv;
         g.zs_cap = zs_cap;
@@ -558,11 +553,9 @@ int run_update(const sd_plan* p, const float* x0, const float* xt, const float* 
     u.B = rows;
     u.J = p->J;
     u.D = p->D;
-    u.diag = sd::diag_flags();
 #ifdef SD_DEBUG_LDS
     u.dbg = sd::debug_counters();
 #endif
-    if (sd::diag_flags() & sd::kDiagSelfCheck) u.dbg = sd::diag_buffer();  // diagnostics only
     u.dump_x0 = g_dump.x0;
     u.dump_xt = g_dump.xt;
     u.dump_ev = g_dump.ev;
@@ -616,17 +609,6 @@ int sd_debug_snapshot(float* arena, int64_t slot_floats, int64_t y_floats, int32
     g_snap.half = y_floats;
     g_snap.nslots = arena ? nslots : 0;
     g_snap.meta.assign(3 * (size_t)std::max(nslots, 0), 0);
-    return SD_OK;
-}
-// Diagnostics only: copy (and with reset != 0, then zero) the SKELDIFF_DIAG bit-15 buffer
-// (sd_internal.h, kDiagWords words)
-int sd_debug_diag_buffer(uint32_t* host, int64_t words, int32_t reset) {
-    unsigned* b = sd::diag_buffer();
-    const int64_t n = std::min<int64_t>(words, sd::kDiagWords);
-    SD_HIP(hipDeviceSynchronize());
-    if (host && n > 0) SD_HIP(hipMemcpy(host, b, n * sizeof(unsigned), hipMemcpyDeviceToHost));
-    if (reset) SD_HIP(hipMemset(b, 0, sd::kDiagWords * sizeof(unsigned)));
-    SD_HIP(hipDeviceSynchronize());
     return SD_OK;
 }
 // Diagnostics only: the first posterior update of the next sampling calls stores its inputs
@@ -961,25 +943,20 @@ static WS shift_ws(const sd_plan* p, const WS& w, int64_t r0) {
     return o;
 }
 
-// number of row chains for `rows` rows and the first row of chain i (i = 0 .. n)
+// number of row chains for `rows` rows (multiples of 32 rows each; the plan's row_chains option,
+// default 3).  Every route runs with any chain count: the kernels share CUs with each other's
+// workgroups (the row-chain hazard of rounds 1-2 was packed-FP32 code, which the
+// build no longer emits), and the results are bitwise independent of the chain count.
 static int chain_count(const sd_plan* p, int64_t rows, int64_t cond_repeat, int64_t* unit) {
-    const int64_t g = 32;  // a chain starts on a row block; x_cond rows via x1_row0
+    (void)cond_repeat;  // a chain starting inside a sequence's futures reads x_cond via x1_row0
+    const int64_t g = 32;
     *unit = g;
     const int64_t units = rows / g;
-    int n = std::max(1, std::min(p->chains, (int)sd_plan::kMaxChains));
+    // auto (0): 3 chains (+ the caller's stream = HIP's default 4 hardware queues; a 4th chain
+    // shares a queue: config 2 11.9k vs 15.9k futures/s), 2 on the small-batch split route
+    // (400 rows: 6,380 vs 5,870 with three; tools/sweep_routes.py, profiles/r03a)
+    int n = p->chains > 0 ? std::min(p->chains, (int)sd_plan::kMaxChains) : rows <= sd::split_rows_default() ? 2 : 3;
     if (units < n) n = (int)std::max<int64_t>(1, units);
-    // the split route (small batches) runs on one stream: its kernels gave run-to-run different
-    // rows when two chains' launches shared CUs, and the single chain is as fast
-    // there (one 400-row chain 5,565 vs three 5,764 futures/s)
-    if (p->split == 2 || (p->split == 0 && rows <= sd::split_rows_default())) n = 1;
-    // v5 (J > 21): its GEMM phase (k_gl4t) holds the CU under concurrent chains,
-    // and one chain measured faster (MANO J = 51: 2,411 vs 2,338 futures/s with three)
-    if (p->J > 21 && p->variant == 0) n = 1;
-    // J = 17 / 21 (bf16: J = 17), default options: the tiled split route, on one chain
-    // (sd_graph_linear_v4.hip split_route; its GEMM phase would hold whole CUs beside other chains)
-    if (p->split == 0 && p->gl4_cfg == 0 && (p->variant == 0 || p->variant == 4) &&
-        (p->J == 17 || (p->J == 21 && p->prec != 2) || (p->J == 16 && p->prec == 0 && rows >= 3200)))
-        n = 1;
     return n;
 }
 static int64_t chain_row(int i, int n, int64_t rows, int64_t unit) {
@@ -1058,7 +1035,7 @@ static int record_loop(const sd_plan* p, const float* x_T, const float* x_cond, 
             // 5 % faster than the single-chain 32 x 96 choice at B = 3200, 3 chains
             const int64_t wg813 = (c.n + 31) / 32 * 2;  // 32 x 96 workgroups of an N = 192 layer
             int rc = run_denoiser(p, c.cur, xc, cond_repeat, t, c.w.x0, c.n, c.w, cs[i], nullptr, r0 % cond_repeat,
-                                  (nch > 1 && wg813 >= 32) ? 812 : 0, nullptr, bf, bf, rows, nch > 1, r0, (int)k);
+                                  (nch > 1 && wg813 >= 32) ? 812 : 0, nullptr, bf, bf, rows, r0, (int)k);
             if (rc) return rc;
             float* nxt = (t == 0) ? out + r0 * JD : (((T - 1 - t) & 1) ? c.w.img1 : c.w.img0);
             const float* eps = (!dev_noise && t > 0) ? eps_all + r0 * step_rs + k * JD : nullptr;
@@ -1125,6 +1102,7 @@ int sd_sample_loop(const sd_plan* p, const float* x_T, const float* x_cond, int6
     SD_HIP(hipMemsetAsync(ws_status(w), 0, sizeof(unsigned), s));
     int64_t unit = 32;
     const int nch = chain_count(p, rows, cond_repeat, &unit);
+    mp->last_chains.store(nch);
     std::unique_lock<std::mutex> lk(mp->cmu, std::defer_lock);  // fork/join objects are shared
     hipStream_t cs[sd_plan::kMaxChains];
     cs[0] = s;
@@ -1136,8 +1114,10 @@ int sd_sample_loop(const sd_plan* p, const float* x_T, const float* x_cond, int6
     }
     if (!(flags & SD_FLAG_GRAPH)) {
         if ((rc = fork_chains(mp, s, nch, cs))) return rc;
+        sd::g_route_bits = 0;
         rc = record_loop(p, x_T, x_cond, cond_repeat, eps_all, seed, row0, out, means_out, noise_out, timages_out,
                          start_out, rows, w, flags, false, cs, nch, unit, -1);
+        mp->last_route.store(sd::g_route_bits);
         if (rc) return rc;
         return join_chains(mp, s, nch, cs);
     }
@@ -1170,6 +1150,7 @@ int sd_sample_loop(const sd_plan* p, const float* x_T, const float* x_cond, int6
     if (!set) {
         set = std::make_shared<GraphSet>();
         std::vector<hipGraphExec_t>& execs = set->execs;
+        sd::g_route_bits = 0;
         for (int i = 0; i < nch; ++i) {
             hipGraph_t graph = nullptr;
             hipGraphExec_t exec = nullptr;
@@ -1187,8 +1168,12 @@ int sd_sample_loop(const sd_plan* p, const float* x_T, const float* x_cond, int6
                 return fail(SD_E_HIP, std::string("graph capture: ") + hipGetErrorString(e));
             }
             execs.push_back(exec);
+            hipEvent_t ev = nullptr;
+            SD_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+            set->done.push_back(ev);
         }
-        std::shared_ptr<GraphSet> evicted;  // destroyed (after a device drain) outside the lock
+        set->route_bits = sd::g_route_bits;
+        std::shared_ptr<GraphSet> evicted;  // destroyed (after its own launches) outside the lock
         {
             std::lock_guard<std::mutex> g(mp->gmu);
             auto& cache = mp->graphs;
@@ -1199,8 +1184,12 @@ int sd_sample_loop(const sd_plan* p, const float* x_T, const float* x_cond, int6
             cache[key] = set;
         }
     }
+    mp->last_route.store(set->route_bits);
     if ((rc = fork_chains(mp, s, nch, cs))) return rc;
-    for (int i = 0; i < nch; ++i) SD_HIP(hipGraphLaunch(set->execs[i], cs[i]));
+    for (int i = 0; i < nch; ++i) {
+        SD_HIP(hipGraphLaunch(set->execs[i], cs[i]));
+        SD_HIP(hipEventRecord(set->done[i], cs[i]));
+    }
     return join_chains(mp, s, nch, cs);
 }
 
@@ -1302,7 +1291,7 @@ int sd_plan_set_option(sd_plan* p, int32_t option, int64_t value) {
             p->gl4_cfg = (int)value;
             return SD_OK;
         case SD_OPT_ROW_CHAINS:
-            if (value < 1 || value > sd_plan::kMaxChains) return fail(SD_E_INVALID, "row chains must be in [1, 8]");
+            if (value < 0 || value > sd_plan::kMaxChains) return fail(SD_E_INVALID, "row chains must be in [0 (auto), 8]");
             p->chains = (int)value;
             return SD_OK;
         case SD_OPT_PRECISION: return sd_plan_set_precision(p, (int32_t)value);
@@ -1311,9 +1300,12 @@ int sd_plan_set_option(sd_plan* p, int32_t option, int64_t value) {
                 return fail(SD_E_INVALID, "gl4 staging must be 0 (LDS-DMA), 1 (registers) or 2 (diagnostic)");
             p->gl4_stage = (int)value;
             return SD_OK;
+        case SD_OPT_LAST_CHAINS:
+        case SD_OPT_LAST_ROUTE: return fail(SD_E_INVALID, "SD_OPT_LAST_CHAINS / SD_OPT_LAST_ROUTE are read-only");
         case SD_OPT_SPLIT_ROUTE:
-            if (value < 0 || value > 3)
-                return fail(SD_E_INVALID, "split route must be 0 (auto), 1 (never), 2 (always) or 3 (always, tiled phase 1)");
+            if (value < 0 || value > 4)
+                return fail(SD_E_INVALID, "split route must be 0 (auto), 1 (never), 2 (always), 3 (always, tiled phase 1) "
+                                          "or 4 (tiled phase 1 except to_qkv + attention)");
             p->split = (int)value;
             return SD_OK;
         default: return fail(SD_E_INVALID, "unknown option " + std::to_string(option));
@@ -1329,6 +1321,8 @@ int sd_plan_get_option(const sd_plan* p, int32_t option, int64_t* value) {
         case SD_OPT_PRECISION: *value = p->prec; return SD_OK;
         case SD_OPT_GL4_STAGING: *value = p->gl4_stage; return SD_OK;
         case SD_OPT_SPLIT_ROUTE: *value = p->split; return SD_OK;
+        case SD_OPT_LAST_CHAINS: *value = p->last_chains.load(); return SD_OK;
+        case SD_OPT_LAST_ROUTE: *value = p->last_route.load(); return SD_OK;
         default: return fail(SD_E_INVALID, "unknown option " + std::to_string(option));
     }
 }
@@ -1356,7 +1350,7 @@ int sd_plan_set_precision(sd_plan* p, int32_t mode) {
 
 int sd_set_row_chains(int32_t n) {
     if (n == -1) return g_chains;
-    if (n < 1 || n > sd_plan::kMaxChains) return fail(SD_E_INVALID, "row chains must be in [1, 8]");
+    if (n < 0 || n > sd_plan::kMaxChains) return fail(SD_E_INVALID, "row chains must be in [0 (auto), 8]");
     const int old = g_chains;
     g_chains = n;
     return old;

@@ -112,15 +112,29 @@ class SamplingEngine:
 
     OPTIONS = {"kernel_variant": _lib.SD_OPT_KERNEL_VARIANT, "gl4_tile": _lib.SD_OPT_GL4_TILE,
                "row_chains": _lib.SD_OPT_ROW_CHAINS, "gl4_staging": _lib.SD_OPT_GL4_STAGING,
-               "split_route": _lib.SD_OPT_SPLIT_ROUTE}
+               "split_route": _lib.SD_OPT_SPLIT_ROUTE, "last_chains": _lib.SD_OPT_LAST_CHAINS,
+               "last_route": _lib.SD_OPT_LAST_ROUTE}
+    READ_ONLY = ("last_chains", "last_route")
+    # sample(): check the f16 range guard after each call (a host sync on the workspace status
+    # word) where the plan's kernels can set it; False leaves the call asynchronous
+    range_guard = True
+
+    def range_guard_needed(self) -> bool:
+        """True when the plan's graph-linear kernels can raise SD_STATUS_F16_RANGE: the split-f16
+        tiles (kernel variant 0 / 4) in f32 or half precision; the exact-f32 kernels and the bf16
+        mode never do."""
+        return bool(self.range_guard) and self._precision != self.PRECISIONS["bf16"] and \
+            self._options.get("kernel_variant", 0) in (0, 4)
 
     def set_option(self, name: str, value: int) -> None:
         """Per-plan kernel option (sd_plan_set_option): "kernel_variant" (0 auto, 1..5),
         "gl4_tile" (<waves><row tiles><col tiles>, 0 auto), "row_chains" (1..8), "gl4_staging"
-        (0 LDS-DMA with the CU held exclusively, 1 register-staged).  Kept across plan rebuilds;
+        (0 LDS-DMA, 1 register-staged), "split_route" (0 auto, 1 never, 2 k_gl4y, 3 k_gl4t);
+        get_option("last_chains") reads the row chains the last sample_loop ran.  Kept across plan rebuilds;
         other engines (plans) in the process are unaffected."""
-        if name not in self.OPTIONS:
-            raise SkelDiffError(f"unknown option {name!r}; one of {sorted(self.OPTIONS)}")
+        if name not in self.OPTIONS or name in self.READ_ONLY:
+            raise SkelDiffError(f"unknown or read-only option {name!r}; one of "
+                                f"{sorted(set(self.OPTIONS) - set(self.READ_ONLY))}")
         if self._plan is not None:
             check(_lib.lib().sd_plan_set_option(self._plan, self.OPTIONS[name], int(value)))
         self._options[name] = int(value)

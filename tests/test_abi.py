@@ -85,14 +85,21 @@ def test_plan_options_validated_on_host():
     assert lib.sd_plan_create(ctypes.byref(h), ctypes.byref(d)) == 0, lib.sd_last_error()
     try:
         v = ctypes.c_int64()
-        for value in (0, 1, 2, 3):
+        for value in (0, 1, 2, 3, 4):
             assert lib.sd_plan_set_option(h, _lib.SD_OPT_SPLIT_ROUTE, value) == 0
             assert lib.sd_plan_get_option(h, _lib.SD_OPT_SPLIT_ROUTE, ctypes.byref(v)) == 0 and v.value == value
-        assert lib.sd_plan_set_option(h, _lib.SD_OPT_SPLIT_ROUTE, 4) == -1
+        assert lib.sd_plan_set_option(h, _lib.SD_OPT_SPLIT_ROUTE, 5) == -1
         assert b"split route" in lib.sd_last_error()
-        assert lib.sd_plan_set_option(h, _lib.SD_OPT_ROW_CHAINS, 0) == -1
+        assert lib.sd_plan_set_option(h, _lib.SD_OPT_ROW_CHAINS, -1) == -1
+        assert lib.sd_plan_set_option(h, _lib.SD_OPT_ROW_CHAINS, 0) == 0  # auto
         assert lib.sd_plan_set_option(h, _lib.SD_OPT_ROW_CHAINS, 8) == 0
         assert lib.sd_plan_set_option(h, _lib.SD_OPT_GL4_STAGING, 3) == -1
         assert lib.sd_plan_set_option(h, 99, 0) == -1
+        # SD_OPT_LAST_CHAINS: read-only, 0 before the plan's first sampling call
+        assert lib.sd_plan_get_option(h, _lib.SD_OPT_LAST_CHAINS, ctypes.byref(v)) == 0 and v.value == 0
+        assert lib.sd_plan_set_option(h, _lib.SD_OPT_LAST_CHAINS, 1) == -1
+        assert b"read-only" in lib.sd_last_error()
+        assert lib.sd_plan_get_option(h, _lib.SD_OPT_LAST_ROUTE, ctypes.byref(v)) == 0 and v.value == 0
+        assert lib.sd_plan_set_option(h, _lib.SD_OPT_LAST_ROUTE, 1) == -1
     finally:
         lib.sd_plan_destroy(h)

@@ -5,13 +5,16 @@ surface (VERDICT r01 "what's missing" 1-3):
   first 5 and the last 5 reverse steps against the oracle fed the same Philox normals, plus
   graph == eager bitwise, finiteness, determinism and the t = 0 clamp; the reference's own T=1000
   chain is in test_gpu_parity.py::test_release_sample_matches_reference[release_h36m16_T1000];
-* config 2 exactly as bench.py times it (J=16, B=3200, T=100, 3 row chains, 32x64 tiles,
-  hipGraph, reused output buffer, device noise): every per-step record bitwise equal to one chain
-  run eagerly, and the first 3 steps against the oracle on the rows at the chain boundaries;
+* config 2 exactly as bench.py times it (J=16, B=3200, T=100, 3 row chains on the tiled split
+  route, hipGraph, reused output buffer, device noise): every per-step record bitwise equal to
+  one chain run eagerly, and the first 3 steps against the oracle on the rows at the chain
+  boundaries;
+* row chains sharing CUs on every route and at the strong-scaling shard sizes,
+  each asserting the chain count the call ran (SD_OPT_LAST_CHAINS);
 * per-layer activations of the Denoiser (sd_denoiser_trace) against the reference's forward hooks;
 * Denoiser(use_attention=False), diffusion_activation='tanh', return_timages and noise
   interpolation against the reference's outputs (tests/golden/variants_h36m16_T10.npz);
-* two plans with different kernel options sampling concurrently in one process.
+* two plans sampling concurrently in one process (different options; two default plans).
 
 Tolerance: 1e-4 absolute on generated latents (north star); the per-layer activations 1e-5."""
 import threading
@@ -84,10 +87,11 @@ def test_config4_t1000_graph_first_and_last_steps(cuda):
 
 
 def test_config2_as_benched(cuda):
-    """BASELINE config 2 with the bench's exact launch configuration: 3 row chains (32 x 64
-    graph-linear tiles), hipGraph, device noise, reused output buffer; every per-step record of
-    the whole T = 100 chain bitwise equal to one chain run eagerly; first 3 steps vs the oracle on
-    the rows either side of each chain boundary."""
+    """BASELINE config 2 with the bench's exact launch configuration: default plan options (the
+    tiled split route, k_gl4t + k_gl4 MODE 2 / 3, on 3 row chains whose kernels share CUs),
+    hipGraph, device noise, reused output buffer; every per-step record of the whole T = 100 chain
+    bitwise equal to one chain run eagerly; first 3 steps vs the oracle on the rows either side of
+    each chain boundary."""
     from bench import build_config
 
     d, x_cond, rows = build_config("amass16", cuda, T=100)
@@ -97,12 +101,15 @@ def test_config2_as_benched(cuda):
     out = torch.empty((rows, J, D), device=cuda)
     a = eng.sample_loop(rows, x_cond=x_cond, seed=seed, graph=True, out=out, record=(True, True))
     a = [t.clone() for t in (a[0], a[1], a[2], a[4])]  # img, start, noise_t, imgs
+    assert eng.get_option("last_chains") == 3
     eng.set_option("row_chains", 1)
     b = eng.sample_loop(rows, x_cond=x_cond, seed=seed, graph=False, record=(True, True))
     b = [b[0], b[1], b[2], b[4]]
+    assert eng.get_option("last_chains") == 1
     # the exact bench.py call (no records, output buffer reused, start not kept)
     eng.set_option("row_chains", 3)
     c = eng.sample_loop(rows, x_cond=x_cond, seed=seed, graph=True, out=out, keep_start=False)[0]
+    assert eng.get_option("last_chains") == 3
     torch.cuda.synchronize()
     for x, y in zip(a, b):
         assert torch.equal(x, y)
@@ -121,23 +128,49 @@ def test_config2_as_benched(cuda):
         assert _max_err(imgs[sel, k], x) < TOL, (k, _max_err(imgs[sel, k], x))
 
 
-def test_register_staging_shares_cus_bitwise(cuda):
-    """SD_OPT_GL4_STAGING = 1 (register-staged weight stages, no whole-CU LDS reservation): the
-    co-residency that corrupts the LDS-DMA stages is bitwise safe here, and the
-    arithmetic is the default path's (same products, same order)."""
+@pytest.mark.parametrize("route,staging", [(1, 0), (1, 1), (3, 0), (2, 0)])
+def test_row_chains_share_cus_bitwise(route, staging, cuda):
+    """Row chains whose kernels share CUs (no whole-CU reservations) on each route
+    -- one-kernel k_gl4 (LDS-DMA and register-staged weight stages), tiled k_gl4t + MODE 2 / 3,
+    per-wave k_gl4y + MODE 2 / 3 -- at config 2's full batch (T = 10): 3 and 2 chains, graph and
+    eager, bitwise equal to one chain; the chain count each call ran is asserted."""
     from bench import build_config
 
     d, x_cond, rows = build_config("amass16", cuda, T=10)
     eng = d.engine
+    eng.set_option("split_route", route)
+    eng.set_option("gl4_staging", staging)
+    eng.set_option("row_chains", 1)
     ref = eng.sample_loop(rows, x_cond=x_cond, seed=3)[0].clone()
-    eng.set_option("gl4_staging", 1)
+    assert eng.get_option("last_chains") == 1
     for n in (3, 2):
         eng.set_option("row_chains", n)
         for graph in (False, True):
             x = eng.sample_loop(rows, x_cond=x_cond, seed=3, graph=graph)[0]
             torch.cuda.synchronize()
-            assert torch.equal(x, ref), (n, graph)
-    assert eng.get_option("gl4_staging") == 1
+            assert eng.get_option("last_chains") == n
+            assert torch.equal(x, ref), (route, staging, n, graph, _max_err(x, ref))
+    assert eng.status(rows) == 0
+
+
+@pytest.mark.parametrize("batch", [32, 16, 8])
+def test_strong_scaling_shards_chain_invariant(batch, cuda):
+    """The per-rank shards of config 2 under strong scaling on 2 / 4 / 8 GPUs (1,600 / 800 / 400
+    rows, J = 16 f32, T = 100, default routes): three row chains equal one chain bitwise over the
+    whole T = 100 chain, graph replay and eager, with the chain count asserted."""
+    from bench import build_config
+
+    d, x_cond, rows = build_config("amass16", cuda, T=100, batch=batch)
+    eng = d.engine
+    eng.set_option("row_chains", 1)
+    ref = eng.sample_loop(rows, x_cond=x_cond, seed=17, row0=rows)[0].clone()
+    assert eng.get_option("last_chains") == 1
+    eng.set_option("row_chains", 3)
+    for graph in (True, False):
+        x = eng.sample_loop(rows, x_cond=x_cond, seed=17, row0=rows, graph=graph)[0]
+        torch.cuda.synchronize()
+        assert eng.get_option("last_chains") == 3
+        assert torch.equal(x, ref), (rows, graph, _max_err(x, ref))
 
 
 @pytest.mark.parametrize("cfg,batch,kw", [("h36m_t1000", 1, {}), ("amass16", 4, {}), ("amass16", 12, {}),
@@ -171,7 +204,7 @@ def test_split_route_bitwise(cfg, batch, kw, cuda):
 def test_tiled_split_route_bitwise(cfg, batch, T, prec, cuda):
     """SD_OPT_SPLIT_ROUTE = 3 (DESIGN.md §4d''): the tiled GEMM phase k_gl4t (128 rows x 192
     columns of one node per workgroup) + k_gl4 MODE 2 / 3 is bitwise equal to the one-kernel
-    route, graph and eager, on one row chain and on three (where k_gl4t holds its CU: §4c)."""
+    route, graph and eager, on one row chain and on three (sharing CUs, §4c)."""
     from bench import build_config
 
     d, x_cond, rows = build_config(cfg, cuda, T=T, batch=batch)
@@ -187,6 +220,7 @@ def test_tiled_split_route_bitwise(cfg, batch, T, prec, cuda):
         for graph in (False, True):
             got = eng.sample_loop(rows, x_cond=x_cond, seed=13, graph=graph, record=(False, True))
             torch.cuda.synchronize()
+            assert eng.get_option("last_chains") == min(chains, rows // 32)
             assert torch.equal(got[0], ref[0]) and torch.equal(got[4], ref[1]), (cfg, chains, graph)
     assert eng.status(rows) == 0
 
@@ -210,8 +244,8 @@ def test_split_route_shard_equals_full_batch(cuda):
 
 
 def test_exact_variant_row_chains_bitwise(cuda):
-    """The exact-f32 kernels (v3, LDS-DMA stages of <= 64 KB, CU shareable) with three concurrent
-    row chains, graph replay, equal one chain run eagerly bit for bit (config 2, T = 10)."""
+    """The exact-f32 kernels (v3, LDS-DMA stages) with three concurrent row chains, graph replay,
+    equal one chain run eagerly bit for bit (config 2, T = 10)."""
     from bench import build_config
 
     d, x_cond, rows = build_config("amass16", cuda, T=10)
@@ -223,22 +257,24 @@ def test_exact_variant_row_chains_bitwise(cuda):
     for graph in (False, True, True):
         x = eng.sample_loop(rows, x_cond=x_cond, seed=21, graph=graph)[0]
         torch.cuda.synchronize()
+        assert eng.get_option("last_chains") == 3
         assert torch.equal(x, ref), graph
 
 
-def test_split_route_runs_one_chain_deterministic(cuda):
-    """At or below the split-route threshold the plan runs a single row chain (DESIGN.md §4c:
-    concurrent chains on the split kernels gave run-to-run different rows); 200 rows at T = 100
-    with row_chains = 3 requested: repeated runs, eager and graph, are bitwise identical."""
+def test_split_route_row_chains_deterministic(cuda):
+    """The small-batch split route (k_gl4y + k_gl4 MODE 2 / 3; 200 rows at T = 100) on three row
+    chains: repeated runs, eager and graph, are bitwise identical and equal one chain."""
     from bench import build_config
 
     d, x_cond, rows = build_config("amass16", cuda, T=100, batch=4)
     eng = d.engine
-    eng.set_option("row_chains", 3)
+    eng.set_option("row_chains", 1)
     ref = eng.sample_loop(rows, x_cond=x_cond, seed=5)[0].clone()
+    eng.set_option("row_chains", 3)
     for graph in (False, False, True, True):
         x = eng.sample_loop(rows, x_cond=x_cond, seed=5, graph=graph)[0]
         torch.cuda.synchronize()
+        assert eng.get_option("last_chains") == 3
         assert torch.equal(x, ref), graph
 
 
@@ -290,9 +326,9 @@ def test_sample_surface_variants(case, cuda):
 
 def test_two_plans_with_different_options_concurrently(cuda):
     """Kernel options are plan state (sd_plan_set_option), not process globals: plan A (auto
-    kernels, 3 row chains) and plan B (exact-f32 v3, 1 chain, register staging) sample at the same
-    time on two streams from two threads; each equals its own solo result bitwise, and the two
-    agree within the split-f16 vs exact-f32 difference."""
+    kernels, 3 row chains -- checked by SD_OPT_LAST_CHAINS) and plan B (exact-f32 v3, 1 chain,
+    register staging) sample at the same time on two streams from two threads; each equals its
+    own solo result bitwise, and the two agree within the split-f16 vs exact-f32 difference."""
     z = golden("release_h36m16_T100")
     da = build_release_diffusion(z, cuda)
     db = build_release_diffusion(z, cuda)
@@ -325,6 +361,40 @@ def test_two_plans_with_different_options_concurrently(cuda):
     assert torch.equal(res["b"], solo_b), _max_err(res["b"], solo_b)
     assert _max_err(solo_a, solo_b) < TOL
     assert da.engine.get_option("kernel_variant") == 0 and db.engine.get_option("kernel_variant") == 3
+    assert da.engine.get_option("last_chains") == 3 and db.engine.get_option("last_chains") == 1
+
+
+@pytest.mark.parametrize("cfg,batch", [("freeman17", 64), ("amass16", 8)])
+def test_two_default_plans_concurrently(cfg, batch, cuda):
+    """Two plans with DEFAULT options sampling at the same time from two threads on two streams
+    (ADVICE r02): at J = 17 full batch (tiled split route, 3 chains each) and at 400 rows (k_gl4y
+    split route): every kernel of one call may share CUs with the other call's; each result equals
+    its solo run bitwise."""
+    from bench import build_config
+
+    da, xa, rows = build_config(cfg, cuda, T=10, batch=batch)
+    db, xb, _ = build_config(cfg, cuda, T=10, batch=batch, seq0=batch)
+    solo = {"a": da.engine.sample_loop(rows, x_cond=xa, seed=1)[0].clone(),
+            "b": db.engine.sample_loop(rows, x_cond=xb, seed=2)[0].clone()}
+    torch.cuda.synchronize()
+    res = {}
+
+    def run(name, d, x, seed):
+        s = torch.cuda.Stream(cuda)
+        with torch.cuda.stream(s):
+            for _ in range(4):
+                res[name] = d.engine.sample_loop(rows, x_cond=x, seed=seed)[0]
+        s.synchronize()
+
+    th = [threading.Thread(target=run, args=("a", da, xa, 1)), threading.Thread(target=run, args=("b", db, xb, 2))]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    torch.cuda.synchronize()
+    for k in ("a", "b"):
+        assert torch.equal(res[k], solo[k]), (k, _max_err(res[k], solo[k]))
+    assert da.engine.get_option("last_chains") == (3 if rows > 640 else 2)  # auto row chains
 
 
 def test_graph_linear_rejects_aliased_output(cuda):

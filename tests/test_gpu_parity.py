@@ -234,11 +234,14 @@ def test_full_size_config2_step_and_properties(cuda):
     assert torch.equal(part, a[300:400])
 
 
+@pytest.mark.parametrize("route", [1, 0])
 @pytest.mark.parametrize("graph", [False, True])
-def test_row_chains_bitwise_invariant(graph, cuda):
+def test_row_chains_bitwise_invariant(graph, route, cuda):
     """sd_set_row_chains: the batch is split into row ranges whose T-step chains run on forked
     streams.  Rows are independent, so latents and every per-step record are bitwise those of a
-    single chain -- device noise (row0-shifted Philox) and given noise (row-offset eps) alike."""
+    single chain -- device noise (row0-shifted Philox) and given noise (row-offset eps) alike --
+    on the one-kernel route (split_route 1) and the auto route (k_gl4y at this size); the chain
+    count each call ran is asserted (SD_OPT_LAST_CHAINS)."""
     z = golden("release_h36m16_T10")
     d = build_release_diffusion(z, cuda)
     J, T = 16, 10
@@ -250,6 +253,7 @@ def test_row_chains_bitwise_invariant(graph, cuda):
     start = torch.randn((rows, J, 96), generator=g).to(cuda)
     samp = torch.randn((rows, T - 1, J, 96), generator=g).to(cuda)
     L = _lib.lib()
+    d.engine.set_option("split_route", route)
     res = {}
     for n in (1, 2, 3, 8):
         d.engine.set_option("row_chains", n)
@@ -257,13 +261,16 @@ def test_row_chains_bitwise_invariant(graph, cuda):
         b = d.engine.sample_loop(rows, x_cond=xc, start_noise=start, sampling_noise=samp, record=(False, True),
                                  graph=graph)
         torch.cuda.synchronize()
+        assert d.engine.get_option("last_chains") == min(n, rows // 32)
         res[n] = [t.clone() for t in (a[0], a[1], a[2], a[3], b[0], b[4])]
     for n in (2, 3, 8):
         for x, y in zip(res[1], res[n]):
             assert torch.equal(x, y), n
-    assert L.sd_set_row_chains(0) < 0 and L.sd_set_row_chains(9) < 0
+    assert L.sd_set_row_chains(-2) < 0 and L.sd_set_row_chains(9) < 0
     with pytest.raises(_lib.SkelDiffError):
         d.engine.set_option("row_chains", 9)
+    with pytest.raises(_lib.SkelDiffError):
+        d.engine.set_option("last_chains", 1)
 
 
 def test_sharded_eval_single_rank(cuda):

@@ -1,16 +1,16 @@
 #!/bin/bash
-# Round-end measurement session (one gpurun call): the default bench line, the rocprofv3 trace +
-# PMC traffic passes of the same command (tools/profile.sh), one line per BASELINE config
-# (tools/bench_configs.sh) and the strong-scaling per-rank proxies (64 sequences over 2 / 4 / 8
-# ranks = 32 / 16 / 8 sequences on one GPU).  Output under gpurun_out/.
-set -u
-TAG=${TAG:-r02}
-mkdir -p gpurun_out/$TAG
-timeout -k 10 600 python bench.py > gpurun_out/$TAG/bench.json 2> gpurun_out/$TAG/bench.err || { echo "bench failed"; exit 1; }
-echo "bench ok"
-bash tools/profile.sh $TAG || exit 1
-CFGS=${CFGS:-"amass21 freeman17 freeman17_half freeman17_bf16 mano51 h36m_t1000"} bash tools/bench_configs.sh || exit 1
-for b in 32 16 8; do
-  timeout -k 10 300 python bench.py --batch $b --no-cpu-baseline --no-exact-line --profile-reps 2 > gpurun_out/$TAG/strong_b$b.json 2>> gpurun_out/$TAG/bench.err || exit 1
-  echo "strong proxy b=$b $(python -c "import json;d=json.load(open('gpurun_out/$TAG/strong_b$b.json'));print(round(d['value']), round(d['ms_per_step'],2))")"
-done
+# One GPU session: the GPU test suite, then the route / row-chain sweep (tools/sweep_routes.py).
+# usage: bash tools/gpu_round.sh <tag> [sweep args...]
+TAG=${1:-r03}
+shift
+OUT=gpurun_out/$TAG
+mkdir -p $OUT
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $OUT/pytest_gpu.log 2>&1
+rc=$?
+echo "pytest rc=$rc: $(tail -1 $OUT/pytest_gpu.log)"
+[ $rc -eq 0 ] || exit $rc
+timeout -k 10 900 python -u tools/sweep_routes.py "$@" > $OUT/sweep.log 2>&1
+rc=$?
+echo "sweep rc=$rc"
+grep BEST $OUT/sweep.log
+exit $rc
