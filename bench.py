@@ -325,6 +325,9 @@ def main():
             dist.barrier()
         torch.cuda.synchronize(dev)
         elapsed = time.perf_counter() - t0
+        # what the timed calls ran (read before the profiling / exact-f32 calls below)
+        row_chains = eng.get_option("last_chains")
+        route_bits = eng.get_option("last_route")
         assert torch.isfinite(out).all(), "non-finite latents"
         if dist:
             tt = torch.tensor([elapsed], device=dev, dtype=torch.float64)
@@ -352,8 +355,6 @@ def main():
 
     value = world_rows(world, rows, args.scaling, batch, futures) * args.steps / elapsed
     variant = eng.get_option("kernel_variant")
-    row_chains = eng.get_option("last_chains")
-    route_bits = eng.get_option("last_route")
     kernels = [name for bit, name in sorted(_lib.ROUTE_BITS.items()) if route_bits & bit]
     split = bool(route_bits & (1 | 2 | 4 | 8)) and not (route_bits & 64)  # split-f16 products (v4 / v5 GEMM phase)
     tiled = bool(route_bits & 8) and J <= 21

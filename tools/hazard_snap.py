@@ -8,9 +8,8 @@ last slot.  Prints the first slots where the two runs differ, where in the tile 
 grid the differences sit, and whether the differing values are another position's or an older
 write's (addressing, lost stores) or new values (arithmetic).
 Load the CU-sharing diagnostic build (SKELDIFF_LIB=.../libskeldiff_share.so) to reproduce.
-With SKELDIFF_DIAG bit 15 the update kernel self-checks (k_update_chk) and the split-route
-kernels log their workgroups; the failing update threads are then listed with the kernels that
-shared their CU while they ran.
+HAZARD_DUMP=1 also dumps the inputs the first posterior update computed from (x0, x_t, sigma
+eps: sd_debug_update_dump) and compares them between the two runs.
 usage: python tools/hazard_snap.py [chains] [T]"""
 import ctypes
 import os
@@ -33,15 +32,9 @@ J = d.channels
 lib = _lib.lib()
 lib.sd_debug_snapshot.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64, ctypes.c_int32]
 lib.sd_debug_snapshot_meta.argtypes = [ctypes.c_int32, ctypes.POINTER(ctypes.c_int32)]
-lib.sd_debug_diag_buffer.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32]
 lib.sd_debug_update_dump.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
 DUMP = os.environ.get("HAZARD_DUMP") == "1"  # the first update's inputs (sd_debug_update_dump)
 dumps = {}
-SELF = (int(os.environ.get("SKELDIFF_DIAG", "0")) >> 15) & 1
-DW = 1 << 22  # kDiagWords
-UPD_BASE, UPD_MAX = 16, 1 << 15
-WG_BASE = UPD_BASE + 16 * UPD_MAX
-diag = {}
 YF = rows * J * 768
 SLOT = YF + rows * J * 256
 NS = T * CALLS
@@ -55,8 +48,6 @@ def run(nch):
     eng.sample_loop(rows, x_cond=xc, seed=77, row0=0, graph=False, out=out, keep_start=False)  # plan + warm
     torch.cuda.synchronize()
     lib.sd_debug_snapshot(arena.data_ptr(), SLOT, YF, NS)
-    if SELF:
-        lib.sd_debug_diag_buffer(None, 0, 1)
     if DUMP:
         dm = torch.full((3, rows, J, 96), float("nan"), device=dev)
         lib.sd_debug_update_dump(dm[0].data_ptr(), dm[1].data_ptr(), dm[2].data_ptr())
@@ -65,11 +56,6 @@ def run(nch):
     if DUMP:
         lib.sd_debug_update_dump(None, None, None)
         dumps[nch] = dm
-    if SELF:
-        buf = (ctypes.c_uint32 * DW)()
-        lib.sd_debug_diag_buffer(buf, DW, 1)
-        import numpy as np
-        diag[nch] = np.frombuffer(buf, dtype=np.uint32).copy()
     meta = []
     for s in range(NS):
         m = (ctypes.c_int32 * 3)()
@@ -213,61 +199,3 @@ if DUMP:
                     if fr > 0.05:
                         hits.append((lab, sl // CALLS, sl % CALLS, region, round(fr, 3)))
         print(f"   wrong values found in the snapshot slots (run, step, call, region, fraction): {hits[:20]}")
-
-TAGS = {1: "k_gl4t", 2: "k_gl4 MODE0", 3: "k_gl4 MODE1", 4: "k_gl4 MODE2", 5: "k_gl4 MODE3", 10: "k_update_chk"}
-for nch, buf in sorted(diag.items()):
-    import numpy as np
-    nbad, nwg = int(buf[0]), int(buf[1])
-    print(f"\n== self-check, {nch} chain(s): {nbad} failing update threads, {nwg} logged workgroups")
-    wg = buf[WG_BASE: WG_BASE + 8 * min(nwg, (DW - WG_BASE) // 8)].reshape(-1, 8).astype(np.int64)
-    tag, hw, xcc = wg[:, 0], wg[:, 2], wg[:, 3]
-    t0 = wg[:, 4] | (wg[:, 5] << 32)
-    t1 = wg[:, 6] | (wg[:, 7] << 32)
-    cu = (xcc << 16) | ((hw >> 8) & 0x7F)  # XCC, SE / SH / CU
-    simd = (hw >> 4) & 3
-    for tg in sorted(set(tag.tolist())):
-        m = tag == tg
-        print(f"   {TAGS.get(tg, tg)}: {int(m.sum())} workgroups, mean {float((t1[m] - t0[m]).mean()) / 100:.1f} us")
-    if nbad == 0:
-        continue
-    rec = buf[UPD_BASE: UPD_BASE + 16 * min(nbad, UPD_MAX)].reshape(-1, 16).astype(np.int64)
-    bits = rec[:, 1] >> 16
-    hist = {b: int((bits & b != 0).sum()) for b in (1, 2, 4, 8, 16)}
-    print(f"   failing checks (1 x0 reg/reload, 2 x_t, 4 noise, 8 recompute, 16 stored): {hist}")
-    rows_bad = sorted(set(rec[:, 0].tolist()))
-    print(f"   rows {len(rows_bad)} (first {rows_bad[:10]}), d values {sorted(set((rec[:, 1] & 0xFFFF).tolist()))[:12]}")
-    # values: register vs reload of the first failing element
-    f = lambda u: np.frombuffer(np.array(u, dtype=np.uint32).tobytes(), dtype=np.float32)
-    print(f"   first records (row, d, bits, j|bits, reg, reload, HW_ID simd/wave): "
-          + "; ".join(f"({r[0]}, {r[1] & 0xFFFF}, {r[1] >> 16}, {r[8] & 0xFF}|{r[8] >> 8}, {f([r[9]])[0]:.5g}, {f([r[11]])[0]:.5g}, "
-                      f"{(r[2] >> 4) & 3}/{r[2] & 15})" for r in rec[:6]))
-    # workgroups of failing threads and what shared their CU meanwhile
-    ucu = (rec[:, 3] << 16) | ((rec[:, 2] >> 8) & 0x7F)
-    ut0 = rec[:, 4] | (rec[:, 5] << 32)
-    ut1 = rec[:, 6] | (rec[:, 7] << 32)
-    seen, co = set(), {}
-    for i in range(len(rec)):
-        key = (int(ucu[i]), int(rec[i, 13]))
-        if key in seen:
-            continue
-        seen.add(key)
-        m = (cu == ucu[i]) & (t0 < ut1[i]) & (t1 > ut0[i]) & (tag != 10)
-        for tg in set(tag[m].tolist()):
-            co[tg] = co.get(tg, 0) + 1
-        if len(seen) <= 5:
-            others = [(TAGS.get(int(a), a), int(b)) for a, b in zip(tag[m], simd[m])]
-            print(f"   failing update workgroup {rec[i, 13]} on CU {int(ucu[i]):#x}: co-resident {others[:8]}")
-    print(f"   failing update workgroups: {len(seen)}; co-resident kernel kinds over them: "
-          f"{ {TAGS.get(k, k): v for k, v in co.items()} }")
-    # the same for the update workgroups that did not fail
-    upd = np.nonzero(tag == 10)[0]
-    okc, nok = {}, 0
-    bad_wg = {k[1] for k in seen}
-    for i in upd[:4000]:
-        if int(wg[i, 1]) in bad_wg:
-            continue
-        nok += 1
-        m = (cu == cu[i]) & (t0 < t1[i]) & (t1 > t0[i]) & (tag != 10)
-        for tg in set(tag[m].tolist()):
-            okc[tg] = okc.get(tg, 0) + 1
-    print(f"   passing update workgroups sampled: {nok}; co-resident kinds: { {TAGS.get(k, k): v for k, v in okc.items()} }")

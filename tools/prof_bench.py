@@ -5,7 +5,8 @@ stats there, and record the per-layer HBM traffic in profiles/pmc_traffic.json u
 
 Per kernel (PMC passes, averaged over its dispatches): HBM read = 2 x FETCH_SIZE (gfx950 counts
 half the bytes of a wide coalesced stream, MI355X_MICROARCH.md §HBM), write = WRITE_SIZE (exact
-for 16-B-per-lane stores), MFMA busy = SQ_VALU_MFMA_BUSY_CYCLES / (SQ_BUSY_CYCLES x 4 SIMDs) per CU.
+for 16-B-per-lane stores), MFMA busy = SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE / 8 XCDs x 1,024
+SIMDs): the share of the dispatch's SIMD-cycles the matrix pipes were busy.
 One graph-linear layer = one GEMM-phase dispatch (k_gl4t / k_gl4y) + one mixing-phase dispatch
 (k_gl4 MODE 2 / 3) on the split routes, or one k_gl4 dispatch on the one-kernel route.
 usage: python tools/prof_bench.py gpurun_out/prof_<tag> <tag> [config]"""
@@ -76,7 +77,7 @@ rows = pm["config"]["rows_per_gpu"] if pm else None
 route_bits = pm["config"].get("route_bits") if pm else None
 if pmc:
     lines += ["", "## PMC per dispatch (separate passes; T = 4 run of the same configuration)", "",
-              "| kernel | dispatches | HBM read MB (2 x FETCH) | write MB | MFMA busy % | wait-inst % | wait % |",
+              "| kernel | dispatches | HBM read MB (2 x FETCH) | write MB | MFMA busy % of SIMD-cycles | wait-inst % | wait % |",
               "|---|---|---|---|---|---|---|"]
     layer_bytes, layers = 0.0, 0
     for k, c in sorted(pmc.items(), key=lambda kv: -sum(kv[1].get("FETCH_SIZE", [0]))):
@@ -84,8 +85,8 @@ if pmc:
         nd = max(len(v) for v in c.values())
         rd = 2 * avg.get("FETCH_SIZE", 0) * 1024 / 1e6
         wr = avg.get("WRITE_SIZE", 0) * 1024 / 1e6
-        busy = avg.get("SQ_BUSY_CYCLES", 0)
-        mfma = avg.get("SQ_VALU_MFMA_BUSY_CYCLES", 0) / (busy * 4) * 100 if busy else float("nan")
+        gui = avg.get("GRBM_GUI_ACTIVE", 0) / 8  # summed over the 8 XCDs
+        mfma = avg.get("SQ_VALU_MFMA_BUSY_CYCLES", 0) / (gui * 1024) * 100 if gui else float("nan")
         wave = avg.get("SQ_WAVE_CYCLES", 0)
         wi = avg.get("SQ_WAIT_INST_ANY", 0) / wave * 100 if wave else float("nan")
         wa = avg.get("SQ_WAIT_ANY", 0) / wave * 100 if wave else float("nan")
