@@ -299,6 +299,10 @@ int sd_gru_encode(const sd_gru_decoder_desc* desc, const float* x, int64_t rows,
  * results do not depend on n.  Returns the previous n; n = -1 only queries; SD_E_INVALID
  * outside [0, 8]. */
 int sd_set_row_chains(int32_t n);
+/* Process-wide form of the posterior-update kernel (test hook, like sd_set_kernel_variant): 1
+ * (default) the J x J projections on v_mfma_f32_16x16x4_f32 (J <= 32, nonisotropic), 0 the
+ * element-per-thread forms; both give the same bits.  Returns the previous value; -1 queries. */
+int32_t sd_set_update_kernel(int32_t v);
 /* Arithmetic of the plan's graph-linear launches.  mode 0 (default):
  * f32-accurate -- 3 split f16 products per f32 product, within the f32-vs-f64 drift.  mode 1:
  * half -- one f16 product (x and W rounded to f16), f32 accumulate, f32 activations in HBM; the

@@ -30,7 +30,7 @@ EXPORTED = (
     "sd_plan_set_precision", "sd_mm_ade_fde", "sd_gru_decode_workspace_bytes", "sd_gru_decode",
     "sd_gru_encode_workspace_bytes", "sd_gru_encode", "sd_gl_train_workspace_bytes", "sd_gl_train_forward",
     "sd_gl_train_backward", "sd_plan_set_option", "sd_plan_get_option", "sd_denoiser_trace",
-    "sd_workspace_status",
+    "sd_workspace_status", "sd_set_update_kernel",
 )
 
 # sd_plan_set_option keys (include/skeldiff.h)
@@ -107,6 +107,7 @@ def _declare(lib: ctypes.CDLL) -> None:
         "sd_test_attention": (ctypes.c_int, [vp, vp, i64, i32, i32, i32, vp]),
         "sd_set_kernel_variant": (ctypes.c_int, [i32, i32]),
         "sd_set_row_chains": (ctypes.c_int, [i32]),
+        "sd_set_update_kernel": (ctypes.c_int, [i32]),
         "sd_plan_set_precision": (ctypes.c_int, [vp, i32]),
         "sd_plan_set_option": (ctypes.c_int, [vp, i32, i64]),
         "sd_plan_get_option": (ctypes.c_int, [vp, i32, ctypes.POINTER(ctypes.c_int64)]),

@@ -328,13 +328,19 @@ __global__ __launch_bounds__(256) void k_gl4y(const GLArgs p, int ntile_c, int64
 // at CT = 6 vs 2.2 B in the one-kernel k_gl4 32 x 64 tile).  Per accumulator element the MFMA
 // sequence (x_hi W'_hi, x_hi W'_lo, x_lo W'_hi per chunk), RMS sum, scale and bias arithmetic are
 // k_gl4's, so phase 2 (k_gl4 MODE 2 / 3) reproduces the one-kernel route bit for bit.
-template <bool RMS, int PREC, int CT, int NCH, bool ROWMAJOR, int PF = 4>  // NCH: 16-deep k chunks (K / 16)
-__global__ __launch_bounds__(256, 2) void k_gl4t(const GLArgs p, int ncg, int64_t ntile_r, const YOut yo) {
+// WRES (resident weights, K = 192): the workgroup copies the node's whole weight slice for its CT
+// tiles (NCH chunks, 144 KiB at CT = 6) into LDS once, then every wave runs its K loop with no
+// barrier at all; NWV waves = NWV consecutive 32-row tiles.  Same products in the same order.
+template <bool RMS, int PREC, int CT, int NCH, bool ROWMAJOR, int PF = 4, int NWV = 4, bool WRES = false>
+__global__ __launch_bounds__(NWV * 64, WRES ? 1 : 2) void k_gl4t(const GLArgs p, int ncg, int64_t ntile_r, const YOut yo) {
+    constexpr int NT = NWV * 64;
     constexpr int TILE_H = PREC ? 512 : 1024;   // halves of one 32-column tile per chunk
     constexpr int PPT = TILE_H / 8;             // 16-B pieces per tile
-    constexpr int NP = (CT * PPT + 255) / 256;  // staged pieces per thread
+    constexpr int NP = (CT * PPT + NT - 1) / NT;  // staged pieces per thread
     constexpr int TS = 36;                      // floats per row of a wave's 32 x 32 output transpose
-    constexpr int SB = 2 * CT * TILE_H * 2 > 4 * 32 * TS * 4 ? 2 * CT * TILE_H * 2 : 4 * 32 * TS * 4;
+    constexpr int SBW = (WRES ? NCH : 2) * CT * TILE_H * 2;
+    constexpr int SB = SBW > NWV * 32 * TS * 4 ? SBW : NWV * 32 * TS * 4;
+    static_assert(!WRES || SB <= 160 * 1024, "resident weight slice exceeds the LDS");
     __shared__ __attribute__((aligned(16))) char smem_raw[SB];  // weight stages, then the transposes
     _Float16(*sW)[CT * TILE_H] = reinterpret_cast<_Float16(*)[CT * TILE_H]>(smem_raw);
     const int tid = threadIdx.x, lane = tid & 63, l32 = lane & 31, h = lane >> 5;
@@ -349,10 +355,10 @@ __global__ __launch_bounds__(256, 2) void k_gl4t(const GLArgs p, int ncg, int64_
     // (N = 768: 5.9 MB of split weights for all 10 types did not fit a 4 MB L2 when every XCD
     // walked every node: 196 MB fetched per launch for ~45 MB of operands)
     const int cg = (int)(u % ncg);
-    const int64_t nrg = (ntile_r + 3) / 4;
+    const int64_t nrg = (ntile_r + NWV - 1) / NWV;
     const int j = (int)((u / ncg) / nrg);
     const int64_t rgi = (u / ncg) % nrg;
-    const int64_t tr = rgi * 4 + wave;
+    const int64_t tr = rgi * NWV + wave;
     const bool live = tr < ntile_r;  // wave-uniform; a dead wave still stages weights and joins barriers
     const int64_t row0 = (live ? tr : 0) * 32;
     constexpr int nchunk = NCH;
@@ -366,13 +372,13 @@ __global__ __launch_bounds__(256, 2) void k_gl4t(const GLArgs p, int ncg, int64_
     const _Float16* wsrc[NP];
 #pragma unroll
     for (int k = 0; k < NP; ++k) {
-        const int q = min(tid + 256 * k, CT * PPT - 1);
+        const int q = min(tid + NT * k, CT * PPT - 1);
         wsrc[k] = p.wsp + ((int64_t)p.ntype[j] * nchunk * p.wsp_nct + cg * CT + q / PPT) * 1024 + (q % PPT) * 8;
     }
     const int64_t wcs = (int64_t)p.wsp_nct * 1024;  // halves per chunk
     // the carried pieces as named registers, loaded unconditionally from clamped sources (an
     // array under conditional loads was placed in scratch, with a vmcnt(0) before every store)
-    static_assert(NP <= 4, "staged pieces per thread");
+    static_assert(WRES || NP <= 4, "staged pieces per thread");
     uint4 w0, w1, w2, w3;
     auto load_w = [&](int c) {
         const int64_t o = c * wcs;
@@ -383,11 +389,11 @@ __global__ __launch_bounds__(256, 2) void k_gl4t(const GLArgs p, int ncg, int64_
     };
     auto store_w = [&](int sl) {
         uint4* d = reinterpret_cast<uint4*>(&sW[sl][tid * 8]);
-        constexpr bool FULL = CT * PPT % 256 == 0;
+        constexpr bool FULL = CT * PPT % NT == 0;
         if (FULL || tid < CT * PPT) d[0] = w0;
-        if constexpr (NP > 1) if (FULL || tid + 256 < CT * PPT) d[256] = w1;
-        if constexpr (NP > 2) if (FULL || tid + 512 < CT * PPT) d[512] = w2;
-        if constexpr (NP > 3) if (FULL || tid + 768 < CT * PPT) d[768] = w3;
+        if constexpr (NP > 1) if (FULL || tid + NT < CT * PPT) d[NT] = w1;
+        if constexpr (NP > 2) if (FULL || tid + 2 * NT < CT * PPT) d[2 * NT] = w2;
+        if constexpr (NP > 3) if (FULL || tid + 3 * NT < CT * PPT) d[3 * NT] = w3;
     };
     floatx4 xa[PF], xb[PF];
     auto issue_x = [&](int c, int sl) {
@@ -420,7 +426,7 @@ __global__ __launch_bounds__(256, 2) void k_gl4t(const GLArgs p, int ncg, int64_
 #pragma unroll
         for (int e = 0; e < 16; ++e) acc[ct][e] = 0.f;
     float ss = 0.f, amx = 0.f;
-    auto compute = [&](int c, int sl, int ws) {
+    auto compute = [&](int c, int sl, const _Float16* wst) {  // wst: the chunk's CT tiles in LDS
         if constexpr (PREC == 2) {  // bf16 mode: one bf16 product per k step (k_gl4 PREC 2's arithmetic)
             const bool bsrc = (c << 4) < p.K1 ? p.x1_bf16 : p.x2_bf16;  // wave-uniform
             bf16x8 xb16;
@@ -436,7 +442,7 @@ __global__ __launch_bounds__(256, 2) void k_gl4t(const GLArgs p, int ncg, int64_
                 const floatx8 q = f * f;
                 ss += ((q[0] + q[1]) + (q[2] + q[3])) + ((q[4] + q[5]) + (q[6] + q[7]));
             }
-            const _Float16* wt = &sW[ws][lane * 8];
+            const _Float16* wt = wst + lane * 8;
 #pragma unroll
             for (int ct = 0; ct < CT; ++ct) {
                 const bf16x8 wb = *reinterpret_cast<const bf16x8*>(wt + ct * TILE_H);
@@ -454,7 +460,7 @@ __global__ __launch_bounds__(256, 2) void k_gl4t(const GLArgs p, int ncg, int64_
         const halfx8 xh = __builtin_convertvector(f, halfx8);
         halfx8 xl;
         if constexpr (!PREC) xl = __builtin_convertvector(f - __builtin_convertvector(xh, floatx8), halfx8);
-        const _Float16* wt = &sW[ws][lane * 8];
+        const _Float16* wt = wst + lane * 8;
 #pragma unroll
         for (int ct = 0; ct < CT; ++ct) {
             const halfx8 wh = *reinterpret_cast<const halfx8*>(wt + ct * TILE_H);
@@ -467,6 +473,51 @@ __global__ __launch_bounds__(256, 2) void k_gl4t(const GLArgs p, int ncg, int64_
             acc[ct] = t;
         }
     };
+    if constexpr (WRES) {
+        // x of the first PF chunks in flight, then the whole weight slice [chunk][tile][piece] to
+        // LDS in batches of 8 pieces per thread (unconditional clamped loads), one barrier, and a
+        // K loop without barriers
+#pragma unroll
+        for (int i = 0; i < PF; ++i) issue_x(i, i);
+        constexpr int TOT = NCH * CT * PPT, PER = (TOT + NT - 1) / NT, BATCH = 8;
+        const _Float16* wb = p.wsp + ((int64_t)p.ntype[j] * nchunk * p.wsp_nct + cg * CT) * 1024;
+        uint4* dst = reinterpret_cast<uint4*>(smem_raw);
+#pragma unroll
+        for (int b0 = 0; b0 < PER; b0 += BATCH) {
+            uint4 v[BATCH];
+#pragma unroll
+            for (int i = 0; i < BATCH; ++i) {
+                const int q = min(tid + NT * (b0 + i), TOT - 1);
+                const int c = q / (CT * PPT), r = q % (CT * PPT);
+                v[i] = *reinterpret_cast<const uint4*>(wb + ((int64_t)c * p.wsp_nct + r / PPT) * 1024 + (r % PPT) * 8);
+            }
+#pragma unroll
+            for (int i = 0; i < BATCH; ++i)
+                if (tid + NT * (b0 + i) < TOT) dst[tid + NT * (b0 + i)] = v[i];
+        }
+        __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this thread's pieces are in LDS
+        asm volatile("" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        const _Float16* sw = reinterpret_cast<const _Float16*>(smem_raw);
+        if (live) {
+            if constexpr (PF == NCH) {  // every x chunk already in flight
+#pragma unroll
+                for (int c = 0; c < NCH; ++c) compute(c, c, sw + c * (CT * TILE_H));
+            } else {
+#pragma nounroll
+                for (int c0 = 0; c0 < nchunk; c0 += PF) {
+#pragma unroll
+                    for (int i = 0; i < PF; ++i) {
+                        const int c = c0 + i;
+                        compute(c, i, sw + c * (CT * TILE_H));
+                        asm volatile("" ::: "memory");
+                        issue_x(min(c + PF, nchunk - 1), i);
+                    }
+                }
+            }
+        }
+    } else {
     load_w(0);
 #pragma unroll
     for (int i = 0; i < PF; ++i)
@@ -490,11 +541,12 @@ __global__ __launch_bounds__(256, 2) void k_gl4t(const GLArgs p, int ncg, int64_
             // made the waitcnt pass merge both paths and drain the x ring every chunk
             load_w(min(c + 1, nchunk - 1));
             asm volatile("" ::: "memory");  // keep w(c + 1) older than x(c + PF): store_w(c + 1) waits for it alone
-            compute(c, i, i & 1);
+            compute(c, i, sW[i & 1]);
             asm volatile("" ::: "memory");
-            issue_x(min(c + PF, nchunk - 1), i);
+            if constexpr (PF < NCH) issue_x(min(c + PF, nchunk - 1), i);
         }
     }
+    }  // staged K loop
     __syncthreads();  // every wave past its last chunk: the stages become the output transposes
     if (!live) return;
     if (p.status && __builtin_amdgcn_ballot_w64(amx >= 65504.0f) != 0 && lane == 0) atomicOr(p.status, 1u);
@@ -1489,18 +1541,43 @@ hipError_t launch_gemm_split(const GLArgs& a, bool rms, float* z, int64_t z_rs, 
     return launch_gl4y<true>(a, rms, ntc, ntile_r, yo, s);
 }
 
-template <int CT, int NCH, bool ROWMAJOR>
-static hipError_t launch_gl4t_ct(const GLArgs& a, bool rms, int64_t ntile_r, const YOut& yo, hipStream_t s) {
+// k_gl4t's K = 192 form (SKELDIFF_GL4T_CFG, read at load): 0 = weights staged per chunk, x 4 chunks
+// ahead, 4 waves (two workgroups per CU); 1 = the same with every x chunk in flight from the
+// start; 2 / 3 = resident weights, every x chunk in flight, 4 / 8 waves; 4 = resident weights, x
+// 4 chunks ahead, 8 waves
+static int g_gl4t_cfg = [] {
+    const char* e = getenv("SKELDIFF_GL4T_CFG");
+    const int v = e ? atoi(e) : 0;
+    return (v >= 0 && v <= 4) ? v : 0;
+}();
+
+template <int CT, int NCH, bool ROWMAJOR, int NWV, bool WRES, int PF = 4>
+static hipError_t launch_gl4t_v(const GLArgs& a, bool rms, int64_t ntile_r, const YOut& yo, hipStream_t s) {
     const int ncg = a.N / (32 * CT);
-    const dim3 grid((unsigned)(((ntile_r + 3) / 4) * a.J * ncg)), block(256);
-    auto kt = a.prec == 1 ? (rms ? k_gl4t<true, 1, CT, NCH, ROWMAJOR> : k_gl4t<false, 1, CT, NCH, ROWMAJOR>)
-                          : (rms ? k_gl4t<true, 0, CT, NCH, ROWMAJOR> : k_gl4t<false, 0, CT, NCH, ROWMAJOR>);
+    const dim3 grid((unsigned)(((ntile_r + NWV - 1) / NWV) * a.J * ncg)), block(NWV * 64);
+    auto kt = a.prec == 1 ? (rms ? k_gl4t<true, 1, CT, NCH, ROWMAJOR, PF, NWV, WRES> : k_gl4t<false, 1, CT, NCH, ROWMAJOR, PF, NWV, WRES>)
+                          : (rms ? k_gl4t<true, 0, CT, NCH, ROWMAJOR, PF, NWV, WRES> : k_gl4t<false, 0, CT, NCH, ROWMAJOR, PF, NWV, WRES>);
     if constexpr (!ROWMAJOR) {  // bf16 mode (precision 2): the split route's scratch output only
-        if (a.prec == 2) kt = rms ? k_gl4t<true, 2, CT, NCH, false> : k_gl4t<false, 2, CT, NCH, false>;
+        if (a.prec == 2)
+            kt = rms ? k_gl4t<true, 2, CT, NCH, false, PF, NWV, WRES> : k_gl4t<false, 2, CT, NCH, false, PF, NWV, WRES>;
     }
     g_route_bits |= kRouteGemmTiled;
     hipLaunchKernelGGL(kt, grid, block, 0, s, a, ncg, ntile_r, yo);
     return hipGetLastError();
+}
+
+template <int CT, int NCH, bool ROWMAJOR>
+static hipError_t launch_gl4t_ct(const GLArgs& a, bool rms, int64_t ntile_r, const YOut& yo, hipStream_t s) {
+    if constexpr (NCH == 12) {
+        switch (g_gl4t_cfg) {
+            case 1: return launch_gl4t_v<CT, NCH, ROWMAJOR, 4, false, 12>(a, rms, ntile_r, yo, s);
+            case 2: return launch_gl4t_v<CT, NCH, ROWMAJOR, 4, true, 12>(a, rms, ntile_r, yo, s);
+            case 3: return launch_gl4t_v<CT, NCH, ROWMAJOR, 8, true, 12>(a, rms, ntile_r, yo, s);
+            case 4: return launch_gl4t_v<CT, NCH, ROWMAJOR, 8, true, 4>(a, rms, ntile_r, yo, s);
+            default: break;
+        }
+    }
+    return launch_gl4t_v<CT, NCH, ROWMAJOR, 4, false>(a, rms, ntile_r, yo, s);
 }
 
 // the release Denoiser's shapes: K = 192 (12 chunks), 256 (to_out, 16) or 384 (24), N a multiple

@@ -1348,6 +1348,11 @@ int sd_plan_set_precision(sd_plan* p, int32_t mode) {
     return SD_OK;
 }
 
+int32_t sd_set_update_kernel(int32_t v) {
+    if (v != -1 && v != 0 && v != 1) return fail(SD_E_INVALID, "update kernel must be 0 or 1 (-1 queries)");
+    return sd::set_update_kernel(v);
+}
+
 int sd_set_row_chains(int32_t n) {
     if (n == -1) return g_chains;
     if (n < 0 || n > sd_plan::kMaxChains) return fail(SD_E_INVALID, "row chains must be in [0 (auto), 8]");
