@@ -951,7 +951,8 @@ static int chain_count(const sd_plan* p, int64_t rows, int64_t cond_repeat, int6
     (void)cond_repeat;  // a chain starting inside a sequence's futures reads x_cond via x1_row0
     const int64_t g = 32;
     *unit = g;
-    const int64_t units = rows / g;
+    // a partial last unit counts: 50 rows (config 4, one sequence) run as chains of 32 + 18 rows
+    const int64_t units = (rows + g - 1) / g;
     // auto (0): 3 chains (+ the caller's stream = HIP's default 4 hardware queues; a 4th chain
     // shares a queue: config 2 11.9k vs 15.9k futures/s), 2 on the small-batch split route
     // (400 rows: 6,380 vs 5,870 with three; tools/sweep_routes.py, profiles/r03a)
@@ -960,7 +961,7 @@ static int chain_count(const sd_plan* p, int64_t rows, int64_t cond_repeat, int6
     return n;
 }
 static int64_t chain_row(int i, int n, int64_t rows, int64_t unit) {
-    return i >= n ? rows : (rows / unit) * i / n * unit;
+    return i >= n ? rows : std::min(rows, (rows + unit - 1) / unit * i / n * unit);
 }
 
 // Creates the auxiliary streams / fork-join events chains 1 .. n-1 use (caller holds cmu).

@@ -34,7 +34,9 @@ RELEASE_FIXTURES = ["release_h36m16_T10", "release_h36m16_T100", "release_amass2
                     # BASELINE config 3 (MANO J=51) at T=100 and config 4 (H36M J=16) at T=1000
                     "release_mano51_T100", "release_h36m16_T1000",
                     # config 3's hip-included label: AMASS-MANO J=52 (if_consider_hip=True)
-                    "release_mano52_T10"]
+                    "release_mano52_T10",
+                    # round 3: the J=52 label at config 3's T=100
+                    "release_mano52_T100"]
 
 
 _SKEL_BY_J = {16: "h36m16", 21: "amass21", 17: "freeman17", 51: "mano51", 52: "mano52"}

@@ -318,6 +318,12 @@ def gen_hip_included():
     gen_release("mano52", 10, B_seq=1, futures=2, with_acts=False)
 
 
+def gen_new_r03():
+    """Round 3: config 3's hip-included label (MANO J = 52) at the benched T = 100, 2 sequences x
+    2 futures, posterior means of four steps kept."""
+    gen_release("mano52", 100, B_seq=2, futures=2, with_acts=False, steps_to_keep=[0, 9, 49, 98])
+
+
 def gen_metrics():
     """The reference's multimodal metrics (src/metrics/multimodal.py) on synthetic samples: latent
     APD (L1) and APD (L2) over 50 futures of (J=16, 96) latents, and ADE / FDE of (frames, J*3)
@@ -391,6 +397,9 @@ def main():
     if sys.argv[1:] == ["hip"]:
         gen_hip_included()
         return
+    if sys.argv[1:] == ["r03"]:
+        gen_new_r03()
+        return
     gen_metrics()
     gen_decoder()
     gen_covariances()
@@ -402,6 +411,7 @@ def main():
     gen_release("mano51", 10, B_seq=1, futures=2, with_acts=False)
     gen_new_r02()
     gen_hip_included()
+    gen_new_r03()
 
 
 if __name__ == "__main__":

@@ -246,8 +246,9 @@ def test_row_chains_bitwise_invariant(graph, route, cuda):
     d = build_release_diffusion(z, cuda)
     J, T = 16, 10
     g = torch.Generator().manual_seed(3)
-    # 17 sequences x 6 futures = 102 rows: 3 chain units of 32 rows + a ragged tail; chains start
-    # inside a sequence's futures (row 32 = sequence 5, future 2), exercising the x_cond phase
+    # 17 sequences x 6 futures = 102 rows: 3 chain units of 32 rows + a ragged 6-row unit (up to 4
+    # chains, the last one 6 rows); chains start inside a sequence's futures (row 32 = sequence 5,
+    # future 2), exercising the x_cond phase
     xc = (torch.rand((17, J, 96), generator=g) * 2 - 1).to(cuda)
     rows = 102
     start = torch.randn((rows, J, 96), generator=g).to(cuda)
@@ -261,7 +262,7 @@ def test_row_chains_bitwise_invariant(graph, route, cuda):
         b = d.engine.sample_loop(rows, x_cond=xc, start_noise=start, sampling_noise=samp, record=(False, True),
                                  graph=graph)
         torch.cuda.synchronize()
-        assert d.engine.get_option("last_chains") == min(n, rows // 32)
+        assert d.engine.get_option("last_chains") == min(n, (rows + 31) // 32)
         res[n] = [t.clone() for t in (a[0], a[1], a[2], a[3], b[0], b[4])]
     for n in (2, 3, 8):
         for x, y in zip(res[1], res[n]):
