@@ -362,7 +362,7 @@ def main():
     route = ("tiled split (k_gl4t + k_gl4 MODE 2/3)" if tiled and not route_bits & (1 | 2) else
              "tiled split + one-kernel fused attention" if tiled else
              "small-batch split (k_gl4y + k_gl4 MODE 2/3)" if small else
-             "v5 (k_gl4t + k_gl5_mix)" if route_bits & 32 and split else
+             "v5 (k_gl4t + k_gl5_mixm + k_attention)" if route_bits & 32 and split else
              "one-kernel (k_gl4)" if split else "exact f32")
     half = split and eng.precision in ("half", "bf16")
     fused_attn = ms[1] == 0.0 and cnt[1] == 0   # attention ran inside the graph-linear launches

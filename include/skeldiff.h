@@ -253,12 +253,15 @@ enum {
                                    GEMM phase except for to_qkv + attention (one-kernel fused
                                    tile) */
     SD_OPT_LAST_CHAINS = 7,     /* read-only: row chains the plan's last sd_sample_loop ran (the
-                                   SD_OPT_ROW_CHAINS value, fewer for batches under 32 x n rows);
-                                   0 before the first call */
+                                   SD_OPT_ROW_CHAINS value, fewer for batches of fewer than n
+                                   32-row units, a ragged last unit counting; auto: 1 at <= 128
+                                   rows, 2 at <= SKELDIFF_SPLIT_ROWS, else 3); 0 before the first
+                                   call */
     SD_OPT_LAST_ROUTE = 8       /* read-only: kernels the plan's last sd_sample_loop launched, bits
                                    1 one-kernel k_gl4, 2 fused to_qkv + attention k_gl4, 4 k_gl4y
                                    GEMM phase, 8 k_gl4t GEMM phase, 16 split-route mixing /
-                                   attention phase, 32 v5 (J > 21), 64 exact-f32 kernels */
+                                   attention phase, 32 v5 mixing (J > 21), 64 exact-f32 kernels,
+                                   128 separate k_attention */
 };
 int sd_plan_set_option(sd_plan* plan, int32_t option, int64_t value);
 int sd_plan_get_option(const sd_plan* plan, int32_t option, int64_t* value);
@@ -303,6 +306,10 @@ int sd_set_row_chains(int32_t n);
  * (default) the J x J projections on v_mfma_f32_16x16x4_f32 (J <= 32, nonisotropic), 0 the
  * element-per-thread forms; both give the same bits.  Returns the previous value; -1 queries. */
 int32_t sd_set_update_kernel(int32_t v);
+/* Process-wide form of the J > 21 mixing pass (v5, test hook): 1 (default) G-hat mixing on
+ * v_mfma_f32_16x16x4_f32 with 8 rows per workgroup (k_gl5_mixm), 0 the per-column VALU form
+ * (k_gl5_mix); the same j-ordered fmaf chains.  Returns the previous value; -1 queries. */
+int32_t sd_set_v5_mix(int32_t v);
 /* Arithmetic of the plan's graph-linear launches.  mode 0 (default):
  * f32-accurate -- 3 split f16 products per f32 product, within the f32-vs-f64 drift.  mode 1:
  * half -- one f16 product (x and W rounded to f16), f32 accumulate, f32 activations in HBM; the

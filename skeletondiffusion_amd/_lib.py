@@ -30,7 +30,7 @@ EXPORTED = (
     "sd_plan_set_precision", "sd_mm_ade_fde", "sd_gru_decode_workspace_bytes", "sd_gru_decode",
     "sd_gru_encode_workspace_bytes", "sd_gru_encode", "sd_gl_train_workspace_bytes", "sd_gl_train_forward",
     "sd_gl_train_backward", "sd_plan_set_option", "sd_plan_get_option", "sd_denoiser_trace",
-    "sd_workspace_status", "sd_set_update_kernel",
+    "sd_workspace_status", "sd_set_update_kernel", "sd_set_v5_mix",
 )
 
 # sd_plan_set_option keys (include/skeldiff.h)
@@ -38,7 +38,8 @@ EXPORTED = (
  SD_OPT_SPLIT_ROUTE, SD_OPT_LAST_CHAINS, SD_OPT_LAST_ROUTE) = 1, 2, 3, 4, 5, 6, 7, 8
 # SD_OPT_LAST_ROUTE bits (sd::RouteBits)
 ROUTE_BITS = {1: "k_gl4 one-kernel", 2: "k_gl4 fused to_qkv+attention", 4: "k_gl4y GEMM phase",
-              8: "k_gl4t GEMM phase", 16: "k_gl4 MODE 2/3 mixing phase", 32: "v5 k_gl5", 64: "exact-f32 kernels"}
+              8: "k_gl4t GEMM phase", 16: "k_gl4 MODE 2/3 mixing phase", 32: "v5 k_gl5 mixing", 64: "exact-f32 kernels",
+              128: "k_attention"}
 SD_STATUS_F16_RANGE = 1
 
 
@@ -108,6 +109,7 @@ def _declare(lib: ctypes.CDLL) -> None:
         "sd_set_kernel_variant": (ctypes.c_int, [i32, i32]),
         "sd_set_row_chains": (ctypes.c_int, [i32]),
         "sd_set_update_kernel": (ctypes.c_int, [i32]),
+        "sd_set_v5_mix": (ctypes.c_int, [i32]),
         "sd_plan_set_precision": (ctypes.c_int, [vp, i32]),
         "sd_plan_set_option": (ctypes.c_int, [vp, i32, i64]),
         "sd_plan_get_option": (ctypes.c_int, [vp, i32, ctypes.POINTER(ctypes.c_int64)]),

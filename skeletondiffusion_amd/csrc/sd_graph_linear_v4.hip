@@ -832,6 +832,58 @@ __global__ __launch_bounds__(NW * 64, 1) void k_gl4(const GLArgs p) {
         toff[m] = p.ntype[jn[m]] * (CT * TILE_H);
     }
 
+    // (mixing-epilogue helpers, defined before the phase-2 loads so MODE 2 can issue its residual
+    // loads together with the Y slab's)
+    // Mixing block b (0 <= b < COLS) of a 16-row slab = 16 (row, column) positions; the A lane lr
+    // reads position lr, the output lane (lr = node, lg) owns positions 4 lg .. 4 lg + 3, which
+    // are always 4 consecutive columns of one row (one 16-B piece).  Row-major output: a block is
+    // 16 consecutive columns of one row, so the 4 lanes of a node cover 64 contiguous bytes.
+    // Row-blocked output: a block is 4 rows x 4 columns (lg -> row), so the 4 lanes of a node
+    // cover 4 consecutive rows of one 4-feature group = 64 contiguous bytes of that layout.
+    const bool blk_out = p.out_blk != 0;  // wave-uniform
+    auto a_off = [&](int b) {             // LDS offset (row * YR + col) of this lane's A position
+        return blk_out ? ((b / (COLS / 4)) * 4 + (lr >> 2)) * YR + (b % (COLS / 4)) * 4 + (lr & 3)
+                       : (b / (COLS / 16)) * YR + (b % (COLS / 16)) * 16 + lr;
+    };
+    auto out_pos = [&](int b, int& r, int& cc) {  // row in the slab and first column of this lane's quad
+        if (blk_out) {
+            r = (b / (COLS / 4)) * 4 + lg;
+            cc = (b % (COLS / 4)) * 4;
+        } else {
+            r = b / (COLS / 16);
+            cc = (b % (COLS / 16)) * 16 + 4 * lg;
+        }
+    };
+    // J <= 16: a slab's residual pieces are all loaded before the Y exchange (latency hidden);
+    // J > 16 (two node blocks): per group of PG blocks, halving the registers they hold
+    constexpr bool RES_EARLY = IB == 1;
+    constexpr int PG0 = (IB == 1 && BPW <= 8) ? BPW : (BPW < 4 ? BPW : 4);
+    floatx4 rv[RES_EARLY ? BPW : PG0][IB];
+    auto load_res = [&](int hc, int kfirst, int kcount) {
+#pragma unroll
+        for (int kk = 0; kk < (RES_EARLY ? BPW : PG0); ++kk) {
+            if (kk >= kcount) continue;
+            const int k = kfirst + kk;
+            const int b = k < BPW ? wave + NW * k : COLS;
+            int r, cc;
+            out_pos(min(b, COLS - 1), r, cc);
+            const int64_t row = row0 + 16 * hc + r;
+            const int n = c0 + cc;
+            const bool ok = b < COLS && row < p.B && n < p.N;  // N % 4 == 0 (checked at launch)
+#pragma unroll
+            for (int ib = 0; ib < IB; ++ib) {
+                const int i = ib * 16 + lr;
+                const int64_t ro = p.res_blk ? blk_off(row, i, n, J, p.N) : row * p.res_rs + (int64_t)i * p.N + n;
+                if (PREC == 2 && p.res_bf16)
+                    rv[kk][ib] = (ok && i < J) ? __builtin_convertvector(
+                                                     *reinterpret_cast<const bf16x4*>(reinterpret_cast<const __bf16*>(p.res) + ro), floatx4)
+                                               : floatx4{0.f, 0.f, 0.f, 0.f};
+                else
+                    rv[kk][ib] = (ok && i < J) ? g4(p.res + ro) : floatx4{0.f, 0.f, 0.f, 0.f};
+            }
+        }
+    };
+
     floatx16 acc[NPW][RT][CT];
     uint64_t ts[8];  // DBG 6: phase stamps (s_memrealtime, 100 MHz) + shader clock around the K loop
     uint64_t cs[5];  // DBG 6: shader-clock stamps inside chunk 5
@@ -864,6 +916,8 @@ __global__ __launch_bounds__(NW * 64, 1) void k_gl4(const GLArgs p) {
             float* d;
             if (q < YQ) yv[k] = g4(ysrc(q, d));
         }
+        if constexpr (MODE == 2 && RES_EARLY)  // the residual in flight with the slab (one memory latency)
+            if (p.res) load_res(slab, 0, BPW);
 #pragma unroll
         for (int k = 0; k < NGL; ++k)
             if (tid + k * NTH < J * J) gv[k] = p.G[tid + k * NTH];
@@ -1245,61 +1299,11 @@ __global__ __launch_bounds__(NW * 64, 1) void k_gl4(const GLArgs p) {
             const int i = ib * 16 + lr, jj = 4 * s + lg;
             ga[ib][s] = (i < J && jj < J) ? sG[i * J + jj] : 0.f;
         }
-    // Mixing block b (0 <= b < COLS) of a 16-row slab = 16 (row, column) positions; the A lane lr
-    // reads position lr, the output lane (lr = node, lg) owns positions 4 lg .. 4 lg + 3, which
-    // are always 4 consecutive columns of one row (one 16-B piece).  Row-major output: a block is
-    // 16 consecutive columns of one row, so the 4 lanes of a node cover 64 contiguous bytes.
-    // Row-blocked output: a block is 4 rows x 4 columns (lg -> row), so the 4 lanes of a node
-    // cover 4 consecutive rows of one 4-feature group = 64 contiguous bytes of that layout.
-    const bool blk_out = p.out_blk != 0;  // wave-uniform
-    auto a_off = [&](int b) {             // LDS offset (row * YR + col) of this lane's A position
-        return blk_out ? ((b / (COLS / 4)) * 4 + (lr >> 2)) * YR + (b % (COLS / 4)) * 4 + (lr & 3)
-                       : (b / (COLS / 16)) * YR + (b % (COLS / 16)) * 16 + lr;
-    };
-    auto out_pos = [&](int b, int& r, int& cc) {  // row in the slab and first column of this lane's quad
-        if (blk_out) {
-            r = (b / (COLS / 4)) * 4 + lg;
-            cc = (b % (COLS / 4)) * 4;
-        } else {
-            r = b / (COLS / 16);
-            cc = (b % (COLS / 16)) * 16 + 4 * lg;
-        }
-    };
-    // J <= 16: a slab's residual pieces are all loaded before the Y exchange (latency hidden);
-    // J > 16 (two node blocks): per group of PG blocks, halving the registers they hold
-    constexpr bool RES_EARLY = IB == 1;
-    constexpr int PG0 = (IB == 1 && BPW <= 8) ? BPW : (BPW < 4 ? BPW : 4);
-    floatx4 rv[RES_EARLY ? BPW : PG0][IB];
-    auto load_res = [&](int hc, int kfirst, int kcount) {
-#pragma unroll
-        for (int kk = 0; kk < (RES_EARLY ? BPW : PG0); ++kk) {
-            if (kk >= kcount) continue;
-            const int k = kfirst + kk;
-            const int b = k < BPW ? wave + NW * k : COLS;
-            int r, cc;
-            out_pos(min(b, COLS - 1), r, cc);
-            const int64_t row = row0 + 16 * hc + r;
-            const int n = c0 + cc;
-            const bool ok = b < COLS && row < p.B && n < p.N;  // N % 4 == 0 (checked at launch)
-#pragma unroll
-            for (int ib = 0; ib < IB; ++ib) {
-                const int i = ib * 16 + lr;
-                const int64_t ro = p.res_blk ? blk_off(row, i, n, J, p.N) : row * p.res_rs + (int64_t)i * p.N + n;
-                if (PREC == 2 && p.res_bf16)
-                    rv[kk][ib] = (ok && i < J) ? __builtin_convertvector(
-                                                     *reinterpret_cast<const bf16x4*>(reinterpret_cast<const __bf16*>(p.res) + ro), floatx4)
-                                               : floatx4{0.f, 0.f, 0.f, 0.f};
-                else
-                    rv[kk][ib] = (ok && i < J) ? g4(p.res + ro) : floatx4{0.f, 0.f, 0.f, 0.f};
-            }
-        }
-    };
-
 #pragma unroll
     for (int hc0 = 0; hc0 < (MODE == 2 ? 1 : 2 * RT); ++hc0) {
         const int hc = MODE == 2 ? slab : hc0;
         const int rt = hc >> 1, hf = hc & 1;
-        if (RES_EARLY && p.res) load_res(hc, 0, BPW);  // latency hides under the Y exchange below
+        if (RES_EARLY && MODE != 2 && p.res) load_res(hc, 0, BPW);  // latency hides under the Y exchange below
         if constexpr (MODE != 2) {  // MODE 2: the slab is in sY already
             __syncthreads();        // K loop / previous slab done with the LDS that sY aliases
 #pragma unroll
@@ -1500,18 +1504,31 @@ static int split_route(const GLArgs& a, bool attn) {
     // faster than the one-kernel route on three (FreeMan J = 17 10,954 vs 9,547, AMASS J = 21 8,567
     // vs 8,371 futures/s at 3,200 rows, T = 100; config 5 half 133,002 vs 92,456, bf16 134,084 vs
     // 120,821; AMASS J = 21 bf16 9,563 vs 9,946 keeps the one-kernel route; DESIGN.md §4d'')
-    // J = 16 (f32): the tiled route (one chain) at 3,200 rows and up measured 15,135 / 15,195 vs
-    // 14,947 / 14,917 futures/s for the one-kernel route on three chains (config 2); below that, and
-    // in half / bf16 mode, the one-kernel tiles stay (1,600 rows: 10.9k vs 12.5k)
-    if (a.J == 16) return (a.prec == 0 && rows >= 3200) ? 2 : 0;
+    // J = 16 (f32): the tiled route above the split-route threshold (three row chains sharing CUs,
+    // round 3, same box: 800 rows 8,146 vs 7,516 futures/s for the one-kernel route, 1,600 rows
+    // 12,385 vs 12,473, config 2 15,940 vs 14,972 with the fused one-kernel attention tile); in
+    // half / bf16 mode the one-kernel tiles stay
+    if (a.J == 16) return a.prec == 0 ? 2 : 0;
     return (a.J == 17 || a.J == 21) ? 2 : 0;
 }
+
+// k_gl4y chunks in flight for grids of at most one workgroup per CU (SKELDIFF_GL4Y_PF at load:
+// 8 or 12): with every chunk of a K = 192 layer in flight the wave pays one memory latency
+static int g_gl4y_pf = [] {
+    const char* e = getenv("SKELDIFF_GL4Y_PF");
+    return (e && atoi(e) == 8) ? 8 : 12;
+}();
 
 template <bool ROWMAJOR>
 static hipError_t launch_gl4y(const GLArgs& a, bool rms, int ntc, int64_t ntile_r, const YOut& yo, hipStream_t s) {
     const int64_t units = ntile_r * a.J * ntc;
     const dim3 grid((unsigned)((units + 3) / 4)), block(256);
     g_route_bits |= kRouteGemmWave;
+    if (g_gl4y_pf == 12 && grid.x <= 256 && a.prec == 0) {
+        if (rms) hipLaunchKernelGGL((k_gl4y<true, 0, ROWMAJOR, 12>), grid, block, 0, s, a, ntc, ntile_r, yo);
+        else hipLaunchKernelGGL((k_gl4y<false, 0, ROWMAJOR, 12>), grid, block, 0, s, a, ntc, ntile_r, yo);
+        return hipGetLastError();
+    }
     if (a.prec == 1) {
         if (rms) hipLaunchKernelGGL((k_gl4y<true, 1, ROWMAJOR>), grid, block, 0, s, a, ntc, ntile_r, yo);
         else hipLaunchKernelGGL((k_gl4y<false, 1, ROWMAJOR>), grid, block, 0, s, a, ntc, ntile_r, yo);

@@ -26,6 +26,7 @@ namespace sd {
 namespace {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float floatx4 __attribute__((ext_vector_type(4)));
 
 constexpr int TM = 64, TN = 64, TK = 32;
 
@@ -201,7 +202,127 @@ __global__ __launch_bounds__(256) void k_gl5_mix(const GLArgs p, const float* z,
     }
 }
 
+// The mixing pass on the matrix cores, R rows per workgroup.  k_gl5_mix above is bound by its LDS
+// reads: per source node every wave issues one z read and four 16-B G-hat^T broadcast reads (4 LDS
+// cycles each) for 16 multiply-adds, ~18 LDS cycles per 16 FMAs, with one row per workgroup.  Here
+// per (row b, 64 columns) Z^T = z^T G-hat^T runs on v_mfma_f32_16x16x4_f32: A = z^T[col][j] from
+// the row's z slab in LDS (one 4-B read per lane per MFMA), B = G-hat^T[j][i] in registers (wave w
+// owns output nodes 16 w .. 16 w + 15; ceil(J / 4) fragments, loaded once per workgroup), D[col =
+// 16 cb + 4 l4 + e][i = 16 w + l16]: four consecutive columns of one node per lane, so the
+// residual loads and output stores are 16 B.  The f32 MFMA accumulates its 4 k products as an fmaf
+// chain in k order, so each sum is k_gl5_mix's j-ordered fmaf chain (zero padding adds exact
+// zeros).  The next row's slab is loaded to registers while the current row is mixed (two LDS
+// slab buffers, one barrier per row).  J <= 64, N % 64 == 0, 16-B aligned z / res / out.
+template <int R>
+__global__ __launch_bounds__(256) void k_gl5_mixm(const GLArgs p, const float* z, int64_t z_rs) {
+    constexpr int ZS = 80;                 // floats per slab row (64 + 16: the 4 k lanes of a read hit 4 bank groups)
+    constexpr int SLAB = kMaxNodes * ZS;   // floats per slab buffer (rows >= J stay zero)
+    constexpr int NQ = kMaxNodes * 16;     // 16-B pieces of a full slab
+    constexpr int QPT = NQ / 256;          // pieces per thread (4)
+    __shared__ __attribute__((aligned(16))) float s_z[2 * SLAB];
+    const int tid = threadIdx.x, lane = tid & 63, l16 = lane & 15, l4 = lane >> 4;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int J = p.J, N = p.N, KS = (J + 3) >> 2;
+    const int n0 = blockIdx.y * 64;
+    const int64_t b0 = (int64_t)blockIdx.x * R;
+    const int nrows = (int)min((int64_t)R, p.B - b0);
+    // B fragments: G-hat^T[j = 4 s + l4][i = 16 w + l16] = G-hat[i][j], zero outside J x J
+    const int i = 16 * w + l16;
+    float gb[16];
+#pragma unroll
+    for (int s = 0; s < 16; ++s) {
+        const int j = 4 * s + l4;
+        gb[s] = (s < KS && i < J && j < J) ? p.G[i * J + j] : 0.f;
+    }
+    // FiLM of this lane's four columns per 16-column block
+    float4 fa[4], fb[4];
+#pragma unroll
+    for (int cb = 0; cb < 4; ++cb) {
+        const int n = n0 + 16 * cb + 4 * l4;
+        fa[cb] = p.film ? *reinterpret_cast<const float4*>(p.film + n) : make_float4(1.f, 1.f, 1.f, 1.f);
+        fb[cb] = p.film ? *reinterpret_cast<const float4*>(p.film + N + n) : make_float4(0.f, 0.f, 0.f, 0.f);
+        if (p.film) fa[cb] = make_float4(fa[cb].x + 1.0f, fa[cb].y + 1.0f, fa[cb].z + 1.0f, fa[cb].w + 1.0f);
+    }
+    // slab piece q of thread t: node q >> 4, columns 4 (q & 15) .. + 3 (pieces of nodes >= J: zero)
+    float4 zv[QPT];
+    auto load_slab = [&](int r) {
+        const float* zr = z + (b0 + r) * z_rs + n0;
+#pragma unroll
+        for (int k = 0; k < QPT; ++k) {
+            const int q = tid + 256 * k, j = q >> 4;
+            zv[k] = j < J ? *reinterpret_cast<const float4*>(zr + (int64_t)j * N + 4 * (q & 15)) : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+    };
+    auto store_slab = [&](int buf) {
+#pragma unroll
+        for (int k = 0; k < QPT; ++k) {
+            const int q = tid + 256 * k;
+            *reinterpret_cast<float4*>(s_z + buf * SLAB + (q >> 4) * ZS + 4 * (q & 15)) = zv[k];
+        }
+    };
+    const bool live = i < J;  // this lane's output node
+    float4 rv[4];
+    auto load_res = [&](int r) {
+#pragma unroll
+        for (int cb = 0; cb < 4; ++cb)
+            rv[cb] = (p.res && live) ? *reinterpret_cast<const float4*>(p.res + (b0 + r) * p.res_rs + (int64_t)i * N + n0 + 16 * cb + 4 * l4)
+                                     : make_float4(0.f, 0.f, 0.f, 0.f);
+    };
+    load_slab(0);
+    store_slab(0);
+    __syncthreads();
+    for (int r = 0; r < nrows; ++r) {
+        const int buf = r & 1;
+        if (r + 1 < nrows) load_slab(r + 1);
+        load_res(r);
+        floatx4 acc[4];
+#pragma unroll
+        for (int cb = 0; cb < 4; ++cb) {
+            floatx4 t = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int s = 0; s < 16; ++s) {
+                if (s < KS) {  // wave-uniform
+                    const float a = s_z[buf * SLAB + (4 * s + l4) * ZS + 16 * cb + l16];
+                    t = __builtin_amdgcn_mfma_f32_16x16x4f32(a, gb[s], t, 0, 0, 0);
+                }
+            }
+            acc[cb] = t;
+        }
+        if (live) {
+            float* orow = p.out + (b0 + r) * p.out_rs + (int64_t)i * N + n0 + 4 * l4;
+#pragma unroll
+            for (int cb = 0; cb < 4; ++cb) {
+                float v[4] = {acc[cb][0], acc[cb][1], acc[cb][2], acc[cb][3]};
+                const float fav[4] = {fa[cb].x, fa[cb].y, fa[cb].z, fa[cb].w};
+                const float fbv[4] = {fb[cb].x, fb[cb].y, fb[cb].z, fb[cb].w};
+                const float rvv[4] = {rv[cb].x, rv[cb].y, rv[cb].z, rv[cb].w};
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    if (p.film) v[e] = v[e] * fav[e] + fbv[e];
+                    if (p.act == 1) v[e] = tanhf(v[e]);
+                    v[e] = v[e] + rvv[e];
+                }
+                *reinterpret_cast<float4*>(orow + 16 * cb) = make_float4(v[0], v[1], v[2], v[3]);
+            }
+        }
+        if (r + 1 < nrows) store_slab(buf ^ 1);  // buffer buf ^ 1 was last read in row r - 1
+        __syncthreads();
+    }
+}
+
 }  // namespace
+
+// 1 (default): the mixing pass on k_gl5_mixm where it applies; 0: k_gl5_mix (SKELDIFF_V5_MIX at
+// load, sd_set_v5_mix)
+static int g_mix_mfma = [] {
+    const char* e = getenv("SKELDIFF_V5_MIX");
+    return e ? (atoi(e) != 0) : 1;
+}();
+int set_v5_mix(int v) {
+    const int old = g_mix_mfma;
+    if (v == 0 || v == 1) g_mix_mfma = v;
+    return old;
+}
 
 // Row-major operands only; J <= kMaxNodes.  hipErrorNotSupported where v5 does not apply.
 hipError_t launch_graph_linear_v5(const GLArgs& a, bool rms, hipStream_t s) {
@@ -236,9 +357,18 @@ hipError_t launch_graph_linear_v5(const GLArgs& a, bool rms, hipStream_t s) {
         e = hipGetLastError();
     }
     if (e != hipSuccess) return e;
-    const dim3 g2((unsigned)a.B, (unsigned)((a.N + 63) / 64));
     const int vec = ((uintptr_t)z & 15) == 0 && (a.N & 3) == 0 && (z_rs & 3) == 0;
     g_route_bits |= kRouteV5Mix;
+    // the matrix-core mixing pass: 64-column blocks, 16-B z / residual / output pieces
+    const bool mfma = g_mix_mfma && vec && a.N % 64 == 0 && ((uintptr_t)a.out & 15) == 0 && (a.out_rs & 3) == 0 &&
+                      (!a.res || (((uintptr_t)a.res & 15) == 0 && (a.res_rs & 3) == 0)) && a.B / 8 < 0x7fffffff;
+    if (mfma) {
+        constexpr int R = 8;
+        hipLaunchKernelGGL(k_gl5_mixm<R>, dim3((unsigned)((a.B + R - 1) / R), (unsigned)(a.N / 64)), dim3(256), 0, s, a,
+                           (const float*)z, z_rs);
+        return hipGetLastError();
+    }
+    const dim3 g2((unsigned)a.B, (unsigned)((a.N + 63) / 64));
     hipLaunchKernelGGL(k_gl5_mix, g2, dim3(256), 0, s, a, (const float*)z, z_rs, vec);
     return hipGetLastError();
 }

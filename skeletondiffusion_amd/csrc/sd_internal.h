@@ -79,7 +79,8 @@ enum RouteBits : unsigned {
     kRouteGemmTiled = 8,   // k_gl4t: tiled split route (and v5) GEMM phase
     kRouteMixPhase = 16,   // k_gl4 MODE 2 / 3: split-route mixing / attention phase
     kRouteV5Mix = 32,      // k_gl5_gemm / k_gl5_mix (J > 21)
-    kRouteExact = 64       // exact-f32 generations v1-v3 and k_attention
+    kRouteExact = 64,      // exact-f32 generations v1-v3
+    kRouteAttention = 128  // k_attention: the separate attention kernel (J > 21, unfused routes)
 };
 extern thread_local unsigned g_route_bits;
 
@@ -139,6 +140,7 @@ int set_gl4_stage(int stage);         // returns the previous value, -1 if out o
 hipError_t launch_attention(const AttnArgs& a, hipStream_t s);
 hipError_t launch_update(const UpdArgs& a, hipStream_t s);
 int set_update_kernel(int v);  // 1 k_update_mfma, 0 element-per-thread forms; returns the previous
+int set_v5_mix(int v);         // 1 k_gl5_mixm (matrix cores), 0 k_gl5_mix; returns the previous
 hipError_t launch_noise_fill(float* out, int64_t rows, int64_t n_per_row, uint64_t seed,
                              int64_t row0, int step, const uint64_t* rng_dev, hipStream_t s,
                              int64_t row_shift = 0,   // row_shift: added to row0 (either source)

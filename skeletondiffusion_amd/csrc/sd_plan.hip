@@ -955,8 +955,13 @@ static int chain_count(const sd_plan* p, int64_t rows, int64_t cond_repeat, int6
     const int64_t units = (rows + g - 1) / g;
     // auto (0): 3 chains (+ the caller's stream = HIP's default 4 hardware queues; a 4th chain
     // shares a queue: config 2 11.9k vs 15.9k futures/s), 2 on the small-batch split route
-    // (400 rows: 6,380 vs 5,870 with three; tools/sweep_routes.py, profiles/r03a)
-    int n = p->chains > 0 ? std::min(p->chains, (int)sd_plan::kMaxChains) : rows <= sd::split_rows_default() ? 2 : 3;
+    // (400 rows: 5,920 vs 5,398 on one, 3,279 on three), one at 128 rows and below, where every
+    // kernel is a few microseconds long and a second chain slows both (config 4, 50 rows: 61 vs
+    // 106 futures/s; tools/sweep_routes.py, profiles/r03/ab)
+    int n = p->chains > 0 ? std::min(p->chains, (int)sd_plan::kMaxChains)
+            : rows <= 128                       ? 1
+            : rows <= sd::split_rows_default() ? 2
+                                               : 3;
     if (units < n) n = (int)std::max<int64_t>(1, units);
     return n;
 }
@@ -1352,6 +1357,11 @@ int sd_plan_set_precision(sd_plan* p, int32_t mode) {
 int32_t sd_set_update_kernel(int32_t v) {
     if (v != -1 && v != 0 && v != 1) return fail(SD_E_INVALID, "update kernel must be 0 or 1 (-1 queries)");
     return sd::set_update_kernel(v);
+}
+
+int32_t sd_set_v5_mix(int32_t v) {
+    if (v != -1 && v != 0 && v != 1) return fail(SD_E_INVALID, "v5 mixing form must be 0 or 1 (-1 queries)");
+    return sd::set_v5_mix(v);
 }
 
 int sd_set_row_chains(int32_t n) {

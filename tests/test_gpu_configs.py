@@ -61,18 +61,17 @@ def test_config4_t1000_graph_first_and_last_steps(cuda):
     out = torch.empty((rows, J, D), device=cuda)
     g = eng.sample_loop(rows, x_cond=x_cond, seed=seed, graph=True, out=out, record=(False, True))
     img_g, start, imgs = g[0].clone(), g[1].clone(), g[4]
-    # auto row chains: 50 rows run as two concurrent chains of 32 + 18 rows
-    assert eng.get_option("last_chains") == 2
+    assert eng.get_option("last_chains") == 1  # auto: one chain at 128 rows and below
     g2 = eng.sample_loop(rows, x_cond=x_cond, seed=seed, graph=True, out=out, keep_start=False)[0].clone()
     e = eng.sample_loop(rows, x_cond=x_cond, seed=seed, graph=False)[0]
-    eng.set_option("row_chains", 1)
-    one = eng.sample_loop(rows, x_cond=x_cond, seed=seed, graph=True, record=(False, True))
+    eng.set_option("row_chains", 2)  # two chains of 32 + 18 rows (a ragged last 32-row unit)
+    two = eng.sample_loop(rows, x_cond=x_cond, seed=seed, graph=True, record=(False, True))
     torch.cuda.synchronize()
-    assert eng.get_option("last_chains") == 1
+    assert eng.get_option("last_chains") == 2
     eng.set_option("row_chains", 0)
     assert torch.isfinite(img_g).all() and img_g.abs().max() <= 1.0 + 1e-6  # t = 0: clamp(x0)
     assert torch.equal(img_g, g2) and torch.equal(img_g, e)
-    assert torch.equal(img_g, one[0]) and torch.equal(imgs, one[4])  # chain-count invariant, every step
+    assert torch.equal(img_g, two[0]) and torch.equal(imgs, two[4])  # chain-count invariant, every step
     sd, cfg, bufs = _oracle_setup(d)
     xc = x_cond.cpu()
     r = np.arange(rows)

@@ -1,7 +1,7 @@
 """GPU: the posterior update on the matrix cores (k_update_mfma, sd_kernels.hip) against the
 element-per-thread forms (k_update / k_update_row) it replaces, bitwise -- latents, posterior
 means, noise and timages records -- over the row counts of both of its workgroup shapes (one row
-and four rows per workgroup), J = 16 / 17 / 21, device and given noise, f32 and bf16 latents
+and four rows per workgroup), J = 16 / 17 / 21 and the J <= 64 form (MANO J = 51 / 52), device and given noise, f32 and bf16 latents
 (reference op: nonisotropic.py:196-210 q_posterior + p_sample; the oracle parity of the whole
 chain is in test_gpu_parity.py / test_gpu_configs.py)."""
 import pytest
@@ -13,7 +13,8 @@ pytestmark = pytest.mark.gpu
 
 
 @pytest.mark.parametrize("cfg,batch,prec", [("amass16", 64, "f32"), ("amass16", 1, "f32"), ("amass16", 21, "f32"),
-                                            ("freeman17", 8, "f32"), ("amass21", 30, "f32"), ("freeman17", 24, "bf16")])
+                                            ("freeman17", 8, "f32"), ("amass21", 30, "f32"), ("freeman17", 24, "bf16"),
+                                            ("mano51", 2, "f32"), ("mano52", 1, "f32")])
 @pytest.mark.parametrize("given", [False, True])
 def test_update_mfma_bitwise_vs_elementwise(cfg, batch, prec, given, cuda):
     from bench import build_config

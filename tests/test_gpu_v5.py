@@ -1,0 +1,32 @@
+"""GPU: the J > 21 mixing pass on the matrix cores (k_gl5_mixm, sd_graph_linear_v5.hip) against the
+per-column VALU form (k_gl5_mix) it replaces -- bitwise, over whole sampling chains of the MANO
+Denoisers (config 3: J = 51 and the hip-included J = 52), row counts that leave ragged 8-row
+workgroups, f32 mode (reference op: graph_structural.py:30-43, G-hat mixing of StaticGraphLinear;
+the oracle parity of the chain is test_gpu_parity.py's release_mano51 / release_mano52 goldens)."""
+import pytest
+import torch
+
+from skeletondiffusion_amd import _lib
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("cfg,batch", [("mano51", 3), ("mano51", 1), ("mano52", 2)])
+def test_v5_mix_mfma_bitwise_vs_valu(cfg, batch, cuda):
+    from bench import build_config
+
+    d, x_cond, rows = build_config(cfg, cuda, T=10, batch=batch)
+    eng = d.engine
+    L = _lib.lib()
+    res = {}
+    try:
+        for v in (0, 1):
+            L.sd_set_v5_mix(v)
+            a = eng.sample_loop(rows, x_cond=x_cond, seed=5, record=(True, False), graph=False)
+            torch.cuda.synchronize()
+            res[v] = [t.clone() for t in (a[0], a[3])]  # img, mean_t
+    finally:
+        L.sd_set_v5_mix(1)
+    for name, x, y in zip(("img", "mean_t"), res[0], res[1]):
+        assert torch.equal(x, y), (name, float((x - y).abs().max()))
+    assert L.sd_set_v5_mix(-1) == 1 and L.sd_set_v5_mix(2) < 0

@@ -26,7 +26,7 @@ os.makedirs(dst, exist_ok=True)
 
 
 def short(name):
-    n = name.replace("void ", "")
+    n = name.replace("void ", "").replace("(anonymous namespace)::", "")
     return re.sub(r"\(.*", "", n)
 
 

@@ -36,7 +36,7 @@ for spec in (sys.argv[1:] or DEFAULT):
     steps = 2 if d.num_timesteps >= 1000 else 5
     for route in ROUTES.get(cfg.split("_")[0] if cfg not in ROUTES else cfg, [0]):
         for n in CHAINS:
-            if rows < 32 * n and n > 1:
+            if (rows + 31) // 32 < n and n > 1:
                 continue
             eng.set_option("split_route", route)
             eng.set_option("row_chains", n)
