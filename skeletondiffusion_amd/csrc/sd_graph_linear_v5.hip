@@ -213,16 +213,17 @@ __global__ __launch_bounds__(256) void k_gl5_mix(const GLArgs p, const float* z,
 // chain in k order, so each sum is k_gl5_mix's j-ordered fmaf chain (zero padding adds exact
 // zeros).  The next row's slab is loaded to registers while the current row is mixed (two LDS
 // slab buffers, one barrier per row).  J <= 64, N % 64 == 0, 16-B aligned z / res / out.
-template <int R>
+template <int R, int PD>
 __global__ __launch_bounds__(256) void k_gl5_mixm(const GLArgs p, const float* z, int64_t z_rs) {
     constexpr int ZS = 80;                 // floats per slab row (64 + 16: the 4 k lanes of a read hit 4 bank groups)
-    constexpr int SLAB = kMaxNodes * ZS;   // floats per slab buffer (rows >= J stay zero)
-    constexpr int NQ = kMaxNodes * 16;     // 16-B pieces of a full slab
-    constexpr int QPT = NQ / 256;          // pieces per thread (4)
-    __shared__ __attribute__((aligned(16))) float s_z[2 * SLAB];
+    constexpr int QPT = kMaxNodes * 16 / 256;  // 16-B slab pieces per thread at most (4)
+    // two slab buffers of 4 ceil(J / 4) rows (the k extent of the MFMAs; rows >= J stay zero) in
+    // dynamic LDS: 33 KB at J = 51, four workgroups per CU
+    extern __shared__ __attribute__((aligned(16))) float s_z[];
     const int tid = threadIdx.x, lane = tid & 63, l16 = lane & 15, l4 = lane >> 4;
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int J = p.J, N = p.N, KS = (J + 3) >> 2;
+    const int SLAB = 4 * KS * ZS, NQ = 4 * KS * 16;  // floats per slab buffer, 16-B pieces per slab
     const int n0 = blockIdx.y * 64;
     const int64_t b0 = (int64_t)blockIdx.x * R;
     const int nrows = (int)min((int64_t)R, p.B - b0);
@@ -234,47 +235,52 @@ __global__ __launch_bounds__(256) void k_gl5_mixm(const GLArgs p, const float* z
         const int j = 4 * s + l4;
         gb[s] = (s < KS && i < J && j < J) ? p.G[i * J + j] : 0.f;
     }
-    // FiLM of this lane's four columns per 16-column block
-    float4 fa[4], fb[4];
-#pragma unroll
-    for (int cb = 0; cb < 4; ++cb) {
-        const int n = n0 + 16 * cb + 4 * l4;
-        fa[cb] = p.film ? *reinterpret_cast<const float4*>(p.film + n) : make_float4(1.f, 1.f, 1.f, 1.f);
-        fb[cb] = p.film ? *reinterpret_cast<const float4*>(p.film + N + n) : make_float4(0.f, 0.f, 0.f, 0.f);
-        if (p.film) fa[cb] = make_float4(fa[cb].x + 1.0f, fa[cb].y + 1.0f, fa[cb].z + 1.0f, fa[cb].w + 1.0f);
+    // FiLM (scale + 1 | shift) of the workgroup's 64 columns, in LDS (read per row: registers
+    // held across the row loop would cost an occupancy step)
+    float* s_f = s_z + 2 * SLAB;
+    if (tid < 64) {
+        s_f[tid] = p.film ? p.film[n0 + tid] + 1.0f : 1.0f;
+        s_f[64 + tid] = p.film ? p.film[N + n0 + tid] : 0.0f;
     }
-    // slab piece q of thread t: node q >> 4, columns 4 (q & 15) .. + 3 (pieces of nodes >= J: zero)
-    float4 zv[QPT];
-    auto load_slab = [&](int r) {
+    // slab piece q of thread t: node q >> 4, columns 4 (q & 15) .. + 3 (pieces of nodes >= J: zero).
+    // PD = 2: a register ring of two slabs and two residual sets -- slab r + 2 and the residual of
+    // row r + 1 are loaded while row r is mixed (about two rows of cover for each load); PD = 1:
+    // slab r + 1 and row r's residual are loaded at the start of row r (one set each).
+    float4 zv[PD][QPT];
+    auto load_slab = [&](int r, int sl) {
         const float* zr = z + (b0 + r) * z_rs + n0;
 #pragma unroll
         for (int k = 0; k < QPT; ++k) {
             const int q = tid + 256 * k, j = q >> 4;
-            zv[k] = j < J ? *reinterpret_cast<const float4*>(zr + (int64_t)j * N + 4 * (q & 15)) : make_float4(0.f, 0.f, 0.f, 0.f);
+            zv[sl][k] = (j < J && q < NQ) ? *reinterpret_cast<const float4*>(zr + (int64_t)j * N + 4 * (q & 15)) : make_float4(0.f, 0.f, 0.f, 0.f);
         }
     };
-    auto store_slab = [&](int buf) {
+    auto store_slab = [&](int buf, int sl) {
 #pragma unroll
         for (int k = 0; k < QPT; ++k) {
             const int q = tid + 256 * k;
-            *reinterpret_cast<float4*>(s_z + buf * SLAB + (q >> 4) * ZS + 4 * (q & 15)) = zv[k];
+            if (q < NQ) *reinterpret_cast<float4*>(s_z + buf * SLAB + (q >> 4) * ZS + 4 * (q & 15)) = zv[sl][k];
         }
     };
     const bool live = i < J;  // this lane's output node
-    float4 rv[4];
-    auto load_res = [&](int r) {
+    float4 rv[PD][4];
+    auto load_res = [&](int r, int sl) {
 #pragma unroll
         for (int cb = 0; cb < 4; ++cb)
-            rv[cb] = (p.res && live) ? *reinterpret_cast<const float4*>(p.res + (b0 + r) * p.res_rs + (int64_t)i * N + n0 + 16 * cb + 4 * l4)
-                                     : make_float4(0.f, 0.f, 0.f, 0.f);
+            rv[sl][cb] = (p.res && live) ? *reinterpret_cast<const float4*>(p.res + (b0 + r) * p.res_rs + (int64_t)i * N + n0 + 16 * cb + 4 * l4)
+                                         : make_float4(0.f, 0.f, 0.f, 0.f);
     };
-    load_slab(0);
-    store_slab(0);
-    __syncthreads();
-    for (int r = 0; r < nrows; ++r) {
-        const int buf = r & 1;
-        if (r + 1 < nrows) load_slab(r + 1);
-        load_res(r);
+    // row r (slot sl = r & 1, a literal at each call site): its slab is in LDS buffer sl, its
+    // residual in rv[sl]; zv[sl] is free (slab r is in LDS) and zv[sl ^ 1] holds slab r + 1
+    auto row_step = [&](int r, const int sl) {
+        const int zs = PD == 2 ? sl : 0, rs = PD == 2 ? sl : 0;  // ring slots of slab r + PD, residual r
+        if constexpr (PD == 2) {
+            if (r + 2 < nrows) load_slab(r + 2, zs);
+            if (r + 1 < nrows) load_res(r + 1, rs ^ 1);
+        } else {
+            if (r + 1 < nrows) load_slab(r + 1, 0);
+            load_res(r, 0);
+        }
         floatx4 acc[4];
 #pragma unroll
         for (int cb = 0; cb < 4; ++cb) {
@@ -282,7 +288,7 @@ __global__ __launch_bounds__(256) void k_gl5_mixm(const GLArgs p, const float* z
 #pragma unroll
             for (int s = 0; s < 16; ++s) {
                 if (s < KS) {  // wave-uniform
-                    const float a = s_z[buf * SLAB + (4 * s + l4) * ZS + 16 * cb + l16];
+                    const float a = s_z[sl * SLAB + (4 * s + l4) * ZS + 16 * cb + l16];
                     t = __builtin_amdgcn_mfma_f32_16x16x4f32(a, gb[s], t, 0, 0, 0);
                 }
             }
@@ -293,9 +299,11 @@ __global__ __launch_bounds__(256) void k_gl5_mixm(const GLArgs p, const float* z
 #pragma unroll
             for (int cb = 0; cb < 4; ++cb) {
                 float v[4] = {acc[cb][0], acc[cb][1], acc[cb][2], acc[cb][3]};
-                const float fav[4] = {fa[cb].x, fa[cb].y, fa[cb].z, fa[cb].w};
-                const float fbv[4] = {fb[cb].x, fb[cb].y, fb[cb].z, fb[cb].w};
-                const float rvv[4] = {rv[cb].x, rv[cb].y, rv[cb].z, rv[cb].w};
+                const float4 fa = *reinterpret_cast<const float4*>(s_f + 16 * cb + 4 * l4);
+                const float4 fb = *reinterpret_cast<const float4*>(s_f + 64 + 16 * cb + 4 * l4);
+                const float fav[4] = {fa.x, fa.y, fa.z, fa.w};
+                const float fbv[4] = {fb.x, fb.y, fb.z, fb.w};
+                const float rvv[4] = {rv[rs][cb].x, rv[rs][cb].y, rv[rs][cb].z, rv[rs][cb].w};
 #pragma unroll
                 for (int e = 0; e < 4; ++e) {
                     if (p.film) v[e] = v[e] * fav[e] + fbv[e];
@@ -305,8 +313,19 @@ __global__ __launch_bounds__(256) void k_gl5_mixm(const GLArgs p, const float* z
                 *reinterpret_cast<float4*>(orow + 16 * cb) = make_float4(v[0], v[1], v[2], v[3]);
             }
         }
-        if (r + 1 < nrows) store_slab(buf ^ 1);  // buffer buf ^ 1 was last read in row r - 1
+        if (r + 1 < nrows) store_slab(sl ^ 1, PD == 2 ? zs ^ 1 : 0);  // LDS buffer sl ^ 1 was last read in row r - 1
         __syncthreads();
+    };
+    load_slab(0, 0);
+    store_slab(0, 0);
+    if constexpr (PD == 2) {
+        if (nrows > 1) load_slab(1, 1);
+        load_res(0, 0);
+    }
+    __syncthreads();
+    for (int r = 0; r < nrows; r += 2) {
+        row_step(r, 0);
+        if (r + 1 < nrows) row_step(r + 1, 1);
     }
 }
 
@@ -316,11 +335,16 @@ __global__ __launch_bounds__(256) void k_gl5_mixm(const GLArgs p, const float* z
 // load, sd_set_v5_mix)
 static int g_mix_mfma = [] {
     const char* e = getenv("SKELDIFF_V5_MIX");
-    return e ? (atoi(e) != 0) : 1;
+    return e ? std::min(std::max(atoi(e), 0), 2) : 1;  // 2: the two-deep register ring (A/B)
+}();
+// rows per k_gl5_mixm workgroup (SKELDIFF_V5_ROWS at load: 8 or 16)
+static int g_mix_rows = [] {
+    const char* e = getenv("SKELDIFF_V5_ROWS");
+    return (e && atoi(e) == 16) ? 16 : 8;
 }();
 int set_v5_mix(int v) {
     const int old = g_mix_mfma;
-    if (v == 0 || v == 1) g_mix_mfma = v;
+    if (v >= 0 && v <= 2) g_mix_mfma = v;
     return old;
 }
 
@@ -363,9 +387,15 @@ hipError_t launch_graph_linear_v5(const GLArgs& a, bool rms, hipStream_t s) {
     const bool mfma = g_mix_mfma && vec && a.N % 64 == 0 && ((uintptr_t)a.out & 15) == 0 && (a.out_rs & 3) == 0 &&
                       (!a.res || (((uintptr_t)a.res & 15) == 0 && (a.res_rs & 3) == 0)) && a.B / 8 < 0x7fffffff;
     if (mfma) {
-        constexpr int R = 8;
-        hipLaunchKernelGGL(k_gl5_mixm<R>, dim3((unsigned)((a.B + R - 1) / R), (unsigned)(a.N / 64)), dim3(256), 0, s, a,
-                           (const float*)z, z_rs);
+        const dim3 blk(256);
+        const unsigned ncb = (unsigned)(a.N / 64);
+        const size_t lds = (2 * 4 * (size_t)((a.J + 3) / 4) * 80 + 128) * sizeof(float);  // <= 41.5 KB (J <= 64)
+        if (g_mix_mfma == 2)
+            hipLaunchKernelGGL((k_gl5_mixm<8, 2>), dim3((unsigned)((a.B + 7) / 8), ncb), blk, lds, s, a, (const float*)z, z_rs);
+        else if (g_mix_rows == 16)
+            hipLaunchKernelGGL((k_gl5_mixm<16, 1>), dim3((unsigned)((a.B + 15) / 16), ncb), blk, lds, s, a, (const float*)z, z_rs);
+        else
+            hipLaunchKernelGGL((k_gl5_mixm<8, 1>), dim3((unsigned)((a.B + 7) / 8), ncb), blk, lds, s, a, (const float*)z, z_rs);
         return hipGetLastError();
     }
     const dim3 g2((unsigned)a.B, (unsigned)((a.N + 63) / 64));
