@@ -1,10 +1,11 @@
 #!/bin/bash
-# Same-box repeat of the mid-batch / small-batch chain sweeps (tools/sweep_routes.py), twice.
-OUT=gpurun_out/ab3_r03
+# Same-box A/B on config 2 (tools/sweep_routes.py, auto route, 2 / 3 row chains): k_gl4t N = 192
+# layers on 192- vs 96-column workgroups (SKELDIFF_GL4T_CT3), alternated twice.
+OUT=gpurun_out/ab4_r03
 mkdir -p $OUT
 for i in 1 2; do
-  SWEEP_ROUTES=0,1 SWEEP_CHAINS=1,3 timeout -k 10 300 python -u tools/sweep_routes.py amass16:16 > $OUT/mid$i.log 2>&1
-  rc=$?; echo "mid$i rc=$rc: $(grep '^{' $OUT/mid$i.log | python3 -c "import json,sys; print(' '.join(f\"{r['config']}/r{r['split_route']}c{r['ran_chains']}={r['futures_per_s']:.0f}\" for r in map(json.loads, sys.stdin)))")"; [ $rc -eq 0 ] || exit $rc
-  SWEEP_ROUTES=0 SWEEP_CHAINS=1,2 timeout -k 10 300 python -u tools/sweep_routes.py h36m_t1000 > $OUT/c4_$i.log 2>&1
-  rc=$?; echo "c4_$i rc=$rc: $(grep '^{' $OUT/c4_$i.log | python3 -c "import json,sys; print(' '.join(f\"{r['config']}/r{r['split_route']}c{r['ran_chains']}={r['futures_per_s']:.0f}\" for r in map(json.loads, sys.stdin)))")"; [ $rc -eq 0 ] || exit $rc
+  for E in "SKELDIFF_GL4T_CT3=0" "SKELDIFF_GL4T_CT3=1"; do
+    env $E SWEEP_ROUTES=0 SWEEP_CHAINS=2,3 timeout -k 10 300 python -u tools/sweep_routes.py amass16 > $OUT/s.log 2>&1
+    rc=$?; echo "$E rc=$rc: $(grep '^{' $OUT/s.log | python3 -c "import json,sys; print(' '.join(f\"c{r['ran_chains']}={r['futures_per_s']:.0f}\" for r in map(json.loads, sys.stdin)))")"; [ $rc -eq 0 ] || exit $rc
+  done
 done
