@@ -1597,13 +1597,20 @@ static hipError_t launch_gl4t_ct(const GLArgs& a, bool rms, int64_t ntile_r, con
     return launch_gl4t_v<CT, NCH, ROWMAJOR, 4, false>(a, rms, ntile_r, yo, s);
 }
 
+// SKELDIFF_GL4T_CT3=1 (A/B): N = 192, K = 192 layers on 96-column workgroups (two column groups
+// sharing each x tile; fewer accumulators, more waves per SIMD)
+static int g_gl4t_ct3 = [] {
+    const char* e = getenv("SKELDIFF_GL4T_CT3");
+    return e ? atoi(e) : 0;
+}();
+
 // the release Denoiser's shapes: K = 192 (12 chunks), 256 (to_out, 16) or 384 (24), N a multiple
 // of 96 (192 wide layers, 768 to_qkv, 96 final_glin); hipErrorNotSupported otherwise (k_gl4y)
 template <bool ROWMAJOR>
 static hipError_t launch_gl4t(const GLArgs& a, bool rms, int64_t ntile_r, const YOut& yo, hipStream_t s) {
     const int K = a.K1 + a.K2;
     if (a.K1 % 16 || (a.x1_div != 1 && a.x1_blk)) return hipErrorNotSupported;
-    if (a.N % 192 == 0) {
+    if (a.N % 192 == 0 && !(g_gl4t_ct3 && a.N == 192 && K == 192)) {
         if (K == 192) return launch_gl4t_ct<6, 12, ROWMAJOR>(a, rms, ntile_r, yo, s);
         if (K == 256) return launch_gl4t_ct<6, 16, ROWMAJOR>(a, rms, ntile_r, yo, s);
         if (K == 384) return launch_gl4t_ct<6, 24, ROWMAJOR>(a, rms, ntile_r, yo, s);

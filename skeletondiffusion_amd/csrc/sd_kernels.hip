@@ -829,31 +829,31 @@ __global__ __launch_bounds__(256) void k_update_mfma(const UpdArgs p) {
             if (16 * ib >= J) continue;  // wave-uniform: an output block of padding only
             const int sl = AREG ? ib : 0;
             if constexpr (!AREG) load_a(ib, 0);
+            // D^T = X^T Tab^T: A = the row's x0 / x_t / sigma eps fragment, B = the table's, so
+            // D[n = 16 ct + 4 l4 + e][i = 16 ib + l16] -- four consecutive features of one node
+            // per lane, 16-B stores (the same fmaf chain over j as Tab X: fmaf is symmetric)
             floatx4 m1 = {0.f, 0.f, 0.f, 0.f}, m2 = m1, nz = m1;
 #pragma unroll
             for (int ks = 0; ks < KS; ++ks) {
-                m1 = __builtin_amdgcn_mfma_f32_16x16x4f32(A[0][sl][ks], bxa[ks], m1, 0, 0, 0);
-                m2 = __builtin_amdgcn_mfma_f32_16x16x4f32(A[1][sl][ks], bta[ks], m2, 0, 0, 0);
-                nz = __builtin_amdgcn_mfma_f32_16x16x4f32(A[2][sl][ks], be[ks], nz, 0, 0, 0);
+                m1 = __builtin_amdgcn_mfma_f32_16x16x4f32(bxa[ks], A[0][sl][ks], m1, 0, 0, 0);
+                m2 = __builtin_amdgcn_mfma_f32_16x16x4f32(bta[ks], A[1][sl][ks], m2, 0, 0, 0);
+                nz = __builtin_amdgcn_mfma_f32_16x16x4f32(be[ks], A[2][sl][ks], nz, 0, 0, 0);
             }
-            // D[i = 16 ib + 4 l4 + e][n]
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                const int i = 16 * ib + 4 * l4 + e;
-                if (i >= J) continue;
-                const float mean = m1[e] + m2[e];
-                const float v = (p.noise_mode != 0) ? mean + nz[e] : mean;
-                const int64_t o = rb + i * D + n;
-                if (p.out_bf16) {
-                    const __bf16 vb = (__bf16)v;
-                    reinterpret_cast<__bf16*>(p.out)[o] = vb;
-                    if (p.out2) p.out2[row * p.out2_rs + i * D + n] = (float)vb;
-                } else {
-                    p.out[o] = v;
-                    if (p.out2) p.out2[row * p.out2_rs + i * D + n] = v;
-                }
-                if (p.mean_out) p.mean_out[row * p.mean_rs + i * D + n] = mean;
+            const int i = 16 * ib + l16;
+            if (i >= J) continue;
+            const int n4 = 16 * ct + 4 * l4;
+            const floatx4 mean = m1 + m2;
+            const floatx4 v = (p.noise_mode != 0) ? mean + nz : mean;
+            const int64_t o = rb + i * D + n4;
+            if (p.out_bf16) {
+                const bf16x4 vb = __builtin_convertvector(v, bf16x4);
+                *reinterpret_cast<bf16x4*>(reinterpret_cast<__bf16*>(p.out) + o) = vb;
+                if (p.out2) *reinterpret_cast<floatx4*>(p.out2 + row * p.out2_rs + i * D + n4) = __builtin_convertvector(vb, floatx4);
+            } else {
+                *reinterpret_cast<floatx4*>(p.out + o) = v;
+                if (p.out2) *reinterpret_cast<floatx4*>(p.out2 + row * p.out2_rs + i * D + n4) = v;
             }
+            if (p.mean_out) *reinterpret_cast<floatx4*>(p.mean_out + row * p.mean_rs + i * D + n4) = mean;
         }
     }
 }

@@ -109,7 +109,7 @@ def test_bf16_mode_validation(cuda):
 
     d, _, _ = build_config("mano51", cuda, T=10, batch=1, futures=2)
     with pytest.raises(SkelDiffError):
-        d.engine.set_precision("bf16")  # J = 51 runs on the exact-f32 v5 kernels
+        d.engine.set_precision("bf16")  # J = 51 runs on v5 (k_gl4t + k_gl5_mixm), which has no bf16 storage form
     z = golden("release_h36m16_T10")
     d = build_release_diffusion(z, cuda)
     d.engine.set_precision("bf16")
