@@ -344,6 +344,16 @@ int sd_gl_train_backward(const float* x, const float* z, const float* dy, const 
                          float* dW, float* dbias, float* dghat, void* workspace, size_t workspace_bytes,
                          void* stream);
 
+/* Attention over joints under autograd (training side; reference attention.py:122-136, the part
+ * between to_qkv and to_out): qkv (rows, J, 3 * heads * dim_head) as to_qkv writes it.
+ * sd_attn_train_forward: out (rows, J, heads * dim_head) = softmax((q scale) k^T) v per head.
+ * sd_attn_train_backward: dqkv (rows, J, 3 * heads * dim_head) from dout, P recomputed.
+ * 1 <= J <= 64, 1 <= dim_head <= 64; f32; one workgroup per (row, head). */
+int sd_attn_train_forward(const float* qkv, float* out, int64_t rows, int32_t J, int32_t heads, int32_t dim_head,
+                          float scale, void* stream);
+int sd_attn_train_backward(const float* qkv, const float* dout, float* dqkv, int64_t rows, int32_t J, int32_t heads,
+                           int32_t dim_head, float scale, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -30,7 +30,8 @@ EXPORTED = (
     "sd_plan_set_precision", "sd_mm_ade_fde", "sd_gru_decode_workspace_bytes", "sd_gru_decode",
     "sd_gru_encode_workspace_bytes", "sd_gru_encode", "sd_gl_train_workspace_bytes", "sd_gl_train_forward",
     "sd_gl_train_backward", "sd_plan_set_option", "sd_plan_get_option", "sd_denoiser_trace",
-    "sd_workspace_status", "sd_set_update_kernel", "sd_set_v5_mix",
+    "sd_workspace_status", "sd_set_update_kernel", "sd_set_v5_mix", "sd_attn_train_forward",
+    "sd_attn_train_backward",
 )
 
 # sd_plan_set_option keys (include/skeldiff.h)
@@ -129,6 +130,8 @@ def _declare(lib: ctypes.CDLL) -> None:
         "sd_gl_train_forward": (ctypes.c_int, [vp, vp, vp, vp, i32, vp, i64, i32, i32, i32, vp, vp, vp]),
         "sd_gl_train_backward": (ctypes.c_int, [vp, vp, vp, vp, vp, i32, vp, i64, i32, i32, i32, vp, vp, vp, vp, vp,
                                                 sz, vp]),
+        "sd_attn_train_forward": (ctypes.c_int, [vp, vp, i64, i32, i32, i32, ctypes.c_float, vp]),
+        "sd_attn_train_backward": (ctypes.c_int, [vp, vp, vp, i64, i32, i32, i32, ctypes.c_float, vp]),
         "sd_profile_step": (ctypes.c_int, [vp, vp, vp, i64, i32, i64, vp, sz, i32, ctypes.POINTER(ctypes.c_float),
                                            ctypes.POINTER(ctypes.c_int32), vp]),
     }

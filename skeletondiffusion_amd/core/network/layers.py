@@ -210,6 +210,12 @@ class Attention(nn.Module):
     def forward(self, x):
         b, n, _ = x.shape
         qkv = self.to_qkv(x)
+        if (qkv.is_cuda and torch.is_grad_enabled() and qkv.dtype == torch.float32 and _training.hip_training_enabled()
+                and isinstance(self.q_norm, nn.Identity) and isinstance(self.k_norm, nn.Identity)
+                and (not self.training or self.attn_dropout.p == 0.0) and 1 <= n <= 64 and 1 <= self.dim_head <= 64):
+            # training on the device: the attention core forward + backward on HIP (sd_train.hip)
+            out = _training.attention_core(qkv, self.heads, self.dim_head, self.scale)
+            return self.out_dropout(self.to_out(out))
         q, k, v = (c.reshape(b, n, self.heads, self.dim_head).permute(0, 2, 3, 1)
                    for c in qkv.chunk(3, dim=-1))                       # (b, h, c, n)
         q, k = self.q_norm(q), self.k_norm(k)

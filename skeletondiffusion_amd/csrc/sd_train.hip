@@ -393,6 +393,108 @@ int splits_for(int64_t rows) {
 
 int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
 
+
+// ---- attention over joints, training side (attention.py:122-136 under autograd) ---------------
+// One workgroup per (row b, head h).  qkv (rows, J, 3 hid) row-major as to_qkv writes it, q at
+// head h's columns [h dh, (h + 1) dh), k at hid + ..., v at 2 hid + ...; out (rows, J, hid).
+//   S = (q scale) k^T, P = softmax_j(S), O = P v                                   (forward)
+//   dV = P^T dO, dP = dO V^T, dS = P (dP - rowsum(P dP)), dQ = scale dS K, dK = dS^T (q scale)
+// The head's q / k / v (and dO) go to LDS once; every product is a short f32 dot product from
+// LDS (J, dh <= 64: at most 64 x 64 per operand).  P is recomputed in the backward instead of
+// stored (one J x J product per (row, head)).  Row-wise softmax: one thread per query row.
+template <bool BWD>
+__global__ __launch_bounds__(256) void k_attn_train(const float* __restrict__ qkv, const float* __restrict__ dout,
+                                                     float* __restrict__ out, int J, int heads, int dh, float scale) {
+    extern __shared__ __attribute__((aligned(16))) float sm[];
+    const int tid = threadIdx.x;
+    const int64_t b = blockIdx.x / heads;
+    const int h = blockIdx.x % heads;
+    const int hid = heads * dh, JD = J * dh;
+    const int DP = dh + 1;  // LDS row stride (odd: column walks across rows are conflict-free)
+    const int JP = J + 1;
+    float* sq = sm;               // [J][DP] q * scale
+    float* sk = sq + J * DP;      // [J][DP]
+    float* sv = sk + J * DP;      // [J][DP]
+    float* sP = sv + J * DP;      // [J][JP] P
+    float* sO = sP + J * JP;      // BWD: [J][DP] dO
+    float* sS = sO + J * DP;      // BWD: [J][JP] dS
+    const float* base = qkv + b * (int64_t)J * 3 * hid + h * dh;
+    for (int e = tid; e < JD; e += 256) {
+        const int n = e / dh, c = e - n * dh;
+        const float* r = base + (int64_t)n * 3 * hid + c;
+        sq[n * DP + c] = r[0] * scale;
+        sk[n * DP + c] = r[hid];
+        sv[n * DP + c] = r[2 * hid];
+        if (BWD) sO[n * DP + c] = dout[(b * J + n) * (int64_t)hid + h * dh + c];
+    }
+    __syncthreads();
+    for (int e = tid; e < J * J; e += 256) {
+        const int n = e / J, j = e - n * J;
+        float acc = 0.f;
+        for (int c = 0; c < dh; ++c) acc = fmaf(sq[n * DP + c], sk[j * DP + c], acc);
+        sP[n * JP + j] = acc;
+    }
+    __syncthreads();
+    if (tid < J) {  // softmax over j of row n = tid
+        float* row = sP + tid * JP;
+        float m = -INFINITY;
+        for (int j = 0; j < J; ++j) m = fmaxf(m, row[j]);
+        float sum = 0.f;
+        for (int j = 0; j < J; ++j) {
+            const float e = expf(row[j] - m);
+            row[j] = e;
+            sum += e;
+        }
+        const float inv = 1.0f / sum;
+        for (int j = 0; j < J; ++j) row[j] *= inv;
+    }
+    __syncthreads();
+    if constexpr (!BWD) {
+        for (int e = tid; e < JD; e += 256) {  // O[n][d] = sum_j P[n][j] v[j][d]
+            const int n = e / dh, d = e - n * dh;
+            float acc = 0.f;
+            for (int j = 0; j < J; ++j) acc = fmaf(sP[n * JP + j], sv[j * DP + d], acc);
+            out[(b * J + n) * (int64_t)hid + h * dh + d] = acc;
+        }
+        return;
+    } else {
+        // dP[n][j] = sum_d dO[n][d] v[j][d], kept in sS for the moment
+        for (int e = tid; e < J * J; e += 256) {
+            const int n = e / J, j = e - n * J;
+            float acc = 0.f;
+            for (int d = 0; d < dh; ++d) acc = fmaf(sO[n * DP + d], sv[j * DP + d], acc);
+            sS[n * JP + j] = acc;
+        }
+        __syncthreads();
+        if (tid < J) {  // dS = P (dP - sum_j P dP), row n = tid
+            const float* pr = sP + tid * JP;
+            float* dr = sS + tid * JP;
+            float r = 0.f;
+            for (int j = 0; j < J; ++j) r = fmaf(pr[j], dr[j], r);
+            for (int j = 0; j < J; ++j) dr[j] = pr[j] * (dr[j] - r);
+        }
+        __syncthreads();
+        float* g = out + b * (int64_t)J * 3 * hid + h * dh;  // dqkv
+        for (int e = tid; e < JD; e += 256) {
+            const int n = e / dh, c = e - n * dh;  // n: a query row (dq) and a key / value row (dk, dv)
+            float dq = 0.f, dk = 0.f, dv = 0.f;
+            for (int j = 0; j < J; ++j) {
+                dq = fmaf(sS[n * JP + j], sk[j * DP + c], dq);  // sum_j dS[n][j] k[j][c]
+                dk = fmaf(sS[j * JP + n], sq[j * DP + c], dk);  // sum_m dS[m][n] (q scale)[m][c]
+                dv = fmaf(sP[j * JP + n], sO[j * DP + c], dv);  // sum_m P[m][n] dO[m][c]
+            }
+            float* r = g + (int64_t)n * 3 * hid + c;
+            r[0] = dq * scale;
+            r[hid] = dk;
+            r[2 * hid] = dv;
+        }
+    }
+}
+
+size_t attn_train_lds(int J, int dh, bool bwd) {
+    const size_t f = (size_t)3 * J * (dh + 1) + (size_t)J * (J + 1);
+    return (bwd ? f + (size_t)J * (dh + 1) + (size_t)J * (J + 1) : f) * sizeof(float);
+}
 }  // namespace
 }  // namespace sd
 
@@ -508,6 +610,44 @@ int sd_gl_train_backward(const float* x, const float* z, const float* dy, const 
         TR_HIP(sd::sum_parts(part, (int)chunks, n, dbias, s));
     }
     return SD_OK;
+}
+
+int sd_attn_train_forward(const float* qkv, float* out, int64_t rows, int32_t J, int32_t heads, int32_t dim_head,
+                          float scale, void* stream) {
+    if (rows < 0 || J < 1 || J > 64 || heads < 1 || dim_head < 1 || dim_head > 64)
+        return sd::set_error(SD_E_INVALID, "sd_attn_train_forward: 1 <= J <= 64, 1 <= dim_head <= 64");
+    if (rows == 0) return SD_OK;
+    if (!qkv || !out) return sd::set_error(SD_E_INVALID, "sd_attn_train_forward: null buffer");
+    if (rows * heads > 0x7fffffffLL) return sd::set_error(SD_E_INVALID, "sd_attn_train_forward: too many rows");
+    const size_t lds = sd::attn_train_lds(J, dim_head, false);
+    if (lds > 64 * 1024) {
+        const hipError_t e = hipFuncSetAttribute((const void*)sd::k_attn_train<false>,
+                                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        if (e != hipSuccess) return sd::set_error(SD_E_HIP, std::string("k_attn_train: ") + hipGetErrorString(e));
+    }
+    hipLaunchKernelGGL(sd::k_attn_train<false>, dim3((unsigned)(rows * heads)), dim3(256), lds, (hipStream_t)stream,
+                       qkv, (const float*)nullptr, out, J, heads, dim_head, scale);
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? SD_OK : sd::set_error(SD_E_HIP, std::string("k_attn_train: ") + hipGetErrorString(e));
+}
+
+int sd_attn_train_backward(const float* qkv, const float* dout, float* dqkv, int64_t rows, int32_t J, int32_t heads,
+                           int32_t dim_head, float scale, void* stream) {
+    if (rows < 0 || J < 1 || J > 64 || heads < 1 || dim_head < 1 || dim_head > 64)
+        return sd::set_error(SD_E_INVALID, "sd_attn_train_backward: 1 <= J <= 64, 1 <= dim_head <= 64");
+    if (rows == 0) return SD_OK;
+    if (!qkv || !dout || !dqkv) return sd::set_error(SD_E_INVALID, "sd_attn_train_backward: null buffer");
+    if (rows * heads > 0x7fffffffLL) return sd::set_error(SD_E_INVALID, "sd_attn_train_backward: too many rows");
+    const size_t lds = sd::attn_train_lds(J, dim_head, true);
+    if (lds > 64 * 1024) {
+        const hipError_t e = hipFuncSetAttribute((const void*)sd::k_attn_train<true>,
+                                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        if (e != hipSuccess) return sd::set_error(SD_E_HIP, std::string("k_attn_train: ") + hipGetErrorString(e));
+    }
+    hipLaunchKernelGGL(sd::k_attn_train<true>, dim3((unsigned)(rows * heads)), dim3(256), lds, (hipStream_t)stream,
+                       qkv, dout, dqkv, J, heads, dim_head, scale);
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? SD_OK : sd::set_error(SD_E_HIP, std::string("k_attn_train: ") + hipGetErrorString(e));
 }
 
 }  // extern "C"

@@ -114,6 +114,45 @@ class GraphLinearFunction(torch.autograd.Function):
                 dg, None)
 
 
+class AttentionCoreFunction(torch.autograd.Function):
+    """out = softmax((q scale) k^T) v per head over the joint axis, from to_qkv's output
+    (reference attention.py:122-136, without dropout / q-k norms), forward and backward on HIP
+    (`sd_attn_train_forward` / `_backward`, csrc/sd_train.hip).  qkv (..., J, 3 * heads * dim_head)
+    -> (..., J, heads * dim_head)."""
+
+    @staticmethod
+    def forward(ctx, qkv, heads: int, dim_head: int, scale: float):
+        J, W = qkv.shape[-2], qkv.shape[-1]
+        if W != 3 * heads * dim_head:
+            raise ValueError(f"qkv width {W} != 3 * {heads} * {dim_head}")
+        lead = qkv.shape[:-2]
+        qc = qkv.reshape(-1, J, W).contiguous()
+        rows = qc.shape[0]
+        out = torch.empty(rows, J, heads * dim_head, device=qkv.device, dtype=torch.float32)
+        _lib.check(_lib.lib().sd_attn_train_forward(qc.data_ptr(), out.data_ptr(), rows, J, heads, dim_head,
+                                                     float(scale), _stream(qkv.device)))
+        ctx.save_for_backward(qc)
+        ctx.meta = (lead, J, heads, dim_head, float(scale))
+        return out.reshape(*lead, J, heads * dim_head)
+
+    @staticmethod
+    def backward(ctx, dout):
+        (qc,) = ctx.saved_tensors
+        lead, J, heads, dim_head, scale = ctx.meta
+        dc = dout.reshape(-1, J, heads * dim_head).contiguous().float()
+        dqkv = torch.empty_like(qc)
+        _lib.check(_lib.lib().sd_attn_train_backward(qc.data_ptr(), dc.data_ptr(), dqkv.data_ptr(), qc.shape[0], J,
+                                                      heads, dim_head, scale, _stream(qc.device)))
+        return dqkv.reshape(*lead, J, 3 * heads * dim_head), None, None, None
+
+
+def attention_core(qkv: torch.Tensor, heads: int, dim_head: int, scale: float) -> torch.Tensor:
+    """HIP attention core under autograd (fp32 device tensors, J <= 64, dim_head <= 64)."""
+    if not qkv.is_cuda or qkv.dtype != torch.float32:
+        raise ValueError("attention_core: the HIP training path needs fp32 device tensors")
+    return AttentionCoreFunction.apply(qkv, heads, dim_head, scale)
+
+
 def graph_linear(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor], ghat: torch.Tensor,
                  node_types: Optional[torch.Tensor]) -> torch.Tensor:
     """HIP StaticGraphLinear under autograd (fp32 device tensors)."""

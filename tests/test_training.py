@@ -154,6 +154,7 @@ def test_release_training_step_on_hip(name):
     assert training.hip_training_enabled()
     loss_g, lw, mout = d_gpu.p_losses(xs.to(dev), t_train.to(dev), noise=noise.to(dev), x_cond=xc.to(dev))
     assert "GraphLinearFunctionBackward" in _grad_fn_names(loss_g), "HIP graph-linear not on the training path"
+    assert "AttentionCoreFunctionBackward" in _grad_fn_names(loss_g), "HIP attention core not on the training path"
     loss_g.mean().backward()
     torch.cuda.synchronize()
     # the reference's own loss (gen_golden.py, reference p_losses on CPU)
@@ -206,3 +207,49 @@ def test_gl_train_abi_validation_on_host():
     assert L.sd_gl_train_forward(None, None, None, None, 0, None, 4, 16, 8, 8, None, None, None) < 0   # null buffers
     assert L.sd_gl_train_backward(None, None, None, None, None, 0, None, 4, 16, 8, 8, None, None, None, None,
                                   None, 0, None) < 0                                                  # null input
+
+
+def _ref_attention(qkv, heads, dh, scale):
+    """The reference's attention core (attention.py:122-136) on (rows, J, 3 heads dh)."""
+    b, n, _ = qkv.shape
+    q, k, v = (c.reshape(b, n, heads, dh).permute(0, 2, 3, 1) for c in qkv.chunk(3, dim=-1))
+    attn = torch.einsum("bhcn,bhcj->bhnj", q * scale, k).softmax(dim=-1)
+    out = torch.einsum("bhnj,bhdj->bhnd", attn, v)
+    return out.permute(0, 2, 1, 3).reshape(b, n, heads * dh)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("J,heads,dh,rows", [(16, 8, 32, 300), (17, 8, 32, 33), (21, 8, 32, 7), (51, 8, 32, 5),
+                                              (52, 2, 64, 3), (64, 4, 64, 2), (16, 8, 32, 1), (16, 8, 32, 0)])
+def test_attention_core_vs_autograd(J, heads, dh, rows):
+    """sd_attn_train_forward / _backward (training.AttentionCoreFunction) against float64 autograd
+    of the reference formula: out, and dqkv from a random upstream gradient."""
+    g = torch.Generator().manual_seed(J * 100 + heads + rows)
+    qkv = torch.randn(rows, J, 3 * heads * dh, generator=g, dtype=torch.float64)
+    dout = torch.randn(rows, J, heads * dh, generator=g, dtype=torch.float64)
+    scale = dh ** -0.5
+    ref_in = qkv.clone().requires_grad_(True)
+    ref = _ref_attention(ref_in, heads, dh, scale)
+    (ref * dout).sum().backward()
+    dev = torch.device("cuda:0")
+    x = qkv.float().to(dev).requires_grad_(True)
+    out = training.attention_core(x, heads, dh, scale)
+    out.backward(dout.float().to(dev))
+    torch.cuda.synchronize()
+    assert out.shape == (rows, J, heads * dh)
+    _close(out, ref, "out")
+    _close(x.grad, ref_in.grad, "dqkv")
+
+
+def test_attention_core_abi_validation_on_host():
+    """Argument checks of the attention training ABI run before any device work."""
+    from skeletondiffusion_amd import _lib
+    L = _lib.lib()
+    assert L.sd_attn_train_forward(None, None, 4, 0, 8, 32, 1.0, None) < 0       # J = 0
+    assert b"J" in L.sd_last_error()
+    assert L.sd_attn_train_forward(None, None, 4, 65, 8, 32, 1.0, None) < 0      # J > 64
+    assert L.sd_attn_train_forward(None, None, 4, 16, 8, 65, 1.0, None) < 0      # dim_head > 64
+    assert L.sd_attn_train_forward(None, None, 4, 16, 8, 32, 1.0, None) < 0      # null buffers
+    assert L.sd_attn_train_backward(None, None, None, 4, 16, 8, 32, 1.0, None) < 0
+    with pytest.raises(ValueError):
+        training.attention_core(torch.zeros(2, 16, 96), 1, 32, 1.0)                # host tensor
