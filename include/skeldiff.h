@@ -353,6 +353,13 @@ int sd_attn_train_forward(const float* qkv, float* out, int64_t rows, int32_t J,
                           float scale, void* stream);
 int sd_attn_train_backward(const float* qkv, const float* dout, float* dqkv, int64_t rows, int32_t J, int32_t heads,
                            int32_t dim_head, float scale, void* stream);
+/* FiLM + tanh of a ResnetBlock's first Block under autograd (reference attention.py:67-75):
+ * y (rows, J, C), ss (rows, 2C) = scale | shift (the time MLP's output, broadcast over the J nodes):
+ * out = tanh(y (scale + 1) + shift); backward: dy (rows, J, C) and dss (rows, 2C) from dout.
+ * rows <= 65535 for the backward. */
+int sd_film_tanh_forward(const float* y, const float* ss, float* out, int64_t rows, int32_t J, int32_t C, void* stream);
+int sd_film_tanh_backward(const float* y, const float* ss, const float* out, const float* dout, float* dy, float* dss,
+                          int64_t rows, int32_t J, int32_t C, void* stream);
 
 #ifdef __cplusplus
 }

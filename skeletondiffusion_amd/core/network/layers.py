@@ -183,7 +183,19 @@ class ResnetBlock(nn.Module):
     def forward(self, x, time_emb=None):
         scale_shift = None
         if self.mlp is not None and time_emb is not None:
-            scale_shift = self.mlp(time_emb).unsqueeze(1).chunk(2, dim=-1)
+            ss = self.mlp(time_emb).unsqueeze(1)
+            if (ss.is_cuda and torch.is_grad_enabled() and ss.dtype == torch.float32 and x.dim() == 3
+                    and _training.hip_training_enabled() and isinstance(self.block1.norm, nn.Identity)
+                    and x.shape[0] <= 65535):
+                # training on the device: block1's FiLM + tanh forward and backward on HIP
+                y = self.block1.proj(x)
+                if y.dtype == torch.float32:
+                    h = self.block2(_training.film_tanh(y, ss))
+                    return h + self.res_linear(x)
+                scale_shift = ss.chunk(2, dim=-1)
+                h = self.block2(self.block1.act(y * (scale_shift[0] + 1) + scale_shift[1]))
+                return h + self.res_linear(x)
+            scale_shift = ss.chunk(2, dim=-1)
         h = self.block2(self.block1(x, scale_shift=scale_shift))
         return h + self.res_linear(x)
 

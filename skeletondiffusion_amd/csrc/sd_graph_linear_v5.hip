@@ -213,7 +213,7 @@ __global__ __launch_bounds__(256) void k_gl5_mix(const GLArgs p, const float* z,
 // chain in k order, so each sum is k_gl5_mix's j-ordered fmaf chain (zero padding adds exact
 // zeros).  The next row's slab is loaded to registers while the current row is mixed (two LDS
 // slab buffers, one barrier per row).  J <= 64, N % 64 == 0, 16-B aligned z / res / out.
-template <int R, int PD>
+template <int R, int PD, bool TR = false>  // TR: mix with G-hat^T (the training backward, dz = G-hat^T dy)
 __global__ __launch_bounds__(256) void k_gl5_mixm(const GLArgs p, const float* z, int64_t z_rs) {
     constexpr int ZS = 80;                 // floats per slab row (64 + 16: the 4 k lanes of a read hit 4 bank groups)
     constexpr int QPT = kMaxNodes * 16 / 256;  // 16-B slab pieces per thread at most (4)
@@ -233,7 +233,7 @@ __global__ __launch_bounds__(256) void k_gl5_mixm(const GLArgs p, const float* z
 #pragma unroll
     for (int s = 0; s < 16; ++s) {
         const int j = 4 * s + l4;
-        gb[s] = (s < KS && i < J && j < J) ? p.G[i * J + j] : 0.f;
+        gb[s] = (s < KS && i < J && j < J) ? p.G[TR ? j * J + i : i * J + j] : 0.f;
     }
     // FiLM (scale + 1 | shift) of the workgroup's 64 columns, in LDS (read per row: registers
     // held across the row loop would cost an occupancy step)
@@ -346,6 +346,29 @@ int set_v5_mix(int v) {
     const int old = g_mix_mfma;
     if (v >= 0 && v <= 2) g_mix_mfma = v;
     return old;
+}
+
+// The mixing pass alone (the training graph-linear, sd_train.hip): out[r, i, :] = sum_j M[i, j]
+// z[r, j, :] with M = G-hat (transpose 0) or G-hat^T (1), z and out (rows, J, N) row-major; the same
+// j-ordered fmaf chains as sd_train.hip's k_mix.  hipErrorNotSupported unless N % 64 == 0 with
+// 16-B aligned buffers and J <= 64.
+hipError_t launch_mix_mfma(const float* z, const float* G, float* out, int64_t rows, int J, int N, bool transpose,
+                           hipStream_t s) {
+    if (J < 1 || J > kMaxNodes || N % 64 || ((uintptr_t)z & 15) || ((uintptr_t)out & 15) || rows / 8 >= 0x7fffffff)
+        return hipErrorNotSupported;
+    if (rows <= 0) return hipSuccess;
+    GLArgs a{};
+    a.G = G;
+    a.out = out;
+    a.out_rs = (int64_t)J * N;
+    a.B = rows;
+    a.N = N;
+    a.J = J;
+    const size_t lds = (2 * 4 * (size_t)((J + 3) / 4) * 80 + 128) * sizeof(float);
+    const dim3 grid((unsigned)((rows + 7) / 8), (unsigned)(N / 64));
+    if (transpose) hipLaunchKernelGGL((k_gl5_mixm<8, 1, true>), grid, dim3(256), lds, s, a, z, (int64_t)J * N);
+    else hipLaunchKernelGGL((k_gl5_mixm<8, 1, false>), grid, dim3(256), lds, s, a, z, (int64_t)J * N);
+    return hipGetLastError();
 }
 
 // Row-major operands only; J <= kMaxNodes.  hipErrorNotSupported where v5 does not apply.

@@ -140,7 +140,9 @@ int set_gl4_stage(int stage);         // returns the previous value, -1 if out o
 hipError_t launch_attention(const AttnArgs& a, hipStream_t s);
 hipError_t launch_update(const UpdArgs& a, hipStream_t s);
 int set_update_kernel(int v);  // 1 k_update_mfma, 0 element-per-thread forms; returns the previous
-int set_v5_mix(int v);         // 1 k_gl5_mixm (matrix cores), 0 k_gl5_mix; returns the previous
+int set_v5_mix(int v);
+hipError_t launch_mix_mfma(const float* z, const float* G, float* out, int64_t rows, int J, int N, bool transpose,
+                           hipStream_t s);  // G-hat (or G-hat^T) mixing of (rows, J, N), v5's MFMA pass         // 1 k_gl5_mixm (matrix cores), 0 k_gl5_mix; returns the previous
 hipError_t launch_noise_fill(float* out, int64_t rows, int64_t n_per_row, uint64_t seed,
                              int64_t row0, int step, const uint64_t* rng_dev, hipStream_t s,
                              int64_t row_shift = 0,   // row_shift: added to row0 (either source)

@@ -194,6 +194,12 @@ __global__ __launch_bounds__(256) void k_gemm(GemmArgs g) {
 // One workgroup per (row, 64-column chunk): the J x 64 input slab and M^T in LDS; each thread owns
 // one column and RPT consecutive output rows (RPT * 4 >= J), fed per source node by one LDS read
 // of the input and RPT / 4 16-B broadcast reads of M^T[j][i0 ..] (not two LDS reads per FMA).
+// SKELDIFF_TRAIN_MIX=0 at load: the per-column k_mix everywhere (A/B)
+static int g_train_mix_mfma = [] {
+    const char* e = getenv("SKELDIFF_TRAIN_MIX");
+    return e ? atoi(e) : 1;
+}();
+
 template <int RPT>
 __global__ __launch_bounds__(256) void k_mix(const float* __restrict__ in, const float* __restrict__ ghat,
                                              float* __restrict__ out, int J, int N, int transpose) {
@@ -234,6 +240,13 @@ __global__ __launch_bounds__(256) void k_mix(const float* __restrict__ in, const
 
 hipError_t launch_mix(const float* in, const float* ghat, float* out, int64_t rows, int J, int N, int transpose,
                       hipStream_t s) {
+    // the matrix-core mixing pass (sd_graph_linear_v5.hip, k_gl5_mixm) for J > 32, where at least
+    // three of its four waves own output nodes (at J = 16 three of four idle: 27.9 vs 15.8 us per
+    // launch for the per-column form below, profiles/train_r03); the same fmaf chains
+    if (g_train_mix_mfma && J > 32) {
+        const hipError_t e = launch_mix_mfma(in, ghat, out, rows, J, N, transpose != 0, s);
+        if (e != hipErrorNotSupported) return e;
+    }
     const dim3 grid((unsigned)rows, (unsigned)((N + 63) / 64));
     if (J <= 16) hipLaunchKernelGGL(k_mix<4>, grid, dim3(256), 0, s, in, ghat, out, J, N, transpose);
     else if (J <= 32) hipLaunchKernelGGL(k_mix<8>, grid, dim3(256), 0, s, in, ghat, out, J, N, transpose);
@@ -495,6 +508,41 @@ size_t attn_train_lds(int J, int dh, bool bwd) {
     const size_t f = (size_t)3 * J * (dh + 1) + (size_t)J * (J + 1);
     return (bwd ? f + (size_t)J * (dh + 1) + (size_t)J * (J + 1) : f) * sizeof(float);
 }
+
+// ---- FiLM + tanh of a ResnetBlock's first Block (attention.py:67-75 under autograd) -----------
+// out[b, j, c] = tanh(y[b, j, c] * (ss[b, c] + 1) + ss[b, C + c]), ss = the time MLP's (B, 2C)
+// output (scale | shift, broadcast over the J nodes); the multiply and add rounded separately, as
+// torch evaluates x * (scale + 1) + shift.  Backward: dpre = dout (1 - out^2),
+// dy = dpre (scale + 1), dscale[b, c] = sum_j dpre y, dshift[b, c] = sum_j dpre (j in order).
+__global__ __launch_bounds__(256) void k_film_tanh(const float* __restrict__ y, const float* __restrict__ ss,
+                                                    float* __restrict__ out, int64_t n, int J, int C) {
+    const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (e >= n) return;
+    const int c = (int)(e % C);
+    const int64_t b = e / ((int64_t)J * C);
+    const float sc = __fadd_rn(ss[b * 2 * C + c], 1.0f);
+    out[e] = tanhf(__fadd_rn(__fmul_rn(y[e], sc), ss[b * 2 * C + C + c]));
+}
+
+__global__ __launch_bounds__(256) void k_film_tanh_bwd(const float* __restrict__ y, const float* __restrict__ ss,
+                                                        const float* __restrict__ out, const float* __restrict__ dout,
+                                                        float* __restrict__ dy, float* __restrict__ dss, int J, int C) {
+    const int64_t b = blockIdx.y;
+    const int c = blockIdx.x * 256 + threadIdx.x;
+    if (c >= C) return;
+    const float sc = __fadd_rn(ss[b * 2 * C + c], 1.0f);
+    float gs = 0.f, gh = 0.f;
+    for (int j = 0; j < J; ++j) {
+        const int64_t o = (b * J + j) * (int64_t)C + c;
+        const float t = out[o];
+        const float dp = dout[o] * (1.0f - t * t);
+        dy[o] = dp * sc;
+        gs += dp * y[o];
+        gh += dp;
+    }
+    dss[b * 2 * C + c] = gs;
+    dss[b * 2 * C + C + c] = gh;
+}
 }  // namespace
 }  // namespace sd
 
@@ -648,6 +696,28 @@ int sd_attn_train_backward(const float* qkv, const float* dout, float* dqkv, int
                        qkv, dout, dqkv, J, heads, dim_head, scale);
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? SD_OK : sd::set_error(SD_E_HIP, std::string("k_attn_train: ") + hipGetErrorString(e));
+}
+
+int sd_film_tanh_forward(const float* y, const float* ss, float* out, int64_t rows, int32_t J, int32_t C, void* stream) {
+    if (rows < 0 || J < 1 || C < 1) return sd::set_error(SD_E_INVALID, "sd_film_tanh_forward: bad shape");
+    if (rows == 0) return SD_OK;
+    if (!y || !ss || !out) return sd::set_error(SD_E_INVALID, "sd_film_tanh_forward: null buffer");
+    const int64_t n = rows * J * (int64_t)C;
+    hipLaunchKernelGGL(sd::k_film_tanh, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, y, ss, out,
+                       n, J, C);
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? SD_OK : sd::set_error(SD_E_HIP, std::string("k_film_tanh: ") + hipGetErrorString(e));
+}
+
+int sd_film_tanh_backward(const float* y, const float* ss, const float* out, const float* dout, float* dy, float* dss,
+                          int64_t rows, int32_t J, int32_t C, void* stream) {
+    if (rows < 0 || J < 1 || C < 1 || rows > 65535) return sd::set_error(SD_E_INVALID, "sd_film_tanh_backward: bad shape");
+    if (rows == 0) return SD_OK;
+    if (!y || !ss || !out || !dout || !dy || !dss) return sd::set_error(SD_E_INVALID, "sd_film_tanh_backward: null buffer");
+    hipLaunchKernelGGL(sd::k_film_tanh_bwd, dim3((unsigned)((C + 255) / 256), (unsigned)rows), dim3(256), 0,
+                       (hipStream_t)stream, y, ss, out, dout, dy, dss, J, C);
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? SD_OK : sd::set_error(SD_E_HIP, std::string("k_film_tanh_bwd: ") + hipGetErrorString(e));
 }
 
 }  // extern "C"

@@ -153,6 +153,42 @@ def attention_core(qkv: torch.Tensor, heads: int, dim_head: int, scale: float) -
     return AttentionCoreFunction.apply(qkv, heads, dim_head, scale)
 
 
+class FilmTanhFunction(torch.autograd.Function):
+    """tanh(y (scale + 1) + shift) with (scale | shift) = ss (rows, 1, 2C) broadcast over the J
+    nodes -- a ResnetBlock's first Block after its graph-linear (reference attention.py:67-75) --
+    forward and backward on HIP (`sd_film_tanh_forward` / `_backward`)."""
+
+    @staticmethod
+    def forward(ctx, y, ss):
+        rows, J, C = y.shape
+        yc = y.contiguous()
+        sc = ss.reshape(rows, 2 * C).contiguous()
+        out = torch.empty_like(yc)
+        _lib.check(_lib.lib().sd_film_tanh_forward(yc.data_ptr(), sc.data_ptr(), out.data_ptr(), rows, J, C,
+                                                    _stream(y.device)))
+        ctx.save_for_backward(yc, sc, out)
+        ctx.ss_shape = ss.shape
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        yc, sc, out = ctx.saved_tensors
+        rows, J, C = yc.shape
+        dc = dout.contiguous().float()
+        dy = torch.empty_like(yc)
+        dss = torch.empty_like(sc)
+        _lib.check(_lib.lib().sd_film_tanh_backward(yc.data_ptr(), sc.data_ptr(), out.data_ptr(), dc.data_ptr(),
+                                                     dy.data_ptr(), dss.data_ptr(), rows, J, C, _stream(yc.device)))
+        return dy, dss.reshape(ctx.ss_shape)
+
+
+def film_tanh(y: torch.Tensor, ss: torch.Tensor) -> torch.Tensor:
+    """HIP FiLM + tanh under autograd: y (rows, J, C) fp32 on the device, ss (rows, 1, 2C)."""
+    if not y.is_cuda or y.dtype != torch.float32 or ss.dtype != torch.float32:
+        raise ValueError("film_tanh: the HIP training path needs fp32 device tensors")
+    return FilmTanhFunction.apply(y, ss)
+
+
 def graph_linear(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor], ghat: torch.Tensor,
                  node_types: Optional[torch.Tensor]) -> torch.Tensor:
     """HIP StaticGraphLinear under autograd (fp32 device tensors)."""

@@ -155,6 +155,7 @@ def test_release_training_step_on_hip(name):
     loss_g, lw, mout = d_gpu.p_losses(xs.to(dev), t_train.to(dev), noise=noise.to(dev), x_cond=xc.to(dev))
     assert "GraphLinearFunctionBackward" in _grad_fn_names(loss_g), "HIP graph-linear not on the training path"
     assert "AttentionCoreFunctionBackward" in _grad_fn_names(loss_g), "HIP attention core not on the training path"
+    assert "FilmTanhFunctionBackward" in _grad_fn_names(loss_g), "HIP FiLM + tanh not on the training path"
     loss_g.mean().backward()
     torch.cuda.synchronize()
     # the reference's own loss (gen_golden.py, reference p_losses on CPU)
@@ -253,3 +254,26 @@ def test_attention_core_abi_validation_on_host():
     assert L.sd_attn_train_backward(None, None, None, 4, 16, 8, 32, 1.0, None) < 0
     with pytest.raises(ValueError):
         training.attention_core(torch.zeros(2, 16, 96), 1, 32, 1.0)                # host tensor
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("rows,J,C", [(257, 16, 192), (5, 21, 192), (1, 51, 96), (0, 16, 192)])
+def test_film_tanh_vs_autograd(rows, J, C):
+    """sd_film_tanh_forward / _backward (training.FilmTanhFunction) against float64 autograd of the
+    reference's Block epilogue x * (scale + 1) + shift -> tanh (attention.py:67-75)."""
+    g = torch.Generator().manual_seed(rows + J + C)
+    y = torch.randn(rows, J, C, generator=g, dtype=torch.float64)
+    ss = torch.randn(rows, 1, 2 * C, generator=g, dtype=torch.float64) * 0.5
+    dout = torch.randn(rows, J, C, generator=g, dtype=torch.float64)
+    yr, sr = y.clone().requires_grad_(True), ss.clone().requires_grad_(True)
+    sc, sh = sr.chunk(2, dim=-1)
+    ref = torch.tanh(yr * (sc + 1) + sh)
+    (ref * dout).sum().backward()
+    dev = torch.device("cuda:0")
+    yg, sg = y.float().to(dev).requires_grad_(True), ss.float().to(dev).requires_grad_(True)
+    out = training.film_tanh(yg, sg)
+    out.backward(dout.float().to(dev))
+    torch.cuda.synchronize()
+    _close(out, ref, "out")
+    _close(yg.grad, yr.grad, "dy")
+    _close(sg.grad, sr.grad, "dss")

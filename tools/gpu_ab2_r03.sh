@@ -5,6 +5,8 @@ OUT=gpurun_out/train_r03
 mkdir -p $OUT
 timeout -k 10 400 python -u -m pytest tests/test_training.py -m gpu -x -q --timeout 300 --timeout-method thread > $OUT/pytest_train.log 2>&1
 rc=$?; echo "training tests rc=$rc: $(tail -1 $OUT/pytest_train.log)"; [ $rc -eq 0 ] || exit $rc
+SKELDIFF_TRAIN_MIX=0 timeout -k 10 300 python -u tools/bench_train.py --J 16 --rows 1024 --steps 10 --warmup 3 --modes hip > $OUT/train16_mix0.json 2> $OUT/train16_mix0.err
+echo "train J=16 per-column k_mix: $(python3 -c "import json;d=json.load(open('$OUT/train16_mix0.json'));print(round(d['hip']['ms_per_step'],2),'ms')")"
 for J in 16 21; do
   timeout -k 10 300 python -u tools/bench_train.py --J $J --rows 1024 --steps 10 --warmup 3 > $OUT/train$J.json 2> $OUT/train$J.err
   rc=$?; echo "train J=$J rc=$rc: $(python3 -c "import json;d=json.load(open('$OUT/train$J.json'));print(round(d['hip']['ms_per_step'],2),'ms vs torch',round(d['torch_ops_same_gpu']['ms_per_step'],2),'ms speedup',round(d['speedup'],2))")"; [ $rc -eq 0 ] || exit $rc
