@@ -756,10 +756,20 @@ __global__ __launch_bounds__(256) void k_update_mfma(const UpdArgs p) {
             bt[q][ks] = p.xt_bf16 ? (float)reinterpret_cast<const __bf16*>(p.xt)[rb + jc * D + n] : p.xt[rb + jc * D + n];
         }
     }
-    for (int q = tid; q < 3 * JP * JP; q += 256) {
-        const int m = q / (JP * JP), ij = q % (JP * JP), i = ij / JP, j = ij % JP;
-        const float* tab = m == 0 ? p.C1 : m == 1 ? p.C2 : p.U;
-        sTab[q] = (i < J && j < J) ? tab[i * J + j] : 0.f;
+    {  // the three tables to LDS: every load of this thread issued before the first store (a
+       // load -> store loop waited out one memory latency per element: 48 per thread at JP = 64)
+        constexpr int TPT = (3 * JP * JP + 255) / 256;
+        float tv[TPT];
+#pragma unroll
+        for (int k = 0; k < TPT; ++k) {
+            const int q = tid + 256 * k;
+            const int m = q / (JP * JP), ij = q % (JP * JP), i = ij / JP, j = ij % JP;
+            const float* tab = m == 0 ? p.C1 : m == 1 ? p.C2 : p.U;
+            tv[k] = (q < 3 * JP * JP && i < J && j < J) ? tab[i * J + j] : 0.f;
+        }
+#pragma unroll
+        for (int k = 0; k < TPT; ++k)
+            if (tid + 256 * k < 3 * JP * JP) sTab[tid + 256 * k] = tv[k];
     }
     uint64_t seed = p.seed;
     int64_t row0 = p.row0;
