@@ -1,14 +1,14 @@
 #!/bin/bash
-# Training side: kernel parity tests, the training-step bench (HIP vs torch ops) at J = 16 / 21,
-# and a kernel trace of the HIP step.
-OUT=gpurun_out/train_r03
+# XCD-aligned k_gl4t / MODE 2 block mapping (SKELDIFF_XCD_ALIGN): bitwise route
+# tests with it on, same-box config-2 A/B (1 and 3 chains, alternated), PMC traffic with it on.
+OUT=gpurun_out/xcd_r03
 mkdir -p $OUT
-timeout -k 10 400 python -u -m pytest tests/test_training.py -m gpu -x -q --timeout 300 --timeout-method thread > $OUT/pytest_train.log 2>&1
-rc=$?; echo "training tests rc=$rc: $(tail -1 $OUT/pytest_train.log)"; [ $rc -eq 0 ] || exit $rc
-SKELDIFF_TRAIN_MIX=0 timeout -k 10 300 python -u tools/bench_train.py --J 16 --rows 1024 --steps 10 --warmup 3 --modes hip > $OUT/train16_mix0.json 2> $OUT/train16_mix0.err
-echo "train J=16 per-column k_mix: $(python3 -c "import json;d=json.load(open('$OUT/train16_mix0.json'));print(round(d['hip']['ms_per_step'],2),'ms')")"
-for J in 16 21; do
-  timeout -k 10 300 python -u tools/bench_train.py --J $J --rows 1024 --steps 10 --warmup 3 > $OUT/train$J.json 2> $OUT/train$J.err
-  rc=$?; echo "train J=$J rc=$rc: $(python3 -c "import json;d=json.load(open('$OUT/train$J.json'));print(round(d['hip']['ms_per_step'],2),'ms vs torch',round(d['torch_ops_same_gpu']['ms_per_step'],2),'ms speedup',round(d['speedup'],2))")"; [ $rc -eq 0 ] || exit $rc
+SKELDIFF_XCD_ALIGN=1 timeout -k 10 400 python -u -m pytest tests/test_gpu_configs.py -m gpu -x -q --timeout 300 --timeout-method thread -k "tiled_split_route_bitwise or config2_as_benched or share_cus or shard" > $OUT/pytest.log 2>&1
+rc=$?; echo "aligned tests rc=$rc: $(tail -1 $OUT/pytest.log)"; [ $rc -eq 0 ] || exit $rc
+for i in 1 2; do
+  for E in 0 1; do
+    SKELDIFF_XCD_ALIGN=$E SWEEP_ROUTES=0 SWEEP_CHAINS=1,3 timeout -k 10 300 python -u tools/sweep_routes.py amass16 > $OUT/s.log 2>&1
+    rc=$?; echo "XCD_ALIGN=$E rc=$rc: $(grep '^{' $OUT/s.log | python3 -c "import json,sys; print(' '.join(f\"c{r['ran_chains']}={r['futures_per_s']:.0f}\" for r in map(json.loads, sys.stdin)))")"; [ $rc -eq 0 ] || exit $rc
+  done
 done
-bash tools/prof_train.sh && cp gpurun_out/prof_train/run_kernel_stats.csv $OUT/train_kernel_stats.csv
+SKELDIFF_XCD_ALIGN=1 bash tools/prof_bench.sh r03x
