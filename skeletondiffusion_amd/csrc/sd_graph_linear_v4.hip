@@ -331,6 +331,12 @@ __global__ __launch_bounds__(256) void k_gl4y(const GLArgs p, int ntile_c, int64
 // WRES (resident weights, K = 192): the workgroup copies the node's whole weight slice for its CT
 // tiles (NCH chunks, 144 KiB at CT = 6) into LDS once, then every wave runs its K loop with no
 // barrier at all; NWV waves = NWV consecutive 32-row tiles.  Same products in the same order.
+#ifdef SD_GL4T_STAMPS
+// diagnostic build only (tools/gl4t_stamps.py): per workgroup of the N = 192, K = 192 launches,
+// s_memrealtime at entry, after the K loop, after the Y stores, and the CU id; overwritten by
+// every such launch (the last one of a forward is read back)
+__device__ unsigned long long g_gl4t_stamps[8192 * 4];
+#endif
 template <bool RMS, int PREC, int CT, int NCH, bool ROWMAJOR, int PF = 4, int NWV = 4, bool WRES = false>
 __global__ __launch_bounds__(NWV * 64, WRES ? 1 : 2) void k_gl4t(const GLArgs p, int ncg, int64_t ntile_r, const YOut yo) {
     constexpr int NT = NWV * 64;
@@ -346,6 +352,11 @@ __global__ __launch_bounds__(NWV * 64, WRES ? 1 : 2) void k_gl4t(const GLArgs p,
     const int tid = threadIdx.x, lane = tid & 63, l32 = lane & 31, h = lane >> 5;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int J = p.J;
+#ifdef SD_GL4T_STAMPS
+    constexpr bool STAMP = CT == 6 && NCH == 12 && !RMS && PREC == 0 && !ROWMAJOR;
+    unsigned long long st0 = 0;
+    if (STAMP && tid == 0) st0 = wall_clock64();
+#endif
     // XCD-aware order (k_gl4's): consecutive u -- the column groups of one (row group, node), which
     // read the same x -- on one XCD (blocks b, b + 8, ... share one), so x reaches that L2 once
     const int nwg = gridDim.x, xcd = blockIdx.x & 7, q8 = nwg >> 3, r8 = nwg & 7;
@@ -548,6 +559,13 @@ __global__ __launch_bounds__(NWV * 64, WRES ? 1 : 2) void k_gl4t(const GLArgs p,
     }
     }  // staged K loop
     __syncthreads();  // every wave past its last chunk: the stages become the output transposes
+#ifdef SD_GL4T_STAMPS
+    if (STAMP && tid == 0 && blockIdx.x < 8192) {
+        g_gl4t_stamps[blockIdx.x * 4 + 0] = st0;
+        g_gl4t_stamps[blockIdx.x * 4 + 1] = wall_clock64();
+        g_gl4t_stamps[blockIdx.x * 4 + 3] = __smid();
+    }
+#endif
     if (!live) return;
     if (p.status && __builtin_amdgcn_ballot_w64(amx >= 65504.0f) != 0 && lane == 0) atomicOr(p.status, 1u);
     float sc[16];
@@ -582,6 +600,12 @@ __global__ __launch_bounds__(NWV * 64, WRES ? 1 : 2) void k_gl4t(const GLArgs p,
         }
         __builtin_amdgcn_wave_barrier();
     }
+#ifdef SD_GL4T_STAMPS
+    if (STAMP && lane == 0 && blockIdx.x < 8192) {
+        __builtin_amdgcn_s_waitcnt(0);  // this wave's stores issued and acknowledged
+        atomicMax(&g_gl4t_stamps[blockIdx.x * 4 + 2], wall_clock64());
+    }
+#endif
 }
 
 // Epilogue of the fused to_qkv + Attention kernel (MODE 1), J <= 32, dh = 32, 8 waves, a
@@ -1744,3 +1768,15 @@ hipError_t launch_qkv_attention_v4(const GLArgs& a, bool rms, hipStream_t s) {
 }
 
 }  // namespace sd
+
+#ifdef SD_GL4T_STAMPS
+extern "C" int sd_debug_gl4t_stamps(unsigned long long* host, int nwg, int reset) {
+    if (reset) {
+        static unsigned long long zeros[8192 * 4] = {};
+        return hipMemcpyToSymbol(HIP_SYMBOL(sd::g_gl4t_stamps), zeros, sizeof(zeros)) == hipSuccess ? 0 : -3;
+    }
+    if (nwg < 0 || nwg > 8192) return -1;
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(sd::g_gl4t_stamps), (size_t)nwg * 4 * sizeof(unsigned long long)) ==
+                   hipSuccess ? 0 : -3;
+}
+#endif
