@@ -337,10 +337,10 @@ static int g_mix_mfma = [] {
     const char* e = getenv("SKELDIFF_V5_MIX");
     return e ? std::min(std::max(atoi(e), 0), 2) : 1;  // 2: the two-deep register ring (A/B)
 }();
-// rows per k_gl5_mixm workgroup (SKELDIFF_V5_ROWS at load: 8 or 16)
+// rows per k_gl5_mixm workgroup (SKELDIFF_V5_ROWS at load: 4, 8 or 16)
 static int g_mix_rows = [] {
     const char* e = getenv("SKELDIFF_V5_ROWS");
-    return (e && atoi(e) == 16) ? 16 : 8;
+    return (e && (atoi(e) == 16 || atoi(e) == 4)) ? atoi(e) : 8;
 }();
 int set_v5_mix(int v) {
     const int old = g_mix_mfma;
@@ -415,6 +415,8 @@ hipError_t launch_graph_linear_v5(const GLArgs& a, bool rms, hipStream_t s) {
         const size_t lds = (2 * 4 * (size_t)((a.J + 3) / 4) * 80 + 128) * sizeof(float);  // <= 41.5 KB (J <= 64)
         if (g_mix_mfma == 2)
             hipLaunchKernelGGL((k_gl5_mixm<8, 2>), dim3((unsigned)((a.B + 7) / 8), ncb), blk, lds, s, a, (const float*)z, z_rs);
+        else if (g_mix_rows == 4)
+            hipLaunchKernelGGL((k_gl5_mixm<4, 1>), dim3((unsigned)((a.B + 3) / 4), ncb), blk, lds, s, a, (const float*)z, z_rs);
         else if (g_mix_rows == 16)
             hipLaunchKernelGGL((k_gl5_mixm<16, 1>), dim3((unsigned)((a.B + 15) / 16), ncb), blk, lds, s, a, (const float*)z, z_rs);
         else
