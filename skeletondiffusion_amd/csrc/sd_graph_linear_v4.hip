@@ -336,6 +336,7 @@ __global__ __launch_bounds__(256) void k_gl4y(const GLArgs p, int ntile_c, int64
 // s_memrealtime at entry, after the K loop, after the Y stores, and the CU id; overwritten by
 // every such launch (the last one of a forward is read back)
 __device__ unsigned long long g_gl4t_stamps[8192 * 4];
+__device__ unsigned long long g_gl4t_chunk[8192 * 16];  // per workgroup: s_memrealtime after each chunk's barrier
 #endif
 template <bool RMS, int PREC, int CT, int NCH, bool ROWMAJOR, int PF = 4, int NWV = 4, bool WRES = false>
 __global__ __launch_bounds__(NWV * 64, WRES ? 1 : 2) void k_gl4t(const GLArgs p, int ncg, int64_t ntile_r, const YOut yo) {
@@ -548,6 +549,9 @@ __global__ __launch_bounds__(NWV * 64, WRES ? 1 : 2) void k_gl4t(const GLArgs p,
             asm volatile("" ::: "memory");
             __builtin_amdgcn_s_barrier();
             asm volatile("" ::: "memory");
+#ifdef SD_GL4T_STAMPS
+            if (STAMP && tid == 0 && blockIdx.x < 8192 && c < 16) g_gl4t_chunk[blockIdx.x * 16 + c] = wall_clock64();
+#endif
             // unconditional loads (past the end: a clamped, unused chunk): a branch around them
             // made the waitcnt pass merge both paths and drain the x ring every chunk
             load_w(min(c + 1, nchunk - 1));
@@ -1777,6 +1781,11 @@ extern "C" int sd_debug_gl4t_stamps(unsigned long long* host, int nwg, int reset
     }
     if (nwg < 0 || nwg > 8192) return -1;
     return hipMemcpyFromSymbol(host, HIP_SYMBOL(sd::g_gl4t_stamps), (size_t)nwg * 4 * sizeof(unsigned long long)) ==
+                   hipSuccess ? 0 : -3;
+}
+extern "C" int sd_debug_gl4t_chunk_stamps(unsigned long long* host, int nwg) {
+    if (nwg < 0 || nwg > 8192) return -1;
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(sd::g_gl4t_chunk), (size_t)nwg * 16 * sizeof(unsigned long long)) ==
                    hipSuccess ? 0 : -3;
 }
 #endif

@@ -44,3 +44,12 @@ for rep in range(3):
     print(f"  distinct CUs {len(np.unique(cu))}; workgroups per CU max {np.bincount(cu.astype(np.int64)).max()}")
     hist = np.histogram(k / 1e3, bins=8)
     print("  loop-end histogram (us):", [f"{b:.1f}:{c}" for b, c in zip(hist[1][:-1], hist[0])])
+    if os.environ.get("SKELDIFF_GL4T_CFG", "0") in ("0", "1"):  # per-chunk barrier stamps (staged forms)
+        ch = np.zeros((nwg, 16), dtype=np.uint64)
+        fc = L.sd_debug_gl4t_chunk_stamps
+        fc.restype = ctypes.c_int
+        fc.argtypes = [ctypes.c_void_p, ctypes.c_int]
+        assert fc(ch.ctypes.data, nwg) == 0
+        c = (ch[:, :12].astype(np.int64) - base) * 10  # ns after the launch's first entry
+        print("  chunk barrier passed (median over workgroups, us):", " ".join(f"{np.median(c[:, i]) / 1e3:.2f}" for i in range(12)))
+        print("  per-chunk gaps (median, us):", " ".join(f"{np.median(c[:, i + 1] - c[:, i]) / 1e3:.2f}" for i in range(11)))
