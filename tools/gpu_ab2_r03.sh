@@ -1,12 +1,12 @@
 #!/bin/bash
-# MANO mixing pass: 4 / 8 rows per k_gl5_mixm workgroup (SKELDIFF_V5_ROWS), same box, alternated.
-OUT=gpurun_out/mix4_r03
+# Training side: kernel parity tests, the training-step bench (HIP vs torch ops) at J = 16 / 21,
+# and a kernel trace of the HIP step.
+OUT=gpurun_out/train_r03c
 mkdir -p $OUT
-timeout -k 10 300 env SKELDIFF_V5_ROWS=4 python -u -m pytest tests/test_gpu_v5.py -m gpu -x -q --timeout 200 --timeout-method thread > $OUT/pytest.log 2>&1
-rc=$?; echo "v5 tests (4 rows) rc=$rc: $(tail -1 $OUT/pytest.log)"; [ $rc -eq 0 ] || exit $rc
-for i in 1 2; do
-  for R in 8 4; do
-    SKELDIFF_V5_ROWS=$R SWEEP_ROUTES=0 SWEEP_CHAINS=3 timeout -k 10 300 python -u tools/sweep_routes.py mano51 > $OUT/s.log 2>&1
-    rc=$?; echo "V5_ROWS=$R rc=$rc: $(grep '^{' $OUT/s.log | python3 -c "import json,sys; print(' '.join(f\"{r['config']}={r['futures_per_s']:.0f}\" for r in map(json.loads, sys.stdin)))")"; [ $rc -eq 0 ] || exit $rc
-  done
+timeout -k 10 400 python -u -m pytest tests/test_training.py -m gpu -x -q --timeout 300 --timeout-method thread > $OUT/pytest_train.log 2>&1
+rc=$?; echo "training tests rc=$rc: $(tail -1 $OUT/pytest_train.log)"; [ $rc -eq 0 ] || exit $rc
+for J in 16 21; do
+  timeout -k 10 300 python -u tools/bench_train.py --J $J --rows 1024 --steps 10 --warmup 3 > $OUT/train$J.json 2> $OUT/train$J.err
+  rc=$?; echo "train J=$J rc=$rc: $(python3 -c "import json;d=json.load(open('$OUT/train$J.json'));print(round(d['hip']['ms_per_step'],2),'ms vs torch',round(d['torch_ops_same_gpu']['ms_per_step'],2),'ms speedup',round(d['speedup'],2))")"; [ $rc -eq 0 ] || exit $rc
 done
+bash tools/prof_train.sh && cp gpurun_out/prof_train/run_kernel_stats.csv $OUT/train_kernel_stats.csv
