@@ -336,6 +336,7 @@ __global__ __launch_bounds__(256) void k_gl4y(const GLArgs p, int ntile_c, int64
 // s_memrealtime at entry, after the K loop, after the Y stores, and the CU id; overwritten by
 // every such launch (the last one of a forward is read back)
 __device__ unsigned long long g_gl4t_stamps[8192 * 4];
+__device__ unsigned long long g_gl4t_clock[8192 * 2];  // shader clock (s_memtime) at entry and loop end
 __device__ unsigned long long g_gl4t_chunk[8192 * 16];  // per workgroup: s_memrealtime after each chunk's barrier
 #endif
 template <bool RMS, int PREC, int CT, int NCH, bool ROWMAJOR, int PF = 4, int NWV = 4, bool WRES = false>
@@ -355,8 +356,11 @@ __global__ __launch_bounds__(NWV * 64, WRES ? 1 : 2) void k_gl4t(const GLArgs p,
     const int J = p.J;
 #ifdef SD_GL4T_STAMPS
     constexpr bool STAMP = CT == 6 && NCH == 12 && !RMS && PREC == 0 && !ROWMAJOR;
-    unsigned long long st0 = 0;
-    if (STAMP && tid == 0) st0 = wall_clock64();
+    unsigned long long st0 = 0, ck0 = 0;
+    if (STAMP && tid == 0) {
+        st0 = wall_clock64();
+        ck0 = clock64();
+    }
 #endif
     // XCD-aware order (k_gl4's): consecutive u -- the column groups of one (row group, node), which
     // read the same x -- on one XCD (blocks b, b + 8, ... share one), so x reaches that L2 once
@@ -568,6 +572,8 @@ __global__ __launch_bounds__(NWV * 64, WRES ? 1 : 2) void k_gl4t(const GLArgs p,
         g_gl4t_stamps[blockIdx.x * 4 + 0] = st0;
         g_gl4t_stamps[blockIdx.x * 4 + 1] = wall_clock64();
         g_gl4t_stamps[blockIdx.x * 4 + 3] = __smid();
+        g_gl4t_clock[blockIdx.x * 2] = ck0;
+        g_gl4t_clock[blockIdx.x * 2 + 1] = clock64();
     }
 #endif
     if (!live) return;
@@ -1781,6 +1787,11 @@ extern "C" int sd_debug_gl4t_stamps(unsigned long long* host, int nwg, int reset
     }
     if (nwg < 0 || nwg > 8192) return -1;
     return hipMemcpyFromSymbol(host, HIP_SYMBOL(sd::g_gl4t_stamps), (size_t)nwg * 4 * sizeof(unsigned long long)) ==
+                   hipSuccess ? 0 : -3;
+}
+extern "C" int sd_debug_gl4t_clock(unsigned long long* host, int nwg) {
+    if (nwg < 0 || nwg > 8192) return -1;
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(sd::g_gl4t_clock), (size_t)nwg * 2 * sizeof(unsigned long long)) ==
                    hipSuccess ? 0 : -3;
 }
 extern "C" int sd_debug_gl4t_chunk_stamps(unsigned long long* host, int nwg) {

@@ -42,6 +42,15 @@ for rep in range(3):
     print(f"  stores (loop end -> last store acked): median {np.median(e - k) / 1e3:.2f} us, max {np.max(e - k) / 1e3:.2f}")
     print(f"  loop end: median {np.median(k) / 1e3:.2f} / max {k.max() / 1e3:.2f} us; store end: median {np.median(e) / 1e3:.2f} us")
     print(f"  distinct CUs {len(np.unique(cu))}; workgroups per CU max {np.bincount(cu.astype(np.int64)).max()}")
+    ckb = np.zeros((nwg, 2), dtype=np.uint64)
+    fk = L.sd_debug_gl4t_clock
+    fk.restype = ctypes.c_int
+    fk.argtypes = [ctypes.c_void_p, ctypes.c_int]
+    assert fk(ckb.ctypes.data, nwg) == 0
+    cyc = ckb[:, 1].astype(np.int64) - ckb[:, 0].astype(np.int64)
+    ghz = cyc / np.maximum(k - s, 1)  # shader cycles per ns over the K loop
+    print(f"  shader clock over the K loop: median {np.median(ghz):.2f} GHz; K-loop cycles median {np.median(cyc):.0f} "
+          f"({np.median(cyc) / 12:.0f} per 16-deep chunk; 18 MFMAs = 576 issue cycles)")
     hist = np.histogram(k / 1e3, bins=8)
     print("  loop-end histogram (us):", [f"{b:.1f}:{c}" for b, c in zip(hist[1][:-1], hist[0])])
     if os.environ.get("SKELDIFF_GL4T_CFG", "0") in ("0", "1"):  # per-chunk barrier stamps (staged forms)
