@@ -361,6 +361,35 @@ int sd_film_tanh_forward(const float* y, const float* ss, float* out, int64_t ro
 int sd_film_tanh_backward(const float* y, const float* ss, const float* out, const float* dout, float* dy, float* dss,
                           int64_t rows, int32_t J, int32_t C, void* stream);
 
+/* Row-wise L1 normalisation of a learnable influence matrix under autograd (reference
+ * graph_structural.py:107, F.normalize(G, p=1, dim=1)): ghat[i][j] = G[i][j] / max(sum_k |G[i][k]|, eps);
+ * the backward writes dG from dghat.  J x J row-major, 1 <= J <= 64, f32. */
+int sd_l1norm_rows_forward(const float* G, float* ghat, int32_t J, float eps, void* stream);
+int sd_l1norm_rows_backward(const float* G, const float* dghat, float* dG, int32_t J, float eps, void* stream);
+/* PreNorm's RMSNorm under autograd (reference attention.py:30-36): x (R, C), R vectors of C
+ * features, out = x / max(||x||, eps) * g * scale (scale = sqrt(C)); the forward also writes
+ * dnorm (R) = max(||x||, eps) for the backward, which writes dx (R, C) and dg (C), the latter
+ * summed over vectors in a fixed order through a workspace of sd_rmsnorm_workspace_bytes.
+ * 1 <= C <= 1024. */
+size_t sd_rmsnorm_workspace_bytes(int64_t R, int32_t C);
+int sd_rmsnorm_forward(const float* x, const float* g, float* out, float* dnorm, int64_t R, int32_t C, float scale,
+                       float eps, void* stream);
+int sd_rmsnorm_backward(const float* x, const float* g, const float* dnorm, const float* dy, float* dx, float* dg,
+                        int64_t R, int32_t C, float scale, float eps, void* workspace, size_t workspace_bytes,
+                        void* stream);
+/* Mahalanobis loss of NonisotropicGaussianDiffusion reduced per row (reference
+ * nonisotropic.py:177-190 and base.py:297-298): model_out, target (rows, J, F), S =
+ * mahalanobis_S_sqrt_recip (T, J, J), t (rows) int64 timesteps;
+ * loss[r] = mean_{i,f} |(S[t_r] D_r)[i][f]| (mse: squared), D = target - model_out when
+ * pred_noise, else model_out - target.  The backward writes d model_out (rows, J, F) from dloss
+ * (rows).  1 <= J <= 64, 1 <= F <= 256, f32. */
+int sd_mahalanobis_loss_forward(const float* model_out, const float* target, const float* S, const int64_t* t,
+                                int64_t rows, int32_t J, int32_t F, int32_t pred_noise, int32_t mse, float* loss,
+                                void* stream);
+int sd_mahalanobis_loss_backward(const float* model_out, const float* target, const float* S, const int64_t* t,
+                                 const float* dloss, int64_t rows, int32_t J, int32_t F, int32_t pred_noise,
+                                 int32_t mse, float* dmodel_out, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

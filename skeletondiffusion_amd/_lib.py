@@ -31,7 +31,9 @@ EXPORTED = (
     "sd_gru_encode_workspace_bytes", "sd_gru_encode", "sd_gl_train_workspace_bytes", "sd_gl_train_forward",
     "sd_gl_train_backward", "sd_plan_set_option", "sd_plan_get_option", "sd_denoiser_trace",
     "sd_workspace_status", "sd_set_update_kernel", "sd_set_v5_mix", "sd_attn_train_forward",
-    "sd_attn_train_backward", "sd_film_tanh_forward", "sd_film_tanh_backward",
+    "sd_attn_train_backward", "sd_film_tanh_forward", "sd_film_tanh_backward", "sd_l1norm_rows_forward",
+    "sd_l1norm_rows_backward", "sd_rmsnorm_workspace_bytes", "sd_rmsnorm_forward", "sd_rmsnorm_backward",
+    "sd_mahalanobis_loss_forward", "sd_mahalanobis_loss_backward",
 )
 
 # sd_plan_set_option keys (include/skeldiff.h)
@@ -134,6 +136,14 @@ def _declare(lib: ctypes.CDLL) -> None:
         "sd_attn_train_backward": (ctypes.c_int, [vp, vp, vp, i64, i32, i32, i32, ctypes.c_float, vp]),
         "sd_film_tanh_forward": (ctypes.c_int, [vp, vp, vp, i64, i32, i32, vp]),
         "sd_film_tanh_backward": (ctypes.c_int, [vp, vp, vp, vp, vp, vp, i64, i32, i32, vp]),
+        "sd_l1norm_rows_forward": (ctypes.c_int, [vp, vp, i32, ctypes.c_float, vp]),
+        "sd_l1norm_rows_backward": (ctypes.c_int, [vp, vp, vp, i32, ctypes.c_float, vp]),
+        "sd_rmsnorm_workspace_bytes": (sz, [i64, i32]),
+        "sd_rmsnorm_forward": (ctypes.c_int, [vp, vp, vp, vp, i64, i32, ctypes.c_float, ctypes.c_float, vp]),
+        "sd_rmsnorm_backward": (ctypes.c_int, [vp, vp, vp, vp, vp, vp, i64, i32, ctypes.c_float, ctypes.c_float, vp,
+                                               sz, vp]),
+        "sd_mahalanobis_loss_forward": (ctypes.c_int, [vp, vp, vp, vp, i64, i32, i32, i32, i32, vp, vp]),
+        "sd_mahalanobis_loss_backward": (ctypes.c_int, [vp, vp, vp, vp, vp, i64, i32, i32, i32, i32, vp, vp]),
         "sd_profile_step": (ctypes.c_int, [vp, vp, vp, i64, i32, i64, vp, sz, i32, ctypes.POINTER(ctypes.c_float),
                                            ctypes.POINTER(ctypes.c_int32), vp]),
     }

@@ -188,6 +188,11 @@ class LatentDiffusion(nn.Module):
         return ModelPrediction(pred_noise, x_start)
 
     # -- forward process (training) -----------------------------------------------------------
+    def loss_rows(self, model_out, target, t):
+        """loss_funct reduced 'b ... -> b' by the mean (reference base.py:297-298)."""
+        loss = self.loss_funct(model_out, target, t)
+        return loss.reshape(loss.shape[0], -1).mean(dim=1)
+
     def p_losses(self, x_start, t, noise=None, x_cond=None, n_train_samples=1):
         b = x_start.shape[0]
         if n_train_samples > 1:
@@ -210,8 +215,7 @@ class LatentDiffusion(nn.Module):
             target = self.predict_v(x_start, t, noise)
         else:
             raise ValueError(f"unknown objective {self.objective}")
-        loss = self.loss_funct(model_out, target, t)
-        loss = loss.reshape(loss.shape[0], -1).mean(dim=1)
+        loss = self.loss_rows(model_out, target, t)
         return loss, extract(self.loss_weight, t.view(b, -1)[:, 0], loss.shape[0:1]), model_out
 
     def forward(self, x, *args, x_cond=None, **kwargs):

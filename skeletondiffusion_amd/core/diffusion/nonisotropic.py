@@ -10,6 +10,7 @@ from __future__ import annotations
 
 import torch
 
+from ... import training as _training
 from .base import LatentDiffusion, default, extract
 
 __all__ = ["NonisotropicGaussianDiffusion", "compute_covariance_matrices", "extract_matrix"]
@@ -151,6 +152,20 @@ class NonisotropicGaussianDiffusion(LatentDiffusion):
         if self.loss_reduction_type == "mse":
             return loss ** 2
         raise AssertionError("Not implemented")
+
+    def loss_rows(self, model_out, target, t):
+        """The Mahalanobis loss reduced per row.  On the device under autograd (fp32, J <= 64,
+        F <= 256, loss_funct not overridden) it is one fused HIP kernel each way
+        (training.mahalanobis_loss, sd_train.hip `k_mahalanobis`); otherwise loss_funct + mean."""
+        if (model_out.is_cuda and torch.is_grad_enabled() and model_out.dtype == torch.float32 and model_out.dim() == 3
+                and _training.hip_training_enabled() and type(self).loss_funct is NonisotropicGaussianDiffusion.loss_funct
+                and self.loss_reduction_type in ("l1", "mse") and self.objective in ("pred_noise", "pred_x0")
+                and model_out.shape[1] <= _training.MAX_NODES and model_out.shape[2] <= 256
+                and self.mahalanobis_S_sqrt_recip.dtype == torch.float32 and target.shape == model_out.shape
+                and t.numel() == model_out.shape[0]):
+            return _training.mahalanobis_loss(model_out, target, self.mahalanobis_S_sqrt_recip, t.reshape(-1),
+                                              self.objective == "pred_noise", self.loss_reduction_type == "mse")
+        return super().loss_rows(model_out, target, t)
 
     # -- reverse process (torch reference forms of the HIP update) -------------------------------
     def q_posterior_mean(self, x_start, x_t, t):

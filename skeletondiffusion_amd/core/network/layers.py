@@ -81,7 +81,14 @@ class StaticGraphLinear(nn.Module):
             init.uniform_(self.bias, -bound, bound)
 
     def ghat(self) -> torch.Tensor:
-        return F.normalize(self.G, p=1.0, dim=1) if self.learn_influence else self.G
+        if not self.learn_influence:
+            return self.G
+        G = self.G
+        if (G.is_cuda and torch.is_grad_enabled() and G.dtype == torch.float32 and _training.hip_training_enabled()
+                and G.dim() == 2 and G.shape[0] == G.shape[1] <= _training.MAX_NODES):
+            # training on the device: one HIP launch each way (sd_train.hip k_l1norm_rows)
+            return _training.l1norm_rows(G, 1e-12)
+        return F.normalize(G, p=1.0, dim=1)
 
     def forward(self, x: torch.Tensor, g: Optional[torch.Tensor] = None) -> torch.Tensor:
         g = self.ghat() if g is None else g
@@ -119,6 +126,10 @@ class RMSNorm(nn.Module):
         self.g = Parameter(torch.ones(1, 1, dim))
 
     def forward(self, x):
+        if (x.is_cuda and torch.is_grad_enabled() and x.dtype == torch.float32 and self.g.dtype == torch.float32
+                and _training.hip_training_enabled() and x.shape[-1] <= 1024 and self.g.numel() == x.shape[-1]):
+            # training on the device: forward + backward on HIP (sd_train.hip k_rmsnorm)
+            return _training.rmsnorm(x, self.g, x.shape[-1] ** 0.5, 1e-12)
         return F.normalize(x, dim=-1) * self.g * (x.shape[-1] ** 0.5)
 
 

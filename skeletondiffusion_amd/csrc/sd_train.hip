@@ -543,6 +543,155 @@ __global__ __launch_bounds__(256) void k_film_tanh_bwd(const float* __restrict__
     dss[b * 2 * C + c] = gs;
     dss[b * 2 * C + C + c] = gh;
 }
+
+// ---- Ghat = G / max(rowsum|G|, eps) of a learnable influence matrix (graph_structural.py:107,
+// F.normalize(G, p=1, dim=1)) ---------------------------------------------------------------------
+// One workgroup of 64 threads: thread i owns row i (J <= 64, a J x J matrix is at most 16 KB and
+// L2-resident).  Backward, with d_i = max(n_i, eps):
+//   dG[i][j] = dGhat[i][j] / d_i - [n_i >= eps] sign(G[i][j]) (sum_k dGhat[i][k] G[i][k]) / d_i^2
+__global__ __launch_bounds__(64) void k_l1norm_rows(const float* __restrict__ G, const float* __restrict__ dout,
+                                                    float* __restrict__ out, int J, float eps, int bwd) {
+    const int i = threadIdx.x;
+    if (i >= J) return;
+    const float* g = G + (int64_t)i * J;
+    float n = 0.f;
+    for (int j = 0; j < J; ++j) n += fabsf(g[j]);
+    const float d = fmaxf(n, eps);
+    float* o = out + (int64_t)i * J;
+    if (!bwd) {
+        for (int j = 0; j < J; ++j) o[j] = g[j] / d;
+        return;
+    }
+    const float* dg = dout + (int64_t)i * J;
+    float dot = 0.f;
+    for (int j = 0; j < J; ++j) dot = fmaf(dg[j], g[j], dot);
+    const float c = n >= eps ? dot / (d * d) : 0.f;
+    for (int j = 0; j < J; ++j) {
+        const float sg = g[j] > 0.f ? 1.f : (g[j] < 0.f ? -1.f : 0.f);
+        o[j] = dg[j] / d - sg * c;
+    }
+}
+
+// ---- RMSNorm of PreNorm (attention.py:30-36): out = (x / max(||x||, 1e-12)) g sqrt(C) ---------
+// x (R, C) with R = rows x J vectors of C features; one wave per vector, kRmsRows vectors per
+// workgroup.  The forward saves d = max(||x||, eps) per vector.  Backward, v = dy g s:
+//   dx = v / d - [n >= eps] x (sum_c v_c x_c) / (d^2 n),    dg[c] = sum_vectors dy_c s x_c / d
+// dg leaves as one partial per workgroup (waves summed in order), summed by sum_parts in order.
+constexpr int kRmsRows = 64;
+constexpr int kRmsMaxC = 1024;
+
+__device__ __forceinline__ float wave_sum(float v) {
+    for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+template <bool BWD>
+__global__ __launch_bounds__(256) void k_rmsnorm(const float* __restrict__ x, const float* __restrict__ g,
+                                                 const float* __restrict__ dy, float* __restrict__ out,
+                                                 float* __restrict__ dnorm, float* __restrict__ dg_part, int64_t R,
+                                                 int C, float s, float eps) {
+    __shared__ float acc[BWD ? 4 * kRmsMaxC : 1];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int64_t r0 = (int64_t)blockIdx.x * kRmsRows;
+    if constexpr (BWD) {
+        for (int c = threadIdx.x; c < 4 * C; c += 256) acc[c] = 0.f;
+        __syncthreads();
+    }
+    for (int q = w; q < kRmsRows; q += 4) {
+        const int64_t r = r0 + q;
+        if (r >= R) break;
+        const float* xr = x + r * C;
+        if constexpr (!BWD) {
+            float ss = 0.f;
+            for (int c = lane; c < C; c += 64) ss = fmaf(xr[c], xr[c], ss);
+            const float n = sqrtf(wave_sum(ss));
+            const float d = fmaxf(n, eps);
+            for (int c = lane; c < C; c += 64) out[r * C + c] = (xr[c] / d) * g[c] * s;
+            if (lane == 0) dnorm[r] = d;
+        } else {
+            const float* dr = dy + r * C;
+            const float d = dnorm[r];
+            float ss = 0.f, dot = 0.f;
+            for (int c = lane; c < C; c += 64) {
+                ss = fmaf(xr[c], xr[c], ss);
+                dot = fmaf(dr[c] * g[c] * s, xr[c], dot);
+            }
+            const float n = sqrtf(wave_sum(ss));
+            dot = wave_sum(dot);
+            const float k = n >= eps ? dot / (d * d * n) : 0.f;
+            for (int c = lane; c < C; c += 64) {
+                const float v = dr[c] * g[c] * s;
+                out[r * C + c] = v / d - xr[c] * k;
+                acc[w * C + c] += dr[c] * s * (xr[c] / d);
+            }
+        }
+    }
+    if constexpr (BWD) {
+        __syncthreads();
+        for (int c = threadIdx.x; c < C; c += 256)
+            dg_part[(int64_t)blockIdx.x * C + c] = ((acc[c] + acc[C + c]) + acc[2 * C + c]) + acc[3 * C + c];
+    }
+}
+
+// ---- Mahalanobis loss of NonisotropicGaussianDiffusion (nonisotropic.py:177-190 + the
+// 'b ... -> b' mean of base.py:298) ------------------------------------------------------------------
+// Per row r: D = sgn (model_out - target) (J x F), M = S[t_r] D with S = mahalanobis_S_sqrt_recip
+// (T, J, J); loss[r] = mean_{i,f} |M| (l1) or M^2 (mse).  One workgroup per row; D and S[t_r]
+// staged in LDS, M in LDS, sums in a fixed order.  Backward recomputes M:
+//   dM = (l1: sign(M), mse: 2M) * (dloss[r] / (J F)),   d model_out = sgn S^T dM.
+template <bool BWD>
+__global__ __launch_bounds__(256) void k_mahalanobis(const float* __restrict__ mo, const float* __restrict__ tg,
+                                                     const float* __restrict__ S, const int64_t* __restrict__ t,
+                                                     const float* __restrict__ dloss, float* __restrict__ out, int J,
+                                                     int F, float sgn, int mse) {
+    extern __shared__ __attribute__((aligned(16))) float sm[];
+    const int64_t r = blockIdx.x;
+    const int JF = J * F;
+    float* sD = sm;              // [J][F]
+    float* sM = sD + JF;         // [J][F]
+    float* sS = sM + JF;         // [J][J]
+    float* red = sS + J * J;     // [256]
+    const float* m = mo + r * JF;
+    const float* tt = tg + r * JF;
+    const float* St = S + t[r] * (int64_t)J * J;
+    for (int e = threadIdx.x; e < JF; e += 256) sD[e] = sgn * (m[e] - tt[e]);
+    for (int e = threadIdx.x; e < J * J; e += 256) sS[e] = St[e];
+    __syncthreads();
+    float part = 0.f;
+    for (int e = threadIdx.x; e < JF; e += 256) {
+        const int i = e / F, f = e - i * F;
+        float a = 0.f;
+        for (int j = 0; j < J; ++j) a = fmaf(sS[i * J + j], sD[j * F + f], a);
+        sM[e] = a;
+        part += mse ? a * a : fabsf(a);
+    }
+    if constexpr (!BWD) {
+        red[threadIdx.x] = part;
+        __syncthreads();
+        if (threadIdx.x < 64) {
+            const float v = ((red[threadIdx.x] + red[threadIdx.x + 64]) + red[threadIdx.x + 128]) + red[threadIdx.x + 192];
+            const float tot = wave_sum(v);
+            if (threadIdx.x == 0) out[r] = tot / (float)JF;
+        }
+    } else {
+        __syncthreads();
+        const float w = dloss[r] / (float)JF;
+        for (int e = threadIdx.x; e < JF; e += 256) {
+            const float a = sM[e];
+            sM[e] = (mse ? 2.f * a : (a > 0.f ? 1.f : (a < 0.f ? -1.f : 0.f))) * w;
+        }
+        __syncthreads();
+        float* o = out + r * JF;
+        for (int e = threadIdx.x; e < JF; e += 256) {
+            const int j = e / F, f = e - j * F;
+            float a = 0.f;
+            for (int i = 0; i < J; ++i) a = fmaf(sS[i * J + j], sM[i * F + f], a);
+            o[e] = sgn * a;
+        }
+    }
+}
+
+size_t mahalanobis_lds(int J, int F) { return ((size_t)2 * J * F + (size_t)J * J + 256) * sizeof(float); }
 }  // namespace
 }  // namespace sd
 
@@ -718,6 +867,100 @@ int sd_film_tanh_backward(const float* y, const float* ss, const float* out, con
                        (hipStream_t)stream, y, ss, out, dout, dy, dss, J, C);
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? SD_OK : sd::set_error(SD_E_HIP, std::string("k_film_tanh_bwd: ") + hipGetErrorString(e));
+}
+
+int sd_l1norm_rows_forward(const float* G, float* ghat, int32_t J, float eps, void* stream) {
+    if (J < 1 || J > 64) return sd::set_error(SD_E_INVALID, "sd_l1norm_rows_forward: 1 <= J <= 64");
+    if (!G || !ghat) return sd::set_error(SD_E_INVALID, "sd_l1norm_rows_forward: null buffer");
+    hipLaunchKernelGGL(sd::k_l1norm_rows, dim3(1), dim3(64), 0, (hipStream_t)stream, G, (const float*)nullptr, ghat, J,
+                       eps, 0);
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? SD_OK : sd::set_error(SD_E_HIP, std::string("k_l1norm_rows: ") + hipGetErrorString(e));
+}
+
+int sd_l1norm_rows_backward(const float* G, const float* dghat, float* dG, int32_t J, float eps, void* stream) {
+    if (J < 1 || J > 64) return sd::set_error(SD_E_INVALID, "sd_l1norm_rows_backward: 1 <= J <= 64");
+    if (!G || !dghat || !dG) return sd::set_error(SD_E_INVALID, "sd_l1norm_rows_backward: null buffer");
+    hipLaunchKernelGGL(sd::k_l1norm_rows, dim3(1), dim3(64), 0, (hipStream_t)stream, G, dghat, dG, J, eps, 1);
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? SD_OK : sd::set_error(SD_E_HIP, std::string("k_l1norm_rows: ") + hipGetErrorString(e));
+}
+
+size_t sd_rmsnorm_workspace_bytes(int64_t R, int32_t C) {
+    if (R < 0 || C < 1) return 0;
+    return (size_t)sd::ceil_div(R, sd::kRmsRows) * C * sizeof(float);
+}
+
+int sd_rmsnorm_forward(const float* x, const float* g, float* out, float* dnorm, int64_t R, int32_t C, float scale,
+                       float eps, void* stream) {
+    if (R < 0 || C < 1 || C > sd::kRmsMaxC) return sd::set_error(SD_E_INVALID, "sd_rmsnorm_forward: 1 <= C <= 1024");
+    if (R == 0) return SD_OK;
+    if (!x || !g || !out || !dnorm) return sd::set_error(SD_E_INVALID, "sd_rmsnorm_forward: null buffer");
+    if (sd::ceil_div(R, sd::kRmsRows) > 0x7fffffffLL) return sd::set_error(SD_E_INVALID, "sd_rmsnorm_forward: too many rows");
+    hipLaunchKernelGGL(sd::k_rmsnorm<false>, dim3((unsigned)sd::ceil_div(R, sd::kRmsRows)), dim3(256), 0,
+                       (hipStream_t)stream, x, g, (const float*)nullptr, out, dnorm, (float*)nullptr, R, C, scale, eps);
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? SD_OK : sd::set_error(SD_E_HIP, std::string("k_rmsnorm: ") + hipGetErrorString(e));
+}
+
+int sd_rmsnorm_backward(const float* x, const float* g, const float* dnorm, const float* dy, float* dx, float* dg,
+                        int64_t R, int32_t C, float scale, float eps, void* workspace, size_t workspace_bytes,
+                        void* stream) {
+    if (R < 0 || C < 1 || C > sd::kRmsMaxC) return sd::set_error(SD_E_INVALID, "sd_rmsnorm_backward: 1 <= C <= 1024");
+    hipStream_t s = (hipStream_t)stream;
+    if (R == 0) {
+        if (dg) TR_HIP(hipMemsetAsync(dg, 0, (size_t)C * sizeof(float), s));
+        return SD_OK;
+    }
+    if (!x || !g || !dnorm || !dy || !dx || !dg) return sd::set_error(SD_E_INVALID, "sd_rmsnorm_backward: null buffer");
+    if (!workspace || workspace_bytes < sd_rmsnorm_workspace_bytes(R, C))
+        return sd::set_error(SD_E_INVALID, "sd_rmsnorm_backward: workspace too small");
+    const int64_t blocks = sd::ceil_div(R, sd::kRmsRows);
+    if (blocks > 0x7fffffffLL) return sd::set_error(SD_E_INVALID, "sd_rmsnorm_backward: too many rows");
+    float* part = (float*)workspace;
+    hipLaunchKernelGGL(sd::k_rmsnorm<true>, dim3((unsigned)blocks), dim3(256), 0, s, x, g, dy, dx, (float*)dnorm, part, R,
+                       C, scale, eps);
+    TR_HIP(hipGetLastError());
+    TR_HIP(sd::sum_parts(part, (int)blocks, C, dg, s));
+    return SD_OK;
+}
+
+int sd_mahalanobis_loss_forward(const float* model_out, const float* target, const float* S, const int64_t* t,
+                                int64_t rows, int32_t J, int32_t F, int32_t pred_noise, int32_t mse, float* loss,
+                                void* stream) {
+    if (rows < 0 || J < 1 || J > 64 || F < 1 || F > 256)
+        return sd::set_error(SD_E_INVALID, "sd_mahalanobis_loss_forward: 1 <= J <= 64, 1 <= F <= 256");
+    if (rows == 0) return SD_OK;
+    if (!model_out || !target || !S || !t || !loss)
+        return sd::set_error(SD_E_INVALID, "sd_mahalanobis_loss_forward: null buffer");
+    if (rows > 0x7fffffffLL) return sd::set_error(SD_E_INVALID, "sd_mahalanobis_loss_forward: too many rows");
+    const size_t lds = sd::mahalanobis_lds(J, F);
+    if (lds > 64 * 1024)
+        TR_HIP(hipFuncSetAttribute((const void*)sd::k_mahalanobis<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                   (int)lds));
+    hipLaunchKernelGGL(sd::k_mahalanobis<false>, dim3((unsigned)rows), dim3(256), lds, (hipStream_t)stream, model_out,
+                       target, S, t, (const float*)nullptr, loss, J, F, pred_noise ? -1.f : 1.f, mse);
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? SD_OK : sd::set_error(SD_E_HIP, std::string("k_mahalanobis: ") + hipGetErrorString(e));
+}
+
+int sd_mahalanobis_loss_backward(const float* model_out, const float* target, const float* S, const int64_t* t,
+                                 const float* dloss, int64_t rows, int32_t J, int32_t F, int32_t pred_noise,
+                                 int32_t mse, float* dmodel_out, void* stream) {
+    if (rows < 0 || J < 1 || J > 64 || F < 1 || F > 256)
+        return sd::set_error(SD_E_INVALID, "sd_mahalanobis_loss_backward: 1 <= J <= 64, 1 <= F <= 256");
+    if (rows == 0) return SD_OK;
+    if (!model_out || !target || !S || !t || !dloss || !dmodel_out)
+        return sd::set_error(SD_E_INVALID, "sd_mahalanobis_loss_backward: null buffer");
+    if (rows > 0x7fffffffLL) return sd::set_error(SD_E_INVALID, "sd_mahalanobis_loss_backward: too many rows");
+    const size_t lds = sd::mahalanobis_lds(J, F);
+    if (lds > 64 * 1024)
+        TR_HIP(hipFuncSetAttribute((const void*)sd::k_mahalanobis<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                   (int)lds));
+    hipLaunchKernelGGL(sd::k_mahalanobis<true>, dim3((unsigned)rows), dim3(256), lds, (hipStream_t)stream, model_out,
+                       target, S, t, dloss, dmodel_out, J, F, pred_noise ? -1.f : 1.f, mse);
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? SD_OK : sd::set_error(SD_E_HIP, std::string("k_mahalanobis: ") + hipGetErrorString(e));
 }
 
 }  // extern "C"

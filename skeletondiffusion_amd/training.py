@@ -197,3 +197,123 @@ def graph_linear(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Ten
     if x.dtype != torch.float32 or weight.dtype != torch.float32:
         raise ValueError("graph_linear: the HIP training path is fp32")
     return GraphLinearFunction.apply(x, weight, bias, ghat, node_types)
+
+
+class L1NormRowsFunction(torch.autograd.Function):
+    """Ghat = G / max(rowsum|G|, eps) (F.normalize(G, p=1, dim=1), reference
+    graph_structural.py:107) with forward and backward on HIP (`sd_l1norm_rows_forward` /
+    `_backward`): one launch each way instead of torch's norm / clamp / div chain and its
+    backward per StaticGraphLinear call."""
+
+    @staticmethod
+    def forward(ctx, G, eps: float):
+        Gc = G.contiguous()
+        J = Gc.shape[0]
+        out = torch.empty_like(Gc)
+        _lib.check(_lib.lib().sd_l1norm_rows_forward(Gc.data_ptr(), out.data_ptr(), J, float(eps), _stream(G.device)))
+        ctx.save_for_backward(Gc)
+        ctx.eps = float(eps)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        (Gc,) = ctx.saved_tensors
+        dc = dout.contiguous().float()
+        dG = torch.empty_like(Gc)
+        _lib.check(_lib.lib().sd_l1norm_rows_backward(Gc.data_ptr(), dc.data_ptr(), dG.data_ptr(), Gc.shape[0], ctx.eps,
+                                                       _stream(Gc.device)))
+        return dG, None
+
+
+def l1norm_rows(G: torch.Tensor, eps: float = 1e-12) -> torch.Tensor:
+    """HIP row-wise L1 normalisation of a (J, J) fp32 device matrix under autograd (J <= 64)."""
+    if not G.is_cuda or G.dtype != torch.float32 or G.dim() != 2 or G.shape[0] != G.shape[1] or G.shape[0] > MAX_NODES:
+        raise ValueError("l1norm_rows: the HIP training path needs a (J, J) fp32 device matrix, J <= 64")
+    return L1NormRowsFunction.apply(G, eps)
+
+
+class RMSNormFunction(torch.autograd.Function):
+    """PreNorm's RMSNorm, x / max(||x||, eps) * g * sqrt(C) over the last axis (reference
+    attention.py:30-36), forward and backward on HIP (`sd_rmsnorm_forward` / `_backward`)."""
+
+    @staticmethod
+    def forward(ctx, x, g, scale: float, eps: float):
+        C = x.shape[-1]
+        xc = x.reshape(-1, C).contiguous()
+        gc = g.reshape(C).contiguous()
+        R = xc.shape[0]
+        out = torch.empty_like(xc)
+        dnorm = torch.empty(R, device=x.device, dtype=torch.float32)
+        _lib.check(_lib.lib().sd_rmsnorm_forward(xc.data_ptr(), gc.data_ptr(), out.data_ptr(), dnorm.data_ptr(), R, C,
+                                                  float(scale), float(eps), _stream(x.device)))
+        ctx.save_for_backward(xc, gc, dnorm)
+        ctx.meta = (x.shape, g.shape, float(scale), float(eps))
+        return out.reshape(x.shape)
+
+    @staticmethod
+    def backward(ctx, dout):
+        xc, gc, dnorm = ctx.saved_tensors
+        xshape, gshape, scale, eps = ctx.meta
+        R, C = xc.shape
+        dc = dout.reshape(R, C).contiguous().float()
+        dx = torch.empty_like(xc)
+        dg = torch.empty(C, device=xc.device, dtype=torch.float32)
+        L = _lib.lib()
+        ws_bytes = L.sd_rmsnorm_workspace_bytes(R, C)
+        ws = torch.empty(max(1, (ws_bytes + 3) // 4), device=xc.device, dtype=torch.float32)
+        _lib.check(L.sd_rmsnorm_backward(xc.data_ptr(), gc.data_ptr(), dnorm.data_ptr(), dc.data_ptr(), dx.data_ptr(),
+                                         dg.data_ptr(), R, C, scale, eps, ws.data_ptr(), ws_bytes, _stream(xc.device)))
+        return dx.reshape(xshape), dg.reshape(gshape), None, None
+
+
+def rmsnorm(x: torch.Tensor, g: torch.Tensor, scale: float, eps: float = 1e-12) -> torch.Tensor:
+    """HIP RMSNorm under autograd: x (..., C) and g (C elements) fp32 on the device, C <= 1024."""
+    if not x.is_cuda or x.dtype != torch.float32 or g.dtype != torch.float32 or x.shape[-1] > 1024:
+        raise ValueError("rmsnorm: the HIP training path needs fp32 device tensors with C <= 1024")
+    return RMSNormFunction.apply(x, g, scale, eps)
+
+
+class MahalanobisLossFunction(torch.autograd.Function):
+    """Per-row Mahalanobis loss of NonisotropicGaussianDiffusion: mean over (J, F) of
+    |S[t] D| (l1) or (S[t] D)^2 (mse), D = target - model_out (pred_noise) or model_out - target
+    (reference nonisotropic.py:177-190 + the 'b ... -> b' mean of base.py:298), forward and
+    backward on HIP (`sd_mahalanobis_loss_forward` / `_backward`).  The target gets the negated
+    gradient of model_out."""
+
+    @staticmethod
+    def forward(ctx, model_out, target, S, t, pred_noise: bool, mse: bool):
+        rows, J, F = model_out.shape
+        mo = model_out.contiguous()
+        tg = target.contiguous().float()
+        Sc = S.contiguous()
+        tc = t.to(device=mo.device, dtype=torch.int64).contiguous()
+        loss = torch.empty(rows, device=mo.device, dtype=torch.float32)
+        _lib.check(_lib.lib().sd_mahalanobis_loss_forward(mo.data_ptr(), tg.data_ptr(), Sc.data_ptr(), tc.data_ptr(),
+                                                           rows, J, F, int(pred_noise), int(mse), loss.data_ptr(),
+                                                           _stream(mo.device)))
+        ctx.save_for_backward(mo, tg, Sc, tc)
+        ctx.flags = (int(pred_noise), int(mse))
+        return loss
+
+    @staticmethod
+    def backward(ctx, dloss):
+        mo, tg, Sc, tc = ctx.saved_tensors
+        pred_noise, mse = ctx.flags
+        rows, J, F = mo.shape
+        dl = dloss.contiguous().float()
+        dmo = torch.empty_like(mo)
+        _lib.check(_lib.lib().sd_mahalanobis_loss_backward(mo.data_ptr(), tg.data_ptr(), Sc.data_ptr(), tc.data_ptr(),
+                                                            dl.data_ptr(), rows, J, F, pred_noise, mse, dmo.data_ptr(),
+                                                            _stream(mo.device)))
+        need_mo, need_tg = ctx.needs_input_grad[0], ctx.needs_input_grad[1]
+        return (dmo if need_mo else None), (-dmo if need_tg else None), None, None, None, None
+
+
+def mahalanobis_loss(model_out: torch.Tensor, target: torch.Tensor, S: torch.Tensor, t: torch.Tensor,
+                     pred_noise: bool, mse: bool) -> torch.Tensor:
+    """HIP per-row Mahalanobis loss under autograd: model_out / target (rows, J, F) fp32 on the
+    device, S (T, J, J), t (rows,) timesteps; J <= 64, F <= 256."""
+    if (not model_out.is_cuda or model_out.dtype != torch.float32 or model_out.dim() != 3
+            or model_out.shape[1] > MAX_NODES or model_out.shape[2] > 256 or S.dtype != torch.float32):
+        raise ValueError("mahalanobis_loss: the HIP training path needs (rows, J <= 64, F <= 256) fp32 device tensors")
+    return MahalanobisLossFunction.apply(model_out, target, S, t, pred_noise, mse)

@@ -156,6 +156,10 @@ def test_release_training_step_on_hip(name):
     assert "GraphLinearFunctionBackward" in _grad_fn_names(loss_g), "HIP graph-linear not on the training path"
     assert "AttentionCoreFunctionBackward" in _grad_fn_names(loss_g), "HIP attention core not on the training path"
     assert "FilmTanhFunctionBackward" in _grad_fn_names(loss_g), "HIP FiLM + tanh not on the training path"
+    assert "RMSNormFunctionBackward" in _grad_fn_names(loss_g), "HIP RMSNorm not on the training path"
+    assert "MahalanobisLossFunctionBackward" in _grad_fn_names(loss_g), "HIP loss not on the training path"
+    if d_gpu.model.init_lin.learn_influence:
+        assert "L1NormRowsFunctionBackward" in _grad_fn_names(loss_g), "HIP G-hat not on the training path"
     loss_g.mean().backward()
     torch.cuda.synchronize()
     # the reference's own loss (gen_golden.py, reference p_losses on CPU)
@@ -277,3 +281,112 @@ def test_film_tanh_vs_autograd(rows, J, C):
     _close(out, ref, "out")
     _close(yg.grad, yr.grad, "dy")
     _close(sg.grad, sr.grad, "dss")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("J,zero_row", [(16, False), (21, True), (51, False), (64, True), (1, False)])
+def test_l1norm_rows_vs_autograd(J, zero_row):
+    """sd_l1norm_rows_forward / _backward (training.L1NormRowsFunction) against float64 autograd of
+    F.normalize(G, p=1, dim=1) (graph_structural.py:107), a zero row included (the eps clamp)."""
+    g = torch.Generator().manual_seed(J)
+    G = torch.randn(J, J, generator=g, dtype=torch.float64)
+    if zero_row:
+        G[J // 2] = 0.0
+    dout = torch.randn(J, J, generator=g, dtype=torch.float64)
+    Gr = G.clone().requires_grad_(True)
+    ref = F.normalize(Gr, p=1.0, dim=1)
+    (ref * dout).sum().backward()
+    dev = torch.device("cuda:0")
+    Gg = G.float().to(dev).requires_grad_(True)
+    out = training.l1norm_rows(Gg)
+    out.backward(dout.float().to(dev))
+    torch.cuda.synchronize()
+    _close(out, ref, "ghat")
+    _close(Gg.grad, Gr.grad, "dG")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("rows,J,C", [(257, 16, 192), (5, 21, 192), (1, 51, 96), (3, 16, 1024), (0, 16, 192)])
+def test_rmsnorm_vs_autograd(rows, J, C):
+    """sd_rmsnorm_forward / _backward (training.RMSNormFunction) against float64 autograd of the
+    reference's RMSNorm (attention.py:30-36), one all-zero vector included (the eps clamp)."""
+    g = torch.Generator().manual_seed(rows * 7 + J + C)
+    x = torch.randn(rows, J, C, generator=g, dtype=torch.float64)
+    if rows:
+        x[0, J - 1] = 0.0
+    gain = 1 + 0.3 * torch.randn(1, 1, C, generator=g, dtype=torch.float64)
+    dout = torch.randn(rows, J, C, generator=g, dtype=torch.float64)
+    xr, gr = x.clone().requires_grad_(True), gain.clone().requires_grad_(True)
+    ref = F.normalize(xr, dim=-1) * gr * (C ** 0.5)
+    (ref * dout).sum().backward()
+    dev = torch.device("cuda:0")
+    xg, gg = x.float().to(dev).requires_grad_(True), gain.float().to(dev).requires_grad_(True)
+    out = training.rmsnorm(xg, gg, C ** 0.5)
+    out.backward(dout.float().to(dev))
+    torch.cuda.synchronize()
+    assert out.shape == (rows, J, C) and gg.grad.shape == (1, 1, C)
+    _close(out, ref, "out")
+    _close(xg.grad, xr.grad, "dx")
+    if rows:
+        _close(gg.grad, gr.grad, "dg")
+    else:
+        assert float(gg.grad.abs().max()) == 0.0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("rows,J,F_,pred_noise,mse", [(257, 16, 96, True, False), (33, 21, 96, False, False),
+                                                      (5, 51, 96, True, True), (2, 64, 256, False, True),
+                                                      (1, 17, 96, True, False), (0, 16, 96, True, False)])
+def test_mahalanobis_loss_vs_autograd(rows, J, F_, pred_noise, mse):
+    """sd_mahalanobis_loss_forward / _backward (training.MahalanobisLossFunction) against float64
+    autograd of the reference's loss_funct + per-row mean (nonisotropic.py:177-190,
+    base.py:297-298): the loss and d model_out / d target from a random per-row upstream gradient."""
+    g = torch.Generator().manual_seed(rows + 13 * J + F_ + 2 * int(mse))
+    T = 10
+    mo = torch.randn(rows, J, F_, generator=g, dtype=torch.float64)
+    tg = torch.randn(rows, J, F_, generator=g, dtype=torch.float64)
+    S = torch.randn(T, J, J, generator=g, dtype=torch.float64) / J ** 0.5
+    t = torch.randint(0, T, (rows,), generator=g)
+    dl = torch.rand(rows, generator=g, dtype=torch.float64) + 0.5
+    mr, tr = mo.clone().requires_grad_(True), tg.clone().requires_grad_(True)
+    diff = tr - mr if pred_noise else mr - tr
+    m = (S[t] @ diff).abs()
+    ref = (m ** 2 if mse else m).reshape(rows, -1).mean(dim=1)
+    (ref * dl).sum().backward()
+    dev = torch.device("cuda:0")
+    mg, tgg = mo.float().to(dev).requires_grad_(True), tg.float().to(dev).requires_grad_(True)
+    loss = training.mahalanobis_loss(mg, tgg, S.float().to(dev), t.to(dev), pred_noise, mse)
+    loss.backward(dl.float().to(dev))
+    torch.cuda.synchronize()
+    assert loss.shape == (rows,)
+    _close(loss, ref, "loss")
+    _close(mg.grad, mr.grad, "d model_out")
+    _close(tgg.grad, tr.grad, "d target")
+
+
+def test_new_training_abi_validation_on_host():
+    """Argument checks of the G-hat / RMSNorm / loss training ABI run before any device work."""
+    from skeletondiffusion_amd import _lib
+    L = _lib.lib()
+    assert L.sd_l1norm_rows_forward(None, None, 0, 1e-12, None) < 0          # J = 0
+    assert b"J" in L.sd_last_error()
+    assert L.sd_l1norm_rows_forward(None, None, 65, 1e-12, None) < 0         # J > 64
+    assert L.sd_l1norm_rows_forward(None, None, 16, 1e-12, None) < 0         # null buffers
+    assert L.sd_l1norm_rows_backward(None, None, None, 16, 1e-12, None) < 0
+    assert L.sd_rmsnorm_workspace_bytes(1024 * 16, 192) == 256 * 192 * 4     # one dg partial per 64 vectors
+    assert L.sd_rmsnorm_workspace_bytes(-1, 192) == 0
+    assert L.sd_rmsnorm_forward(None, None, None, None, 4, 1025, 1.0, 1e-12, None) < 0   # C > 1024
+    assert L.sd_rmsnorm_forward(None, None, None, None, 0, 192, 1.0, 1e-12, None) == 0   # empty
+    assert L.sd_rmsnorm_forward(None, None, None, None, 4, 192, 1.0, 1e-12, None) < 0    # null buffers
+    assert L.sd_rmsnorm_backward(None, None, None, None, None, None, 4, 192, 1.0, 1e-12, None, 0, None) < 0
+    assert L.sd_mahalanobis_loss_forward(None, None, None, None, 4, 65, 96, 1, 0, None, None) < 0   # J > 64
+    assert L.sd_mahalanobis_loss_forward(None, None, None, None, 4, 16, 257, 1, 0, None, None) < 0  # F > 256
+    assert L.sd_mahalanobis_loss_forward(None, None, None, None, 0, 16, 96, 1, 0, None, None) == 0  # empty
+    assert L.sd_mahalanobis_loss_backward(None, None, None, None, None, 4, 16, 96, 1, 0, None, None) < 0
+    with pytest.raises(ValueError):
+        training.rmsnorm(torch.zeros(2, 16, 8), torch.ones(8), 8 ** 0.5)      # host tensor
+    with pytest.raises(ValueError):
+        training.l1norm_rows(torch.eye(4))
+    with pytest.raises(ValueError):
+        training.mahalanobis_loss(torch.zeros(2, 16, 96), torch.zeros(2, 16, 96), torch.zeros(3, 16, 16),
+                                  torch.zeros(2, dtype=torch.long), True, False)
