@@ -90,13 +90,35 @@ class StaticGraphLinear(nn.Module):
             return _training.l1norm_rows(G, 1e-12)
         return F.normalize(G, p=1.0, dim=1)
 
+    def _hip_ok(self, x: torch.Tensor, g: torch.Tensor) -> bool:
+        # the node-type validity check reads the (host) type vector: done once per (vector,
+        # version, weight shape), not per call
+        nt = self.node_type_index
+        key = (id(nt), None if nt is None else nt._version, tuple(self.weight.shape), tuple(g.shape), x.shape[-2],
+               x.dim())
+        if getattr(self, "_hip_ok_key", None) != key:
+            self._hip_ok_val = _training.hip_shapes_ok(x, self.weight, g, nt)
+            self._hip_ok_key, self._hip_ok_src = key, nt  # the reference keeps id(nt) unique
+        return self._hip_ok_val
+
+    def _node_types_on(self, device: torch.device) -> Optional[torch.Tensor]:
+        # device copy of the node-type vector, cached (one host-to-device copy, not one per call)
+        nt = self.node_type_index
+        if nt is None:
+            return None
+        key = (id(nt), nt._version, device)
+        if getattr(self, "_nt_dev_key", None) != key:
+            self._nt_dev = nt.to(device=device, dtype=torch.int64).contiguous()
+            self._nt_dev_key, self._nt_dev_src = key, nt
+        return self._nt_dev
+
     def forward(self, x: torch.Tensor, g: Optional[torch.Tensor] = None) -> torch.Tensor:
         g = self.ghat() if g is None else g
         if (x.is_cuda and torch.is_grad_enabled() and x.dtype == torch.float32
                 and self.weight.dtype == torch.float32 and _training.hip_training_enabled()
-                and _training.hip_shapes_ok(x, self.weight, g, self.node_type_index)):
+                and self._hip_ok(x, g)):
             # training on the device: forward + backward on the HIP kernels (sd_train.hip)
-            return _training.graph_linear(x, self.weight, self.bias, g, self.node_type_index)
+            return _training.graph_linear(x, self.weight, self.bias, g, self._node_types_on(x.device))
         if self.node_type_index is not None:
             w = self.weight[self.node_type_index.to(self.weight.device)]       # (J, out, in)
             y = torch.einsum("noi,bni->bno", w, x)

@@ -27,6 +27,7 @@ namespace {
 constexpr int TM = 64, TN = 64, TK = 32;
 constexpr int TE = TM * TK / 256;  // staged elements per thread and operand
 typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 // Strided batched GEMM: for batch z (grid.z = nbatch * splits):
 //   node mode (by_type = 0): group = {node j = batch}, t = type(j)
@@ -331,6 +332,55 @@ __global__ __launch_bounds__(256) void k_dghat_part(const float* __restrict__ dy
     for (int p = tid; p < J * J; p += 256) part[(int64_t)blockIdx.x * J * J + p] = s_acc[p / J][p % J];
 }
 
+// J <= 16: the same partial dghat on v_mfma_f32_16x16x4_f32 (a 32x32 tile would leave three
+// quarters of its products on padding): lane (node i = l & 15, quad kq = l >> 4) loads features
+// k0 + 16u + 4kq .. +3 of its dy and z rows (16 B each, four 16-feature steps in flight) and feeds
+// them as four k-steps; A and B share the permutation, so the sum over features is exact.
+// One row per wave at a time; the 4 waves' tiles are summed in LDS in wave order.  N % 4 == 0.
+__global__ __launch_bounds__(256) void k_dghat_part16(const float* __restrict__ dy, const float* __restrict__ z,
+                                                      float* __restrict__ part, int64_t rows, int J, int N,
+                                                      int rows_per_chunk) {
+    __shared__ float s_acc[16][17];
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int i = lane & 15, kq = lane >> 4;
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    const int64_t r0 = (int64_t)blockIdx.x * rows_per_chunk;
+    const int64_t r1 = min(rows, r0 + rows_per_chunk);
+    for (int64_t r = r0 + w; r < r1; r += 4) {
+        const float* dyr = dy + (r * J + i) * N;
+        const float* zr = z + (r * J + i) * N;
+        for (int k0 = 0; k0 < N; k0 += 64) {
+            float4 va[4], vb[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int k = k0 + 16 * u + 4 * kq;
+                const bool ok = i < J && k < N;
+                va[u] = ok ? *(const float4*)(dyr + k) : make_float4(0.f, 0.f, 0.f, 0.f);
+                vb[u] = ok ? *(const float4*)(zr + k) : make_float4(0.f, 0.f, 0.f, 0.f);
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                acc = __builtin_amdgcn_mfma_f32_16x16x4f32(va[u].x, vb[u].x, acc, 0, 0, 0);
+                acc = __builtin_amdgcn_mfma_f32_16x16x4f32(va[u].y, vb[u].y, acc, 0, 0, 0);
+                acc = __builtin_amdgcn_mfma_f32_16x16x4f32(va[u].z, vb[u].z, acc, 0, 0, 0);
+                acc = __builtin_amdgcn_mfma_f32_16x16x4f32(va[u].w, vb[u].w, acc, 0, 0, 0);
+            }
+        }
+    }
+    // C/D map: col = lane & 15, row = 4 (lane >> 4) + reg
+    for (int ww = 0; ww < 4; ++ww) {
+        if (w == ww) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int ii = 4 * kq + q;
+                s_acc[ii][i] = (ww == 0 ? 0.f : s_acc[ii][i]) + acc[q];
+            }
+        }
+        __syncthreads();
+    }
+    for (int p = tid; p < J * J; p += 256) part[(int64_t)blockIdx.x * J * J + p] = s_acc[p / J][p % J];
+}
+
 // partial dbias over a row range: part[chunk][t][n] = sum_{r in chunk, j: type j = t} dz[r,j,n]
 __global__ __launch_bounds__(256) void k_dbias_part(const float* __restrict__ dz, const int64_t* __restrict__ types,
                                                     float* __restrict__ part, int64_t rows, int J, int N,
@@ -396,7 +446,7 @@ hipError_t launch_gemm(const GemmArgs& g, dim3 grid, hipStream_t s) {
 }
 
 constexpr int kRowsPerChunk = 16;  // dbias partials
-constexpr int kDghatRows = 8;      // dghat partials (2 rows per wave)
+constexpr int kDghatRows = 4;      // dghat partials (one row per wave)
 
 int splits_for(int64_t rows) {
     // dW reduction: about 64 rows per split, at most 32 splits
@@ -764,7 +814,10 @@ int sd_gl_train_backward(const float* x, const float* z, const float* dy, const 
     // dghat first (reads dy and z, independent of dz)
     if (dghat) {
         const int64_t chunks = sd::ceil_div(rows, sd::kDghatRows);
-        if (J <= 32)
+        if (J <= 16 && (N & 3) == 0)
+            hipLaunchKernelGGL(sd::k_dghat_part16, dim3((unsigned)chunks), dim3(256), 0, s, dy, z, part, rows, J, N,
+                               sd::kDghatRows);
+        else if (J <= 32)
             hipLaunchKernelGGL(sd::k_dghat_part<1>, dim3((unsigned)chunks), dim3(256), 0, s, dy, z, part, rows, J, N,
                                sd::kDghatRows);
         else

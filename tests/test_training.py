@@ -351,7 +351,7 @@ def test_mahalanobis_loss_vs_autograd(rows, J, F_, pred_noise, mse):
     mr, tr = mo.clone().requires_grad_(True), tg.clone().requires_grad_(True)
     diff = tr - mr if pred_noise else mr - tr
     m = (S[t] @ diff).abs()
-    ref = (m ** 2 if mse else m).reshape(rows, -1).mean(dim=1)
+    ref = (m ** 2 if mse else m).reshape(rows, J * F_).mean(dim=1)
     (ref * dl).sum().backward()
     dev = torch.device("cuda:0")
     mg, tgg = mo.float().to(dev).requires_grad_(True), tg.float().to(dev).requires_grad_(True)
