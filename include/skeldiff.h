@@ -363,9 +363,11 @@ int sd_film_tanh_backward(const float* y, const float* ss, const float* out, con
 
 /* Row-wise L1 normalisation of a learnable influence matrix under autograd (reference
  * graph_structural.py:107, F.normalize(G, p=1, dim=1)): ghat[i][j] = G[i][j] / max(sum_k |G[i][k]|, eps);
- * the backward writes dG from dghat.  J x J row-major, 1 <= J <= 64, f32. */
-int sd_l1norm_rows_forward(const float* G, float* ghat, int32_t J, float eps, void* stream);
-int sd_l1norm_rows_backward(const float* G, const float* dghat, float* dG, int32_t J, float eps, void* stream);
+ * the backward writes dG from dghat.  `count` contiguous J x J row-major matrices (one launch for
+ * all of a Denoiser's learnable G), 1 <= J <= 64, f32. */
+int sd_l1norm_rows_forward(const float* G, float* ghat, int32_t J, int32_t count, float eps, void* stream);
+int sd_l1norm_rows_backward(const float* G, const float* dghat, float* dG, int32_t J, int32_t count, float eps,
+                            void* stream);
 /* PreNorm's RMSNorm under autograd (reference attention.py:30-36): x (R, C), R vectors of C
  * features, out = x / max(||x||, eps) * g * scale (scale = sqrt(C)); the forward also writes
  * dnorm (R) = max(||x||, eps) for the backward, which writes dx (R, C) and dg (C), the latter

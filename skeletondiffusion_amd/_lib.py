@@ -136,8 +136,8 @@ def _declare(lib: ctypes.CDLL) -> None:
         "sd_attn_train_backward": (ctypes.c_int, [vp, vp, vp, i64, i32, i32, i32, ctypes.c_float, vp]),
         "sd_film_tanh_forward": (ctypes.c_int, [vp, vp, vp, i64, i32, i32, vp]),
         "sd_film_tanh_backward": (ctypes.c_int, [vp, vp, vp, vp, vp, vp, i64, i32, i32, vp]),
-        "sd_l1norm_rows_forward": (ctypes.c_int, [vp, vp, i32, ctypes.c_float, vp]),
-        "sd_l1norm_rows_backward": (ctypes.c_int, [vp, vp, vp, i32, ctypes.c_float, vp]),
+        "sd_l1norm_rows_forward": (ctypes.c_int, [vp, vp, i32, i32, ctypes.c_float, vp]),
+        "sd_l1norm_rows_backward": (ctypes.c_int, [vp, vp, vp, i32, i32, ctypes.c_float, vp]),
         "sd_rmsnorm_workspace_bytes": (sz, [i64, i32]),
         "sd_rmsnorm_forward": (ctypes.c_int, [vp, vp, vp, vp, i64, i32, ctypes.c_float, ctypes.c_float, vp]),
         "sd_rmsnorm_backward": (ctypes.c_int, [vp, vp, vp, vp, vp, vp, i64, i32, ctypes.c_float, ctypes.c_float, vp,

@@ -9,6 +9,7 @@ from __future__ import annotations
 import torch
 from torch import nn
 
+from ... import training as _training
 from .layers import (Attention, PreNorm, RandomOrLearnedSinusoidalPosEmb, Residual, ResnetBlock,
                      SinusoidalPosEmb, StaticGraphLinear)
 
@@ -74,6 +75,20 @@ class Denoiser(nn.Module):
         return self.init_lin.learn_influence
 
     def forward(self, x, time, x_self_cond=None, x_cond=None):
+        # training on the device: all learnable G-hat of the graph-linears normalised in one HIP
+        # launch each way (training.l1norm_rows_many) instead of one per layer call
+        gls = [m for m in self.modules() if isinstance(m, StaticGraphLinear) and m.hip_ghat_ok()]
+        if len(gls) > 1 and len({tuple(m.G.shape) for m in gls}) == 1 and len({m.G.device for m in gls}) == 1:
+            for m, gh in zip(gls, _training.l1norm_rows_many([m.G for m in gls], 1e-12)):
+                m._ghat_batched = gh
+            try:
+                return self._forward(x, time, x_self_cond, x_cond)
+            finally:
+                for m in gls:
+                    m._ghat_batched = None
+        return self._forward(x, time, x_self_cond, x_cond)
+
+    def _forward(self, x, time, x_self_cond=None, x_cond=None):
         if self.self_condition:
             x_self_cond = x_self_cond if x_self_cond is not None else torch.zeros_like(x)
             x = torch.cat((x_self_cond, x), dim=-1)

@@ -80,9 +80,18 @@ class StaticGraphLinear(nn.Module):
             bound = 1 / math.sqrt(fan_in)
             init.uniform_(self.bias, -bound, bound)
 
+    def hip_ghat_ok(self) -> bool:
+        G = self.G
+        return (self.learn_influence and isinstance(G, torch.Tensor) and G.is_cuda and torch.is_grad_enabled()
+                and G.dtype == torch.float32 and _training.hip_training_enabled() and G.dim() == 2
+                and G.shape[0] == G.shape[1] <= _training.MAX_NODES)
+
     def ghat(self) -> torch.Tensor:
         if not self.learn_influence:
             return self.G
+        pre = getattr(self, "_ghat_batched", None)
+        if pre is not None:  # set by Denoiser.forward: every G normalised in one launch
+            return pre
         G = self.G
         if (G.is_cuda and torch.is_grad_enabled() and G.dtype == torch.float32 and _training.hip_training_enabled()
                 and G.dim() == 2 and G.shape[0] == G.shape[1] <= _training.MAX_NODES):

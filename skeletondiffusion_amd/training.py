@@ -200,36 +200,51 @@ def graph_linear(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Ten
 
 
 class L1NormRowsFunction(torch.autograd.Function):
-    """Ghat = G / max(rowsum|G|, eps) (F.normalize(G, p=1, dim=1), reference
-    graph_structural.py:107) with forward and backward on HIP (`sd_l1norm_rows_forward` /
-    `_backward`): one launch each way instead of torch's norm / clamp / div chain and its
-    backward per StaticGraphLinear call."""
+    """Ghat_k = G_k / max(rowsum|G_k|, eps) (F.normalize(G, p=1, dim=1), reference
+    graph_structural.py:107) for L matrices G_1 .. G_L of one size, forward and backward on HIP
+    (`sd_l1norm_rows_forward` / `_backward`, one launch each way for all L): the Denoiser
+    normalises all its learnable G at once per forward instead of torch's norm / clamp / div chain
+    and its backward per StaticGraphLinear call.  apply(eps, G_1, ..., G_L) -> (Ghat_1, ..., Ghat_L)."""
 
     @staticmethod
-    def forward(ctx, G, eps: float):
-        Gc = G.contiguous()
-        J = Gc.shape[0]
+    def forward(ctx, eps: float, *Gs):
+        Gc = torch.stack([g.detach() for g in Gs]).contiguous()
+        L, J = Gc.shape[0], Gc.shape[1]
         out = torch.empty_like(Gc)
-        _lib.check(_lib.lib().sd_l1norm_rows_forward(Gc.data_ptr(), out.data_ptr(), J, float(eps), _stream(G.device)))
+        _lib.check(_lib.lib().sd_l1norm_rows_forward(Gc.data_ptr(), out.data_ptr(), J, L, float(eps),
+                                                      _stream(Gc.device)))
         ctx.save_for_backward(Gc)
         ctx.eps = float(eps)
-        return out
+        return tuple(out.unbind(0))
 
     @staticmethod
-    def backward(ctx, dout):
+    def backward(ctx, *douts):
         (Gc,) = ctx.saved_tensors
-        dc = dout.contiguous().float()
+        L, J = Gc.shape[0], Gc.shape[1]
+        dc = torch.stack([torch.zeros_like(Gc[0]) if d is None else d.float() for d in douts]).contiguous()
         dG = torch.empty_like(Gc)
-        _lib.check(_lib.lib().sd_l1norm_rows_backward(Gc.data_ptr(), dc.data_ptr(), dG.data_ptr(), Gc.shape[0], ctx.eps,
+        _lib.check(_lib.lib().sd_l1norm_rows_backward(Gc.data_ptr(), dc.data_ptr(), dG.data_ptr(), J, L, ctx.eps,
                                                        _stream(Gc.device)))
-        return dG, None
+        return (None,) + tuple(dG.unbind(0))
+
+
+def l1norm_rows_many(Gs, eps: float = 1e-12):
+    """HIP row-wise L1 normalisation of L (J, J) fp32 device matrices under autograd (J <= 64), one
+    launch each way."""
+    Gs = list(Gs)
+    if not Gs:
+        return ()
+    J = Gs[0].shape[0]
+    for G in Gs:
+        if (not G.is_cuda or G.dtype != torch.float32 or G.dim() != 2 or tuple(G.shape) != (J, J)
+                or J > MAX_NODES or G.device != Gs[0].device):
+            raise ValueError("l1norm_rows: the HIP training path needs (J, J) fp32 device matrices, J <= 64")
+    return L1NormRowsFunction.apply(eps, *Gs)
 
 
 def l1norm_rows(G: torch.Tensor, eps: float = 1e-12) -> torch.Tensor:
-    """HIP row-wise L1 normalisation of a (J, J) fp32 device matrix under autograd (J <= 64)."""
-    if not G.is_cuda or G.dtype != torch.float32 or G.dim() != 2 or G.shape[0] != G.shape[1] or G.shape[0] > MAX_NODES:
-        raise ValueError("l1norm_rows: the HIP training path needs a (J, J) fp32 device matrix, J <= 64")
-    return L1NormRowsFunction.apply(G, eps)
+    """HIP row-wise L1 normalisation of one (J, J) fp32 device matrix under autograd (J <= 64)."""
+    return l1norm_rows_many([G], eps)[0]
 
 
 class RMSNormFunction(torch.autograd.Function):

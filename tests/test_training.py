@@ -306,6 +306,29 @@ def test_l1norm_rows_vs_autograd(J, zero_row):
 
 
 @pytest.mark.gpu
+def test_l1norm_rows_batched_vs_autograd():
+    """Several G in one launch each way (training.l1norm_rows_many, what Denoiser.forward uses):
+    each output and gradient equals float64 autograd of its own F.normalize; an output with no
+    upstream gradient contributes zeros."""
+    J, L = 21, 5
+    g = torch.Generator().manual_seed(99)
+    Gs = [torch.randn(J, J, generator=g, dtype=torch.float64) for _ in range(L)]
+    Gs[2][3] = 0.0
+    douts = [torch.randn(J, J, generator=g, dtype=torch.float64) for _ in range(L)]
+    dev = torch.device("cuda:0")
+    Gg = [G.float().to(dev).requires_grad_(True) for G in Gs]
+    outs = training.l1norm_rows_many(Gg)
+    sum((o * d.float().to(dev)).sum() for k, (o, d) in enumerate(zip(outs, douts)) if k != 4).backward()
+    torch.cuda.synchronize()
+    for k in range(L):
+        Gr = Gs[k].clone().requires_grad_(True)
+        ref = F.normalize(Gr, p=1.0, dim=1)
+        (ref * (douts[k] if k != 4 else torch.zeros_like(douts[k]))).sum().backward()
+        _close(outs[k], ref, f"ghat[{k}]")
+        _close(Gg[k].grad, Gr.grad, f"dG[{k}]")
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("rows,J,C", [(257, 16, 192), (5, 21, 192), (1, 51, 96), (3, 16, 1024), (0, 16, 192)])
 def test_rmsnorm_vs_autograd(rows, J, C):
     """sd_rmsnorm_forward / _backward (training.RMSNormFunction) against float64 autograd of the
@@ -368,12 +391,14 @@ def test_new_training_abi_validation_on_host():
     """Argument checks of the G-hat / RMSNorm / loss training ABI run before any device work."""
     from skeletondiffusion_amd import _lib
     L = _lib.lib()
-    assert L.sd_l1norm_rows_forward(None, None, 0, 1e-12, None) < 0          # J = 0
+    assert L.sd_l1norm_rows_forward(None, None, 0, 1, 1e-12, None) < 0       # J = 0
     assert b"J" in L.sd_last_error()
-    assert L.sd_l1norm_rows_forward(None, None, 65, 1e-12, None) < 0         # J > 64
-    assert L.sd_l1norm_rows_forward(None, None, 16, 1e-12, None) < 0         # null buffers
-    assert L.sd_l1norm_rows_backward(None, None, None, 16, 1e-12, None) < 0
-    assert L.sd_rmsnorm_workspace_bytes(1024 * 16, 192) == 256 * 192 * 4     # one dg partial per 64 vectors
+    assert L.sd_l1norm_rows_forward(None, None, 65, 1, 1e-12, None) < 0      # J > 64
+    assert L.sd_l1norm_rows_forward(None, None, 16, -1, 1e-12, None) < 0     # count < 0
+    assert L.sd_l1norm_rows_forward(None, None, 16, 0, 1e-12, None) == 0     # nothing to do
+    assert L.sd_l1norm_rows_forward(None, None, 16, 1, 1e-12, None) < 0      # null buffers
+    assert L.sd_l1norm_rows_backward(None, None, None, 16, 1, 1e-12, None) < 0
+    assert L.sd_rmsnorm_workspace_bytes(1024 * 16, 192) == 1024 * 192 * 4    # one dg partial per 16 vectors
     assert L.sd_rmsnorm_workspace_bytes(-1, 192) == 0
     assert L.sd_rmsnorm_forward(None, None, None, None, 4, 1025, 1.0, 1e-12, None) < 0   # C > 1024
     assert L.sd_rmsnorm_forward(None, None, None, None, 0, 192, 1.0, 1e-12, None) == 0   # empty
