@@ -82,6 +82,10 @@ typedef struct sd_plan_desc {
 
 int32_t sd_abi_version(void);
 const char* sd_last_error(void);
+/* How the device code was built: "no-packed-fp32" for the product build (skeletondiffusion_amd/
+ * build.py compiles every kernel without packed-FP32 instructions, DESIGN.md §4c, and checks the
+ * linked code objects); the Python binding refuses to load a library that says otherwise. */
+const char* sd_build_info(void);
 
 int sd_plan_create(sd_plan** out, const sd_plan_desc* desc);
 void sd_plan_destroy(sd_plan* plan);
@@ -97,6 +101,10 @@ int sd_plan_set_tensor(sd_plan* plan, const char* name, const float* data, int64
                        void* stream);
 /* Pack weights (G-hat, RMSNorm gain folding, time/FiLM tables, posterior tables). */
 int sd_plan_finalize(sd_plan* plan, void* stream);
+
+/* dims_out[4] = {J (num_nodes), D (latent_dim), T (timesteps), cond_dim} of the plan (host-side
+ * shape validation at the boundary, e.g. the skeldiff::sample_loop torch op). */
+int sd_plan_dims(const sd_plan* plan, int32_t* dims_out);
 
 /* Bytes of device workspace needed for `rows` latent rows. */
 size_t sd_workspace_bytes(const sd_plan* plan, int64_t rows);
@@ -224,18 +232,18 @@ int sd_test_attention(const float* qkv, float* out, int64_t rows, int32_t J, int
 int sd_test_qkv_attention(const float* x, int32_t K, const float* W, const int64_t* node_types, const float* ghat,
                           float* out, int64_t rows, int32_t J, int32_t heads, int32_t rms, int32_t layout,
                           void* stream);
-/* Process DEFAULT of the kernel generation for plans created afterwards and for the sd_test_*
- * hooks (a plan keeps its own copy: SD_OPT_KERNEL_VARIANT / SD_OPT_GL4_TILE):
+/* Test hook: the kernel generation of the sd_test_* entry points ONLY (plans never read it; a
+ * plan's generation is its SD_OPT_KERNEL_VARIANT / SD_OPT_GL4_TILE):
  * gl_variant 0 = auto (v4 split-f16 where available, else exact-f32 v3/v2/v5), 1..3 = exact-f32
  * generations, 4 = v4, 5 = v5; gl4_tile = <waves><row tiles><col tiles> (e.g. 822) or 0 = auto,
  * -1 leaves it.  Returns the previous gl_variant, or -1 for an invalid one (nothing changed);
  * gl_variant = -1 only queries (returns the current value). */
-int sd_set_kernel_variant(int32_t gl_variant, int32_t gl4_tile);
+int sd_test_set_kernel_variant(int32_t gl_variant, int32_t gl4_tile);
 
 /* Per-plan kernel options (read by the launches recorded after the call; part of the graph
- * cache key).  A plan starts from the process defaults (sd_set_kernel_variant,
- * sd_set_row_chains, SKELDIFF_* environment at load); two plans may hold different options and
- * sample concurrently.  SD_E_INVALID for an unknown option or value. */
+ * cache key).  There is no process-wide kernel state: a plan starts from the SKELDIFF_*
+ * environment read at library load and keeps its own options, so two plans may hold different
+ * options and sample concurrently.  SD_E_INVALID for an unknown option or value. */
 enum {
     SD_OPT_KERNEL_VARIANT = 1,  /* 0 auto, 1..5 force a graph-linear generation */
     SD_OPT_GL4_TILE = 2,        /* v4 tile <waves><row tiles><col tiles>, 0 = per shape */
@@ -257,11 +265,17 @@ enum {
                                    32-row units, a ragged last unit counting; auto: 1 at <= 128
                                    rows, 2 at <= SKELDIFF_SPLIT_ROWS, else 3); 0 before the first
                                    call */
-    SD_OPT_LAST_ROUTE = 8       /* read-only: kernels the plan's last sd_sample_loop launched, bits
+    SD_OPT_LAST_ROUTE = 8,      /* read-only: kernels the plan's last sd_sample_loop launched, bits
                                    1 one-kernel k_gl4, 2 fused to_qkv + attention k_gl4, 4 k_gl4y
                                    GEMM phase, 8 k_gl4t GEMM phase, 16 split-route mixing /
                                    attention phase, 32 v5 mixing (J > 21), 64 exact-f32 kernels,
                                    128 separate k_attention */
+    SD_OPT_UPDATE_KERNEL = 9,   /* posterior update: 0 (default) the J x J projections on
+                                   v_mfma_f32_16x16x4_f32 where they apply (nonisotropic, J <= 64),
+                                   1 the element-per-thread forms; both give the same bits */
+    SD_OPT_V5_MIX = 10          /* J > 21 mixing pass (v5): 0 (default) G-hat mixing on
+                                   v_mfma_f32_16x16x4_f32 (k_gl5_mixm), 1 the VALU form (k_gl5_mix);
+                                   the same j-ordered fmaf chains */
 };
 int sd_plan_set_option(sd_plan* plan, int32_t option, int64_t value);
 int sd_plan_get_option(const sd_plan* plan, int32_t option, int64_t* value);
@@ -295,21 +309,6 @@ int sd_gru_decode(const sd_gru_decoder_desc* desc, const float* x, const float* 
 size_t sd_gru_encode_workspace_bytes(const sd_gru_decoder_desc* desc, int64_t rows, int32_t frames);
 int sd_gru_encode(const sd_gru_decoder_desc* desc, const float* x, int64_t rows, int32_t frames, float* z,
                   void* workspace, size_t workspace_bytes, void* stream);
-/* Process DEFAULT of the row chains of sd_sample_loop for plans created afterwards (a plan keeps
- * its own: SD_OPT_ROW_CHAINS; SKELDIFF_CHAINS at load, default 0 = auto): the batch is split into
- * n row ranges (multiples of 32 rows; fewer when the batch is small) whose
- * T-step chains run on forked streams and overlap on the GPU.  Rows are independent, so the
- * results do not depend on n.  Returns the previous n; n = -1 only queries; SD_E_INVALID
- * outside [0, 8]. */
-int sd_set_row_chains(int32_t n);
-/* Process-wide form of the posterior-update kernel (test hook, like sd_set_kernel_variant): 1
- * (default) the J x J projections on v_mfma_f32_16x16x4_f32 (J <= 32, nonisotropic), 0 the
- * element-per-thread forms; both give the same bits.  Returns the previous value; -1 queries. */
-int32_t sd_set_update_kernel(int32_t v);
-/* Process-wide form of the J > 21 mixing pass (v5, test hook): 1 (default) G-hat mixing on
- * v_mfma_f32_16x16x4_f32 with 8 rows per workgroup (k_gl5_mixm), 0 the per-column VALU form
- * (k_gl5_mix); the same j-ordered fmaf chains.  Returns the previous value; -1 queries. */
-int32_t sd_set_v5_mix(int32_t v);
 /* Arithmetic of the plan's graph-linear launches.  mode 0 (default):
  * f32-accurate -- 3 split f16 products per f32 product, within the f32-vs-f64 drift.  mode 1:
  * half -- one f16 product (x and W rounded to f16), f32 accumulate, f32 activations in HBM; the
@@ -381,15 +380,16 @@ int sd_rmsnorm_backward(const float* x, const float* g, const float* dnorm, cons
                         void* stream);
 /* Mahalanobis loss of NonisotropicGaussianDiffusion reduced per row (reference
  * nonisotropic.py:177-190 and base.py:297-298): model_out, target (rows, J, F), S =
- * mahalanobis_S_sqrt_recip (T, J, J), t (rows) int64 timesteps;
+ * mahalanobis_S_sqrt_recip (T, J, J), t (rows) int64 timesteps (a row whose t is outside [0, T) gets a NaN
+ * loss / gradient: no out-of-range table read);
  * loss[r] = mean_{i,f} |(S[t_r] D_r)[i][f]| (mse: squared), D = target - model_out when
  * pred_noise, else model_out - target.  The backward writes d model_out (rows, J, F) from dloss
  * (rows).  1 <= J <= 64, 1 <= F <= 256, f32. */
 int sd_mahalanobis_loss_forward(const float* model_out, const float* target, const float* S, const int64_t* t,
-                                int64_t rows, int32_t J, int32_t F, int32_t pred_noise, int32_t mse, float* loss,
+                                int32_t T, int64_t rows, int32_t J, int32_t F, int32_t pred_noise, int32_t mse, float* loss,
                                 void* stream);
 int sd_mahalanobis_loss_backward(const float* model_out, const float* target, const float* S, const int64_t* t,
-                                 const float* dloss, int64_t rows, int32_t J, int32_t F, int32_t pred_noise,
+                                 int32_t T, const float* dloss, int64_t rows, int32_t J, int32_t F, int32_t pred_noise,
                                  int32_t mse, float* dmodel_out, void* stream);
 
 #ifdef __cplusplus

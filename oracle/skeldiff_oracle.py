@@ -440,7 +440,9 @@ def philox_normal(seed: int, rows: np.ndarray, step: int, n_per_row: int) -> np.
       ctr = (quad index within the row, step, row_lo, row_hi), key = (seed_lo, seed_hi);
       u_i = ((x_i >> 8) + 0.5) * 2^-24 in (0,1);
       (z0, z1) = sqrt(-2 ln u0) * (cos 2pi u1, sin 2pi u1), (z2, z3) likewise from (u2, u3).
-    """
+    The transform is evaluated exactly (float64, then rounded); the device evaluates the same
+    formula on the hardware log2 / sqrt / sin / cos (sd_kernels.hip box_muller), within 2e-5 of
+    this (tests/test_gpu_parity.py::test_device_normals_match_oracle)."""
     assert n_per_row % 4 == 0
     rows = np.asarray(rows, dtype=np.uint64)
     nq = n_per_row // 4

@@ -21,16 +21,16 @@ SD_FLAG_DEVICE_NOISE = 4
 
 # every symbol include/skeldiff.h declares (checked by tests/test_abi.py)
 EXPORTED = (
-    "sd_abi_version", "sd_last_error", "sd_plan_create", "sd_plan_destroy", "sd_plan_num_tensors",
-    "sd_plan_tensor_name", "sd_plan_tensor_numel", "sd_plan_set_tensor", "sd_plan_finalize",
+    "sd_abi_version", "sd_last_error", "sd_build_info", "sd_plan_create", "sd_plan_destroy", "sd_plan_num_tensors",
+    "sd_plan_tensor_name", "sd_plan_tensor_numel", "sd_plan_dims", "sd_plan_set_tensor", "sd_plan_finalize",
     "sd_workspace_bytes", "sd_denoiser_forward", "sd_p_sample_update", "sd_sample_loop",
     "sd_noise_fill", "sd_philox_raw", "sd_plan_kernels_per_step", "sd_plan_step_flops", "sd_profile_step",
-    "sd_test_graph_linear", "sd_test_attention", "sd_set_kernel_variant", "sd_test_qkv_attention",
-    "sd_test_graph_linear_layout", "sd_pairwise_distances", "sd_ade_fde", "sd_set_row_chains",
+    "sd_test_graph_linear", "sd_test_attention", "sd_test_set_kernel_variant", "sd_test_qkv_attention",
+    "sd_test_graph_linear_layout", "sd_pairwise_distances", "sd_ade_fde",
     "sd_plan_set_precision", "sd_mm_ade_fde", "sd_gru_decode_workspace_bytes", "sd_gru_decode",
     "sd_gru_encode_workspace_bytes", "sd_gru_encode", "sd_gl_train_workspace_bytes", "sd_gl_train_forward",
     "sd_gl_train_backward", "sd_plan_set_option", "sd_plan_get_option", "sd_denoiser_trace",
-    "sd_workspace_status", "sd_set_update_kernel", "sd_set_v5_mix", "sd_attn_train_forward",
+    "sd_workspace_status", "sd_attn_train_forward",
     "sd_attn_train_backward", "sd_film_tanh_forward", "sd_film_tanh_backward", "sd_l1norm_rows_forward",
     "sd_l1norm_rows_backward", "sd_rmsnorm_workspace_bytes", "sd_rmsnorm_forward", "sd_rmsnorm_backward",
     "sd_mahalanobis_loss_forward", "sd_mahalanobis_loss_backward",
@@ -38,7 +38,7 @@ EXPORTED = (
 
 # sd_plan_set_option keys (include/skeldiff.h)
 (SD_OPT_KERNEL_VARIANT, SD_OPT_GL4_TILE, SD_OPT_ROW_CHAINS, SD_OPT_PRECISION, SD_OPT_GL4_STAGING,
- SD_OPT_SPLIT_ROUTE, SD_OPT_LAST_CHAINS, SD_OPT_LAST_ROUTE) = 1, 2, 3, 4, 5, 6, 7, 8
+ SD_OPT_SPLIT_ROUTE, SD_OPT_LAST_CHAINS, SD_OPT_LAST_ROUTE, SD_OPT_UPDATE_KERNEL, SD_OPT_V5_MIX) = range(1, 11)
 # SD_OPT_LAST_ROUTE bits (sd::RouteBits)
 ROUTE_BITS = {1: "k_gl4 one-kernel", 2: "k_gl4 fused to_qkv+attention", 4: "k_gl4y GEMM phase",
               8: "k_gl4t GEMM phase", 16: "k_gl4 MODE 2/3 mixing phase", 32: "v5 k_gl5 mixing", 64: "exact-f32 kernels",
@@ -89,6 +89,7 @@ def _declare(lib: ctypes.CDLL) -> None:
     sig = {
         "sd_abi_version": (i32, []),
         "sd_last_error": (ctypes.c_char_p, []),
+        "sd_build_info": (ctypes.c_char_p, []),
         "sd_plan_create": (ctypes.c_int, [ctypes.POINTER(vp), ctypes.POINTER(SDPlanDesc)]),
         "sd_plan_destroy": (None, [vp]),
         "sd_plan_num_tensors": (i32, [vp]),
@@ -97,6 +98,7 @@ def _declare(lib: ctypes.CDLL) -> None:
         "sd_plan_set_tensor": (ctypes.c_int, [vp, ctypes.c_char_p, vp, i64, vp]),
         "sd_plan_finalize": (ctypes.c_int, [vp, vp]),
         "sd_workspace_bytes": (sz, [vp, i64]),
+        "sd_plan_dims": (ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_int32)]),
         "sd_denoiser_forward": (ctypes.c_int, [vp, vp, vp, i64, i32, vp, i64, vp, sz, vp]),
         "sd_workspace_status": (ctypes.c_int, [vp, vp, sz, ctypes.POINTER(ctypes.c_uint32), vp]),
         "sd_denoiser_trace": (ctypes.c_int, [vp, vp, vp, i64, i32, vp, i64, vp, sz, ctypes.POINTER(vp), i32, vp]),
@@ -109,10 +111,7 @@ def _declare(lib: ctypes.CDLL) -> None:
         "sd_test_graph_linear": (ctypes.c_int, [vp, i32, i64, vp, i32, vp, vp, ctypes.POINTER(ctypes.c_int64), vp,
                                                 vp, i32, vp, vp, i64, i32, i32, i32, vp]),
         "sd_test_attention": (ctypes.c_int, [vp, vp, i64, i32, i32, i32, vp]),
-        "sd_set_kernel_variant": (ctypes.c_int, [i32, i32]),
-        "sd_set_row_chains": (ctypes.c_int, [i32]),
-        "sd_set_update_kernel": (ctypes.c_int, [i32]),
-        "sd_set_v5_mix": (ctypes.c_int, [i32]),
+        "sd_test_set_kernel_variant": (ctypes.c_int, [i32, i32]),
         "sd_plan_set_precision": (ctypes.c_int, [vp, i32]),
         "sd_plan_set_option": (ctypes.c_int, [vp, i32, i64]),
         "sd_plan_get_option": (ctypes.c_int, [vp, i32, ctypes.POINTER(ctypes.c_int64)]),
@@ -142,8 +141,8 @@ def _declare(lib: ctypes.CDLL) -> None:
         "sd_rmsnorm_forward": (ctypes.c_int, [vp, vp, vp, vp, i64, i32, ctypes.c_float, ctypes.c_float, vp]),
         "sd_rmsnorm_backward": (ctypes.c_int, [vp, vp, vp, vp, vp, vp, i64, i32, ctypes.c_float, ctypes.c_float, vp,
                                                sz, vp]),
-        "sd_mahalanobis_loss_forward": (ctypes.c_int, [vp, vp, vp, vp, i64, i32, i32, i32, i32, vp, vp]),
-        "sd_mahalanobis_loss_backward": (ctypes.c_int, [vp, vp, vp, vp, vp, i64, i32, i32, i32, i32, vp, vp]),
+        "sd_mahalanobis_loss_forward": (ctypes.c_int, [vp, vp, vp, vp, i32, i64, i32, i32, i32, i32, vp, vp]),
+        "sd_mahalanobis_loss_backward": (ctypes.c_int, [vp, vp, vp, vp, i32, vp, i64, i32, i32, i32, i32, vp, vp]),
         "sd_profile_step": (ctypes.c_int, [vp, vp, vp, i64, i32, i64, vp, sz, i32, ctypes.POINTER(ctypes.c_float),
                                            ctypes.POINTER(ctypes.c_int32), vp]),
     }
@@ -166,6 +165,12 @@ def lib() -> ctypes.CDLL:
                     "(hipcc --offload-arch=gfx950).  There is no CPU fallback for sampling.")
             handle = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
             _declare(handle)
+            info = handle.sd_build_info().decode()
+            # the product library is built without packed-FP32 instructions; a
+            # diagnostic build is loaded only when named explicitly through SKELDIFF_LIB
+            if info != "no-packed-fp32" and not os.environ.get("SKELDIFF_LIB"):
+                raise SkelDiffError(f"{LIB_PATH} was built as {info!r}, not the product build "
+                                    "(no-packed-fp32): rebuild it with skeletondiffusion_amd.build.build_library()")
             _lib = handle
     return _lib
 

@@ -297,9 +297,14 @@ class LatentDiffusion(nn.Module):
                                            seed=seed, row0=row0)
 
         res = run()
-        # the range guard reads the workspace status word (a host sync) only where a kernel can
-        # set it: the split-f16 graph-linear tiles (engine.range_guard = False skips it)
-        if self.engine.range_guard_needed() and self.engine.status(shape[0]) & _lib.SD_STATUS_F16_RANGE:
+        # the f16 range guard, only where a kernel can set it (the split-f16 graph-linear tiles):
+        # deferred by default (an async copy of the status word, read at a later call: sample()
+        # stays asynchronous); engine.range_guard = "sync" waits and re-runs a hit on exact f32
+        mode = self.engine.range_guard_mode()
+        if mode == "deferred":
+            self.engine.check_range_guard()
+            self.engine.defer_status(shape[0])
+        elif mode == "sync" and self.engine.status(shape[0]) & _lib.SD_STATUS_F16_RANGE:
             # an activation left the f16 range of the split-f16 kernels: the whole chain again on
             # the exact-f32 kernels (same seed / noise, so the same sample)
             warnings.warn("activation outside the f16 range of the split-f16 kernels: re-sampling with the "

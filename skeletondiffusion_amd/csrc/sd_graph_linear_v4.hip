@@ -1442,12 +1442,6 @@ static int g_gl4_stage = [] {
     return (v >= 0 && v <= 2) ? v : 0;
 }();
 int gl4_stage_default() { return g_gl4_stage; }
-int set_gl4_stage(int stage) {
-    if (stage < 0 || stage > 2) return -1;
-    const int old = g_gl4_stage;
-    g_gl4_stage = stage;
-    return old;
-}
 
 template <int J, int NW, int RT, int CT, int DBG = 0, int MODE = 0, int XP = 0, int PREC = 0, int STG = 0>
 static hipError_t gl4_launch_t(const GLArgs& a, bool rms, hipStream_t s);
@@ -1496,11 +1490,6 @@ static int g_gl4_cfg = [] {
     return e ? atoi(e) : 0;
 }();
 int gl4_tile_default() { return g_gl4_cfg; }
-int set_gl4_tile(int cfg) {
-    const int old = g_gl4_cfg;
-    g_gl4_cfg = cfg;
-    return old;
-}
 
 // ---- split route (small grids) -------------------------------------------------
 // A one-kernel launch is one workgroup's K-loop latency however few workgroups it has: at 50

@@ -332,8 +332,8 @@ __global__ __launch_bounds__(256) void k_gl5_mixm(const GLArgs p, const float* z
 }  // namespace
 
 // 1 (default): the mixing pass on k_gl5_mixm where it applies; 0: k_gl5_mix (SKELDIFF_V5_MIX at
-// load, sd_set_v5_mix)
-static int g_mix_mfma = [] {
+// load: a diagnostic default under the per-plan SD_OPT_V5_MIX, which selects k_gl5_mix when set)
+static const int g_mix_mfma = [] {
     const char* e = getenv("SKELDIFF_V5_MIX");
     return e ? std::min(std::max(atoi(e), 0), 2) : 1;  // 2: the two-deep register ring (A/B)
 }();
@@ -342,11 +342,6 @@ static int g_mix_rows = [] {
     const char* e = getenv("SKELDIFF_V5_ROWS");
     return (e && (atoi(e) == 16 || atoi(e) == 4)) ? atoi(e) : 8;
 }();
-int set_v5_mix(int v) {
-    const int old = g_mix_mfma;
-    if (v >= 0 && v <= 2) g_mix_mfma = v;
-    return old;
-}
 
 // The mixing pass alone (the training graph-linear, sd_train.hip): out[r, i, :] = sum_j M[i, j]
 // z[r, j, :] with M = G-hat (transpose 0) or G-hat^T (1), z and out (rows, J, N) row-major; the same
@@ -407,7 +402,7 @@ hipError_t launch_graph_linear_v5(const GLArgs& a, bool rms, hipStream_t s) {
     const int vec = ((uintptr_t)z & 15) == 0 && (a.N & 3) == 0 && (z_rs & 3) == 0;
     g_route_bits |= kRouteV5Mix;
     // the matrix-core mixing pass: 64-column blocks, 16-B z / residual / output pieces
-    const bool mfma = g_mix_mfma && vec && a.N % 64 == 0 && ((uintptr_t)a.out & 15) == 0 && (a.out_rs & 3) == 0 &&
+    const bool mfma = g_mix_mfma && !a.v5_valu && vec && a.N % 64 == 0 && ((uintptr_t)a.out & 15) == 0 && (a.out_rs & 3) == 0 &&
                       (!a.res || (((uintptr_t)a.res & 15) == 0 && (a.res_rs & 3) == 0)) && a.B / 8 < 0x7fffffff;
     if (mfma) {
         const dim3 blk(256);

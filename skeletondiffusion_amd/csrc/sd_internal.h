@@ -34,6 +34,9 @@ struct GLArgs {
     // v4 split route for small grids (phase 1 GEMM per (tile, node) into the zs scratch, phase 2
     // mixing epilogue; bitwise identical to the one-kernel route): 0 auto, 1 never, 2 always
     int split;
+    // v5 (J > 21) mixing pass (SD_OPT_V5_MIX): 0 the matrix-core form k_gl5_mixm, 1 the VALU form
+    // k_gl5_mix (the same j-ordered fmaf chains)
+    int v5_valu;
     int64_t route_rows;  // rows of the whole sampling call on this device (row chains: all chains); 0 = B
     const float* x2; int64_t x2_rs; int K2;               // optional second input (cat along K)
     const float* W;                                       // (types, N, K1+K2), K contiguous
@@ -114,6 +117,7 @@ struct UpdArgs {
     int64_t B; int J; int D;
     unsigned* dbg;  // SD_DEBUG_LDS builds only
     int x0_bf16, xt_bf16, out_bf16;  // bf16 latents (precision mode 2); out2 / records stay f32
+    int elementwise;  // SD_OPT_UPDATE_KERNEL: 0 k_update_mfma where it applies, 1 the element-per-thread forms
     // diagnostics only (sd_debug_update_dump): the J values of x0 (activation + clamp applied),
     // x_t and sigma eps each thread computed from, stored after its outputs; null = off
     float* dump_x0; float* dump_xt; float* dump_ev;
@@ -131,18 +135,13 @@ hipError_t launch_gemm_split(const GLArgs& a, bool rms, float* z, int64_t z_rs, 
 // process defaults that new plans (and the sd_test_* hooks) start from: SKELDIFF_GL_VARIANT
 // (0 auto, 1..5), SKELDIFF_GL4_CFG (<NW><RT><CT>, 0 auto), SKELDIFF_GL4_STAGE (0 / 1), read at load
 int graph_linear_variant();
-int set_graph_linear_variant(int v);  // returns the previous value, -1 if v is out of range
 int gl4_tile_default();
-int set_gl4_tile(int cfg);            // returns the previous value
 int gl4_stage_default();
 int64_t split_rows_default();         // SKELDIFF_SPLIT_ROWS: auto split route at or below this many rows
-int set_gl4_stage(int stage);         // returns the previous value, -1 if out of range
 hipError_t launch_attention(const AttnArgs& a, hipStream_t s);
 hipError_t launch_update(const UpdArgs& a, hipStream_t s);
-int set_update_kernel(int v);  // 1 k_update_mfma, 0 element-per-thread forms; returns the previous
-int set_v5_mix(int v);
 hipError_t launch_mix_mfma(const float* z, const float* G, float* out, int64_t rows, int J, int N, bool transpose,
-                           hipStream_t s);  // G-hat (or G-hat^T) mixing of (rows, J, N), v5's MFMA pass         // 1 k_gl5_mixm (matrix cores), 0 k_gl5_mix; returns the previous
+                           hipStream_t s);  // G-hat (or G-hat^T) mixing of (rows, J, N), v5's MFMA pass
 hipError_t launch_noise_fill(float* out, int64_t rows, int64_t n_per_row, uint64_t seed,
                              int64_t row0, int step, const uint64_t* rng_dev, hipStream_t s,
                              int64_t row_shift = 0,   // row_shift: added to row0 (either source)

@@ -212,13 +212,6 @@ static int g_gl_variant = [] {
 
 int graph_linear_variant() { return g_gl_variant; }
 
-int set_graph_linear_variant(int v) {
-    if (v < 0 || v > 5) return -1;
-    const int old = g_gl_variant;
-    g_gl_variant = v;
-    return old;
-}
-
 // 0 (default): v4 (f32-accurate split-f16 MFMA) where the plan prepared split weights and the
 // skeleton has an instantiation; otherwise the exact-f32 kernels per shape: v3 (node-split
 // waves, 32x32 f32 MFMA) for N < 512, where it measured 1.15-1.25x faster than v2; v2 with
@@ -398,7 +391,8 @@ hipError_t launch_attention(const AttnArgs& a, hipStream_t s) {
 // Counter-based noise: Philox4x32-10 (Salmon et al. SC'11) + Box-Muller.
 // ctr = (quad q within the row, step, row lo, row hi), key = (seed lo, seed hi);
 // u = ((x >> 8) + 0.5) * 2^-24; z = sqrt(-2 ln u0) * (cos, sin)(2 pi u1), (u2, u3) likewise.
-// Identical stream in oracle/skeldiff_oracle.py:philox_normal.
+// The same stream as oracle/skeldiff_oracle.py:philox_normal: the Philox words bit for bit, the
+// normals within the hardware transcendentals' error (box_muller).
 // =============================================================================================
 
 __device__ __forceinline__ uint4 philox(uint4 c, uint32_t k0, uint32_t k1) {
@@ -415,11 +409,15 @@ __device__ __forceinline__ uint4 philox(uint4 c, uint32_t k0, uint32_t k1) {
 
 __device__ __forceinline__ float u01(uint32_t x) { return ((float)(x >> 8) + 0.5f) * 5.9604644775390625e-8f; }
 
+// Box-Muller on the hardware transcendentals: v_log_f32 (log2), v_sqrt_f32, and v_sin_f32 /
+// v_cos_f32, whose argument is in revolutions (sin(2 pi x) for |x| <= 256), so 2 pi u1 is never
+// formed.  u0 >= 2^-25 keeps every operand a normal float.  Within ~1e-6 of the exact transform
+// (the oracle's float64 philox_normal; tests/test_gpu_parity.py holds the normals to 2e-5), at a
+// dozen instructions per pair instead of the libm logf / sincospif / sqrtf sequences.
 __device__ __forceinline__ floatx2 box_muller(uint32_t a, uint32_t b) {
-    const float rad = sqrtf(-2.0f * logf(u01(a)));
-    float sn, cs;
-    sincospif(2.0f * u01(b), &sn, &cs);
-    return floatx2{rad * cs, rad * sn};
+    const float rad = __builtin_amdgcn_sqrtf(-1.38629436111989061f * __builtin_amdgcn_logf(u01(a)));  // -2 ln 2 log2 u0
+    const float r1 = u01(b);
+    return floatx2{rad * __builtin_amdgcn_cosf(r1), rad * __builtin_amdgcn_sinf(r1)};
 }
 
 __device__ __forceinline__ uint4 philox_at(uint64_t seed, uint64_t row, int step, uint32_t quad) {
@@ -874,20 +872,11 @@ static int64_t g_update_rows = [] {
     return e ? (int64_t)atoll(e) : (int64_t)1024;
 }();
 
-// 1 (default): k_update_mfma where it applies; 0: the element-per-thread k_update / k_update_row
-// forms (SKELDIFF_UPDATE_KERNEL at load, sd_set_update_kernel)
-static int g_update_mfma = [] {
-    const char* e = getenv("SKELDIFF_UPDATE_KERNEL");
-    return e ? (atoi(e) != 0) : 1;
-}();
-int set_update_kernel(int v) {
-    const int old = g_update_mfma;
-    if (v == 0 || v == 1) g_update_mfma = v;
-    return old;
-}
-
 hipError_t launch_update(const UpdArgs& a, hipStream_t s) {
     if (a.B <= 0) return hipSuccess;
+    // k_update_mfma where it applies, unless the plan asks for the element-per-thread forms
+    // (SD_OPT_UPDATE_KERNEL; both give the same bits)
+    const bool g_update_mfma = !a.elementwise;
     // the wave's column tiles (all of them in flight): D / 16 tiles over 4 / R waves, at most 6
     const int Rm = a.B <= g_update_rows ? 1 : 4;
     if (g_update_mfma && !a.iso && a.J > 32 && a.J <= 64 && a.D % 16 == 0 && (a.D / 16 + 3) / 4 <= 2) {
@@ -902,7 +891,9 @@ hipError_t launch_update(const UpdArgs& a, hipStream_t s) {
         hipLaunchKernelGGL((k_update_mfma<64, 1, 2>), dim3((unsigned)a.B), dim3(256), lds, s, a);
         return hipGetLastError();
     }
-    if (g_update_mfma && !a.iso && a.J <= 32 && a.D % 16 == 0 && (a.D / 16 + 4 / Rm - 1) / (4 / Rm) <= 6) {
+    // the instantiations below cover MT column tiles per wave, cstep = 4 / R apart: R = 1 -> MT = 2
+    // (tiles w, w + 4: D <= 128), R = 4 -> MT = 6 (tiles 0..5: D <= 96); wider rows take the forms below
+    if (g_update_mfma && !a.iso && a.J <= 32 && a.D % 16 == 0 && a.D / 16 <= (Rm == 1 ? 8 : 6)) {
         // small batches: one row per workgroup (4 waves share its column tiles), else 4 rows
         const int R = Rm;
         const dim3 grid((unsigned)((a.B + R - 1) / R));

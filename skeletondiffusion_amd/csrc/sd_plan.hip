@@ -85,7 +85,7 @@ struct GraphKey {
     int32_t flags;
     int32_t chains;
     int32_t prec;
-    int32_t variant, gl4_cfg, gl4_stage, split;  // the plan's kernel options at capture time
+    int32_t variant, gl4_cfg, gl4_stage, split, upd_elem, v5_valu;  // the plan's kernel options at capture time
     void* stream;
     bool operator<(const GraphKey& o) const { return std::memcmp(this, &o, sizeof(GraphKey)) < 0; }
 };
@@ -96,7 +96,11 @@ struct GraphKey {
 // (an event recorded behind each launch: no device-wide drain, other streams are not waited for).
 struct GraphSet {
     std::vector<hipGraphExec_t> execs;
-    std::vector<hipEvent_t> done;  // one per exec, recorded on the exec's stream after each launch
+    // one per exec, recorded on the exec's stream after each launch; every launch first makes its
+    // stream wait for the previous launch's record (under `mu`), so the last record completing
+    // means every launch of the exec is done
+    std::vector<hipEvent_t> done;
+    std::mutex mu;
     unsigned route_bits = 0;       // sd::RouteBits the captured chains launch
     ~GraphSet() {
         for (auto e : done) {
@@ -137,7 +141,7 @@ UpdDump g_dump;
 // different chains then run concurrently, so one chain's idle CUs (a 200-workgroup graph linear
 // on 256 CUs, the last wave of a 800-workgroup attention launch) take the other chain's
 // workgroups instead of waiting for the next kernel boundary.
-static int g_chains = [] {
+static const int g_chains = [] {
     const char* e = getenv("SKELDIFF_CHAINS");
     const int v = e ? atoi(e) : 0;
     return (v >= 0 && v <= 8) ? v : 0;  // 0: per batch size (chain_count)
@@ -156,6 +160,8 @@ struct sd_plan {
     int prec = 0;          // sd_plan_set_precision: 0 f32-accurate, 1 half (f16 products)
     // kernel options (sd_plan_set_option), initialised from the process defaults at creation
     int variant = 0, gl4_cfg = 0, gl4_stage = 0, split = 0, chains = 0;
+    int upd_elem = 0;  // SD_OPT_UPDATE_KERNEL: 1 = the element-per-thread update forms
+    int v5_valu = 0;   // SD_OPT_V5_MIX: 1 = the VALU mixing pass of v5
     bool fuse_attention_now() const { return fuse_ok && (variant == 0 || variant == 4); }
     bool blocked_now() const { return blk_ok && fuse_attention_now() && prec != 2; }
     std::vector<void*> allocs;
@@ -317,6 +323,7 @@ sd::GLArgs gl_args(const sd_plan* p, const GL& g, const float* x1, int x1_div, c
     a.gl4_cfg = p->gl4_cfg;
     a.gl4_stage = p->gl4_stage;
     a.split = p->split;
+    a.v5_valu = p->v5_valu;
 #ifdef SD_DEBUG_LDS
     a.dbg = sd::debug_counters();
 #endif
@@ -553,6 +560,7 @@ int run_update(const sd_plan* p, const float* x0, const float* xt, const float* 
     u.B = rows;
     u.J = p->J;
     u.D = p->D;
+    u.elementwise = p->upd_elem;
 #ifdef SD_DEBUG_LDS
     u.dbg = sd::debug_counters();
 #endif
@@ -600,6 +608,11 @@ extern "C" {
 
 int32_t sd_abi_version(void) { return SD_ABI_VERSION; }
 
+#ifndef SD_BUILD_INFO
+#define SD_BUILD_INFO "unknown (built outside build.py)"
+#endif
+const char* sd_build_info(void) { return SD_BUILD_INFO; }
+
 // Diagnostics only (tools/hazard_snap.py; not in include/skeldiff.h): set (arena != null) or clear
 // the snapshot arena of run_denoiser / record_loop.  slot_floats per slot, the first y_floats of
 // it for the phase-1 scratch Y.  Not thread-safe; never used by the product path.
@@ -636,6 +649,10 @@ int sd_plan_create(sd_plan** out, const sd_plan_desc* desc) {
     p->gl4_cfg = sd::gl4_tile_default();
     p->gl4_stage = sd::gl4_stage_default();
     p->chains = g_chains;
+    {  // SKELDIFF_UPDATE_KERNEL=0 at load: new plans start on the element-per-thread update forms
+        const char* e = getenv("SKELDIFF_UPDATE_KERNEL");
+        p->upd_elem = (e && atoi(e) == 0) ? 1 : 0;
+    }
 #ifdef SD_DEBUG_LDS
     (void)sd::debug_counters();  // allocated here, never during a stream capture
 #endif
@@ -1145,6 +1162,8 @@ int sd_sample_loop(const sd_plan* p, const float* x_T, const float* x_cond, int6
     key.gl4_cfg = p->gl4_cfg;
     key.gl4_stage = p->gl4_stage;
     key.split = p->split;
+    key.upd_elem = p->upd_elem;
+    key.v5_valu = p->v5_valu;
     key.stream = stream;
     SD_HIP(sd::launch_set_rng(w.rng, seed, row0, s));
     std::shared_ptr<GraphSet> set;
@@ -1192,11 +1211,24 @@ int sd_sample_loop(const sd_plan* p, const float* x_T, const float* x_cond, int6
     }
     mp->last_route.store(set->route_bits);
     if ((rc = fork_chains(mp, s, nch, cs))) return rc;
-    for (int i = 0; i < nch; ++i) {
-        SD_HIP(hipGraphLaunch(set->execs[i], cs[i]));
-        SD_HIP(hipEventRecord(set->done[i], cs[i]));
+    {
+        std::lock_guard<std::mutex> g(set->mu);
+        for (int i = 0; i < nch; ++i) {
+            SD_HIP(hipStreamWaitEvent(cs[i], set->done[i], 0));  // the exec's previous launch (any stream)
+            SD_HIP(hipGraphLaunch(set->execs[i], cs[i]));
+            SD_HIP(hipEventRecord(set->done[i], cs[i]));
+        }
     }
     return join_chains(mp, s, nch, cs);
+}
+
+int sd_plan_dims(const sd_plan* p, int32_t* dims_out) {
+    if (!p || !dims_out) return fail(SD_E_INVALID, "null argument");
+    dims_out[0] = p->J;
+    dims_out[1] = p->D;
+    dims_out[2] = p->T;
+    dims_out[3] = p->C;
+    return SD_OK;
 }
 
 int sd_plan_step_flops(const sd_plan* p, int64_t rows, double* flops_out) {
@@ -1275,11 +1307,17 @@ int sd_mm_ade_fde(const float* pred, const float* gts, const int64_t* pair_seq, 
     return SD_OK;
 }
 
-int sd_set_kernel_variant(int32_t gl_variant, int32_t gl4_tile) {
-    if (gl_variant == -1) return sd::graph_linear_variant();  // query
-    const int old = sd::set_graph_linear_variant(gl_variant);
-    if (old < 0) return fail(SD_E_INVALID, "gl_variant out of range");
-    if (gl4_tile >= 0) (void)sd::set_gl4_tile(gl4_tile);
+// kernel generation / v4 tile of the sd_test_* hooks only (plans take theirs from SD_OPT_*)
+static int g_test_variant = -1, g_test_tile = -1;  // -1: the process defaults (SKELDIFF_* at load)
+static int test_variant() { return g_test_variant >= 0 ? g_test_variant : sd::graph_linear_variant(); }
+static int test_tile() { return g_test_tile >= 0 ? g_test_tile : sd::gl4_tile_default(); }
+
+int sd_test_set_kernel_variant(int32_t gl_variant, int32_t gl4_tile) {
+    if (gl_variant == -1) return test_variant();  // query
+    if (gl_variant < 0 || gl_variant > 5) return fail(SD_E_INVALID, "gl_variant out of range");
+    const int old = test_variant();
+    g_test_variant = gl_variant;
+    if (gl4_tile >= 0) g_test_tile = gl4_tile;
     return old;
 }
 
@@ -1314,6 +1352,15 @@ int sd_plan_set_option(sd_plan* p, int32_t option, int64_t value) {
                                           "or 4 (tiled phase 1 except to_qkv + attention)");
             p->split = (int)value;
             return SD_OK;
+        case SD_OPT_UPDATE_KERNEL:
+            if (value != 0 && value != 1)
+                return fail(SD_E_INVALID, "update kernel must be 0 (matrix cores where they apply) or 1 (element-per-thread)");
+            p->upd_elem = (int)value;
+            return SD_OK;
+        case SD_OPT_V5_MIX:
+            if (value != 0 && value != 1) return fail(SD_E_INVALID, "v5 mix must be 0 (matrix cores) or 1 (VALU)");
+            p->v5_valu = (int)value;
+            return SD_OK;
         default: return fail(SD_E_INVALID, "unknown option " + std::to_string(option));
     }
 }
@@ -1329,6 +1376,8 @@ int sd_plan_get_option(const sd_plan* p, int32_t option, int64_t* value) {
         case SD_OPT_SPLIT_ROUTE: *value = p->split; return SD_OK;
         case SD_OPT_LAST_CHAINS: *value = p->last_chains.load(); return SD_OK;
         case SD_OPT_LAST_ROUTE: *value = p->last_route.load(); return SD_OK;
+        case SD_OPT_UPDATE_KERNEL: *value = p->upd_elem; return SD_OK;
+        case SD_OPT_V5_MIX: *value = p->v5_valu; return SD_OK;
         default: return fail(SD_E_INVALID, "unknown option " + std::to_string(option));
     }
 }
@@ -1352,24 +1401,6 @@ int sd_plan_set_precision(sd_plan* p, int32_t mode) {
     }
     p->prec = mode;
     return SD_OK;
-}
-
-int32_t sd_set_update_kernel(int32_t v) {
-    if (v != -1 && v != 0 && v != 1) return fail(SD_E_INVALID, "update kernel must be 0 or 1 (-1 queries)");
-    return sd::set_update_kernel(v);
-}
-
-int32_t sd_set_v5_mix(int32_t v) {
-    if (v != -1 && v != 0 && v != 1) return fail(SD_E_INVALID, "v5 mixing form must be 0 or 1 (-1 queries)");
-    return sd::set_v5_mix(v);
-}
-
-int sd_set_row_chains(int32_t n) {
-    if (n == -1) return g_chains;
-    if (n < 0 || n > sd_plan::kMaxChains) return fail(SD_E_INVALID, "row chains must be in [0 (auto), 8]");
-    const int old = g_chains;
-    g_chains = n;
-    return old;
 }
 
 int sd_test_graph_linear(const float* x1, int32_t K1, int64_t x1_div, const float* x2, int32_t K2,
@@ -1425,8 +1456,8 @@ int sd_test_graph_linear_layout(const float* x1, int32_t K1, int64_t x1_div, con
     a.x2_blk = (layout >> 1) & 1;
     a.res_blk = (layout >> 2) & 1;
     a.out_blk = (layout >> 3) & 1;
-    a.variant = sd::graph_linear_variant();
-    a.gl4_cfg = sd::gl4_tile_default();
+    a.variant = test_variant();
+    a.gl4_cfg = test_tile();
     a.gl4_stage = sd::gl4_stage_default();
     sd::SplitW sw;
     if (a.variant == 0 || a.variant == 4) {
@@ -1477,8 +1508,8 @@ int sd_test_qkv_attention(const float* x, int32_t K, const float* W, const int64
     }
     a.attn_heads = heads;
     a.attn_scale = (float)std::pow(32.0, -0.5);
-    a.variant = sd::graph_linear_variant();
-    a.gl4_cfg = sd::gl4_tile_default();
+    a.variant = test_variant();
+    a.gl4_cfg = test_tile();
     a.gl4_stage = sd::gl4_stage_default();
     a.x1_blk = layout & 1;
     a.out_blk = (layout >> 3) & 1;

@@ -698,7 +698,7 @@ __global__ __launch_bounds__(256) void k_rmsnorm(const float* __restrict__ x, co
 //   dM = (l1: sign(M), mse: 2M) * (dloss[r] / (J F)),   d model_out = sgn S^T dM.
 template <bool BWD>
 __global__ __launch_bounds__(256) void k_mahalanobis(const float* __restrict__ mo, const float* __restrict__ tg,
-                                                     const float* __restrict__ S, const int64_t* __restrict__ t,
+                                                     const float* __restrict__ S, const int64_t* __restrict__ t, int T,
                                                      const float* __restrict__ dloss, float* __restrict__ out, int J,
                                                      int F, float sgn, int mse) {
     extern __shared__ __attribute__((aligned(16))) float sm[];
@@ -710,8 +710,12 @@ __global__ __launch_bounds__(256) void k_mahalanobis(const float* __restrict__ m
     float* red = sS + J * J;     // [256]
     const float* m = mo + r * JF;
     const float* tt = tg + r * JF;
-    const float* St = S + t[r] * (int64_t)J * J;
-    for (int e = threadIdx.x; e < JF; e += 256) sD[e] = sgn * (m[e] - tt[e]);
+    // a timestep outside [0, T) reads no table: its row's loss (or gradient) is NaN
+    const int64_t tr = t[r];
+    const bool tok = tr >= 0 && tr < T;
+    const float* St = S + (tok ? tr : 0) * (int64_t)J * J;
+    const float bad = tok ? 0.f : __builtin_nanf("");
+    for (int e = threadIdx.x; e < JF; e += 256) sD[e] = sgn * (m[e] - tt[e]) + bad;
     for (int e = threadIdx.x; e < J * J; e += 256) sS[e] = St[e];
     __syncthreads();
     float part = 0.f;
@@ -990,10 +994,10 @@ int sd_rmsnorm_backward(const float* x, const float* g, const float* dnorm, cons
 }
 
 int sd_mahalanobis_loss_forward(const float* model_out, const float* target, const float* S, const int64_t* t,
-                                int64_t rows, int32_t J, int32_t F, int32_t pred_noise, int32_t mse, float* loss,
+                                int32_t T, int64_t rows, int32_t J, int32_t F, int32_t pred_noise, int32_t mse, float* loss,
                                 void* stream) {
-    if (rows < 0 || J < 1 || J > 64 || F < 1 || F > 256)
-        return sd::set_error(SD_E_INVALID, "sd_mahalanobis_loss_forward: 1 <= J <= 64, 1 <= F <= 256");
+    if (rows < 0 || J < 1 || J > 64 || F < 1 || F > 256 || T < 1)
+        return sd::set_error(SD_E_INVALID, "sd_mahalanobis_loss_forward: 1 <= J <= 64, 1 <= F <= 256, T >= 1");
     if (rows == 0) return SD_OK;
     if (!model_out || !target || !S || !t || !loss)
         return sd::set_error(SD_E_INVALID, "sd_mahalanobis_loss_forward: null buffer");
@@ -1003,16 +1007,16 @@ int sd_mahalanobis_loss_forward(const float* model_out, const float* target, con
         TR_HIP(hipFuncSetAttribute((const void*)sd::k_mahalanobis<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                    (int)lds));
     hipLaunchKernelGGL(sd::k_mahalanobis<false>, dim3((unsigned)rows), dim3(256), lds, (hipStream_t)stream, model_out,
-                       target, S, t, (const float*)nullptr, loss, J, F, pred_noise ? -1.f : 1.f, mse);
+                       target, S, t, T, (const float*)nullptr, loss, J, F, pred_noise ? -1.f : 1.f, mse);
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? SD_OK : sd::set_error(SD_E_HIP, std::string("k_mahalanobis: ") + hipGetErrorString(e));
 }
 
 int sd_mahalanobis_loss_backward(const float* model_out, const float* target, const float* S, const int64_t* t,
-                                 const float* dloss, int64_t rows, int32_t J, int32_t F, int32_t pred_noise,
+                                 int32_t T, const float* dloss, int64_t rows, int32_t J, int32_t F, int32_t pred_noise,
                                  int32_t mse, float* dmodel_out, void* stream) {
-    if (rows < 0 || J < 1 || J > 64 || F < 1 || F > 256)
-        return sd::set_error(SD_E_INVALID, "sd_mahalanobis_loss_backward: 1 <= J <= 64, 1 <= F <= 256");
+    if (rows < 0 || J < 1 || J > 64 || F < 1 || F > 256 || T < 1)
+        return sd::set_error(SD_E_INVALID, "sd_mahalanobis_loss_backward: 1 <= J <= 64, 1 <= F <= 256, T >= 1");
     if (rows == 0) return SD_OK;
     if (!model_out || !target || !S || !t || !dloss || !dmodel_out)
         return sd::set_error(SD_E_INVALID, "sd_mahalanobis_loss_backward: null buffer");
@@ -1022,7 +1026,7 @@ int sd_mahalanobis_loss_backward(const float* model_out, const float* target, co
         TR_HIP(hipFuncSetAttribute((const void*)sd::k_mahalanobis<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                    (int)lds));
     hipLaunchKernelGGL(sd::k_mahalanobis<true>, dim3((unsigned)rows), dim3(256), lds, (hipStream_t)stream, model_out,
-                       target, S, t, dloss, dmodel_out, J, F, pred_noise ? -1.f : 1.f, mse);
+                       target, S, t, T, dloss, dmodel_out, J, F, pred_noise ? -1.f : 1.f, mse);
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? SD_OK : sd::set_error(SD_E_HIP, std::string("k_mahalanobis: ") + hipGetErrorString(e));
 }

@@ -11,11 +11,13 @@ from __future__ import annotations
 
 import ctypes
 import threading
+import warnings
 from typing import Optional, Tuple
 
 import torch
 
 from . import _lib
+from . import ops  # noqa: F401  (registers torch.ops.skeldiff.sample_loop)
 from ._lib import SkelDiffError, check, ptr
 
 
@@ -34,6 +36,7 @@ class SamplingEngine:
         self._graph = False
         self._precision = 0
         self._options = {}  # sd_plan_set_option values, re-applied when the plan is rebuilt
+        self._pending = []  # deferred range-guard reads: (pinned host word, event)
 
     # ---------------------------------------------------------------------------------------
     def __del__(self):
@@ -113,23 +116,68 @@ class SamplingEngine:
     OPTIONS = {"kernel_variant": _lib.SD_OPT_KERNEL_VARIANT, "gl4_tile": _lib.SD_OPT_GL4_TILE,
                "row_chains": _lib.SD_OPT_ROW_CHAINS, "gl4_staging": _lib.SD_OPT_GL4_STAGING,
                "split_route": _lib.SD_OPT_SPLIT_ROUTE, "last_chains": _lib.SD_OPT_LAST_CHAINS,
-               "last_route": _lib.SD_OPT_LAST_ROUTE}
+               "last_route": _lib.SD_OPT_LAST_ROUTE, "update_kernel": _lib.SD_OPT_UPDATE_KERNEL,
+               "v5_mix": _lib.SD_OPT_V5_MIX}
     READ_ONLY = ("last_chains", "last_route")
-    # sample(): check the f16 range guard after each call (a host sync on the workspace status
-    # word) where the plan's kernels can set it; False leaves the call asynchronous
-    range_guard = True
+    # sample()'s f16 range guard (SD_STATUS_F16_RANGE, set on the device by a split-f16 launch
+    # whose input reached |x| >= 65504):
+    #   "deferred" (default) -- the call stays asynchronous: the workspace status word is copied
+    #       to pinned host memory behind it on the same stream and read at the next sample() or
+    #       check_range_guard(); a hit warns that that call's latents are not f32-accurate;
+    #   "sync" -- wait for the status after each call and re-run a hit on the exact-f32 kernels;
+    #   "off" -- not checked.
+    range_guard = "deferred"
 
-    def range_guard_needed(self) -> bool:
-        """True when the plan's graph-linear kernels can raise SD_STATUS_F16_RANGE: the split-f16
-        tiles (kernel variant 0 / 4) in f32 or half precision; the exact-f32 kernels and the bf16
-        mode never do."""
-        return bool(self.range_guard) and self._precision != self.PRECISIONS["bf16"] and \
-            self._options.get("kernel_variant", 0) in (0, 4)
+    def range_guard_mode(self) -> str:
+        """"deferred" / "sync" / "off" where the plan's graph-linear kernels can raise
+        SD_STATUS_F16_RANGE (the split-f16 tiles, kernel variant 0 / 4, in f32 or half
+        precision); "off" for the exact-f32 kernels and the bf16 mode, which never do."""
+        mode = {True: "sync", False: "off", None: "off"}.get(self.range_guard, self.range_guard)
+        if mode not in ("deferred", "sync", "off"):
+            raise SkelDiffError(f"range_guard must be 'deferred', 'sync' or 'off', got {self.range_guard!r}")
+        if self._precision == self.PRECISIONS["bf16"] or self._options.get("kernel_variant", 0) not in (0, 4):
+            return "off"
+        return mode
+
+    def defer_status(self, rows: int) -> None:
+        """Queue an asynchronous copy of the `rows`-row workspace's status word (behind the work
+        already on torch's current stream) for check_range_guard()."""
+        ws, _ = self.workspace(rows)
+        host = torch.empty(1, dtype=torch.int32, pin_memory=True)
+        host.copy_(ws[32:36].view(torch.int32), non_blocking=True)  # sd_workspace_status's word
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream(self._device))
+        with self._ws_lock:
+            self._pending.append((host, ev))
+            del self._pending[:-64]  # bounded: the oldest unchecked calls are dropped
+
+    def check_range_guard(self, wait: bool = False) -> bool:
+        """Read the deferred status of earlier calls whose copies have landed (all of them, waiting,
+        when `wait`); warn and return True if any of them left the f16 range."""
+        with self._ws_lock:
+            pend, self._pending = self._pending, []
+        hit, keep = False, []
+        for host, ev in pend:
+            if wait:
+                ev.synchronize()
+            elif not ev.query():
+                keep.append((host, ev))
+                continue
+            hit = hit or bool(int(host.item()) & _lib.SD_STATUS_F16_RANGE)
+        if keep:
+            with self._ws_lock:
+                self._pending[:0] = keep
+        if hit:
+            warnings.warn("an earlier sample() call had activations outside the f16 range of the split-f16 kernels: "
+                          "its latents are not f32-accurate (set engine.range_guard = 'sync' to re-run such calls "
+                          "on the exact-f32 kernels, or kernel_variant=3)")
+        return hit
 
     def set_option(self, name: str, value: int) -> None:
         """Per-plan kernel option (sd_plan_set_option): "kernel_variant" (0 auto, 1..5),
         "gl4_tile" (<waves><row tiles><col tiles>, 0 auto), "row_chains" (1..8), "gl4_staging"
-        (0 LDS-DMA, 1 register-staged), "split_route" (0 auto, 1 never, 2 k_gl4y, 3 k_gl4t);
+        (0 LDS-DMA, 1 register-staged), "split_route" (0 auto, 1 never, 2 k_gl4y, 3 k_gl4t),
+        "update_kernel" (0 matrix cores, 1 element-per-thread), "v5_mix" (0 matrix cores, 1 VALU);
         get_option("last_chains") reads the row chains the last sample_loop ran.  Kept across plan rebuilds;
         other engines (plans) in the process are unaffected."""
         if name not in self.OPTIONS or name in self.READ_ONLY:
@@ -305,20 +353,11 @@ class SamplingEngine:
         noise_t = torch.empty((rows, tm1, J, D), device=dev) if rec_noise else None
         imgs = torch.empty((rows, tm1, J, D), device=dev) if rec_img else None
         start_out = torch.empty((rows, J, D), device=dev) if (start is None and keep_start) else None
-        ws, nb = self.workspace(rows)
-        args = (plan, ptr(start), ptr(xc), rep, ptr(samp), seed, int(row0), ptr(out), ptr(mean_t), ptr(noise_t),
-                ptr(imgs), ptr(start_out), rows, ptr(ws), nb, flags)
-        cur = torch.cuda.current_stream(dev)
-        if (flags & _lib.SD_FLAG_GRAPH) and cur.cuda_stream == 0:
-            # stream capture is not possible on the legacy default stream: run on a side stream
-            if getattr(self, "_side", None) is None:
-                self._side = torch.cuda.Stream(dev)
-            self._side.wait_stream(cur)
-            with torch.cuda.stream(self._side):
-                check(_lib.lib().sd_sample_loop(*args, self._side.cuda_stream))
-            cur.wait_stream(self._side)
-        else:
-            check(_lib.lib().sd_sample_loop(*args, cur.cuda_stream))
+        ws, _ = self.workspace(rows)
+        # through the torch.library op skeldiff::sample_loop (ops.py): shape / dtype / device
+        # validation against the plan, then sd_sample_loop on torch's current stream
+        torch.ops.skeldiff.sample_loop(plan.value, xc, rep, start, samp, seed, int(row0), out, noise_t, mean_t, imgs,
+                                       start_out, ws, flags)
         start_ret = start.clone() if start is not None else start_out
         return out, start_ret, noise_t, mean_t, imgs
 

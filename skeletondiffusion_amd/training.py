@@ -304,7 +304,7 @@ class MahalanobisLossFunction(torch.autograd.Function):
         tc = t.to(device=mo.device, dtype=torch.int64).contiguous()
         loss = torch.empty(rows, device=mo.device, dtype=torch.float32)
         _lib.check(_lib.lib().sd_mahalanobis_loss_forward(mo.data_ptr(), tg.data_ptr(), Sc.data_ptr(), tc.data_ptr(),
-                                                           rows, J, F, int(pred_noise), int(mse), loss.data_ptr(),
+                                                           Sc.shape[0], rows, J, F, int(pred_noise), int(mse), loss.data_ptr(),
                                                            _stream(mo.device)))
         ctx.save_for_backward(mo, tg, Sc, tc)
         ctx.flags = (int(pred_noise), int(mse))
@@ -318,7 +318,7 @@ class MahalanobisLossFunction(torch.autograd.Function):
         dl = dloss.contiguous().float()
         dmo = torch.empty_like(mo)
         _lib.check(_lib.lib().sd_mahalanobis_loss_backward(mo.data_ptr(), tg.data_ptr(), Sc.data_ptr(), tc.data_ptr(),
-                                                            dl.data_ptr(), rows, J, F, pred_noise, mse, dmo.data_ptr(),
+                                                            Sc.shape[0], dl.data_ptr(), rows, J, F, pred_noise, mse, dmo.data_ptr(),
                                                             _stream(mo.device)))
         need_mo, need_tg = ctx.needs_input_grad[0], ctx.needs_input_grad[1]
         return (dmo if need_mo else None), (-dmo if need_tg else None), None, None, None, None

@@ -14,9 +14,13 @@ WEIGHT_SEED = 1234  # tests/golden/gen_golden.py
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (gfx950) HIP device; run with -m gpu")
+    config.addinivalue_line("markers", "config_parity: the per-BASELINE-config parity tests (configs 1-5), "
+                                       "collected first so that a -x stop elsewhere cannot hide them")
 
 
 def pytest_collection_modifyitems(config, items):
+    # the five per-config parity tests first (stable: file and definition order otherwise kept)
+    items.sort(key=lambda it: 0 if "config_parity" in it.keywords else 1)
     if torch.cuda.is_available():
         return
     skip = pytest.mark.skip(reason="no HIP device in this container (GPU tests run on the MI355X box)")

@@ -50,6 +50,7 @@ def _device_normals(seed, rows, step, J, D):
     return torch.from_numpy(O.philox_normal(seed, np.asarray(rows), step, J * D).reshape(len(rows), J, D))
 
 
+@pytest.mark.config_parity
 def test_config4_t1000_graph_first_and_last_steps(cuda):
     """BASELINE config 4: H36M J=16, 1 sequence x 50 futures, T=1000, hipGraph-captured chain."""
     from bench import build_config
@@ -92,6 +93,7 @@ def test_config4_t1000_graph_first_and_last_steps(cuda):
         assert _max_err(ref, x) < TOL, (t, _max_err(ref, x))
 
 
+@pytest.mark.config_parity
 def test_config2_as_benched(cuda):
     """BASELINE config 2 with the bench's exact launch configuration: default plan options (the
     tiled split route, k_gl4t + k_gl4 MODE 2 / 3, on 3 row chains whose kernels share CUs),
@@ -426,6 +428,7 @@ def test_f16_range_guard_falls_back_to_exact_f32(cuda):
     result equals an exact-f32 plan's."""
     z = golden("release_h36m16_T10")
     d = build_release_diffusion(z, cuda)
+    d.engine.range_guard = "sync"  # opt-in: wait for the status after each call, re-run a hit
     xcs, fu, start, samp = release_inputs(z)
     kw = dict(batch_size=start.shape[0], start_noise=start.to(cuda), sampling_noise=samp.to(cuda))
     d.sample(x_cond=xcs.to(cuda), **kw)
@@ -438,3 +441,27 @@ def test_f16_range_guard_falls_back_to_exact_f32(cuda):
     ref.engine.set_option("kernel_variant", 3)
     img_ref = ref.sample(x_cond=big, **kw)[0]
     assert torch.equal(img, img_ref)
+
+
+def test_f16_range_guard_deferred_by_default(cuda):
+    """The default sample() does not wait for the range guard: the status word is copied behind
+    the call and read later (check_range_guard / the next sample()); a hit warns that the earlier
+    call's latents are not f32-accurate, a clean call does not."""
+    import warnings
+
+    z = golden("release_h36m16_T10")
+    d = build_release_diffusion(z, cuda)
+    assert d.engine.range_guard_mode() == "deferred"
+    xcs, fu, start, samp = release_inputs(z)
+    kw = dict(batch_size=start.shape[0], start_noise=start.to(cuda), sampling_noise=samp.to(cuda))
+    d.sample(x_cond=xcs.to(cuda), **kw)
+    with warnings.catch_warnings():
+        warnings.simplefilter("error")
+        assert d.engine.check_range_guard(wait=True) is False
+    d.sample(x_cond=xcs.to(cuda) * 1e5, **kw)
+    assert len(d.engine._pending) == 1  # queued, not yet read
+    with pytest.warns(UserWarning, match="f16 range"):
+        assert d.engine.check_range_guard(wait=True) is True
+    assert d.engine._pending == []
+    d.engine.set_option("kernel_variant", 3)  # the exact-f32 kernels never raise it
+    assert d.engine.range_guard_mode() == "off"

@@ -106,10 +106,10 @@ def kernel_variant():
     L = _lib.lib()
 
     def set_(v, tile=0):
-        assert L.sd_set_kernel_variant(v, tile) >= 0
+        assert L.sd_test_set_kernel_variant(v, tile) >= 0
 
     yield set_
-    L.sd_set_kernel_variant(0, 0)
+    L.sd_test_set_kernel_variant(0, 0)
 
 
 # every v4 tile instantiation for J=16 and the exact-f32 generations on the release shapes
@@ -132,8 +132,8 @@ def test_graph_linear_v5(case, kernel_variant, cuda):
 
 def test_kernel_variant_rejects_bad_value():
     L = _lib.lib()
-    assert L.sd_set_kernel_variant(9, -1) < 0
-    assert L.sd_set_kernel_variant(0, -1) == 0
+    assert L.sd_test_set_kernel_variant(9, -1) < 0
+    assert L.sd_test_set_kernel_variant(0, -1) == 0
 
 
 def _check_gl(J, nty, K1, K2, N, div, has_bias, has_film, act, has_res, rms, Bseq, cuda):

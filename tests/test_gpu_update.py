@@ -25,17 +25,47 @@ def test_update_mfma_bitwise_vs_elementwise(cfg, batch, prec, given, cuda):
     J = d.channels
     g = torch.Generator().manual_seed(11)
     samp = torch.randn((rows, 9, J, 96), generator=g).to(cuda) if given else None
-    L = _lib.lib()
     res = {}
-    try:
-        for v in (0, 1):
-            L.sd_set_update_kernel(v)
-            a = eng.sample_loop(rows, x_cond=x_cond, seed=4, sampling_noise=samp, record=(True, False), graph=False)
-            b = eng.sample_loop(rows, x_cond=x_cond, seed=4, sampling_noise=samp, record=(False, True), graph=False)
-            torch.cuda.synchronize()
-            res[v] = [t.clone() for t in (a[0], a[1], a[2], a[3], b[4])]  # img, start, noise_t, mean_t, imgs
-    finally:
-        L.sd_set_update_kernel(1)
+    for v in (1, 0):  # SD_OPT_UPDATE_KERNEL: 1 the element-per-thread forms, 0 (default) k_update_mfma
+        eng.set_option("update_kernel", v)
+        a = eng.sample_loop(rows, x_cond=x_cond, seed=4, sampling_noise=samp, record=(True, False), graph=False)
+        b = eng.sample_loop(rows, x_cond=x_cond, seed=4, sampling_noise=samp, record=(False, True), graph=False)
+        torch.cuda.synchronize()
+        res[v] = [t.clone() for t in (a[0], a[1], a[2], a[3], b[4])]  # img, start, noise_t, mean_t, imgs
     for name, x, y in zip(("img", "start", "noise_t", "mean_t", "imgs"), res[0], res[1]):
         assert torch.equal(x, y), (name, float((x - y).abs().max()))
-    assert L.sd_set_update_kernel(-1) == 1 and L.sd_set_update_kernel(2) < 0
+    assert eng.get_option("update_kernel") == 0
+    with pytest.raises(_lib.SkelDiffError):
+        eng.set_option("update_kernel", 2)
+
+
+@pytest.mark.parametrize("dim,batch", [(192, 5), (192, 40), (160, 3), (256, 2)])
+def test_update_mfma_wide_latents(dim, batch, cuda):
+    """Latent widths beyond the 96 of the release configs (check_dims admits any multiple of 16):
+    the matrix-core update covers at most 8 column tiles per row at one row per workgroup and 6 at
+    four, so D = 160 / 192 / 256 must take a form that writes every column (advisor finding, round
+    3) -- bitwise equal to the element-per-thread forms, with every column finite and written."""
+    from conftest import pinned_cov
+    from skeletondiffusion_amd import synthetic
+    from skeletondiffusion_amd.core.diffusion import NonisotropicGaussianDiffusion
+    from skeletondiffusion_amd.core.network import Denoiser
+
+    J, T = 16, 4
+    m = Denoiser(dim=dim, cond_dim=0, out_dim=dim, channels=J, num_nodes=J, depth=1, attn_heads=2,
+                 attn_dim_head=32, learn_influence=True)
+    synthetic.fill_module_(m, 77)
+    S, L, U = pinned_cov(J)
+    d = NonisotropicGaussianDiffusion(Sigma_N=S, Lambda_N=L, U=U, model=m, latent_size=dim, diffusion_timesteps=T,
+                                      diffusion_objective="pred_x0", beta_schedule="cosine").to(cuda).eval()
+    eng = d.engine
+    rows = batch * 3
+    res = {}
+    for v in (1, 0):
+        eng.set_option("update_kernel", v)
+        sentinel = torch.full((rows, J, dim), float("nan"), device=cuda)
+        a = eng.sample_loop(rows, seed=9, record=(True, False), graph=False, out=sentinel)
+        torch.cuda.synchronize()
+        res[v] = [t.clone() for t in (a[0], a[2], a[3])]  # img, noise_t, mean_t
+        assert torch.isfinite(res[v][0]).all() and torch.isfinite(res[v][2]).all(), v
+    for name, x, y in zip(("img", "noise_t", "mean_t"), res[0], res[1]):
+        assert torch.equal(x, y), (name, float((x - y).abs().max()))

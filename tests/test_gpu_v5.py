@@ -17,16 +17,14 @@ def test_v5_mix_mfma_bitwise_vs_valu(cfg, batch, cuda):
 
     d, x_cond, rows = build_config(cfg, cuda, T=10, batch=batch)
     eng = d.engine
-    L = _lib.lib()
     res = {}
-    try:
-        for v in (0, 1):
-            L.sd_set_v5_mix(v)
-            a = eng.sample_loop(rows, x_cond=x_cond, seed=5, record=(True, False), graph=False)
-            torch.cuda.synchronize()
-            res[v] = [t.clone() for t in (a[0], a[3])]  # img, mean_t
-    finally:
-        L.sd_set_v5_mix(1)
+    for v in (1, 0):  # SD_OPT_V5_MIX: 1 the VALU form, 0 (default) the matrix cores
+        eng.set_option("v5_mix", v)
+        a = eng.sample_loop(rows, x_cond=x_cond, seed=5, record=(True, False), graph=False)
+        torch.cuda.synchronize()
+        res[v] = [t.clone() for t in (a[0], a[3])]  # img, mean_t
     for name, x, y in zip(("img", "mean_t"), res[0], res[1]):
         assert torch.equal(x, y), (name, float((x - y).abs().max()))
-    assert L.sd_set_v5_mix(-1) == 1 and L.sd_set_v5_mix(2) < 0
+    assert eng.get_option("v5_mix") == 0
+    with pytest.raises(_lib.SkelDiffError):
+        eng.set_option("v5_mix", 2)

@@ -58,6 +58,7 @@ def test_precision_mode_validation(cuda):
     assert d.engine.precision == "f32"
 
 
+@pytest.mark.config_parity
 def test_bf16_mode_config5_quality_gate_vs_oracle(cuda):
     """BASELINE config 5 as stated: FreeMan J=17, bf16 latents + fp32 Sigma_N projection, one GPU's
     shard of the 11,015 x 50 test set (1,377 sequences x 50 futures = 68,850 rows), T = 10.  The

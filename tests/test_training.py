@@ -404,10 +404,11 @@ def test_new_training_abi_validation_on_host():
     assert L.sd_rmsnorm_forward(None, None, None, None, 0, 192, 1.0, 1e-12, None) == 0   # empty
     assert L.sd_rmsnorm_forward(None, None, None, None, 4, 192, 1.0, 1e-12, None) < 0    # null buffers
     assert L.sd_rmsnorm_backward(None, None, None, None, None, None, 4, 192, 1.0, 1e-12, None, 0, None) < 0
-    assert L.sd_mahalanobis_loss_forward(None, None, None, None, 4, 65, 96, 1, 0, None, None) < 0   # J > 64
-    assert L.sd_mahalanobis_loss_forward(None, None, None, None, 4, 16, 257, 1, 0, None, None) < 0  # F > 256
-    assert L.sd_mahalanobis_loss_forward(None, None, None, None, 0, 16, 96, 1, 0, None, None) == 0  # empty
-    assert L.sd_mahalanobis_loss_backward(None, None, None, None, None, 4, 16, 96, 1, 0, None, None) < 0
+    assert L.sd_mahalanobis_loss_forward(None, None, None, None, 10, 4, 65, 96, 1, 0, None, None) < 0   # J > 64
+    assert L.sd_mahalanobis_loss_forward(None, None, None, None, 10, 4, 16, 257, 1, 0, None, None) < 0  # F > 256
+    assert L.sd_mahalanobis_loss_forward(None, None, None, None, 0, 4, 16, 96, 1, 0, None, None) < 0    # T < 1
+    assert L.sd_mahalanobis_loss_forward(None, None, None, None, 10, 0, 16, 96, 1, 0, None, None) == 0  # empty
+    assert L.sd_mahalanobis_loss_backward(None, None, None, None, 10, None, 4, 16, 96, 1, 0, None, None) < 0
     with pytest.raises(ValueError):
         training.rmsnorm(torch.zeros(2, 16, 8), torch.ones(8), 8 ** 0.5)      # host tensor
     with pytest.raises(ValueError):
@@ -415,3 +416,21 @@ def test_new_training_abi_validation_on_host():
     with pytest.raises(ValueError):
         training.mahalanobis_loss(torch.zeros(2, 16, 96), torch.zeros(2, 16, 96), torch.zeros(3, 16, 16),
                                   torch.zeros(2, dtype=torch.long), True, False)
+
+
+@pytest.mark.gpu
+def test_mahalanobis_loss_out_of_range_timestep_is_nan():
+    """A timestep outside [0, T) reads no table row (advisor finding, round 3): that row's loss and
+    gradient are NaN, the other rows are unaffected."""
+    dev = torch.device("cuda:0")
+    g = torch.Generator().manual_seed(5)
+    T, J, F_ = 4, 16, 96
+    S = (torch.randn(T, J, J, generator=g) / J ** 0.5).to(dev)
+    mo = torch.randn(3, J, F_, generator=g).to(dev).requires_grad_(True)
+    tg = torch.randn(3, J, F_, generator=g).to(dev)
+    t = torch.tensor([1, T, -1], device=dev)
+    loss = training.mahalanobis_loss(mo, tg, S, t, True, False)
+    loss.sum().backward()
+    torch.cuda.synchronize()
+    assert torch.isfinite(loss[0]) and torch.isnan(loss[1]) and torch.isnan(loss[2])
+    assert torch.isfinite(mo.grad[0]).all() and torch.isnan(mo.grad[1]).all() and torch.isnan(mo.grad[2]).all()
