@@ -206,6 +206,27 @@ int sd_mm_ade_fde(const float* pred, const float* gts, const int64_t* pair_seq, 
                   const int64_t* seq_offsets, int64_t nseq, int32_t samples, int32_t frames, int64_t features,
                   float* pair_ade, float* pair_fde, float* mmade, float* mmfde, void* stream);
 
+/* Best-of-k training relaxation (reference src/core/trainer.py:182-222,
+ * Trainer.loss -> to_comparison_space_train -> get_ksimilarity_loss with train_pick_best_sample_among_k
+ * = k): the diffusion loss of nseq sequences x k samples (nseq, k) (p_losses with n_train_samples = k,
+ * base.py:262-300) and a similarity (nseq, k) -- the loss itself in the latent space (sim = NULL),
+ * sd_pose_loss of the decoded samples in the input space, the per-sample ADE (sd_ade_fde
+ * per_sample_ade) in the metric space.
+ * sd_best_of_k: idx_out (nseq) int64 = per sequence the index of the smallest similarity
+ *   (torch.min(dim).indices: the first minimum; the first NaN if any), loss_out (nseq) = the loss at
+ *   that index (torch.gather).  Either output may be NULL.
+ * sd_best_of_k_backward: dloss (nseq, k) = dloss_sel at the selected index, 0 elsewhere.
+ * sd_pose_loss: AutoEncoder.loss(pred, y, reduction='none') (src/core/network/nn/autoencoder.py:80-98)
+ *   per sample: mean over frames and joints of the sum over coordinates of |d| (mse = 0) or d^2 (mse
+ *   = 1); pred (nseq, samples, frames, joints, dims), target (nseq, frames, joints, dims) ->
+ *   per_sample (nseq, samples). */
+int sd_best_of_k(const float* sim, const float* loss, int64_t nseq, int32_t k, int64_t* idx_out, float* loss_out,
+                 void* stream);
+int sd_best_of_k_backward(const float* dloss_sel, const int64_t* idx, int64_t nseq, int32_t k, float* dloss,
+                          void* stream);
+int sd_pose_loss(const float* pred, const float* target, int64_t nseq, int32_t samples, int32_t frames,
+                 int32_t joints, int32_t dims, int32_t mse, float* per_sample, void* stream);
+
 /* Test hooks: one kernel on caller buffers, for the per-kernel numerics tests.
  * sd_test_graph_linear: out(B,J,N) = act(FiLM(ghat @ (s_j W[type j] [x1_j | x2_j] + bias[type j]))) + res,
  *   W (types,N,K1+K2), bias (types,N) or NULL, ghat (J,J), film (2N) or NULL, res (B,J,N) or NULL,

@@ -669,3 +669,26 @@ def gru_encode(sd, node_types, x, prefix="encoder."):
 
 
 __all__ += ["metric_lat_apd", "metric_apd", "metric_ade", "metric_mmade", "gru_decode", "gru_encode"]
+
+
+# ---- best-of-k training relaxation ---------------------------------------------
+
+def pose_loss(pred: torch.Tensor, target: torch.Tensor, mse: bool) -> torch.Tensor:
+    """AutoEncoder.loss(pred, y, reduction='none') (src/core/network/nn/autoencoder.py:80-98):
+    |d| or d^2, summed over coordinates, mean over joints, mean over frames.  pred (b, k, T, J, C),
+    target (b, T, J, C) broadcast over the k samples -> (b, k)."""
+    d = pred - target.unsqueeze(1)
+    e = d * d if mse else d.abs()
+    return e.sum(-1).mean(-1).mean(-1)
+
+
+def best_of_k(loss: torch.Tensor, k: int, sim: Optional[torch.Tensor] = None):
+    """Trainer.get_ksimilarity_loss's selection (src/core/trainer.py:218-220): per sequence the
+    index of the smallest similarity (`min(axis=-1).indices`; the loss itself in latent_space) and
+    `torch.gather` of the loss there -> (selected (b,), idx (b,))."""
+    b = loss.numel() // k
+    s = (loss if sim is None else sim).detach().reshape(b, -1)
+    idx = s.min(dim=-1).indices
+    return torch.gather(loss.reshape(b, -1), dim=1, index=idx.unsqueeze(1)).squeeze(-1), idx
+
+__all__ += ["pose_loss", "best_of_k"]

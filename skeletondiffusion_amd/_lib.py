@@ -33,7 +33,8 @@ EXPORTED = (
     "sd_workspace_status", "sd_attn_train_forward",
     "sd_attn_train_backward", "sd_film_tanh_forward", "sd_film_tanh_backward", "sd_l1norm_rows_forward",
     "sd_l1norm_rows_backward", "sd_rmsnorm_workspace_bytes", "sd_rmsnorm_forward", "sd_rmsnorm_backward",
-    "sd_mahalanobis_loss_forward", "sd_mahalanobis_loss_backward",
+    "sd_mahalanobis_loss_forward", "sd_mahalanobis_loss_backward", "sd_best_of_k", "sd_best_of_k_backward",
+    "sd_pose_loss",
 )
 
 # sd_plan_set_option keys (include/skeldiff.h)
@@ -143,6 +144,9 @@ def _declare(lib: ctypes.CDLL) -> None:
                                                sz, vp]),
         "sd_mahalanobis_loss_forward": (ctypes.c_int, [vp, vp, vp, vp, i32, i64, i32, i32, i32, i32, vp, vp]),
         "sd_mahalanobis_loss_backward": (ctypes.c_int, [vp, vp, vp, vp, i32, vp, i64, i32, i32, i32, i32, vp, vp]),
+        "sd_best_of_k": (ctypes.c_int, [vp, vp, i64, i32, vp, vp, vp]),
+        "sd_best_of_k_backward": (ctypes.c_int, [vp, vp, i64, i32, vp, vp]),
+        "sd_pose_loss": (ctypes.c_int, [vp, vp, i64, i32, i32, i32, i32, i32, vp, vp]),
         "sd_profile_step": (ctypes.c_int, [vp, vp, vp, i64, i32, i64, vp, sz, i32, ctypes.POINTER(ctypes.c_float),
                                            ctypes.POINTER(ctypes.c_int32), vp]),
     }

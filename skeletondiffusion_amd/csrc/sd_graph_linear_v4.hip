@@ -339,14 +339,15 @@ __device__ unsigned long long g_gl4t_stamps[8192 * 4];
 __device__ unsigned long long g_gl4t_clock[8192 * 2];  // shader clock (s_memtime) at entry and loop end
 __device__ unsigned long long g_gl4t_chunk[8192 * 16];  // per workgroup: s_memrealtime after each chunk's barrier
 #endif
-template <bool RMS, int PREC, int CT, int NCH, bool ROWMAJOR, int PF = 4, int NWV = 4, bool WRES = false>
+template <bool RMS, int PREC, int CT, int NCH, bool ROWMAJOR, int PF = 2, int NWV = 4, bool WRES = false>
 __global__ __launch_bounds__(NWV * 64, WRES ? 1 : 2) void k_gl4t(const GLArgs p, int ncg, int64_t ntile_r, const YOut yo) {
     constexpr int NT = NWV * 64;
     constexpr int TILE_H = PREC ? 512 : 1024;   // halves of one 32-column tile per chunk
     constexpr int PPT = TILE_H / 8;             // 16-B pieces per tile
     constexpr int NP = (CT * PPT + NT - 1) / NT;  // staged pieces per thread
     constexpr int TS = 36;                      // floats per row of a wave's 32 x 32 output transpose
-    constexpr int SBW = (WRES ? NCH : 2) * CT * TILE_H * 2;
+    constexpr int NS = PF + 1;                  // LDS-DMA weight ring: chunk c in slot c % NS
+    constexpr int SBW = (WRES ? NCH : NS) * CT * TILE_H * 2;
     constexpr int SB = SBW > NWV * 32 * TS * 4 ? SBW : NWV * 32 * TS * 4;
     static_assert(!WRES || SB <= 160 * 1024, "resident weight slice exceeds the LDS");
     __shared__ __attribute__((aligned(16))) char smem_raw[SB];  // weight stages, then the transposes
@@ -384,33 +385,6 @@ __global__ __launch_bounds__(NWV * 64, WRES ? 1 : 2) void k_gl4t(const GLArgs p,
                                 : p.x1 + ((ac + p.x1_row0) / p.x1_div) * p.x1_rs + (int64_t)j * p.K1 + 8 * h;
     const float* x2r = !p.K2 ? nullptr
                              : p.x2_blk ? p.x2 + blk_off(arow, j, 8 * h, J, p.K2) : p.x2 + ac * p.x2_rs + (int64_t)j * p.K2 + 8 * h;
-    // staged pieces: piece q of a chunk = tile q / PPT, 16-B piece q % PPT of it
-    const _Float16* wsrc[NP];
-#pragma unroll
-    for (int k = 0; k < NP; ++k) {
-        const int q = min(tid + NT * k, CT * PPT - 1);
-        wsrc[k] = p.wsp + ((int64_t)p.ntype[j] * nchunk * p.wsp_nct + cg * CT + q / PPT) * 1024 + (q % PPT) * 8;
-    }
-    const int64_t wcs = (int64_t)p.wsp_nct * 1024;  // halves per chunk
-    // the carried pieces as named registers, loaded unconditionally from clamped sources (an
-    // array under conditional loads was placed in scratch, with a vmcnt(0) before every store)
-    static_assert(WRES || NP <= 4, "staged pieces per thread");
-    uint4 w0, w1, w2, w3;
-    auto load_w = [&](int c) {
-        const int64_t o = c * wcs;
-        w0 = *reinterpret_cast<const uint4*>(wsrc[0] + o);
-        if constexpr (NP > 1) w1 = *reinterpret_cast<const uint4*>(wsrc[1] + o);
-        if constexpr (NP > 2) w2 = *reinterpret_cast<const uint4*>(wsrc[2] + o);
-        if constexpr (NP > 3) w3 = *reinterpret_cast<const uint4*>(wsrc[3] + o);
-    };
-    auto store_w = [&](int sl) {
-        uint4* d = reinterpret_cast<uint4*>(&sW[sl][tid * 8]);
-        constexpr bool FULL = CT * PPT % NT == 0;
-        if (FULL || tid < CT * PPT) d[0] = w0;
-        if constexpr (NP > 1) if (FULL || tid + NT < CT * PPT) d[NT] = w1;
-        if constexpr (NP > 2) if (FULL || tid + 2 * NT < CT * PPT) d[2 * NT] = w2;
-        if constexpr (NP > 3) if (FULL || tid + 3 * NT < CT * PPT) d[3 * NT] = w3;
-    };
     floatx4 xa[PF], xb[PF];
     auto issue_x = [&](int c, int sl) {
         const int k0 = c << 4;
@@ -534,36 +508,72 @@ __global__ __launch_bounds__(NWV * 64, WRES ? 1 : 2) void k_gl4t(const GLArgs p,
             }
         }
     } else {
-    load_w(0);
+    // LDS-DMA weight ring (round 4; tools/gl4t_probe.hip): chunk c's weight slice goes straight
+    // to slot c % NS by global_load_lds_dwordx4 (no VGPRs, no ds_write), issued PF chunks ahead
+    // together with that chunk's x loads, so the loads of every chunk are issued in chunk order and
+    // waiting for chunk c (vmcnt = the ops of the PF - 1 younger chunks) never waits for a younger
+    // one.  (The register-staged form loaded w(c + 1) behind x(c + 1 .. c + 3), so every chunk's
+    // weight wait drained the x ring: 24.0 vs 19.0 us per N = 192 launch at 3,200 rows.)  The
+    // barrier after the wait publishes every wave's pieces of chunk c; slot (c + PF) % NS, refilled
+    // after it, was last read in chunk c - 1, which every wave finished before arriving.
+    // Pieces of wave w per chunk: q0 = 64 w + NT k < CT * PPT (two counts, wave-uniform).
+    constexpr int NPC = CT * PPT;
+    constexpr int XL = 2;  // x loads per chunk and lane
+    constexpr int OPA = (NPC / 64 + NWV - 1) / NWV + XL, OPB = (NPC / 64) / NWV + XL;
+    const bool wa = wave * 64 + NT * ((NPC / 64 + NWV - 1) / NWV - 1) < NPC;
+    const _Float16* wt0 = p.wsp + ((int64_t)p.ntype[j] * nchunk * p.wsp_nct + cg * CT) * 1024;
+    auto fill = [&](int c) {
+        _Float16* dst = sW[c % NS];
 #pragma unroll
-    for (int i = 0; i < PF; ++i)
-        if (i < nchunk) issue_x(i, i);
-    // chunk c: weights of c (loaded one chunk earlier, older than every x load in flight) ->
-    // stage c & 1 (free: every wave passed barrier c - 1 after its reads of chunk c - 2) ->
-    // lgkmcnt(0) + s_barrier (not __syncthreads(): its fence would drain the x loads in flight)
-    // -> weights of c + 1 to registers -> MFMAs on c -> x of c + PF into the freed ring slot
-    static_assert(NCH % PF == 0 && PF % 2 == 0, "ring slot and stage parity fixed per unrolled position");
+        for (int k = 0; k < (NPC / 64 + NWV - 1) / NWV; ++k) {
+            const int q0 = wave * 64 + NT * k;
+            if (q0 >= NPC) continue;  // wave-uniform
+            const int q = q0 + lane;
+            const _Float16* src = wt0 + ((int64_t)c * p.wsp_nct + q / PPT) * 1024 + (q % PPT) * 8;
+            __builtin_amdgcn_global_load_lds((const void*)src, (lds_void*)(dst + (size_t)q0 * 8), 16, 0, 0);
+        }
+    };
+    static_assert(PF >= 1 && PF <= 4 && OPA * (PF - 1) < 64, "vmcnt range");
+    auto wait_chunk = [&](int younger) {  // all but the ops of `younger` later chunks done (folds per unrolled step)
+#define SD_WAITN(n)                                                                     \
+    if (wa) __builtin_amdgcn_s_waitcnt(VmCnt4<OPA * (n)>::imm);                         \
+    else __builtin_amdgcn_s_waitcnt(VmCnt4<OPB * (n)>::imm);
+        if (younger == 0) { SD_WAITN(0) }
+        else if (younger == 1) { SD_WAITN(1) }
+        else if (younger == 2) { SD_WAITN(2 < PF ? 2 : 0) }
+        else { SD_WAITN(3 < PF ? 3 : 0) }
+#undef SD_WAITN
+        asm volatile("" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+    };
+    static_assert(NCH % PF == 0 && NCH >= 2 * PF, "ring positions fixed per unrolled step");
+#pragma unroll
+    for (int i = 0; i < PF; ++i) {
+        fill(i);
+        issue_x(i, i);
+    }
 #pragma nounroll
-    for (int c0 = 0; c0 < nchunk; c0 += PF) {
+    for (int c0 = 0; c0 < nchunk - PF; c0 += PF) {
 #pragma unroll
         for (int i = 0; i < PF; ++i) {
             const int c = c0 + i;
-            store_w(i & 1);
-            __builtin_amdgcn_s_waitcnt(0xC07F);
-            asm volatile("" ::: "memory");
-            __builtin_amdgcn_s_barrier();
-            asm volatile("" ::: "memory");
+            wait_chunk(PF - 1);
 #ifdef SD_GL4T_STAMPS
             if (STAMP && tid == 0 && blockIdx.x < 8192 && c < 16) g_gl4t_chunk[blockIdx.x * 16 + c] = wall_clock64();
 #endif
-            // unconditional loads (past the end: a clamped, unused chunk): a branch around them
-            // made the waitcnt pass merge both paths and drain the x ring every chunk
-            load_w(min(c + 1, nchunk - 1));
-            asm volatile("" ::: "memory");  // keep w(c + 1) older than x(c + PF): store_w(c + 1) waits for it alone
-            compute(c, i, sW[i & 1]);
+            compute(c, i, sW[c % NS]);
             asm volatile("" ::: "memory");
-            if constexpr (PF < NCH) issue_x(min(c + PF, nchunk - 1), i);
+            fill(c + PF);
+            issue_x(c + PF, i);
         }
+    }
+    // the last PF chunks: nothing more to issue, the wait shrinks by one chunk each step
+#pragma unroll
+    for (int i = 0; i < PF; ++i) {
+        wait_chunk(PF - 1 - i);
+        compute(nchunk - PF + i, i, sW[(nchunk - PF + i) % NS]);
+        asm volatile("" ::: "memory");
     }
     }  // staged K loop
     __syncthreads();  // every wave past its last chunk: the stages become the output transposes
@@ -1581,17 +1591,16 @@ hipError_t launch_gemm_split(const GLArgs& a, bool rms, float* z, int64_t z_rs, 
     return launch_gl4y<true>(a, rms, ntc, ntile_r, yo, s);
 }
 
-// k_gl4t's K = 192 form (SKELDIFF_GL4T_CFG, read at load): 0 = weights staged per chunk, x 4 chunks
-// ahead, 4 waves (two workgroups per CU); 1 = the same with every x chunk in flight from the
-// start; 2 / 3 = resident weights, every x chunk in flight, 4 / 8 waves; 4 = resident weights, x
-// 4 chunks ahead, 8 waves
+// k_gl4t's K = 192 form (SKELDIFF_GL4T_CFG, read at load): 0 = LDS-DMA weight ring, weights and x 2
+// chunks ahead, 4 waves (two workgroups per CU); 1 = the same 4 chunks ahead; 2 / 3 = resident
+// weights, every x chunk in flight, 4 / 8 waves; 4 = resident weights, x 4 chunks ahead, 8 waves
 static int g_gl4t_cfg = [] {
     const char* e = getenv("SKELDIFF_GL4T_CFG");
     const int v = e ? atoi(e) : 0;
     return (v >= 0 && v <= 4) ? v : 0;
 }();
 
-template <int CT, int NCH, bool ROWMAJOR, int NWV, bool WRES, int PF = 4>
+template <int CT, int NCH, bool ROWMAJOR, int NWV, bool WRES, int PF = 2>
 static hipError_t launch_gl4t_v(const GLArgs& a, bool rms, int64_t ntile_r, const YOut& yo, hipStream_t s) {
     const int ncg = a.N / (32 * CT);
     const dim3 grid((unsigned)(((ntile_r + NWV - 1) / NWV) * a.J * ncg)), block(NWV * 64);
@@ -1610,7 +1619,7 @@ template <int CT, int NCH, bool ROWMAJOR>
 static hipError_t launch_gl4t_ct(const GLArgs& a, bool rms, int64_t ntile_r, const YOut& yo, hipStream_t s) {
     if constexpr (NCH == 12) {
         switch (g_gl4t_cfg) {
-            case 1: return launch_gl4t_v<CT, NCH, ROWMAJOR, 4, false, 12>(a, rms, ntile_r, yo, s);
+            case 1: return launch_gl4t_v<CT, NCH, ROWMAJOR, 4, false, 4>(a, rms, ntile_r, yo, s);
             case 2: return launch_gl4t_v<CT, NCH, ROWMAJOR, 4, true, 12>(a, rms, ntile_r, yo, s);
             case 3: return launch_gl4t_v<CT, NCH, ROWMAJOR, 8, true, 12>(a, rms, ntile_r, yo, s);
             case 4: return launch_gl4t_v<CT, NCH, ROWMAJOR, 8, true, 4>(a, rms, ntile_r, yo, s);

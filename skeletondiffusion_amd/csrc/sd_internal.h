@@ -166,6 +166,13 @@ hipError_t launch_mm_ade_fde(const float* pred, const float* gts, const int64_t*
                              const int64_t* seq_off, int64_t nseq, int S, int T, int64_t F, float* pair_ade,
                              float* pair_fde, float* mmade, float* mmfde, hipStream_t s);
 
+// best-of-k training relaxation (sd_metrics.hip; trainer.py:182-222)
+hipError_t launch_best_of_k(const float* sim, const float* loss, int64_t nseq, int k, int64_t* idx, float* sel,
+                            hipStream_t s);
+hipError_t launch_best_of_k_bwd(const float* dsel, const int64_t* idx, int64_t nseq, int k, float* dloss, hipStream_t s);
+hipError_t launch_pose_loss(const float* pred, const float* target, int64_t nseq, int S, int T, int J, int C, int mse,
+                            float* out, hipStream_t s);
+
 // plan-finalize helpers (one-time)
 hipError_t launch_sinusoidal(float* emb, int T, int dim, float neg_scale, hipStream_t s);
 hipError_t launch_linear(const float* x, int M, int K, const float* W, const float* b, int N,

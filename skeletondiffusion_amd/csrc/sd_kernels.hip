@@ -409,15 +409,37 @@ __device__ __forceinline__ uint4 philox(uint4 c, uint32_t k0, uint32_t k1) {
 
 __device__ __forceinline__ float u01(uint32_t x) { return ((float)(x >> 8) + 0.5f) * 5.9604644775390625e-8f; }
 
-// Box-Muller on the hardware transcendentals: v_log_f32 (log2), v_sqrt_f32, and v_sin_f32 /
-// v_cos_f32, whose argument is in revolutions (sin(2 pi x) for |x| <= 256), so 2 pi u1 is never
-// formed.  u0 >= 2^-25 keeps every operand a normal float.  Within ~1e-6 of the exact transform
-// (the oracle's float64 philox_normal; tests/test_gpu_parity.py holds the normals to 2e-5), at a
-// dozen instructions per pair instead of the libm logf / sincospif / sqrtf sequences.
+// Box-Muller on the exact uniforms u = (2 m + 1) 2^-25, m = x >> 8 (the oracle's, in float64).  In
+// float32 u is exact below 1/2 only (above, the spacing is 2^-24), so ln u0 is taken as
+// logf(u0) for m < 2^23 and as log1pf(-v), v = 1 - u0 = (2^25 - 2 m - 1) 2^-25 (exact), above:
+// relative accuracy everywhere, including next to u0 = 1 where rad is small (float32 u0 and the
+// hardware v_log_f32 each moved z by up to ~5e-5 there).  (cos, sin)(2 pi u1) by an exact quadrant
+// reduction in integers: n = 2 m + 1, q = round(n / 2^23), theta = (n - q 2^23) 2 pi 2^-25 in
+// [-pi/4, pi/4], degree-9 / -8 Taylor polynomials (truncation < 3e-9) and the quadrant's rotation
+// (~20 VALU per pair, not sincospif's general range reduction).  Within a few ulp of the exact
+// transform; tests/test_gpu_parity.py holds 4.9 M normals to 2e-5 of the oracle.
 __device__ __forceinline__ floatx2 box_muller(uint32_t a, uint32_t b) {
-    const float rad = __builtin_amdgcn_sqrtf(-1.38629436111989061f * __builtin_amdgcn_logf(u01(a)));  // -2 ln 2 log2 u0
-    const float r1 = u01(b);
-    return floatx2{rad * __builtin_amdgcn_cosf(r1), rad * __builtin_amdgcn_sinf(r1)};
+    const uint32_t ma = a >> 8;
+    const float lnu = ma < (1u << 23) ? logf((float)(2u * ma + 1u) * 2.98023223876953125e-8f)
+                                      : log1pf(-(float)((1u << 25) - 2u * ma - 1u) * 2.98023223876953125e-8f);
+    const float rad = __builtin_amdgcn_sqrtf(-2.0f * lnu);
+    const int n = (int)(2u * (b >> 8) + 1u);      // u1 = n 2^-25
+    const int q = (n + (1 << 22)) >> 23;          // nearest quarter turn, 0 .. 4
+    const float th = (float)(n - (q << 23)) * 1.87253514863e-7f;  // 2 pi 2^-25
+    const float t2 = th * th;
+    float sn = fmaf(t2, 2.7557319e-6f, -1.9841270e-4f);      // 1/9!, -1/7!
+    sn = fmaf(t2, sn, 8.3333333e-3f);
+    sn = fmaf(t2, sn, -1.6666667e-1f);
+    sn = fmaf(t2 * th, sn, th);
+    float cs = fmaf(t2, 2.4801587e-5f, -1.3888889e-3f);      // 1/8!, -1/6!
+    cs = fmaf(t2, cs, 4.1666667e-2f);
+    cs = fmaf(t2, cs, -0.5f);
+    cs = fmaf(t2, cs, 1.0f);
+    const int qi = q & 3;
+    const float c2 = (qi & 1) ? sn : cs, s2 = (qi & 1) ? cs : sn;  // quarter turns: (c, s) -> (-s, c)
+    const float cv = (qi == 1 || qi == 2) ? -c2 : c2;
+    const float sv = (qi >= 2) ? -s2 : s2;
+    return floatx2{rad * cv, rad * sv};
 }
 
 __device__ __forceinline__ uint4 philox_at(uint64_t seed, uint64_t row, int step, uint32_t quad) {

@@ -154,7 +154,94 @@ __global__ __launch_bounds__(256) void k_segment_mean(const float* __restrict__ 
     out[i] = b > a ? acc / (float)(b - a) : __builtin_nanf("");
 }
 
+// ---- best-of-k training relaxation (reference trainer.py:207-222, get_ksimilarity_loss) ----------
+// Per sequence the index of the smallest similarity among its k samples -- torch.min(dim).indices:
+// the first minimum, and the first NaN if there is one (torch's min propagates NaN) -- and the
+// diffusion loss at that index (torch.gather).  sim == loss in the latent space.
+__global__ __launch_bounds__(256) void k_best_of_k(const float* __restrict__ sim, const float* __restrict__ loss,
+                                                   int64_t nseq, int k, int64_t* __restrict__ idx,
+                                                   float* __restrict__ sel) {
+    const int64_t b = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (b >= nseq) return;
+    const float* v = sim + b * k;
+    int best = 0;
+    float bv = v[0];
+    for (int j = 1; j < k; ++j) {
+        const float x = v[j];
+        if (bv != bv) break;                  // a NaN already selected: the first NaN wins
+        if (x != x || x < bv) {
+            best = j;
+            bv = x;
+        }
+    }
+    if (idx) idx[b] = best;
+    if (sel) sel[b] = loss[b * k + best];
+}
+
+// gradient of the gather: d loss[b, j] = d sel[b] at j = idx[b], else 0
+__global__ __launch_bounds__(256) void k_best_of_k_bwd(const float* __restrict__ dsel, const int64_t* __restrict__ idx,
+                                                       int64_t nseq, int k, float* __restrict__ dloss) {
+    const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (e >= nseq * k) return;
+    const int64_t b = e / k;
+    dloss[e] = (e - b * k == idx[b]) ? dsel[b] : 0.f;
+}
+
+// AutoEncoder.loss(pred, y, reduction='none') (reference autoencoder.py:80-98): per sample
+// mean over frames of the mean over joints of the sum over coordinates of |d| (l1) or d^2 (mse);
+// pred (nseq, S, T, J, C), target (nseq, T, J, C) (the future, not repeated).  One wave per
+// (sequence, sample); frame sums in frame order.
+__global__ __launch_bounds__(256) void k_pose_loss(const float* __restrict__ pred, const float* __restrict__ target,
+                                                   int64_t nseq, int S, int T, int J, int C, int mse,
+                                                   float* __restrict__ out) {
+    const int lane = threadIdx.x & 63;
+    const int64_t w = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (w >= nseq * S) return;  // wave-uniform
+    const int64_t b = w / S;
+    const int JC = J * C;
+    const float* p = pred + w * (int64_t)T * JC;
+    const float* tg = target + b * (int64_t)T * JC;
+    float acc = 0.f;
+    for (int t = 0; t < T; ++t) {
+        float fr = 0.f;  // sum over joints and coordinates of this frame
+        for (int e = lane; e < JC; e += 64) {
+            const float d = p[(int64_t)t * JC + e] - tg[(int64_t)t * JC + e];
+            fr += mse ? d * d : fabsf(d);
+        }
+        for (int o = 32; o > 0; o >>= 1) fr += __shfl_xor(fr, o);
+        acc += fr / (float)J;
+    }
+    if (lane == 0) out[w] = acc / (float)T;
+}
+
 }  // namespace
+
+hipError_t launch_best_of_k(const float* sim, const float* loss, int64_t nseq, int k, int64_t* idx, float* sel,
+                            hipStream_t s) {
+    if (nseq <= 0) return hipSuccess;
+    if (k < 1) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_best_of_k, dim3((unsigned)((nseq + 255) / 256)), dim3(256), 0, s, sim ? sim : loss, loss,
+                       nseq, k, idx, sel);
+    return hipGetLastError();
+}
+
+hipError_t launch_best_of_k_bwd(const float* dsel, const int64_t* idx, int64_t nseq, int k, float* dloss,
+                                hipStream_t s) {
+    const int64_t n = nseq * k;
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_best_of_k_bwd, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, dsel, idx, nseq, k, dloss);
+    return hipGetLastError();
+}
+
+hipError_t launch_pose_loss(const float* pred, const float* target, int64_t nseq, int S, int T, int J, int C, int mse,
+                            float* out, hipStream_t s) {
+    const int64_t waves = nseq * S;
+    if (waves <= 0) return hipSuccess;
+    if (T < 1 || J < 1 || C < 1) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_pose_loss, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, s, pred, target, nseq, S, T, J, C,
+                       mse, out);
+    return hipGetLastError();
+}
 
 hipError_t launch_pairwise(const float* x, int64_t nseq, int S, int64_t X, float* l1_mean, float* l2_mean,
                            hipStream_t s) {

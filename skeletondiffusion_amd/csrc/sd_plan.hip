@@ -1307,6 +1307,35 @@ int sd_mm_ade_fde(const float* pred, const float* gts, const int64_t* pair_seq, 
     return SD_OK;
 }
 
+int sd_best_of_k(const float* sim, const float* loss, int64_t nseq, int32_t k, int64_t* idx_out, float* loss_out,
+                 void* stream) {
+    if (nseq < 0 || k < 1) return fail(SD_E_INVALID, "best_of_k: nseq >= 0, k >= 1");
+    if (nseq == 0) return SD_OK;
+    if (!loss || (!idx_out && !loss_out)) return fail(SD_E_INVALID, "best_of_k: null buffer");
+    SD_HIP(sd::launch_best_of_k(sim, loss, nseq, k, idx_out, loss_out, (hipStream_t)stream));
+    return SD_OK;
+}
+
+int sd_best_of_k_backward(const float* dloss_sel, const int64_t* idx, int64_t nseq, int32_t k, float* dloss,
+                          void* stream) {
+    if (nseq < 0 || k < 1) return fail(SD_E_INVALID, "best_of_k_backward: nseq >= 0, k >= 1");
+    if (nseq == 0) return SD_OK;
+    if (!dloss_sel || !idx || !dloss) return fail(SD_E_INVALID, "best_of_k_backward: null buffer");
+    SD_HIP(sd::launch_best_of_k_bwd(dloss_sel, idx, nseq, k, dloss, (hipStream_t)stream));
+    return SD_OK;
+}
+
+int sd_pose_loss(const float* pred, const float* target, int64_t nseq, int32_t samples, int32_t frames,
+                 int32_t joints, int32_t dims, int32_t mse, float* per_sample, void* stream) {
+    if (nseq < 0 || samples < 1 || frames < 1 || joints < 1 || dims < 1)
+        return fail(SD_E_INVALID, "pose_loss: samples, frames, joints, dims >= 1");
+    if (nseq == 0) return SD_OK;
+    if (!pred || !target || !per_sample) return fail(SD_E_INVALID, "pose_loss: null buffer");
+    SD_HIP(sd::launch_pose_loss(pred, target, nseq, samples, frames, joints, dims, mse != 0, per_sample,
+                                (hipStream_t)stream));
+    return SD_OK;
+}
+
 // kernel generation / v4 tile of the sd_test_* hooks only (plans take theirs from SD_OPT_*)
 static int g_test_variant = -1, g_test_tile = -1;  // -1: the process defaults (SKELDIFF_* at load)
 static int test_variant() { return g_test_variant >= 0 ? g_test_variant : sd::graph_linear_variant(); }

@@ -332,3 +332,64 @@ def mahalanobis_loss(model_out: torch.Tensor, target: torch.Tensor, S: torch.Ten
             or model_out.shape[1] > MAX_NODES or model_out.shape[2] > 256 or S.dtype != torch.float32):
         raise ValueError("mahalanobis_loss: the HIP training path needs (rows, J <= 64, F <= 256) fp32 device tensors")
     return MahalanobisLossFunction.apply(model_out, target, S, t, pred_noise, mse)
+
+
+# ---- best-of-k training relaxation (reference src/core/trainer.py:182-222) -----
+
+class BestOfKFunction(torch.autograd.Function):
+    """Per sequence the sample whose similarity is smallest and the diffusion loss there:
+    `loss_similarity.view(b, -1).min(axis=-1).indices` + `torch.gather` of get_ksimilarity_loss
+    (trainer.py:207-222), forward and backward on HIP (`sd_best_of_k` / `_backward`).  The
+    similarity carries no gradient (the reference computes it under no_grad)."""
+
+    @staticmethod
+    def forward(ctx, loss, sim, k: int):
+        lv = loss.contiguous().view(-1)
+        nseq = lv.numel() // k
+        sv = None if sim is None else sim.detach().contiguous().float().view(-1)
+        idx = torch.empty(nseq, device=lv.device, dtype=torch.int64)
+        sel = torch.empty(nseq, device=lv.device, dtype=torch.float32)
+        _lib.check(_lib.lib().sd_best_of_k(None if sv is None else sv.data_ptr(), lv.data_ptr(), nseq, k,
+                                           idx.data_ptr(), sel.data_ptr(), _stream(lv.device)))
+        ctx.save_for_backward(idx)
+        ctx.k = k
+        ctx.mark_non_differentiable(idx)
+        return sel, idx
+
+    @staticmethod
+    def backward(ctx, dsel, _didx):
+        (idx,) = ctx.saved_tensors
+        k = ctx.k
+        nseq = idx.numel()
+        dl = torch.empty(nseq * k, device=idx.device, dtype=torch.float32)
+        ds = dsel.contiguous().float()
+        _lib.check(_lib.lib().sd_best_of_k_backward(ds.data_ptr(), idx.data_ptr(), nseq, k, dl.data_ptr(),
+                                                    _stream(idx.device)))
+        return dl, None, None
+
+
+def best_of_k(loss: torch.Tensor, k: int, sim: Optional[torch.Tensor] = None):
+    """(nseq * k,) per-sample diffusion losses (sequence-major: p_losses' repeat_interleave order,
+    base.py:264-268) -> (selected loss (nseq,), index (nseq,)): the sample with the smallest `sim`
+    (nseq * k values; default the loss itself: the latent space) per sequence, as
+    get_ksimilarity_loss (trainer.py:207-222)."""
+    if not loss.is_cuda or loss.dtype != torch.float32 or loss.numel() % k or k < 1:
+        raise ValueError("best_of_k: an fp32 device tensor of nseq * k losses is required")
+    if sim is not None and (sim.numel() != loss.numel() or sim.device != loss.device):
+        raise ValueError("best_of_k: sim must hold one value per loss, on the same device")
+    return BestOfKFunction.apply(loss, sim, int(k))
+
+
+def pose_loss(pred: torch.Tensor, target: torch.Tensor, mse: bool) -> torch.Tensor:
+    """AutoEncoder.loss(pred, target, reduction='none') (autoencoder.py:80-98) on HIP (`sd_pose_loss`),
+    no grad: pred (nseq, S, T, J, C), target (nseq, T, J, C) -> (nseq, S)."""
+    if not pred.is_cuda or pred.dim() != 5 or target.dim() != 4 or pred.shape[0] != target.shape[0] or \
+            tuple(pred.shape[2:]) != tuple(target.shape[1:]):
+        raise ValueError("pose_loss: pred (nseq, S, T, J, C) and target (nseq, T, J, C) device tensors")
+    nseq, S, T, J, C = pred.shape
+    p = pred.detach().contiguous().float()
+    tg = target.detach().contiguous().float()
+    out = torch.empty((nseq, S), device=pred.device, dtype=torch.float32)
+    _lib.check(_lib.lib().sd_pose_loss(p.data_ptr(), tg.data_ptr(), nseq, S, T, J, C, int(bool(mse)), out.data_ptr(),
+                                       _stream(pred.device)))
+    return out

@@ -384,7 +384,54 @@ def gen_decoder():
     _save("decoder", out=out, z_past=z_past, keys=np.array(sorted(m.state_dict().keys())))
 
 
+def gen_best_of_k():
+    """The best-of-k training relaxation with the reference's modules: the release
+    H36M Denoiser's p_losses with n_train_samples = k (base.py:262-300; fixed t and noise), the
+    reference AutoEncoder's decode of the k sampled x0 per sequence and AutoEncoder.loss(reduction=
+    'none') against the future (autoencoder.py:80-98) -- the input_space similarity of the release
+    configs -- and the selection of trainer.py:218-220 (`min(axis=-1).indices` + `torch.gather`,
+    restated: trainer.py imports ignite, absent here).  Also AutoEncoder.loss alone on random poses,
+    l1 and mse."""
+    from src.core.network.nn.autoencoder import AutoEncoder
+
+    _, _, node_types, diff = build_release("h36m16", 10)
+    ae = AutoEncoder(node_types=torch.as_tensor(node_types), **AE_KW).eval()
+    synthetic.fill_module_(ae, AE_SEED)
+    b, k, ph = 3, 4, 12
+    data = torch.from_numpy(synthetic.uniform((b, 16, 96), seed=61))
+    x_cond = torch.from_numpy(synthetic.uniform((b, 16, 96), seed=62))
+    t = torch.tensor([1, 5, 9])
+    noise = torch.from_numpy(synthetic.normal((b * k, 16, 96), seed=63))
+    past = torch.from_numpy(synthetic.normal((b, 30, 16, 3), seed=64)) * 0.3
+    loss, w, samples = diff.p_losses(data, t, noise=noise, x_cond=x_cond, n_train_samples=k)
+    with torch.no_grad():
+        xc = x_cond.repeat_interleave(k, dim=0)
+        out = ae.decode(past.repeat_interleave(k, dim=0), samples, xc, ph).view(b, k, ph, 16, 3)
+        # the future: a perturbed copy of one decoded sample per sequence (2, 0, 3), so the
+        # closest sample is decided by a margin well above the fp32 / HIP-decoder error
+        fut = out[torch.arange(b), torch.tensor([2, 0, 3])] + \
+            torch.from_numpy(synthetic.normal((b, ph, 16, 3), seed=65)) * 1e-4
+        sim = ae.loss(out, fut.unsqueeze(1).repeat_interleave(k, dim=1), reduction="none")
+        idx = sim.view(b, -1).min(axis=-1).indices
+        idx_latent = loss.detach().view(b, -1).min(axis=-1).indices
+    sel = torch.gather(loss.view(b, -1), dim=1, index=idx.unsqueeze(1)).squeeze(-1)
+    final = (sel * w).mean()
+    pred = torch.from_numpy(synthetic.normal((2, 5, 7, 21, 3), seed=66))
+    tgt = torch.from_numpy(synthetic.normal((2, 7, 21, 3), seed=67))
+    ns = types.SimpleNamespace
+    pl1 = AutoEncoder.loss(ns(loss_pose_type="l1"), pred, tgt.unsqueeze(1).repeat_interleave(5, dim=1), reduction="none")
+    pmse = AutoEncoder.loss(ns(loss_pose_type="mse"), pred, tgt.unsqueeze(1).repeat_interleave(5, dim=1),
+                            reduction="none")
+    _save("best_of_k", data=data, x_cond=x_cond, t=t, noise=noise, past=past, fut=fut, k=k, ph=ph,
+          loss=loss.detach(), weight=w, samples=samples.detach(), decoded=out, sim=sim, idx=idx,
+          idx_latent=idx_latent, sel=sel.detach(), final=final.detach(), pose_pred=pred, pose_target=tgt,
+          pose_l1=pl1, pose_mse=pmse)
+
+
 def main():
+    if sys.argv[1:] == ["best_of_k"]:
+        gen_best_of_k()
+        return
     if sys.argv[1:] == ["metrics"]:
         gen_metrics()
         return
@@ -412,6 +459,7 @@ def main():
     gen_new_r02()
     gen_hip_included()
     gen_new_r03()
+    gen_best_of_k()
 
 
 if __name__ == "__main__":
