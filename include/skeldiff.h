@@ -280,7 +280,9 @@ enum {
                                    (k_gl4y), 3 always with the tiled GEMM phase (k_gl4t: 128 rows
                                    x up to 192 columns of one node per workgroup), 4 the tiled
                                    GEMM phase except for to_qkv + attention (one-kernel fused
-                                   tile) */
+                                   tile), 5 the small-batch fused tile (one launch per plain
+                                   graph-linear, J = 16 f32 / half; auto at <= SKELDIFF_SMALL_ROWS
+                                   rows) with the k_gl4y split route for to_qkv + attention */
     SD_OPT_LAST_CHAINS = 7,     /* read-only: row chains the plan's last sd_sample_loop ran (the
                                    SD_OPT_ROW_CHAINS value, fewer for batches of fewer than n
                                    32-row units, a ragged last unit counting; auto: 1 at <= 128
@@ -290,7 +292,7 @@ enum {
                                    1 one-kernel k_gl4, 2 fused to_qkv + attention k_gl4, 4 k_gl4y
                                    GEMM phase, 8 k_gl4t GEMM phase, 16 split-route mixing /
                                    attention phase, 32 v5 mixing (J > 21), 64 exact-f32 kernels,
-                                   128 separate k_attention */
+                                   128 separate k_attention, 256 small-batch fused k_gl4 tile */
     SD_OPT_UPDATE_KERNEL = 9,   /* posterior update: 0 (default) the J x J projections on
                                    v_mfma_f32_16x16x4_f32 where they apply (nonisotropic, J <= 64),
                                    1 the element-per-thread forms; both give the same bits */

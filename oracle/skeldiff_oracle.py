@@ -436,13 +436,15 @@ def philox4x32_10(c0, c1, c2, c3, k0, k1):
 def philox_normal(seed: int, rows: np.ndarray, step: int, n_per_row: int) -> np.ndarray:
     """Normals for global rows `rows` at noise step `step`, `n_per_row` (multiple of 4) each.
 
-    Counter layout (mirrors skeletondiffusion_amd/csrc/sd_noise.hip):
+    Counter layout (mirrors skeletondiffusion_amd/csrc/sd_kernels.hip philox_at):
       ctr = (quad index within the row, step, row_lo, row_hi), key = (seed_lo, seed_hi);
-      u_i = ((x_i >> 8) + 0.5) * 2^-24 in (0,1);
+      u_i = ((x_i >> 8) + 0.5) * 2^-24 = (2 m + 1) 2^-25 in (0,1), m = x_i >> 8;
       (z0, z1) = sqrt(-2 ln u0) * (cos 2pi u1, sin 2pi u1), (z2, z3) likewise from (u2, u3).
-    The transform is evaluated exactly (float64, then rounded); the device evaluates the same
-    formula on the hardware log2 / sqrt / sin / cos (sd_kernels.hip box_muller), within 2e-5 of
-    this (tests/test_gpu_parity.py::test_device_normals_match_oracle)."""
+    The transform is evaluated exactly (float64, then rounded).  The device takes the same exact
+    uniforms in float32 arithmetic (sd_kernels.hip box_muller): ln u0 by the hardware log2 away
+    from 1 and a log1p polynomial of the exact u0 - 1 next to 1, (cos, sin) by an integer quadrant
+    reduction and Taylor polynomials; within 2e-5 of this
+    (tests/test_gpu_parity.py::test_device_normals_match_oracle)."""
     assert n_per_row % 4 == 0
     rows = np.asarray(rows, dtype=np.uint64)
     nq = n_per_row // 4

@@ -205,13 +205,20 @@ hipError_t make_split_weights(const float* W, int ntypes, int N, int K, SplitW* 
 // chunk), RMS sum, range guard and scale arithmetic as in k_gl4, so phase 2 (k_gl4 MODE 2 / 3)
 // reproduces the one-kernel results bit for bit.  Workgroup = 4 waves = 4 column tiles of one
 // (row tile, node): the x fragments are shared through L1.
-// Output: the split route's scratch p.zs as [tile][node][32 rows][N] (all 32 rows of a tile), or
-// (ROWMAJOR, v5 for J > 21) element (row 32 tr + r, node j, column n) at
-// y + tr y_ts + j y_js + r y_rs + n for rows < B only.
+// Output: element (row 32 tr + r, node j, column 32 t + c) at y + tr y_ts + j y_js + t y_cs +
+// r y_rs + c.  The split route's scratch p.zs is column-tiled, [tile][32-column tile][node][32
+// rows][32] (y_cs = J * 1024: every (tile, column tile, node) block is 4 contiguous KiB, written
+// whole by one wave and read back in 1-2 KiB runs by the mixing phase -- round 4; it was
+// [tile][node][32 rows][N], 128-B runs); (ROWMAJOR, v5 for J > 21) row-major z with y_cs = 32,
+// rows < B only.
 struct YOut {
     float* y;
-    int64_t y_rs, y_js, y_ts;
+    int64_t y_rs, y_js, y_ts, y_cs;
 };
+// zs element (row, node j, column n) of the split route's column-tiled scratch
+__device__ __forceinline__ int64_t zs_off(int64_t row, int j, int n, int J, int N) {
+    return ((((row >> 5) * (N >> 5) + (n >> 5)) * J + j) << 10) + ((row & 31) << 5) + (n & 31);
+}
 
 template <bool RMS, int PREC, bool ROWMAJOR, int PF = 8>  // PF: chunks in flight
 __global__ __launch_bounds__(256) void k_gl4y(const GLArgs p, int ntile_c, int64_t ntile_r, const YOut yo) {
@@ -275,19 +282,21 @@ __global__ __launch_bounds__(256) void k_gl4y(const GLArgs p, int ntile_c, int64
             acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(xl, wh[sl], acc, 0, 0, 0);
         }
     };
+    // nchunk % PF == 0 (launch_gl4y): every load issued unconditionally -- a main loop that always
+    // issues, a last round that never does.  (Round 4: the earlier `if (c + PF < nchunk) issue`
+    // form made the waitcnt pass merge the paths and wait vmcnt(1-3) at every chunk, i.e. one
+    // memory latency per chunk instead of one per launch.)
 #pragma unroll
-    for (int i = 0; i < PF; ++i)
-        if (i < nchunk) issue(i, i);
-    for (int c0 = 0; c0 < nchunk; c0 += PF) {
+    for (int i = 0; i < PF; ++i) issue(i, i);
+    for (int c0 = 0; c0 < nchunk - PF; c0 += PF) {
 #pragma unroll
         for (int i = 0; i < PF; ++i) {
-            const int c = c0 + i;
-            if (c < nchunk) {
-                compute(c, i);
-                if (c + PF < nchunk) issue(c + PF, i);
-            }
+            compute(c0 + i, i);
+            issue(c0 + i + PF, i);
         }
     }
+#pragma unroll
+    for (int i = 0; i < PF; ++i) compute(nchunk - PF + i, i);
     if (p.status && __builtin_amdgcn_ballot_w64(amx >= 65504.0f) != 0 && lane == 0) atomicOr(p.status, 1u);
     float sc[16];
 #pragma unroll
@@ -304,16 +313,16 @@ __global__ __launch_bounds__(256) void k_gl4y(const GLArgs p, int ntile_c, int64
     const float bv = (p.bias && ncol < p.N) ? p.bias[p.wrow[j] + ncol] : 0.f;
     if constexpr (ROWMAJOR) {
         if (ncol >= p.N) return;
-        float* y = yo.y + tr * yo.y_ts + j * yo.y_js + ncol;
+        float* y = yo.y + tr * yo.y_ts + j * yo.y_js + tc * yo.y_cs + l32;
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
             const int rr = (r & 3) + 8 * (r >> 2) + 4 * h;
             if (row0 + rr < p.B) y[rr * yo.y_rs] = acc[r] * sc[r] + bv;
         }
-    } else {  // the split route's scratch: every row of the tile, N % 32 == 0
-        float* y = p.zs + ((tr * J + j) * 32) * (int64_t)p.N + ncol;
+    } else {  // the split route's column-tiled scratch: every row of the tile, N % 32 == 0
+        float* y = p.zs + zs_off(row0, j, tc * 32, J, p.N) + l32;
 #pragma unroll
-        for (int r = 0; r < 16; ++r) y[(int64_t)((r & 3) + 8 * (r >> 2) + 4 * h) * p.N] = acc[r] * sc[r] + bv;
+        for (int r = 0; r < 16; ++r) y[((r & 3) + 8 * (r >> 2) + 4 * h) << 5] = acc[r] * sc[r] + bv;
     }
 }
 
@@ -347,7 +356,12 @@ __global__ __launch_bounds__(NWV * 64, WRES ? 1 : 2) void k_gl4t(const GLArgs p,
     constexpr int NP = (CT * PPT + NT - 1) / NT;  // staged pieces per thread
     constexpr int TS = 36;                      // floats per row of a wave's 32 x 32 output transpose
     constexpr int NS = PF + 1;                  // LDS-DMA weight ring: chunk c in slot c % NS
-    constexpr int SBW = (WRES ? NCH : NS) * CT * TILE_H * 2;
+    // x through the LDS-DMA ring too (f32 operands): per slot and wave the chunk's 32 rows x 16 k
+    // image (2 KiB) -- no register-writing global load in the K loop, so the compiler inserts no
+    // vmcnt of its own (with a tracked x load beside an LDS-DMA it drained vmcnt(0) every chunk)
+    constexpr bool XDMA = !WRES && PREC != 2;
+    constexpr int XSB = XDMA ? NS * NWV * 2048 : 0;  // bytes of the x slots (after the weight slots)
+    constexpr int SBW = (WRES ? NCH : NS) * CT * TILE_H * 2 + XSB;
     constexpr int SB = SBW > NWV * 32 * TS * 4 ? SBW : NWV * 32 * TS * 4;
     static_assert(!WRES || SB <= 160 * 1024, "resident weight slice exceeds the LDS");
     __shared__ __attribute__((aligned(16))) char smem_raw[SB];  // weight stages, then the transposes
@@ -518,10 +532,21 @@ __global__ __launch_bounds__(NWV * 64, WRES ? 1 : 2) void k_gl4t(const GLArgs p,
     // after it, was last read in chunk c - 1, which every wave finished before arriving.
     // Pieces of wave w per chunk: q0 = 64 w + NT k < CT * PPT (two counts, wave-uniform).
     constexpr int NPC = CT * PPT;
-    constexpr int XL = 2;  // x loads per chunk and lane
+    constexpr int XL = 2;  // x loads (XDMA: x DMA instructions) per chunk and lane / wave
     constexpr int OPA = (NPC / 64 + NWV - 1) / NWV + XL, OPB = (NPC / 64) / NWV + XL;
     const bool wa = wave * 64 + NT * ((NPC / 64 + NWV - 1) / NWV - 1) < NPC;
     const _Float16* wt0 = p.wsp + ((int64_t)p.ntype[j] * nchunk * p.wsp_nct + cg * CT) * 1024;
+    // XDMA x image of a wave's slot: float k 256 + 4 L (instruction k = 0 / 1, lane L) holds row
+    // row0 + (L & 31), features 16 c + 8 k + 4 (L >> 5) .. + 3, i.e. what lane (l32, h) of the
+    // compute reads as xa (k = h, L = l32) and xb (k = h, L = 32 + l32): the global image of a
+    // row-blocked chunk, gathered per lane from a row-major operand
+    float* const xs0 = reinterpret_cast<float*>(smem_raw + NS * CT * TILE_H * 2) + wave * 512;
+    auto xsrc = [&](int c, int k) -> const float* {  // this lane's DMA source of instruction k
+        const int f = (c << 4) + 8 * k + 4 * h;
+        if (f < p.K1)
+            return p.x1_blk ? p.x1 + blk_off(arow, j, f, J, p.K1) : p.x1 + ((ac + p.x1_row0) / p.x1_div) * p.x1_rs + (int64_t)j * p.K1 + f;
+        return p.x2_blk ? p.x2 + blk_off(arow, j, f - p.K1, J, p.K2) : p.x2 + ac * p.x2_rs + (int64_t)j * p.K2 + (f - p.K1);
+    };
     auto fill = [&](int c) {
         _Float16* dst = sW[c % NS];
 #pragma unroll
@@ -532,6 +557,16 @@ __global__ __launch_bounds__(NWV * 64, WRES ? 1 : 2) void k_gl4t(const GLArgs p,
             const _Float16* src = wt0 + ((int64_t)c * p.wsp_nct + q / PPT) * 1024 + (q % PPT) * 8;
             __builtin_amdgcn_global_load_lds((const void*)src, (lds_void*)(dst + (size_t)q0 * 8), 16, 0, 0);
         }
+        if constexpr (XDMA) {
+            float* xd = xs0 + (c % NS) * (NWV * 512);
+            __builtin_amdgcn_global_load_lds((const void*)xsrc(c, 0), (lds_void*)xd, 16, 0, 0);
+            __builtin_amdgcn_global_load_lds((const void*)xsrc(c, 1), (lds_void*)(xd + 256), 16, 0, 0);
+        }
+    };
+    auto x_lds = [&](int c) {  // XDMA: chunk c's A-operand values into ring slot 0 of xa / xb
+        const float* xs = xs0 + (c % NS) * (NWV * 512) + h * 256 + l32 * 4;
+        xa[0] = *reinterpret_cast<const floatx4*>(xs);
+        xb[0] = *reinterpret_cast<const floatx4*>(xs + 128);
     };
     static_assert(PF >= 1 && PF <= 4 && OPA * (PF - 1) < 64, "vmcnt range");
     auto wait_chunk = [&](int younger) {  // all but the ops of `younger` later chunks done (folds per unrolled step)
@@ -551,7 +586,7 @@ __global__ __launch_bounds__(NWV * 64, WRES ? 1 : 2) void k_gl4t(const GLArgs p,
 #pragma unroll
     for (int i = 0; i < PF; ++i) {
         fill(i);
-        issue_x(i, i);
+        if constexpr (!XDMA) issue_x(i, i);
     }
 #pragma nounroll
     for (int c0 = 0; c0 < nchunk - PF; c0 += PF) {
@@ -562,17 +597,27 @@ __global__ __launch_bounds__(NWV * 64, WRES ? 1 : 2) void k_gl4t(const GLArgs p,
 #ifdef SD_GL4T_STAMPS
             if (STAMP && tid == 0 && blockIdx.x < 8192 && c < 16) g_gl4t_chunk[blockIdx.x * 16 + c] = wall_clock64();
 #endif
-            compute(c, i, sW[c % NS]);
+            if constexpr (XDMA) {
+                x_lds(c);
+                compute(c, 0, sW[c % NS]);
+            } else {
+                compute(c, i, sW[c % NS]);
+            }
             asm volatile("" ::: "memory");
             fill(c + PF);
-            issue_x(c + PF, i);
+            if constexpr (!XDMA) issue_x(c + PF, i);
         }
     }
     // the last PF chunks: nothing more to issue, the wait shrinks by one chunk each step
 #pragma unroll
     for (int i = 0; i < PF; ++i) {
         wait_chunk(PF - 1 - i);
-        compute(nchunk - PF + i, i, sW[(nchunk - PF + i) % NS]);
+        if constexpr (XDMA) {
+            x_lds(nchunk - PF + i);
+            compute(nchunk - PF + i, 0, sW[(nchunk - PF + i) % NS]);
+        } else {
+            compute(nchunk - PF + i, i, sW[(nchunk - PF + i) % NS]);
+        }
         asm volatile("" ::: "memory");
     }
     }  // staged K loop
@@ -603,7 +648,7 @@ __global__ __launch_bounds__(NWV * 64, WRES ? 1 : 2) void k_gl4t(const GLArgs p,
     // wave is past its last chunk), stored as 16-B pieces: 4 dwordx4 instead of 16 dword stores
     // per tile.  Launch shapes: N a multiple of 32 CT (launch_gl4t), so every column is real.
     float* sT = reinterpret_cast<float*>(smem_raw) + wave * 32 * TS;
-    float* y = yo.y + tr * yo.y_ts + j * yo.y_js + (int64_t)cg * CT * 32;  // YOut as k_gl4y's
+    float* y = yo.y + tr * yo.y_ts + j * yo.y_js + (int64_t)cg * CT * yo.y_cs;  // YOut as k_gl4y's
 #pragma unroll
     for (int ct = 0; ct < CT; ++ct) {
         const int ncol = (cg * CT + ct) * 32 + l32;
@@ -616,7 +661,7 @@ __global__ __launch_bounds__(NWV * 64, WRES ? 1 : 2) void k_gl4t(const GLArgs p,
             const int row = 8 * q + (lane >> 3), c4 = (lane & 7) * 4;
             const floatx4 v = *reinterpret_cast<const floatx4*>(sT + row * TS + c4);
             if (!ROWMAJOR || row0 + row < p.B)  // row-major z holds rows < B only
-                *reinterpret_cast<floatx4*>(y + (int64_t)row * yo.y_rs + ct * 32 + c4) = v;
+                *reinterpret_cast<floatx4*>(y + (int64_t)row * yo.y_rs + ct * yo.y_cs + c4) = v;
         }
         __builtin_amdgcn_wave_barrier();
     }
@@ -811,10 +856,19 @@ __device__ __forceinline__ void attention_epilogue(const GLArgs& p, floatx16 (&a
 //   row-major): a bf16 operand is its own A fragment (one 16-B load per 8 k).
 // STG 0: weight stages filled by LDS-DMA (global_load_lds_dwordx4); STG 1: register-staged
 //   (global_load_dwordx4 a chunk ahead, ds_write_b128 after the chunk's MFMAs).
+// MODE 4: small-batch fused tile (DESIGN.md §4d'): one workgroup = one 32-row tile x one 32-column
+//   tile x all J nodes, wave w = node w; each wave walks its node's whole K extent with x and
+//   weight fragments straight from memory into registers, PF4 chunks ahead (k_gl4y's loop: no
+//   LDS, no barriers), then the MODE 0 mixing / FiLM / tanh / residual epilogue.  One launch and
+//   no scratch round trip per layer instead of the split route's two; every output element sees
+//   the same products in the same order, so it is bitwise equal to MODE 0 and the split routes.
 template <int J, int NW, int RT, int CT, bool RMS, int DBG = 0, int MODE = 0, int XP = 0, int PREC = 0, int STG = 0>
 __global__ __launch_bounds__(NW * 64, 1) void k_gl4(const GLArgs p) {
-    static_assert(MODE == 0 || MODE == 2 || (CT == 3 && RT == 1 && J <= 32 && NW == 8), "attention mode: 32 x (q|k|v)");
+    static_assert(MODE == 0 || MODE == 2 || MODE == 4 || (CT == 3 && RT == 1 && J <= 32 && NW == 8),
+                  "attention mode: 32 x (q|k|v)");
     static_assert(MODE < 2 || (RT == 1 && XP == 0 && STG == 0 && DBG == 0), "split-route phase 2: one 32-row tile");
+    static_assert(MODE != 4 || (CT == 1 && PREC != 2), "small-batch fused tile: one 32-column tile, f16 products");
+    constexpr bool PH2 = MODE == 2 || MODE == 3;  // split-route phase 2: Y from the scratch, no K loop
     constexpr int NPW = (J + NW - 1) / NW;  // nodes per wave
     constexpr int KS = (J + 3) / 4;         // 4-deep k steps of the mixing GEMM (K = J padded)
     constexpr int IB = (J + 15) / 16;       // 16-row i blocks of the mixing GEMM
@@ -931,7 +985,7 @@ __global__ __launch_bounds__(NW * 64, 1) void k_gl4(const GLArgs p) {
     floatx16 acc[NPW][RT][CT];
     uint64_t ts[8];  // DBG 6: phase stamps (s_memrealtime, 100 MHz) + shader clock around the K loop
     uint64_t cs[5];  // DBG 6: shader-clock stamps inside chunk 5
-    if constexpr (MODE >= 2) {
+    if constexpr (PH2) {
         // split-route phase 2: the slab's Y (from phase 1's p.zs), G-hat and FiLM all loaded to
         // registers first (one memory round trip), then to LDS, one barrier
         constexpr int C4 = COLS / 4;
@@ -939,16 +993,19 @@ __global__ __launch_bounds__(NW * 64, 1) void k_gl4(const GLArgs p) {
         constexpr int NYL = (YQ + NTH - 1) / NTH, NGL = (J * J + NTH - 1) / NTH;
         constexpr int YS8 = 8 * COLS + 16;  // MODE 3: attention_epilogue's slab layout
         const int64_t tb = (row0 >> 5) * J;
+        // column-tiled zs (zs_off): consecutive q read consecutive 16-B pieces -- one node's rows of
+        // the slab in one column tile are a contiguous 1-2 KiB run
+        (void)tb;
         auto ysrc = [&](int q, float*& dst) -> const float* {
             if constexpr (MODE == 2) {
+                static_assert(MODE != 2 || COLS == 32, "MODE 2: one 32-column tile");
                 const int cc = (q % C4) * 4, r = (q / C4) & 15, j = q / (16 * C4);
                 dst = sY + j * YS + r * YR + cc;
-                return p.zs + ((tb + j) * 32 + 16 * slab + r) * (int64_t)p.N + c0 + cc;
+                return p.zs + zs_off(row0 + 16 * slab + r, j, c0 + cc, J, p.N);
             } else {
-                const int c4 = q % 24, rr = (q / 24) & 7, j = q / 192;
-                const int ct = c4 >> 3, cc = (c4 & 7) * 4;
+                const int cc = (q & 7) * 4, rr = (q >> 3) & 7, j = (q >> 6) % J, ct = (q >> 6) / J;
                 dst = sY + j * YS8 + rr * COLS + 32 * ct + cc;
-                return p.zs + ((tb + j) * 32 + 8 * slab + rr) * (int64_t)p.N + (ctile + ct * p.attn_heads) * 32 + cc;
+                return p.zs + zs_off(row0 + 8 * slab + rr, j, (ctile + ct * p.attn_heads) * 32 + cc, J, p.N);
             }
         };
         floatx4 yv[NYL];
@@ -1180,7 +1237,90 @@ __global__ __launch_bounds__(NW * 64, 1) void k_gl4(const GLArgs p) {
             const int ncol = (MODE == 1 ? (ctile + ct * p.attn_heads) * 32 : c0 + 32 * ct) + l32;
             bv[m][ct] = (p.bias && ncol < p.N) ? p.bias[p.wrow[jn[m]] + ncol] : 0.f;
         }
-    if constexpr (STG == 1) {
+    if constexpr (MODE == 4) {
+        // k_gl4y's K loop per wave (node jn[m]), PF4 chunks in flight in registers (16 waves per
+        // workgroup leave 128 registers per wave: 4 chunks of 16 operand registers + the tile)
+        constexpr int PF4 = 4;
+        const int64_t arow = row0 + l32;
+        const int64_t ac = arow < p.B ? arow : 0;
+        const float* xr1[NPW];
+        const float* xr2[NPW];
+        const _Float16* wb[NPW];
+#pragma unroll
+        for (int m = 0; m < NPW; ++m) {
+            const int j = jn[m];
+            xr1[m] = p.x1_blk ? p.x1 + blk_off(arow, j, 8 * h, J, p.K1)
+                              : p.x1 + ((ac + p.x1_row0) / p.x1_div) * p.x1_rs + (int64_t)j * p.K1 + 8 * h;
+            xr2[m] = !p.K2 ? nullptr
+                           : p.x2_blk ? p.x2 + blk_off(arow, j, 8 * h, J, p.K2) : p.x2 + ac * p.x2_rs + (int64_t)j * p.K2 + 8 * h;
+            wb[m] = p.wsp + ((int64_t)p.ntype[j] * nchunk * p.wsp_nct + ctile) * 1024 + lane * 8;
+        }
+        const int64_t wcs = (int64_t)p.wsp_nct * 1024;  // halves per chunk
+        floatx4 ya[PF4][NPW], yb[PF4][NPW];
+        halfx8 wh4[PF4][NPW], wl4[PF4][NPW];
+        // every load unconditional (a node check only where J % NW != 0): a conditionally issued
+        // load makes the waitcnt pass merge paths and wait for (nearly) every load in flight at
+        // each chunk, which is what k_gl4y's loop gets (vmcnt(2) per chunk in its ISA)
+        auto live = [&](int m) { return J % NW == 0 || wave + NW * m < J; };
+        auto issue = [&](int c, int sl) {
+            const int k0 = c << 4;
+#pragma unroll
+            for (int m = 0; m < NPW; ++m) {
+                if (!live(m)) continue;  // wave-uniform
+                const float* src;
+                int step4;
+                if (k0 < p.K1) {
+                    src = p.x1_blk ? xr1[m] + (k0 << 5) : xr1[m] + k0;
+                    step4 = p.x1_blk ? 128 : 4;
+                } else {
+                    src = p.x2_blk ? xr2[m] + ((k0 - p.K1) << 5) : xr2[m] + (k0 - p.K1);
+                    step4 = p.x2_blk ? 128 : 4;
+                }
+                ya[sl][m] = g4(src);
+                yb[sl][m] = g4(src + step4);
+                const _Float16* w = wb[m] + c * wcs;
+                wh4[sl][m] = *reinterpret_cast<const halfx8*>(w);
+                if constexpr (!PREC) wl4[sl][m] = *reinterpret_cast<const halfx8*>(w + 512);
+            }
+        };
+        auto comp = [&](int c, int sl) {  // compute()'s arithmetic for one chunk
+            const bool rms_chunk = RMS && (c << 4) < p.K1;
+#pragma unroll
+            for (int m = 0; m < NPW; ++m) {
+                if (!live(m)) continue;
+                const floatx8 f = {ya[sl][m].x, ya[sl][m].y, ya[sl][m].z, ya[sl][m].w,
+                                   yb[sl][m].x, yb[sl][m].y, yb[sl][m].z, yb[sl][m].w};
+                if (rms_chunk) {
+                    const floatx8 q = f * f;
+                    ss[m][0] += ((q[0] + q[1]) + (q[2] + q[3])) + ((q[4] + q[5]) + (q[6] + q[7]));
+                }
+                const floatx8 a = __builtin_elementwise_abs(f);
+                amx = fmaxf(amx, fmaxf(fmaxf(fmaxf(a[0], a[1]), fmaxf(a[2], a[3])), fmaxf(fmaxf(a[4], a[5]), fmaxf(a[6], a[7]))));
+                const halfx8 xh = __builtin_convertvector(f, halfx8);
+                floatx16 t = acc[m][0][0];
+                t = __builtin_amdgcn_mfma_f32_32x32x16_f16(xh, wh4[sl][m], t, 0, 0, 0);
+                if constexpr (!PREC) {
+                    const halfx8 xl = __builtin_convertvector(f - __builtin_convertvector(xh, floatx8), halfx8);
+                    t = __builtin_amdgcn_mfma_f32_32x32x16_f16(xh, wl4[sl][m], t, 0, 0, 0);
+                    t = __builtin_amdgcn_mfma_f32_32x32x16_f16(xl, wh4[sl][m], t, 0, 0, 0);
+                }
+                acc[m][0][0] = t;
+            }
+        };
+        // nchunk % PF4 == 0 (checked at launch): a main loop that always issues, a last round that
+        // never does
+#pragma unroll
+        for (int i = 0; i < PF4; ++i) issue(i, i);
+        for (int c0 = 0; c0 < nchunk - PF4; c0 += PF4) {
+#pragma unroll
+            for (int i = 0; i < PF4; ++i) {
+                comp(c0 + i, i);
+                issue(c0 + i + PF4, i);
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < PF4; ++i) comp(nchunk - PF4 + i, i);
+    } else if constexpr (STG == 1) {
         // register-staged weights: the pieces of chunk c+1 this thread carries are loaded right
         // after barrier c (with x(c+1)) and written to the other stage after compute(c); its
         // last reads were in phase c-1, before barrier c.  lgkmcnt(0) + barrier c+1 makes the
@@ -1488,7 +1628,7 @@ static hipError_t gl4_launch_t(const GLArgs& a, bool rms, hipStream_t s) {
         hipError_t e = hipFuncSetAttribute((const void*)kt, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         if (e != hipSuccess) return e;
     }
-    g_route_bits |= MODE >= 2 ? kRouteMixPhase : MODE == 1 ? kRouteFusedAttn : kRouteOneKernel;
+    g_route_bits |= MODE == 4 ? kRouteFusedSmall : MODE >= 2 ? kRouteMixPhase : MODE == 1 ? kRouteFusedAttn : kRouteOneKernel;
     hipLaunchKernelGGL(kt, grid, dim3(NW * 64), lds, s, a);
     return hipGetLastError();
 }
@@ -1521,13 +1661,14 @@ int64_t split_rows_default() { return g_split_rows; }
 // route with the tiled phase 1 (k_gl4t, full batches).  GLArgs::split: 0 auto, 1 never, 2 always
 // (k_gl4y), 3 always (k_gl4t).
 static int split_route(const GLArgs& a, bool attn) {
+    if (a.split == 5 && !attn) return 0;  // the small-batch fused tile (small_fused) took it
     if (a.split == 1 || !a.zs || (a.N & 31) || a.J > 32) return 0;
     if (a.prec == 2 && a.split < 3 && !(a.split == 0 && a.J == 17)) return 0;  // bf16: tiled only (J = 17 auto)
     const int64_t tiles = (a.B + 31) / 32;
     if (tiles * 32 * a.J * (int64_t)a.N > a.zs_cap) return 0;
     if (a.zs == a.out || a.zs == a.x1 || a.zs == a.x2 || a.zs == a.res) return 0;
     if (attn && (a.attn_heads * 96 != a.N)) return 0;
-    if (a.split == 2) return a.prec == 2 ? 0 : 1;
+    if (a.split == 2 || a.split == 5) return a.prec == 2 ? 0 : 1;
     if (a.split == 3) return 2;
     if (a.split == 4) return attn ? 0 : 2;  // tiled GEMM phase; to_qkv + attention on the one-kernel tile
     if (a.gl4_cfg != 0) return 0;
@@ -1552,23 +1693,31 @@ static int g_gl4y_pf = [] {
     return (e && atoi(e) == 8) ? 8 : 12;
 }();
 
+template <bool ROWMAJOR, int PF>
+static void launch_gl4y_pf(const GLArgs& a, bool rms, int ntc, int64_t ntile_r, const YOut& yo, dim3 grid, hipStream_t s) {
+    if (a.prec == 1) {
+        if (rms) hipLaunchKernelGGL((k_gl4y<true, 1, ROWMAJOR, PF>), grid, dim3(256), 0, s, a, ntc, ntile_r, yo);
+        else hipLaunchKernelGGL((k_gl4y<false, 1, ROWMAJOR, PF>), grid, dim3(256), 0, s, a, ntc, ntile_r, yo);
+    } else {
+        if (rms) hipLaunchKernelGGL((k_gl4y<true, 0, ROWMAJOR, PF>), grid, dim3(256), 0, s, a, ntc, ntile_r, yo);
+        else hipLaunchKernelGGL((k_gl4y<false, 0, ROWMAJOR, PF>), grid, dim3(256), 0, s, a, ntc, ntile_r, yo);
+    }
+}
+
 template <bool ROWMAJOR>
 static hipError_t launch_gl4y(const GLArgs& a, bool rms, int ntc, int64_t ntile_r, const YOut& yo, hipStream_t s) {
     const int64_t units = ntile_r * a.J * ntc;
-    const dim3 grid((unsigned)((units + 3) / 4)), block(256);
+    const dim3 grid((unsigned)((units + 3) / 4));
+    const int nchunk = (a.K1 + a.K2) / 16;  // even (launch_graph_linear_v4)
     g_route_bits |= kRouteGemmWave;
-    if (g_gl4y_pf == 12 && grid.x <= 256 && a.prec == 0) {
-        if (rms) hipLaunchKernelGGL((k_gl4y<true, 0, ROWMAJOR, 12>), grid, block, 0, s, a, ntc, ntile_r, yo);
-        else hipLaunchKernelGGL((k_gl4y<false, 0, ROWMAJOR, 12>), grid, block, 0, s, a, ntc, ntile_r, yo);
-        return hipGetLastError();
-    }
-    if (a.prec == 1) {
-        if (rms) hipLaunchKernelGGL((k_gl4y<true, 1, ROWMAJOR>), grid, block, 0, s, a, ntc, ntile_r, yo);
-        else hipLaunchKernelGGL((k_gl4y<false, 1, ROWMAJOR>), grid, block, 0, s, a, ntc, ntile_r, yo);
-    } else {
-        if (rms) hipLaunchKernelGGL((k_gl4y<true, 0, ROWMAJOR>), grid, block, 0, s, a, ntc, ntile_r, yo);
-        else hipLaunchKernelGGL((k_gl4y<false, 0, ROWMAJOR>), grid, block, 0, s, a, ntc, ntile_r, yo);
-    }
+    // chunks in flight: a divisor of nchunk (the K loop's rounds); every chunk of a K = 192 layer
+    // in flight on grids of at most one workgroup per CU
+    if (g_gl4y_pf == 12 && grid.x <= 256 && a.prec == 0 && nchunk % 12 == 0)
+        launch_gl4y_pf<ROWMAJOR, 12>(a, rms, ntc, ntile_r, yo, grid, s);
+    else if (nchunk % 8 == 0) launch_gl4y_pf<ROWMAJOR, 8>(a, rms, ntc, ntile_r, yo, grid, s);
+    else if (nchunk % 6 == 0) launch_gl4y_pf<ROWMAJOR, 6>(a, rms, ntc, ntile_r, yo, grid, s);
+    else if (nchunk % 4 == 0) launch_gl4y_pf<ROWMAJOR, 4>(a, rms, ntc, ntile_r, yo, grid, s);
+    else launch_gl4y_pf<ROWMAJOR, 2>(a, rms, ntc, ntile_r, yo, grid, s);
     return hipGetLastError();
 }
 
@@ -1581,7 +1730,7 @@ hipError_t launch_gemm_split(const GLArgs& a, bool rms, float* z, int64_t z_rs, 
     if (!a.wsp || a.prec == 2 || (a.K1 + a.K2) % 16 || a.K1 % 16 || a.x1_blk || a.x2_blk) return hipErrorNotSupported;
     const int64_t ntile_r = (a.B + 31) / 32;
     const int ntc = (a.N + 31) / 32;
-    const YOut yo{z, z_rs, a.N, 32 * z_rs};
+    const YOut yo{z, z_rs, a.N, 32 * z_rs, 32};
     // the tiled phase (128 rows x up to 192 columns of one node per workgroup) where the shape
     // has one
     if (((uintptr_t)z & 15) == 0 && (z_rs & 3) == 0 && (a.N & 3) == 0) {  // 16-B Y pieces
@@ -1657,7 +1806,7 @@ template <int J>
 static hipError_t gl4_split(const GLArgs& a, bool rms, bool attn, int route, hipStream_t s) {
     const int64_t ntile_r = (a.B + 31) / 32;
     const int ntc = a.N / 32;
-    const YOut yo{a.zs, a.N, 32LL * a.N, 32LL * J * a.N};
+    const YOut yo{a.zs, 32, 1024, (int64_t)(a.N / 32) * J * 1024, (int64_t)J * 1024};  // column-tiled (zs_off)
     hipError_t e = route == 2 ? launch_gl4t<false>(a, rms, ntile_r, yo, s) : hipErrorNotSupported;
     if (e == hipErrorNotSupported) {
         if (a.prec == 2) return hipErrorNotSupported;  // k_gl4y has no bf16 form
@@ -1670,6 +1819,23 @@ static hipError_t gl4_split(const GLArgs& a, bool rms, bool attn, int route, hip
     }
     if (attn) return gl4_launch_t<J, 8, 1, 3, 0, 3, 0, 0, 0>(a, false, s);
     return gl4_launch_t<J, 8, 1, 1, 0, 2, 0, 0, 0>(a, false, s);
+}
+
+// Small-batch fused tile (k_gl4 MODE 4) for the plain graph-linears of J = 16 f32 / half plans:
+// GLArgs::split 5 always; auto (0) at <= SKELDIFF_SMALL_ROWS rows of the call (default 0: off --
+// measured slower than the split route, DESIGN.md §4d': config 4 83.5 vs 116.1 futures/s, 12
+// workgroups each pulling 16 nodes' operands through one CU).  to_qkv + attention keeps the split
+// route.
+static int64_t g_small_rows = [] {
+    const char* e = getenv("SKELDIFF_SMALL_ROWS");
+    return e ? (int64_t)atoll(e) : (int64_t)0;
+}();
+static bool small_fused(const GLArgs& a) {
+    if (a.J != 16 || a.prec == 2 || a.split == 1 || a.split == 2 || a.split == 3 || a.split == 4) return false;
+    if ((a.K1 + a.K2) % 64) return false;  // MODE 4's K loop: chunks in rounds of 4
+    if (a.split == 5) return true;
+    if (a.gl4_cfg != 0) return false;
+    return (a.route_rows > 0 ? a.route_rows : a.B) <= g_small_rows;
 }
 
 static hipError_t gl4_split_dispatch(const GLArgs& a, bool rms, bool attn, int route, hipStream_t s) {
@@ -1688,6 +1854,8 @@ hipError_t launch_graph_linear_v4(const GLArgs& a, bool rms, hipStream_t s) {
     if ((a.N & 3) || ((uintptr_t)a.out & 15) || ((uintptr_t)a.res & 15) || (a.res && (a.res_rs & 3)) || (a.out_rs & 3))
         return hipErrorNotSupported;
     if (!a.wsp || (a.K1 + a.K2) % 32 || a.K1 % 16 || (a.x1_blk && a.x1_div != 1)) return hipErrorNotSupported;
+    if (small_fused(a))
+        return a.prec == 1 ? gl4_launch_t<16, 8, 1, 1, 0, 4, 0, 1, 0>(a, rms, s) : gl4_launch_t<16, 8, 1, 1, 0, 4, 0, 0, 0>(a, rms, s);
     if (a.J == 16 || a.J == 17 || a.J == 21)
         if (const int route = split_route(a, false)) {
             const hipError_t e = gl4_split_dispatch(a, rms, false, route, s);

@@ -27,6 +27,13 @@ namespace {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef float floatx4 __attribute__((ext_vector_type(4)));
+typedef unsigned uint4v __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) void lds_void;
+template <int N>
+struct VmC {  // s_waitcnt vmcnt(N), expcnt / lgkmcnt not waited
+    static_assert(N >= 0 && N < 64, "vmcnt range");
+    static constexpr int imm = (N & 0xF) | (0x7 << 4) | (0xF << 8) | ((N >> 4) << 14);
+};
 
 constexpr int TM = 64, TN = 64, TK = 32;
 
@@ -329,13 +336,155 @@ __global__ __launch_bounds__(256) void k_gl5_mixm(const GLArgs p, const float* z
     }
 }
 
+// k_gl5_mixm with its operands streamed by LDS-DMA (round 4).  k_gl5_mixm loads row r + 1's slab
+// into registers while row r is mixed -- one row (52 MFMAs per wave at J = 51, ~0.8 us) of cover for
+// a memory latency, with the VGPRs of a deeper ring costing occupancy (MFMA busy 29 %, SQ_WAIT_ANY
+// 60 % at J = 51).  Here the z slab AND the residual slab of row r + PF go straight to LDS ring slot
+// (r + PF) % NS by global_load_lds_dwordx4 (no VGPRs), issued after row r's barrier, so PF rows of
+// MFMAs cover each load; the output leaves through raw buffer stores whose out-of-range offsets
+// are dropped by the hardware (dead lanes and rows store nothing without a branch), so every wave
+// issues a fixed number of memory operations per row and the wait for row r is an exact vmcnt.
+// The same MFMA sequence (A = z^T from LDS, B = G-hat^T fragments, k steps in j order) and
+// epilogue as k_gl5_mixm: bitwise equal.  Slab rows are 64 floats with the 16-B pieces of odd rows
+// XOR-swizzled by 4 (the A reads of rows 4 s + l4, l4 = 0 / 1 then hit different bank halves).
+// DMA instruction k of a slab covers rows 4 k .. 4 k + 3 and belongs to wave k % 4.
+template <int R, int PF, bool RES>
+__global__ __launch_bounds__(256, 2) void k_gl5_mixd(const GLArgs p, const float* z, int64_t z_rs) {
+    constexpr int NS = PF + 1;
+    const int J = p.J, N = p.N, KS = (J + 3) >> 2;
+    const int SL = 4 * KS * 64;                   // floats per slab (4 KS rows x 64 columns)
+    extern __shared__ __attribute__((aligned(16))) float s_m[];
+    float* s_zr = s_m;                            // [NS][z | res][SL]
+    float* s_f = s_m + NS * (RES ? 2 : 1) * SL;   // FiLM (scale + 1 | shift)
+    const int tid = threadIdx.x, lane = tid & 63, l16 = lane & 15, l4 = lane >> 4;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int n0 = blockIdx.y * 64;
+    const int64_t b0 = (int64_t)blockIdx.x * R;
+    const int nrows = (int)min((int64_t)R, p.B - b0);
+    const int i = 16 * w + l16;
+    float gb[16];
+#pragma unroll
+    for (int s = 0; s < 16; ++s) {
+        const int j = 4 * s + l4;
+        gb[s] = (s < KS && i < J && j < J) ? p.G[i * J + j] : 0.f;
+    }
+    if (tid < 64) {
+        s_f[tid] = p.film ? p.film[n0 + tid] + 1.0f : 1.0f;
+        s_f[64 + tid] = p.film ? p.film[N + n0 + tid] : 0.0f;
+    }
+    // the k padding rows J .. 4 KS - 1 of every z slot stay zero (never a DMA destination)
+    for (int q = tid; q < NS * (4 * KS - J) * 64; q += 256) {
+        const int sl = q / ((4 * KS - J) * 64), e = q % ((4 * KS - J) * 64);
+        s_zr[sl * (RES ? 2 : 1) * SL + J * 64 + e] = 0.f;
+    }
+    const int nk = KS;                          // DMA instructions per slab
+    const int nkw = (nk - w + 3) >> 2;          // this wave's share (instructions w, w + 4, ...)
+    // a slab's 16-B pieces: lane L of instruction k -> LDS row 4 k + (L >> 4), piece L & 15, which
+    // holds global piece (L & 15) ^ ((row & 1) << 2)
+    auto fill = [&](int r) {  // row r (clamped to a valid row) into slot r % NS
+        const int64_t br = b0 + min(r, nrows - 1);
+        float* dz = s_zr + (r % NS) * (RES ? 2 : 1) * SL;
+        const int row_in = lane >> 4, pc = lane & 15;
+#pragma unroll
+        for (int kk = 0; kk < 4; ++kk) {
+            const int k = w + 4 * kk;
+            if (k >= nk) continue;  // wave-uniform
+            const int row = 4 * k + row_in;
+            const int gp = pc ^ ((row & 1) << 2);
+            const int rowc = min(row, J - 1);  // lanes of rows >= J: a valid source, masked below
+            if (row < J) {
+                __builtin_amdgcn_global_load_lds((const void*)(z + br * z_rs + (int64_t)rowc * N + n0 + 4 * gp),
+                                                 (lds_void*)(dz + 4 * k * 64), 16, 0, 0);
+                if constexpr (RES)
+                    __builtin_amdgcn_global_load_lds((const void*)(p.res + br * p.res_rs + (int64_t)rowc * N + n0 + 4 * gp),
+                                                     (lds_void*)(dz + SL + 4 * k * 64), 16, 0, 0);
+            }
+        }
+    };
+    // output: raw buffer stores relative to the workgroup's first row; out-of-range offsets dropped
+    const int64_t obase = b0 * p.out_rs;
+    const uint32_t oreach = (uint32_t)min((int64_t)nrows * p.out_rs * 4, (int64_t)0x7fffffff);
+    const __amdgpu_buffer_rsrc_t orsrc = __builtin_amdgcn_make_buffer_rsrc(p.out + obase, 0, (int)oreach, 0x00020000);
+    constexpr int ST = 4;                                        // stores per row and wave
+    const int FO = nkw * (RES ? 2 : 1);                          // DMA operations per fill and wave
+    auto wait_row = [&](int younger_fills, int younger_stores) {  // vmcnt: the ops issued after row r's fill
+        const int n = younger_fills * FO + younger_stores * ST;
+        // a switch over the possible immediates (n <= (PF - 1) * 8 + PF * 4)
+        switch (n) {
+#define SD_VMC(v) case v: __builtin_amdgcn_s_waitcnt(VmC<v>::imm); break;
+            SD_VMC(0) SD_VMC(1) SD_VMC(2) SD_VMC(3) SD_VMC(4) SD_VMC(5) SD_VMC(6) SD_VMC(7) SD_VMC(8) SD_VMC(9)
+            SD_VMC(10) SD_VMC(11) SD_VMC(12) SD_VMC(13) SD_VMC(14) SD_VMC(15) SD_VMC(16) SD_VMC(17) SD_VMC(18)
+            SD_VMC(19) SD_VMC(20) SD_VMC(21) SD_VMC(22) SD_VMC(23) SD_VMC(24) SD_VMC(25) SD_VMC(26) SD_VMC(27)
+            SD_VMC(28) SD_VMC(29) SD_VMC(30) SD_VMC(31) SD_VMC(32)
+#undef SD_VMC
+            default: __builtin_amdgcn_s_waitcnt(VmC<0>::imm); break;
+        }
+        asm volatile("" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+    };
+    __syncthreads();  // the zero rows and FiLM before any DMA lands next to them
+#pragma unroll
+    for (int q = 0; q < PF; ++q) fill(q);  // rows 0 .. PF - 1 (clamped rows repeat a valid one)
+    for (int r = 0; r < nrows; ++r) {
+        // order per row m: wait(m), fill(m + PF), compute(m), stores(m); the prologue fills rows
+        // 0 .. PF - 1.  Issued after fill(r): PF - 1 fills (prologue ones included) and min(r, PF)
+        // rows' stores (stores(r - PF) when r >= PF, then fill(m + PF), stores(m) for m < r)
+        const int m0 = max(r - PF + 1, 0);
+        const int yrows = (r - m0) + (r < PF ? (PF - 1 - r) : 0);   // later fills (incl. prologue ones)
+        const int ystores = r - m0 + (r >= PF ? 1 : 0);
+        wait_row(yrows, ystores);
+        fill(r + PF);  // slot (r + PF) % NS = (r - 1) % NS: read in row r - 1, before this barrier
+        const float* zs = s_zr + (r % NS) * (RES ? 2 : 1) * SL;
+        floatx4 acc[4];
+#pragma unroll
+        for (int cb = 0; cb < 4; ++cb) {
+            floatx4 t = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int s = 0; s < 16; ++s) {
+                if (s < KS) {  // wave-uniform
+                    const int row = 4 * s + l4;
+                    const float a = zs[row * 64 + ((((16 * cb + l16) >> 2) ^ ((l4 & 1) << 2)) << 2) + (l16 & 3)];
+                    t = __builtin_amdgcn_mfma_f32_16x16x4f32(a, gb[s], t, 0, 0, 0);
+                }
+            }
+            acc[cb] = t;
+        }
+        const bool live = i < J;
+#pragma unroll
+        for (int cb = 0; cb < 4; ++cb) {
+            float v[4] = {acc[cb][0], acc[cb][1], acc[cb][2], acc[cb][3]};
+            const float4 fa = *reinterpret_cast<const float4*>(s_f + 16 * cb + 4 * l4);
+            const float4 fb = *reinterpret_cast<const float4*>(s_f + 64 + 16 * cb + 4 * l4);
+            const float fav[4] = {fa.x, fa.y, fa.z, fa.w};
+            const float fbv[4] = {fb.x, fb.y, fb.z, fb.w};
+            float rvv[4] = {0.f, 0.f, 0.f, 0.f};
+            if constexpr (RES) {
+                const float4 rq = *reinterpret_cast<const float4*>(zs + SL + min(i, J - 1) * 64 + (((4 * cb + l4) ^ ((min(i, J - 1) & 1) << 2)) << 2));
+                rvv[0] = rq.x; rvv[1] = rq.y; rvv[2] = rq.z; rvv[3] = rq.w;
+            }
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                if (p.film) v[e] = v[e] * fav[e] + fbv[e];
+                if (p.act == 1) v[e] = tanhf(v[e]);
+                v[e] = v[e] + rvv[e];
+            }
+            const int off = live ? (int)((r * p.out_rs + (int64_t)i * N + n0 + 16 * cb + 4 * l4) * 4) : 0x7ffffff0;
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(uint4v, make_float4(v[0], v[1], v[2], v[3])), orsrc,
+                                                   off, 0, 0);
+        }
+    }
+    __builtin_amdgcn_s_waitcnt(VmC<0>::imm);  // the trailing (clamped) fills land before LDS is released
+}
+
 }  // namespace
 
 // 1 (default): the mixing pass on k_gl5_mixm where it applies; 0: k_gl5_mix (SKELDIFF_V5_MIX at
 // load: a diagnostic default under the per-plan SD_OPT_V5_MIX, which selects k_gl5_mix when set)
 static const int g_mix_mfma = [] {
     const char* e = getenv("SKELDIFF_V5_MIX");
-    return e ? std::min(std::max(atoi(e), 0), 2) : 1;  // 2: the two-deep register ring (A/B)
+    // 3 (default): k_gl5_mixd (LDS-DMA ring); 1: k_gl5_mixm; 2: its two-deep register ring (A/B)
+    return e ? std::min(std::max(atoi(e), 0), 3) : 3;
 }();
 // rows per k_gl5_mixm workgroup (SKELDIFF_V5_ROWS at load: 4, 8 or 16)
 static int g_mix_rows = [] {
@@ -404,6 +553,20 @@ hipError_t launch_graph_linear_v5(const GLArgs& a, bool rms, hipStream_t s) {
     // the matrix-core mixing pass: 64-column blocks, 16-B z / residual / output pieces
     const bool mfma = g_mix_mfma && !a.v5_valu && vec && a.N % 64 == 0 && ((uintptr_t)a.out & 15) == 0 && (a.out_rs & 3) == 0 &&
                       (!a.res || (((uintptr_t)a.res & 15) == 0 && (a.res_rs & 3) == 0)) && a.B / 8 < 0x7fffffff;
+    if (mfma && g_mix_mfma == 3 && (int64_t)a.B * a.out_rs * 4 < 0x7fffffff && (!a.res || a.res_rs % 4 == 0)) {
+        // the LDS-DMA form: slabs of 4 ceil(J / 4) rows, 3 slots (rows r, r + 1, r + 2 in flight)
+        constexpr int R = 8, PF = 2;
+        const int KS = (a.J + 3) / 4;
+        const size_t lds = ((size_t)(PF + 1) * (a.res ? 2 : 1) * 4 * KS * 64 + 128) * sizeof(float);
+        auto kt = a.res ? k_gl5_mixd<R, PF, true> : k_gl5_mixd<R, PF, false>;
+        if (lds > 64 * 1024) {
+            const hipError_t e = hipFuncSetAttribute((const void*)kt, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+            if (e != hipSuccess) return e;
+        }
+        hipLaunchKernelGGL(kt, dim3((unsigned)((a.B + R - 1) / R), (unsigned)(a.N / 64)), dim3(256), lds, s, a,
+                           (const float*)z, z_rs);
+        return hipGetLastError();
+    }
     if (mfma) {
         const dim3 blk(256);
         const unsigned ncb = (unsigned)(a.N / 64);

@@ -83,7 +83,8 @@ enum RouteBits : unsigned {
     kRouteMixPhase = 16,   // k_gl4 MODE 2 / 3: split-route mixing / attention phase
     kRouteV5Mix = 32,      // k_gl5_gemm / k_gl5_mix (J > 21)
     kRouteExact = 64,      // exact-f32 generations v1-v3
-    kRouteAttention = 128  // k_attention: the separate attention kernel (J > 21, unfused routes)
+    kRouteAttention = 128,  // k_attention: the separate attention kernel (J > 21, unfused routes)
+    kRouteFusedSmall = 256  // k_gl4 MODE 4: small-batch fused graph-linear tile
 };
 extern thread_local unsigned g_route_bits;
 

@@ -398,8 +398,10 @@ hipError_t launch_attention(const AttnArgs& a, hipStream_t s) {
 __device__ __forceinline__ uint4 philox(uint4 c, uint32_t k0, uint32_t k1) {
 #pragma unroll
     for (int r = 0; r < 10; ++r) {
-        const uint32_t hi0 = __umulhi(0xD2511F53u, c.x), lo0 = 0xD2511F53u * c.x;
-        const uint32_t hi1 = __umulhi(0xCD9E8D57u, c.z), lo1 = 0xCD9E8D57u * c.z;
+        // one 32 x 32 -> 64-bit product per word (v_mad_u64_u32) instead of a mul_hi + mul_lo pair
+        const uint64_t p0 = (uint64_t)0xD2511F53u * c.x, p1 = (uint64_t)0xCD9E8D57u * c.z;
+        const uint32_t hi0 = (uint32_t)(p0 >> 32), lo0 = (uint32_t)p0;
+        const uint32_t hi1 = (uint32_t)(p1 >> 32), lo1 = (uint32_t)p1;
         c = make_uint4(hi1 ^ c.y ^ k0, lo1, hi0 ^ c.w ^ k1, lo0);
         k0 += 0x9E3779B9u;
         k1 += 0xBB67AE85u;
@@ -410,18 +412,27 @@ __device__ __forceinline__ uint4 philox(uint4 c, uint32_t k0, uint32_t k1) {
 __device__ __forceinline__ float u01(uint32_t x) { return ((float)(x >> 8) + 0.5f) * 5.9604644775390625e-8f; }
 
 // Box-Muller on the exact uniforms u = (2 m + 1) 2^-25, m = x >> 8 (the oracle's, in float64).  In
-// float32 u is exact below 1/2 only (above, the spacing is 2^-24), so ln u0 is taken as
-// logf(u0) for m < 2^23 and as log1pf(-v), v = 1 - u0 = (2^25 - 2 m - 1) 2^-25 (exact), above:
-// relative accuracy everywhere, including next to u0 = 1 where rad is small (float32 u0 and the
-// hardware v_log_f32 each moved z by up to ~5e-5 there).  (cos, sin)(2 pi u1) by an exact quadrant
-// reduction in integers: n = 2 m + 1, q = round(n / 2^23), theta = (n - q 2^23) 2 pi 2^-25 in
+// float32 u = n 2^-25 (n = 2 m + 1) is exact below 1/2 only (above, the spacing is 2^-24), and
+// next to u0 = 1, where rad is small, ln u0 needs relative accuracy (float32 u0 and the hardware
+// v_log_f32 each moved z by up to ~5e-5 there).  Two forms, both evaluated and one selected (no
+// lane-divergent branch): u0 > 1 - 2^-6: ln u0 = log1p(x) with x = -(2^25 - n) 2^-25 exact, by its
+// degree-5 Taylor polynomial (truncation < x^5 / 6, 1.4e-10 relative); otherwise v_log_f32 of the
+// float32 u0 (relative rounding 2^-25, i.e. <= 3e-8 absolute in ln u0 where rad >= 0.17).  ~15 VALU
+// instead of a float64 log (~60 FP64 instructions) or ocml's log1pf (~100).  (cos, sin)(2 pi u1) by an exact
+// quadrant reduction in integers: q = round(n / 2^23), theta = (n - q 2^23) 2 pi 2^-25 in
 // [-pi/4, pi/4], degree-9 / -8 Taylor polynomials (truncation < 3e-9) and the quadrant's rotation
 // (~20 VALU per pair, not sincospif's general range reduction).  Within a few ulp of the exact
 // transform; tests/test_gpu_parity.py holds 4.9 M normals to 2e-5 of the oracle.
 __device__ __forceinline__ floatx2 box_muller(uint32_t a, uint32_t b) {
-    const uint32_t ma = a >> 8;
-    const float lnu = ma < (1u << 23) ? logf((float)(2u * ma + 1u) * 2.98023223876953125e-8f)
-                                      : log1pf(-(float)((1u << 25) - 2u * ma - 1u) * 2.98023223876953125e-8f);
+    const uint32_t n0 = 2u * (a >> 8) + 1u;
+    const uint32_t r0 = (1u << 25) - n0;                                   // 1 - u0 = r0 2^-25
+    const float lg = __builtin_amdgcn_logf((float)n0 * 2.98023223876953125e-8f) * 0.693147180559945309f;
+    const float x = -(float)r0 * 2.98023223876953125e-8f;                  // u0 - 1, exact (r0 < 2^19)
+    float pl = fmaf(x, 0.2f, -0.25f);                                      // log1p: x - x^2/2 + ... + x^5/5
+    pl = fmaf(x, pl, 0.333333343f);
+    pl = fmaf(x, pl, -0.5f);
+    pl = fmaf(x, pl, 1.0f);
+    const float lnu = r0 < (1u << 19) ? x * pl : lg;
     const float rad = __builtin_amdgcn_sqrtf(-2.0f * lnu);
     const int n = (int)(2u * (b >> 8) + 1u);      // u1 = n 2^-25
     const int q = (n + (1 << 22)) >> 23;          // nearest quarter turn, 0 .. 4
@@ -750,10 +761,17 @@ __global__ __launch_bounds__(256) void k_update_row(const UpdArgs p) {
 template <int JP, int R, int MT>
 __global__ __launch_bounds__(256) void k_update_mfma(const UpdArgs p) {
     constexpr int KS = JP / 4, IB = JP / 16;
+    // table rows JP + 2 floats apart: an A-fragment read (lanes 0-31 = rows i = l16, k columns l4 in
+    // {0, 1}) then hits 32 distinct banks; at a JP stride the 16 rows shared one or two banks (16-way
+    // conflicts on every ds_read_b32 of the J <= 64 form, which re-reads its fragments per tile)
+    constexpr int TSJ = JP + 2;
     const int J = p.J, D = p.D, JD = J * D, QPR = J * (D >> 2);  // quads per row
     extern __shared__ __attribute__((aligned(16))) float sm[];
-    float* sTab = sm;                        // [3][JP][JP] zero-padded C1, C2, U
-    float* sEv = sm + 3 * JP * JP;           // [R][J][D] sigma_j . eps
+    float* sTab = sm;                        // [3][JP][TSJ] zero-padded C1, C2, U
+    // [R][J][D + 16] sigma_j . eps (16-B aligned; the + 16 puts the k columns l4 = 0 / 1 of a B
+    // fragment read in different bank halves)
+    const int DS = D + 16;
+    float* sEv = sm + ((3 * JP * TSJ + 3) & ~3);
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int64_t rowg = (int64_t)blockIdx.x * R;
@@ -788,8 +806,10 @@ __global__ __launch_bounds__(256) void k_update_mfma(const UpdArgs p) {
             tv[k] = (q < 3 * JP * JP && i < J && j < J) ? tab[i * J + j] : 0.f;
         }
 #pragma unroll
-        for (int k = 0; k < TPT; ++k)
-            if (tid + 256 * k < 3 * JP * JP) sTab[tid + 256 * k] = tv[k];
+        for (int k = 0; k < TPT; ++k) {
+            const int q = tid + 256 * k;
+            if (q < 3 * JP * JP) sTab[(q / JP) * TSJ + q % JP] = tv[k];
+        }
     }
     uint64_t seed = p.seed;
     int64_t row0 = p.row0;
@@ -813,7 +833,7 @@ __global__ __launch_bounds__(256) void k_update_mfma(const UpdArgs p) {
         }
         if (p.noise_out) *reinterpret_cast<floatx4*>(p.noise_out + rw * p.noise_rs + j * D + d) = e;
         if (p.noise_mode != 0) e *= p.sig[j];
-        *reinterpret_cast<floatx4*>(sEv + (rr * J + j) * D + d) = e;
+        *reinterpret_cast<floatx4*>(sEv + (rr * J + j) * DS + d) = e;
         if (p.dump_ev) *reinterpret_cast<floatx4*>(p.dump_ev + rw * JD + j * D + d) = e;
     }
     __syncthreads();
@@ -827,7 +847,7 @@ __global__ __launch_bounds__(256) void k_update_mfma(const UpdArgs p) {
 #pragma unroll
         for (int m = 0; m < 3; ++m)
 #pragma unroll
-            for (int ks = 0; ks < KS; ++ks) A[m][slot][ks] = sTab[(m * JP + 16 * ib + l16) * JP + 4 * ks + l4];
+            for (int ks = 0; ks < KS; ++ks) A[m][slot][ks] = sTab[(m * JP + 16 * ib + l16) * TSJ + 4 * ks + l4];
     };
     if constexpr (AREG) {
 #pragma unroll
@@ -848,7 +868,7 @@ __global__ __launch_bounds__(256) void k_update_mfma(const UpdArgs p) {
             a = fminf(fmaxf(a, -1.f), 1.f);
             bxa[ks] = ok ? a : 0.f;
             bta[ks] = ok ? bt[q][ks] : 0.f;
-            be[ks] = ok ? sEv[(r * J + j) * D + n] : 0.f;
+            be[ks] = ok ? sEv[(r * J + j) * DS + n] : 0.f;
             if (p.dump_x0 && ok) {
                 p.dump_x0[rb + j * D + n] = a;
                 p.dump_xt[rb + j * D + n] = bt[q][ks];
@@ -903,7 +923,7 @@ hipError_t launch_update(const UpdArgs& a, hipStream_t s) {
     const int Rm = a.B <= g_update_rows ? 1 : 4;
     if (g_update_mfma && !a.iso && a.J > 32 && a.J <= 64 && a.D % 16 == 0 && (a.D / 16 + 3) / 4 <= 2) {
         // J <= 64 (MANO J = 51 / 52): one row per workgroup, each wave at most two column tiles
-        const size_t lds = (3 * 64 * 64 + (size_t)a.J * a.D) * sizeof(float);
+        const size_t lds = (((3 * 64 * 66 + 3) & ~(size_t)3) + (size_t)a.J * (a.D + 16)) * sizeof(float);
         if (lds > 160 * 1024) return hipErrorNotSupported;
         if (lds > 64 * 1024) {
             const hipError_t e = hipFuncSetAttribute((const void*)k_update_mfma<64, 1, 2>,
@@ -919,16 +939,18 @@ hipError_t launch_update(const UpdArgs& a, hipStream_t s) {
         // small batches: one row per workgroup (4 waves share its column tiles), else 4 rows
         const int R = Rm;
         const dim3 grid((unsigned)((a.B + R - 1) / R));
-        if (a.J <= 16) {
-            const size_t lds = (3 * 16 * 16 + (size_t)R * a.J * a.D) * sizeof(float);
-            if (R == 1) hipLaunchKernelGGL((k_update_mfma<16, 1, 2>), grid, dim3(256), lds, s, a);
-            else hipLaunchKernelGGL((k_update_mfma<16, 4, 6>), grid, dim3(256), lds, s, a);
-        } else {
-            const size_t lds = (3 * 32 * 32 + (size_t)R * a.J * a.D) * sizeof(float);
-            if (R == 1) hipLaunchKernelGGL((k_update_mfma<32, 1, 2>), grid, dim3(256), lds, s, a);
-            else hipLaunchKernelGGL((k_update_mfma<32, 4, 6>), grid, dim3(256), lds, s, a);
-        }
-        return hipGetLastError();
+        auto go = [&](auto kern, int JP) -> hipError_t {
+            const size_t lds = (((3 * (size_t)JP * (JP + 2) + 3) & ~(size_t)3) + (size_t)R * a.J * (a.D + 16)) * sizeof(float);
+            if (lds > 160 * 1024) return hipErrorNotSupported;
+            if (lds > 64 * 1024) {
+                const hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+                if (e != hipSuccess) return e;
+            }
+            hipLaunchKernelGGL(kern, grid, dim3(256), lds, s, a);
+            return hipGetLastError();
+        };
+        if (a.J <= 16) return R == 1 ? go(k_update_mfma<16, 1, 2>, 16) : go(k_update_mfma<16, 4, 6>, 16);
+        return R == 1 ? go(k_update_mfma<32, 1, 2>, 32) : go(k_update_mfma<32, 4, 6>, 32);
     }
     if (a.B <= g_update_rows && a.D % 2 == 0) {
         const size_t nt = a.iso ? 0 : 3 * (size_t)a.J * a.J + a.J;

@@ -1376,9 +1376,9 @@ int sd_plan_set_option(sd_plan* p, int32_t option, int64_t value) {
         case SD_OPT_LAST_CHAINS:
         case SD_OPT_LAST_ROUTE: return fail(SD_E_INVALID, "SD_OPT_LAST_CHAINS / SD_OPT_LAST_ROUTE are read-only");
         case SD_OPT_SPLIT_ROUTE:
-            if (value < 0 || value > 4)
-                return fail(SD_E_INVALID, "split route must be 0 (auto), 1 (never), 2 (always), 3 (always, tiled phase 1) "
-                                          "or 4 (tiled phase 1 except to_qkv + attention)");
+            if (value < 0 || value > 5)
+                return fail(SD_E_INVALID, "split route must be 0 (auto), 1 (never), 2 (always), 3 (always, tiled phase 1), "
+                                          "4 (tiled phase 1 except to_qkv + attention) or 5 (small-batch fused tile)");
             p->split = (int)value;
             return SD_OK;
         case SD_OPT_UPDATE_KERNEL:

@@ -747,7 +747,7 @@ __global__ __launch_bounds__(256) void k_mahalanobis(const float* __restrict__ m
             const int j = e / F, f = e - j * F;
             float a = 0.f;
             for (int i = 0; i < J; ++i) a = fmaf(sS[i * J + j], sM[i * F + f], a);
-            o[e] = sgn * a;
+            o[e] = sgn * a + bad;  // an out-of-range timestep: NaN (sign(NaN) above gave 0)
         }
     }
 }

@@ -185,9 +185,11 @@ def test_strong_scaling_shards_chain_invariant(batch, cuda):
                                           ("amass21", 4, {}), ("freeman17", 2, {}),
                                           ("amass16", 4, {"precision": "half"})])
 def test_split_route_bitwise(cfg, batch, kw, cuda):
-    """SD_OPT_SPLIT_ROUTE: the small-launch route (k_gl4y GEMM phase per (tile,
-    node, column tile) + k_gl4 MODE 2 / 3 mixing or attention phase) is bitwise equal to the
-    one-kernel route, graph and eager, with the f16 range guard word untouched."""
+    """SD_OPT_SPLIT_ROUTE (DESIGN.md §4d'): the small-launch routes -- 2: k_gl4y GEMM phase per
+    (tile, node, column tile) + k_gl4 MODE 2 / 3 mixing or attention phase; 5: the fused
+    small-batch tile k_gl4 MODE 4 for the plain graph-linears (J = 16) -- are bitwise equal to the
+    one-kernel route, graph and eager, with the f16 range guard word untouched and the kernels
+    each route launched asserted."""
     from bench import build_config
 
     d, x_cond, rows = build_config(cfg, cuda, T=10, batch=batch)
@@ -198,11 +200,18 @@ def test_split_route_bitwise(cfg, batch, kw, cuda):
     eng.set_option("split_route", 1)
     ref = eng.sample_loop(rows, x_cond=x_cond, seed=5, record=(False, True))
     ref = [ref[0].clone(), ref[4].clone()]
-    eng.set_option("split_route", 2)
-    for graph in (False, True):
-        got = eng.sample_loop(rows, x_cond=x_cond, seed=5, graph=graph, record=(False, True))
-        torch.cuda.synchronize()
-        assert torch.equal(got[0], ref[0]) and torch.equal(got[4], ref[1]), (cfg, batch, graph)
+    J = x_cond.shape[1]
+    for route in (2, 5):
+        eng.set_option("split_route", route)
+        for graph in (False, True):
+            got = eng.sample_loop(rows, x_cond=x_cond, seed=5, graph=graph, record=(False, True))
+            torch.cuda.synchronize()
+            assert torch.equal(got[0], ref[0]) and torch.equal(got[4], ref[1]), (cfg, batch, route, graph)
+        bits = eng.get_option("last_route")
+        if route == 5 and J == 16:
+            assert bits & 256 and bits & 4, bits  # MODE 4 tiles + the k_gl4y attention phase 1
+        else:
+            assert not bits & 256, bits
     assert eng.status(rows) == 0
 
 

@@ -233,6 +233,234 @@ __global__ __launch_bounds__(NWV * 64, NWV == 4 ? 2 : 1) void k_probe(const floa
     }
 }
 
+// V1 generalised: CTT 32-column tiles per workgroup (column group fastest in the XCD-aware order,
+// as the library), NN output columns (192 or 768: to_qkv), LDS-DMA weight ring PF ahead.
+template <int NN, int CTT, int NWV, int PF, int F>
+__global__ __launch_bounds__(NWV * 64, 2) void k_ring(const float* __restrict__ x, const _Float16* __restrict__ wsp,
+                                                      float* __restrict__ y, int64_t ntile_r) {
+    constexpr int NT = NWV * 64, NCTT = NN / 32, ncg = NCTT / CTT;
+    constexpr int TILE_H = 1024, PPT = TILE_H / 8, NPC = CTT * PPT;
+    constexpr int NS = PF + 1, TS = 36;
+    constexpr int SBW = NS * CTT * TILE_H * 2;
+    constexpr int SB = SBW > NWV * 32 * TS * 4 ? SBW : NWV * 32 * TS * 4;
+    __shared__ __attribute__((aligned(16))) char smem[SB];
+    _Float16(*sW)[CTT * TILE_H] = reinterpret_cast<_Float16(*)[CTT * TILE_H]>(smem);
+    const int tid = threadIdx.x, lane = tid & 63, l32 = lane & 31, h = lane >> 5;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int nwg = gridDim.x, xcd = blockIdx.x & 7, q8 = nwg >> 3, r8 = nwg & 7;
+    const int64_t u = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (blockIdx.x >> 3);
+    const int cg = (int)(u % ncg);
+    const int64_t nrg = (ntile_r + NWV - 1) / NWV;
+    const int j = (int)((u / ncg) / nrg);
+    const int64_t tr = ((u / ncg) % nrg) * NWV + wave;
+    const bool live = tr < ntile_r;
+    const int64_t row0 = (live ? tr : 0) * 32;
+    const float* xr = x + blk_off(row0 + l32, j, 8 * h);
+    const _Float16* wb = wsp + ((int64_t)c_type[j] * NCH * NCTT + cg * CTT) * 1024;
+    floatx4 xa[PF], xb[PF];
+    auto issue_x = [&](int c, int sl) {
+        xa[sl] = g4(xr + (c << 9));
+        xb[sl] = g4(xr + (c << 9) + 128);
+    };
+    floatx16 acc[CTT];
+#pragma unroll
+    for (int ct = 0; ct < CTT; ++ct)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) acc[ct][e] = 0.f;
+    auto compute = [&](int sl, const _Float16* wst) {
+        const floatx8 f = {xa[sl].x, xa[sl].y, xa[sl].z, xa[sl].w, xb[sl].x, xb[sl].y, xb[sl].z, xb[sl].w};
+        const halfx8 xh = __builtin_convertvector(f, halfx8);
+        const halfx8 xl = __builtin_convertvector(f - __builtin_convertvector(xh, floatx8), halfx8);
+        const _Float16* wt = wst + lane * 8;
+#pragma unroll
+        for (int ct = 0; ct < CTT; ++ct) {
+            const halfx8 wh = *reinterpret_cast<const halfx8*>(wt + ct * TILE_H);
+            const halfx8 wl = *reinterpret_cast<const halfx8*>(wt + ct * TILE_H + 512);
+            if constexpr (F & NOMFMA) {
+                acc[ct][0] += (float)wh[0] + (float)wl[1] + (float)xh[ct & 7] + (float)xl[ct & 7];
+            } else {
+                floatx16 t = __builtin_amdgcn_mfma_f32_32x32x16_f16(xh, wh, acc[ct], 0, 0, 0);
+                t = __builtin_amdgcn_mfma_f32_32x32x16_f16(xh, wl, t, 0, 0, 0);
+                acc[ct] = __builtin_amdgcn_mfma_f32_32x32x16_f16(xl, wh, t, 0, 0, 0);
+            }
+        }
+    };
+    constexpr int KW = (NPC / 64 + NWV - 1) / NWV;
+    auto fill = [&](int c) {
+        _Float16* dst = sW[c % NS];
+#pragma unroll
+        for (int k = 0; k < KW; ++k) {
+            const int q0 = wave * 64 + NT * k;
+            if (q0 >= NPC) continue;
+            const int q = q0 + lane;
+            __builtin_amdgcn_global_load_lds((const void*)(wb + ((int64_t)c * NCTT + q / PPT) * 1024 + (q % PPT) * 8),
+                                             (lds_void*)(dst + (size_t)q0 * 8), 16, 0, 0);
+        }
+    };
+    constexpr int PA = KW + 2, PB = (NPC / 64) / NWV + 2;
+    const bool wa = wave * 64 + NT * (KW - 1) < NPC;
+    auto wait = [&](int n) {
+#define W_(m) if (wa) __builtin_amdgcn_s_waitcnt(((PA * (m)) & 0xF) | (0x7 << 4) | (0xF << 8) | (((PA * (m)) >> 4) << 14)); \
+              else __builtin_amdgcn_s_waitcnt(((PB * (m)) & 0xF) | (0x7 << 4) | (0xF << 8) | (((PB * (m)) >> 4) << 14));
+        if (n == 0) { W_(0) } else if (n == 1) { W_(1) } else if (n == 2) { W_(2) } else { W_(3) }
+#undef W_
+        asm volatile("" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+    };
+#pragma unroll
+    for (int i = 0; i < PF; ++i) {
+        fill(i);
+        issue_x(i, i);
+    }
+#pragma nounroll
+    for (int c0 = 0; c0 < NCH - PF; c0 += PF) {
+#pragma unroll
+        for (int i = 0; i < PF; ++i) {
+            const int c = c0 + i;
+            wait(PF - 1);
+            compute(i, sW[c % NS]);
+            asm volatile("" ::: "memory");
+            fill(c + PF);
+            issue_x(c + PF, i);
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < PF; ++i) {
+        wait(PF - 1 - i);
+        compute(i, sW[(NCH - PF + i) % NS]);
+        asm volatile("" ::: "memory");
+    }
+    __syncthreads();
+    if (!live) return;
+    float* sT = reinterpret_cast<float*>(smem) + wave * 32 * TS;
+    float* yo = y + ((tr * J + j) * 32) * (int64_t)NN + cg * CTT * 32;
+#pragma unroll
+    for (int ct = 0; ct < CTT; ++ct) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) sT[((r & 3) + 8 * (r >> 2) + 4 * h) * TS + l32] = acc[ct][r];
+        __builtin_amdgcn_wave_barrier();
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int row = 8 * q + (lane >> 3), c4 = (lane & 7) * 4;
+            *reinterpret_cast<floatx4*>(yo + (int64_t)row * NN + ct * 32 + c4) = *reinterpret_cast<const floatx4*>(sT + row * TS + c4);
+        }
+        __builtin_amdgcn_wave_barrier();
+    }
+}
+
+// V2: x too by LDS-DMA (each wave its own 2-KiB chunk image per slot), so the K loop holds no
+// register-writing global load: no vmcnt the compiler must guess, all waits counted by hand.
+template <int NN, int CTT, int NWV, int PF, int F>
+__global__ __launch_bounds__(NWV * 64, 2) void k_ring2(const float* __restrict__ x, const _Float16* __restrict__ wsp,
+                                                       float* __restrict__ y, int64_t ntile_r) {
+    constexpr int NT = NWV * 64, NCTT = NN / 32, ncg = NCTT / CTT;
+    constexpr int TILE_H = 1024, PPT = TILE_H / 8, NPC = CTT * PPT;
+    constexpr int NS = PF + 1, TS = 36;
+    constexpr int WSL = CTT * TILE_H * 2;          // bytes of a weight slot
+    constexpr int XSL = NWV * 2048;                // bytes of an x slot (2 KiB per wave)
+    constexpr int SBW = NS * (WSL + XSL);
+    constexpr int SB = SBW > NWV * 32 * TS * 4 ? SBW : NWV * 32 * TS * 4;
+    __shared__ __attribute__((aligned(16))) char smem[SB];
+    const int tid = threadIdx.x, lane = tid & 63, l32 = lane & 31, h = lane >> 5;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int nwg = gridDim.x, xcd = blockIdx.x & 7, q8 = nwg >> 3, r8 = nwg & 7;
+    const int64_t u = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (blockIdx.x >> 3);
+    const int cg = (int)(u % ncg);
+    const int64_t nrg = (ntile_r + NWV - 1) / NWV;
+    const int j = (int)((u / ncg) / nrg);
+    const int64_t tr = ((u / ncg) % nrg) * NWV + wave;
+    const bool live = tr < ntile_r;
+    const int64_t row0 = (live ? tr : 0) * 32;
+    const float* xblk = x + blk_off(row0, j, 0);  // the wave's (row tile, node) region: chunk c at + 512 c floats
+    const _Float16* wb = wsp + ((int64_t)c_type[j] * NCH * NCTT + cg * CTT) * 1024;
+    auto wslot = [&](int sl) { return reinterpret_cast<_Float16*>(smem + sl * (WSL + XSL)); };
+    auto xslot = [&](int sl) { return reinterpret_cast<float*>(smem + sl * (WSL + XSL) + WSL) + wave * 512; };
+    floatx16 acc[CTT];
+#pragma unroll
+    for (int ct = 0; ct < CTT; ++ct)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) acc[ct][e] = 0.f;
+    constexpr int KW = (NPC / 64 + NWV - 1) / NWV;
+    auto fill = [&](int c) {
+        _Float16* dst = wslot(c % NS);
+#pragma unroll
+        for (int k = 0; k < KW; ++k) {
+            const int q0 = wave * 64 + NT * k;
+            if (q0 >= NPC) continue;
+            const int q = q0 + lane;
+            __builtin_amdgcn_global_load_lds((const void*)(wb + ((int64_t)c * NCTT + q / PPT) * 1024 + (q % PPT) * 8),
+                                             (lds_void*)(dst + (size_t)q0 * 8), 16, 0, 0);
+        }
+        float* xd = xslot(c % NS);
+        __builtin_amdgcn_global_load_lds((const void*)(xblk + c * 512 + lane * 4), (lds_void*)xd, 16, 0, 0);
+        __builtin_amdgcn_global_load_lds((const void*)(xblk + c * 512 + 256 + lane * 4), (lds_void*)(xd + 256), 16, 0, 0);
+    };
+    auto compute = [&](int c) {
+        const float* xs = xslot(c % NS);
+        const floatx4 xa = *reinterpret_cast<const floatx4*>(xs + h * 256 + l32 * 4);
+        const floatx4 xb = *reinterpret_cast<const floatx4*>(xs + h * 256 + 128 + l32 * 4);
+        const floatx8 f = {xa.x, xa.y, xa.z, xa.w, xb.x, xb.y, xb.z, xb.w};
+        const halfx8 xh = __builtin_convertvector(f, halfx8);
+        const halfx8 xl = __builtin_convertvector(f - __builtin_convertvector(xh, floatx8), halfx8);
+        const _Float16* wt = wslot(c % NS) + lane * 8;
+#pragma unroll
+        for (int ct = 0; ct < CTT; ++ct) {
+            const halfx8 wh = *reinterpret_cast<const halfx8*>(wt + ct * TILE_H);
+            const halfx8 wl = *reinterpret_cast<const halfx8*>(wt + ct * TILE_H + 512);
+            floatx16 t = __builtin_amdgcn_mfma_f32_32x32x16_f16(xh, wh, acc[ct], 0, 0, 0);
+            t = __builtin_amdgcn_mfma_f32_32x32x16_f16(xh, wl, t, 0, 0, 0);
+            acc[ct] = __builtin_amdgcn_mfma_f32_32x32x16_f16(xl, wh, t, 0, 0, 0);
+        }
+    };
+    constexpr int PA = KW + 2, PB = (NPC / 64) / NWV + 2;
+    const bool wa = wave * 64 + NT * (KW - 1) < NPC;
+    auto wait = [&](int n) {
+#define W_(m) if (wa) __builtin_amdgcn_s_waitcnt(((PA * (m)) & 0xF) | (0x7 << 4) | (0xF << 8) | (((PA * (m)) >> 4) << 14)); \
+              else __builtin_amdgcn_s_waitcnt(((PB * (m)) & 0xF) | (0x7 << 4) | (0xF << 8) | (((PB * (m)) >> 4) << 14));
+        if (n == 0) { W_(0) } else if (n == 1) { W_(1) } else if (n == 2) { W_(2) } else { W_(3) }
+#undef W_
+        asm volatile("" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+    };
+#pragma unroll
+    for (int i = 0; i < PF; ++i) fill(i);
+#pragma nounroll
+    for (int c0 = 0; c0 < NCH - PF; c0 += PF) {
+#pragma unroll
+        for (int i = 0; i < PF; ++i) {
+            const int c = c0 + i;
+            wait(PF - 1);
+            compute(c);
+            asm volatile("" ::: "memory");
+            fill(c + PF);
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < PF; ++i) {
+        wait(PF - 1 - i);
+        compute(NCH - PF + i);
+        asm volatile("" ::: "memory");
+    }
+    __syncthreads();
+    if (!live) return;
+    float* sT = reinterpret_cast<float*>(smem) + wave * 32 * TS;
+    float* yo = y + ((tr * J + j) * 32) * (int64_t)NN + cg * CTT * 32;
+#pragma unroll
+    for (int ct = 0; ct < CTT; ++ct) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) sT[((r & 3) + 8 * (r >> 2) + 4 * h) * TS + l32] = acc[ct][r];
+        __builtin_amdgcn_wave_barrier();
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int row = 8 * q + (lane >> 3), c4 = (lane & 7) * 4;
+            *reinterpret_cast<floatx4*>(yo + (int64_t)row * NN + ct * 32 + c4) = *reinterpret_cast<const floatx4*>(sT + row * TS + c4);
+        }
+        __builtin_amdgcn_wave_barrier();
+    }
+}
+
 // the x stream alone: every wave reads its 24 KB (row tile, node) region in 12 chunks of 2 x 1 KB,
 // PF chunks in flight, and sums it (the bandwidth ceiling of k_gl4t's x access pattern)
 template <int PF>
@@ -256,18 +484,19 @@ int main(int argc, char** argv) {
     const int reps = argc > 2 ? atoi(argv[2]) : 50;
     const int64_t ntile_r = (rows + 31) / 32, rp = ntile_r * 32;
     const size_t nx = rp * J * K, ny = rp * J * N, nw = (size_t)NTYPES * NCH * NCT * 1024;
+    const size_t ny4 = rp * J * 768, nw4 = (size_t)NTYPES * NCH * 24 * 1024;
     float *x, *y;
     _Float16* w;
     CHECK(hipMalloc(&x, nx * 4));
-    CHECK(hipMalloc(&y, ny * 4));
-    CHECK(hipMalloc(&w, nw * 2));
+    CHECK(hipMalloc(&y, ny4 * 4));
+    CHECK(hipMalloc(&w, nw4 * 2));
     {
         std::vector<float> hx(nx);
         for (size_t i = 0; i < nx; ++i) hx[i] = (float)((i * 2654435761u) % 2001) / 1000.f - 1.f;
         CHECK(hipMemcpy(x, hx.data(), nx * 4, hipMemcpyHostToDevice));
-        std::vector<_Float16> hw(nw);
-        for (size_t i = 0; i < nw; ++i) hw[i] = (_Float16)(((i * 40503u) % 2001) / 20000.f - 0.05f);
-        CHECK(hipMemcpy(w, hw.data(), nw * 2, hipMemcpyHostToDevice));
+        std::vector<_Float16> hw(nw4);
+        for (size_t i = 0; i < nw4; ++i) hw[i] = (_Float16)(((i * 40503u) % 2001) / 20000.f - 0.05f);
+        CHECK(hipMemcpy(w, hw.data(), nw4 * 2, hipMemcpyHostToDevice));
     }
     const double bytes = (double)nx * 4 + (double)ny * 4 + (double)nw * 2;
     hipEvent_t e0, e1;
@@ -296,25 +525,30 @@ int main(int argc, char** argv) {
         hipLaunchKernelGGL((k_xstream<12>), dim3((unsigned)(((ntile_r + 3) / 4) * J)), dim3(256), 0, 0, x, y, ntile_r);
     }, (double)nx * 4);
     RUN("V0 production", 0, 0, 4, 4);
-    RUN("V0 acc-native Y", 0, ACCY, 4, 4);
-    RUN("V1 DMA ring PF 2 acc-native Y", 1, ACCY, 4, 2);
-    RUN("V1 DMA ring PF 3 acc-native Y", 1, ACCY, 4, 3);
-    RUN("V1 DMA ring PF 4 acc-native Y", 1, ACCY, 4, 4);
-    RUN("V1 PF 3 accY, no MFMA", 1, ACCY | NOMFMA, 4, 3);
-    RUN("V1 PF 3 accY, no weights", 1, ACCY | NOW, 4, 3);
-    RUN("V1 PF 3 accY, no x", 1, ACCY | NOX, 4, 3);
-    RUN("V0 no MFMA", 0, NOMFMA, 4, 4);
-    RUN("V0 no x loads", 0, NOX, 4, 4);
-    RUN("V0 no weight loads", 0, NOW, 4, 4);
-    RUN("V0 no Y stores", 0, NOY, 4, 4);
-    RUN("V0 only x loads + Y", 0, NOMFMA | NOW, 4, 4);
-    RUN("V0 only MFMA (no x, no w)", 0, NOX | NOW, 4, 4);
-    RUN("V0 only MFMA + Y", 0, NOX | NOW | NOY, 4, 4);
     RUN("V1 DMA ring PF 2", 1, 0, 4, 2);
-    RUN("V1 DMA ring PF 3", 1, 0, 4, 3);
-    RUN("V1 DMA ring PF 4", 1, 0, 4, 4);
-    RUN("V1 DMA ring PF 4 no MFMA", 1, NOMFMA, 4, 4);
-    RUN("V1 DMA ring PF 3, 8 waves", 1, 0, 8, 3);
-    RUN("V1 DMA ring PF 4, 8 waves", 1, 0, 8, 4);
+#define RING(NAME, NN, CTT, NWV, PF, F)                                                                          \
+    timeit(NAME, [&] {                                                                                           \
+        const unsigned g = (unsigned)(((ntile_r + NWV - 1) / NWV) * J * ((NN / 32) / CTT));                       \
+        hipLaunchKernelGGL((k_ring<NN, CTT, NWV, PF, F>), dim3(g), dim3(NWV * 64), 0, 0, x, w, y, ntile_r);      \
+    }, (double)nx * 4 + (double)rp * J * NN * 4 + (double)NTYPES * NCH * (NN / 32) * 2048)
+#define RING2(NAME, NN, CTT, NWV, PF)                                                                            \
+    timeit(NAME, [&] {                                                                                           \
+        const unsigned g = (unsigned)(((ntile_r + NWV - 1) / NWV) * J * ((NN / 32) / CTT));                       \
+        hipLaunchKernelGGL((k_ring2<NN, CTT, NWV, PF, 0>), dim3(g), dim3(NWV * 64), 0, 0, x, w, y, ntile_r);     \
+    }, (double)nx * 4 + (double)rp * J * NN * 4 + (double)NTYPES * NCH * (NN / 32) * 2048)
+    RING2("ring2 (x by DMA) N192 CT6 4w PF2", 192, 6, 4, 2);
+    RING2("ring2 (x by DMA) N192 CT6 4w PF3", 192, 6, 4, 3);
+    RING2("ring2 (x by DMA) N768 CT6 4w PF2", 768, 6, 4, 2);
+    RING2("ring2 (x by DMA) N768 CT6 4w PF3", 768, 6, 4, 3);
+    RING("ring N192 CT6 4w PF2", 192, 6, 4, 2, 0);
+    RING("ring N192 CT3 4w PF2", 192, 3, 4, 2, 0);
+    RING("ring N192 CT3 4w PF3", 192, 3, 4, 3, 0);
+    RING("ring N192 CT2 4w PF2", 192, 2, 4, 2, 0);
+    RING("ring N192 CT6 2w PF2", 192, 6, 2, 2, 0);
+    RING("ring N192 CT3 2w PF2", 192, 3, 2, 2, 0);
+    RING("ring N768 CT6 4w PF2", 768, 6, 4, 2, 0);
+    RING("ring N768 CT6 4w PF3", 768, 6, 4, 3, 0);
+    RING("ring N768 CT3 4w PF2", 768, 3, 4, 2, 0);
+    RING("ring N768 CT6 4w PF2 no MFMA", 768, 6, 4, 2, NOMFMA);
     return 0;
 }

@@ -16,11 +16,11 @@ import bench  # noqa: E402
 
 DEFAULT = ["amass16", "amass16:32", "amass16:16", "amass16:8", "freeman17", "amass21", "mano51", "h36m_t1000",
            "freeman17_bf16:1377:10"]
-ROUTES = {"amass16": [0, 1, 3, 4], "amass21": [0, 1, 3, 4], "freeman17": [0, 1, 3, 4],
-          "freeman17_bf16": [0, 1, 3, 4], "mano51": [0], "h36m_t1000": [0, 1]}
+ROUTES = {"amass16": [0, 1, 2, 3], "amass21": [0, 2, 3], "freeman17": [0, 2, 3],
+          "freeman17_bf16": [0, 1, 3], "mano51": [0], "h36m_t1000": [0, 1, 2, 5]}
 ROUTES = {k: [int(x) for x in os.environ["SWEEP_ROUTES"].split(",")] for k in ROUTES} if os.environ.get("SWEEP_ROUTES") \
     else ROUTES
-CHAINS = [int(x) for x in os.environ.get("SWEEP_CHAINS", "1,2,3,4").split(",")]
+CHAINS = [int(x) for x in os.environ.get("SWEEP_CHAINS", "1,2,3").split(",")]
 dev = torch.device("cuda", 0)
 out_rows = []
 for spec in (sys.argv[1:] or DEFAULT):
