@@ -275,7 +275,7 @@ enum {
                                    2 = 0 (a round-2 diagnostic setting, kept for compatibility) */
     SD_OPT_SPLIT_ROUTE = 6,     /* v4 split route (GEMM phase per (tile, node) + mixing phase,
                                    DESIGN.md §4d'; bitwise identical results): 0 auto (k_gl4y at
-                                   <= SKELDIFF_SPLIT_ROWS rows of the call, default 640; k_gl4t
+                                   <= SKELDIFF_SPLIT_ROWS rows of the call, default 1200; k_gl4t
                                    for full batches where measured faster), 1 never, 2 always
                                    (k_gl4y), 3 always with the tiled GEMM phase (k_gl4t: 128 rows
                                    x up to 192 columns of one node per workgroup), 4 the tiled

@@ -348,7 +348,14 @@ __device__ unsigned long long g_gl4t_stamps[8192 * 4];
 __device__ unsigned long long g_gl4t_clock[8192 * 2];  // shader clock (s_memtime) at entry and loop end
 __device__ unsigned long long g_gl4t_chunk[8192 * 16];  // per workgroup: s_memrealtime after each chunk's barrier
 #endif
-template <bool RMS, int PREC, int CT, int NCH, bool ROWMAJOR, int PF = 2, int NWV = 4, bool WRES = false>
+// RSTG: the round-3 K loop (weights register-staged into two LDS stages one chunk ahead, x in a
+// PF-deep register ring; 24 KiB of LDS at CT = 6 against the LDS-DMA ring's 60 KiB)
+// ILV: per chunk every weight fragment read from LDS first, then the MFMAs product-major (x_hi W_hi
+// for all CT tiles, then x_hi W_lo, then x_lo W_hi): each accumulator sees the same three products
+// in the same order (bitwise equal), but no tile waits on its own LDS read behind the previous
+// tile's MFMAs and consecutive MFMAs are independent
+template <bool RMS, int PREC, int CT, int NCH, bool ROWMAJOR, int PF = 2, int NWV = 4, bool WRES = false, bool RSTG = false,
+          bool ILV = false>
 __global__ __launch_bounds__(NWV * 64, WRES ? 1 : 2) void k_gl4t(const GLArgs p, int ncg, int64_t ntile_r, const YOut yo) {
     constexpr int NT = NWV * 64;
     constexpr int TILE_H = PREC ? 512 : 1024;   // halves of one 32-column tile per chunk
@@ -359,9 +366,9 @@ __global__ __launch_bounds__(NWV * 64, WRES ? 1 : 2) void k_gl4t(const GLArgs p,
     // x through the LDS-DMA ring too (f32 operands): per slot and wave the chunk's 32 rows x 16 k
     // image (2 KiB) -- no register-writing global load in the K loop, so the compiler inserts no
     // vmcnt of its own (with a tracked x load beside an LDS-DMA it drained vmcnt(0) every chunk)
-    constexpr bool XDMA = !WRES && PREC != 2;
+    constexpr bool XDMA = !WRES && !RSTG && PREC != 2;
     constexpr int XSB = XDMA ? NS * NWV * 2048 : 0;  // bytes of the x slots (after the weight slots)
-    constexpr int SBW = (WRES ? NCH : NS) * CT * TILE_H * 2 + XSB;
+    constexpr int SBW = (WRES ? NCH : RSTG ? 2 : NS) * CT * TILE_H * 2 + XSB;
     constexpr int SB = SBW > NWV * 32 * TS * 4 ? SBW : NWV * 32 * TS * 4;
     static_assert(!WRES || SB <= 160 * 1024, "resident weight slice exceeds the LDS");
     __shared__ __attribute__((aligned(16))) char smem_raw[SB];  // weight stages, then the transposes
@@ -465,6 +472,23 @@ __global__ __launch_bounds__(NWV * 64, WRES ? 1 : 2) void k_gl4t(const GLArgs p,
         halfx8 xl;
         if constexpr (!PREC) xl = __builtin_convertvector(f - __builtin_convertvector(xh, floatx8), halfx8);
         const _Float16* wt = wst + lane * 8;
+        if constexpr (ILV) {
+            halfx8 wh[CT], wl[CT];
+#pragma unroll
+            for (int ct = 0; ct < CT; ++ct) {
+                wh[ct] = *reinterpret_cast<const halfx8*>(wt + ct * TILE_H);
+                if constexpr (!PREC) wl[ct] = *reinterpret_cast<const halfx8*>(wt + ct * TILE_H + 512);
+            }
+#pragma unroll
+            for (int ct = 0; ct < CT; ++ct) acc[ct] = __builtin_amdgcn_mfma_f32_32x32x16_f16(xh, wh[ct], acc[ct], 0, 0, 0);
+            if constexpr (!PREC) {
+#pragma unroll
+                for (int ct = 0; ct < CT; ++ct) acc[ct] = __builtin_amdgcn_mfma_f32_32x32x16_f16(xh, wl[ct], acc[ct], 0, 0, 0);
+#pragma unroll
+                for (int ct = 0; ct < CT; ++ct) acc[ct] = __builtin_amdgcn_mfma_f32_32x32x16_f16(xl, wh[ct], acc[ct], 0, 0, 0);
+            }
+            return;
+        }
 #pragma unroll
         for (int ct = 0; ct < CT; ++ct) {
             const halfx8 wh = *reinterpret_cast<const halfx8*>(wt + ct * TILE_H);
@@ -521,6 +545,61 @@ __global__ __launch_bounds__(NWV * 64, WRES ? 1 : 2) void k_gl4t(const GLArgs p,
                 }
             }
         }
+    } else if constexpr (RSTG) {
+    // staged pieces: piece q of a chunk = tile q / PPT, 16-B piece q % PPT of it
+    const _Float16* wsrc[NP];
+#pragma unroll
+    for (int k = 0; k < NP; ++k) {
+        const int q = min(tid + NT * k, CT * PPT - 1);
+        wsrc[k] = p.wsp + ((int64_t)p.ntype[j] * nchunk * p.wsp_nct + cg * CT + q / PPT) * 1024 + (q % PPT) * 8;
+    }
+    const int64_t wcs = (int64_t)p.wsp_nct * 1024;  // halves per chunk
+    // the carried pieces as named registers, loaded unconditionally from clamped sources (an
+    // array under conditional loads was placed in scratch, with a vmcnt(0) before every store)
+    static_assert(NP <= 4, "staged pieces per thread");
+    uint4 w0, w1, w2, w3;
+    auto load_w = [&](int c) {
+        const int64_t o = c * wcs;
+        w0 = *reinterpret_cast<const uint4*>(wsrc[0] + o);
+        if constexpr (NP > 1) w1 = *reinterpret_cast<const uint4*>(wsrc[1] + o);
+        if constexpr (NP > 2) w2 = *reinterpret_cast<const uint4*>(wsrc[2] + o);
+        if constexpr (NP > 3) w3 = *reinterpret_cast<const uint4*>(wsrc[3] + o);
+    };
+    auto store_w = [&](int sl) {
+        uint4* d = reinterpret_cast<uint4*>(&sW[sl][tid * 8]);
+        constexpr bool FULL = CT * PPT % NT == 0;
+        if (FULL || tid < CT * PPT) d[0] = w0;
+        if constexpr (NP > 1) if (FULL || tid + NT < CT * PPT) d[NT] = w1;
+        if constexpr (NP > 2) if (FULL || tid + 2 * NT < CT * PPT) d[2 * NT] = w2;
+        if constexpr (NP > 3) if (FULL || tid + 3 * NT < CT * PPT) d[3 * NT] = w3;
+    };
+    load_w(0);
+#pragma unroll
+    for (int i = 0; i < PF; ++i) issue_x(i, i);
+    // chunk c: weights of c (loaded one chunk earlier, older than every x load in flight) ->
+    // stage c & 1 (free: every wave passed barrier c - 1 after its reads of chunk c - 2) ->
+    // lgkmcnt(0) + s_barrier (not __syncthreads(): its fence would drain the x loads in flight)
+    // -> weights of c + 1 to registers -> MFMAs on c -> x of c + PF into the freed ring slot
+    static_assert(NCH % PF == 0 && PF % 2 == 0, "ring slot and stage parity fixed per unrolled position");
+#pragma nounroll
+    for (int c0 = 0; c0 < nchunk; c0 += PF) {
+#pragma unroll
+        for (int i = 0; i < PF; ++i) {
+            const int c = c0 + i;
+            store_w(i & 1);
+            __builtin_amdgcn_s_waitcnt(0xC07F);
+            asm volatile("" ::: "memory");
+            __builtin_amdgcn_s_barrier();
+            asm volatile("" ::: "memory");
+            // unconditional loads (past the end: a clamped, unused chunk): a branch around them
+            // made the waitcnt pass merge both paths and drain the x ring every chunk
+            load_w(min(c + 1, nchunk - 1));
+            asm volatile("" ::: "memory");  // keep w(c + 1) older than x(c + PF): store_w(c + 1) waits for it alone
+            compute(c, i, sW[i & 1]);
+            asm volatile("" ::: "memory");
+            if constexpr (PF < NCH) issue_x(min(c + PF, nchunk - 1), i);
+        }
+    }
     } else {
     // LDS-DMA weight ring (round 4; tools/gl4t_probe.hip): chunk c's weight slice goes straight
     // to slot c % NS by global_load_lds_dwordx4 (no VGPRs, no ds_write), issued PF chunks ahead
@@ -541,11 +620,18 @@ __global__ __launch_bounds__(NWV * 64, WRES ? 1 : 2) void k_gl4t(const GLArgs p,
     // compute reads as xa (k = h, L = l32) and xb (k = h, L = 32 + l32): the global image of a
     // row-blocked chunk, gathered per lane from a row-major operand
     float* const xs0 = reinterpret_cast<float*>(smem_raw + NS * CT * TILE_H * 2) + wave * 512;
-    auto xsrc = [&](int c, int k) -> const float* {  // this lane's DMA source of instruction k
-        const int f = (c << 4) + 8 * k + 4 * h;
-        if (f < p.K1)
-            return p.x1_blk ? p.x1 + blk_off(arow, j, f, J, p.K1) : p.x1 + ((ac + p.x1_row0) / p.x1_div) * p.x1_rs + (int64_t)j * p.K1 + f;
-        return p.x2_blk ? p.x2 + blk_off(arow, j, f - p.K1, J, p.K2) : p.x2 + ac * p.x2_rs + (int64_t)j * p.K2 + (f - p.K1);
+    // this lane's DMA source of chunk c, instruction k: a base per operand (feature 4 h of chunk 0
+    // of x1, of x2) plus c times the chunk stride (512 floats row-blocked, 16 row-major) plus k
+    // times the half-chunk stride (256 / 8) -- loop-invariant address arithmetic, no division
+    const int c1 = p.K1 >> 4;  // first chunk of x2
+    // (x1r / x2r point at feature 8 h: + 256 h row-blocked, + 8 h row-major; feature 4 h is
+    // + 128 h / + 4 h)
+    const float* xb1 = x1r - (p.x1_blk ? 128 * h : 4 * h);
+    const float* xb2 = !p.K2 ? xb1 : x2r - (p.x2_blk ? 128 * h : 4 * h);
+    const int cs1 = p.x1_blk ? 512 : 16, cs2 = p.x2_blk ? 512 : 16;
+    const int ks1 = p.x1_blk ? 256 : 8, ks2 = p.x2_blk ? 256 : 8;
+    auto xsrc = [&](int c, int k) -> const float* {
+        return c < c1 ? xb1 + (int64_t)c * cs1 + k * ks1 : xb2 + (int64_t)(c - c1) * cs2 + k * ks2;
     };
     auto fill = [&](int c) {
         _Float16* dst = sW[c % NS];
@@ -1649,11 +1735,13 @@ int gl4_tile_default() { return g_gl4_cfg; }
 // the attention epilogue per 8-row slab).  Same arithmetic in the same order as the one-kernel
 // route, so the results are bitwise identical and the route can follow the shard size.
 // Auto threshold on the rows of the whole sampling call (all row chains; GLArgs::route_rows):
-// process default SKELDIFF_SPLIT_ROWS = 640.  Measured (B = 400 / 800 / 1600 at T = 100, three
-// chains): split 5,764 / 9,018 / 11,389 futures/s vs one-kernel 4,440 / 8,666 / 12,594.
+// process default SKELDIFF_SPLIT_ROWS = 1200.  Measured (round 4, same box, T = 100, J = 16 f32,
+// tools/sweep_routes.py, profiles/r04j/sweep.txt; k_gl4y with every chunk in flight): 800 rows
+// 9,648 futures/s (k_gl4y, 2 chains) vs 7,737 (k_gl4t, 3); 1,600 rows 12,109 vs 12,172 (equal);
+// 400 rows 6,165 vs 4,361.
 static int64_t g_split_rows = [] {
     const char* e = getenv("SKELDIFF_SPLIT_ROWS");
-    return e ? (int64_t)atoll(e) : (int64_t)640;
+    return e ? (int64_t)atoll(e) : (int64_t)1200;
 }();
 int64_t split_rows_default() { return g_split_rows; }
 
@@ -1740,24 +1828,27 @@ hipError_t launch_gemm_split(const GLArgs& a, bool rms, float* z, int64_t z_rs, 
     return launch_gl4y<true>(a, rms, ntc, ntile_r, yo, s);
 }
 
-// k_gl4t's K = 192 form (SKELDIFF_GL4T_CFG, read at load): 0 = LDS-DMA weight ring, weights and x 2
-// chunks ahead, 4 waves (two workgroups per CU); 1 = the same 4 chunks ahead; 2 / 3 = resident
-// weights, every x chunk in flight, 4 / 8 waves; 4 = resident weights, x 4 chunks ahead, 8 waves
+// k_gl4t's K loop (SKELDIFF_GL4T_CFG, read at load): 0 = the default form (g_gl4t_default);
+// 5 = the round-3 form (weights register-staged into two LDS stages one chunk ahead, x two chunks
+// ahead in registers; 24 KiB of LDS); 6 = the LDS-DMA ring (weights and x by LDS-DMA, 2 chunks
+// ahead; 60 KiB); 7 = 6 with the product-major MFMA order (ILV); K = 192 only: 1 = the ring 4 chunks ahead; 2 / 3 = resident weights, every x
+// chunk in flight, 4 / 8 waves; 4 = resident weights, x 4 chunks ahead, 8 waves
 static int g_gl4t_cfg = [] {
     const char* e = getenv("SKELDIFF_GL4T_CFG");
     const int v = e ? atoi(e) : 0;
-    return (v >= 0 && v <= 4) ? v : 0;
+    return (v >= 0 && v <= 7) ? v : 0;
 }();
+static constexpr int g_gl4t_default = 6;
 
-template <int CT, int NCH, bool ROWMAJOR, int NWV, bool WRES, int PF = 2>
+template <int CT, int NCH, bool ROWMAJOR, int NWV, bool WRES, int PF = 2, bool RSTG = false, bool ILV = false>
 static hipError_t launch_gl4t_v(const GLArgs& a, bool rms, int64_t ntile_r, const YOut& yo, hipStream_t s) {
     const int ncg = a.N / (32 * CT);
     const dim3 grid((unsigned)(((ntile_r + NWV - 1) / NWV) * a.J * ncg)), block(NWV * 64);
-    auto kt = a.prec == 1 ? (rms ? k_gl4t<true, 1, CT, NCH, ROWMAJOR, PF, NWV, WRES> : k_gl4t<false, 1, CT, NCH, ROWMAJOR, PF, NWV, WRES>)
-                          : (rms ? k_gl4t<true, 0, CT, NCH, ROWMAJOR, PF, NWV, WRES> : k_gl4t<false, 0, CT, NCH, ROWMAJOR, PF, NWV, WRES>);
+    auto kt = a.prec == 1 ? (rms ? k_gl4t<true, 1, CT, NCH, ROWMAJOR, PF, NWV, WRES, RSTG, ILV> : k_gl4t<false, 1, CT, NCH, ROWMAJOR, PF, NWV, WRES, RSTG, ILV>)
+                          : (rms ? k_gl4t<true, 0, CT, NCH, ROWMAJOR, PF, NWV, WRES, RSTG, ILV> : k_gl4t<false, 0, CT, NCH, ROWMAJOR, PF, NWV, WRES, RSTG, ILV>);
     if constexpr (!ROWMAJOR) {  // bf16 mode (precision 2): the split route's scratch output only
         if (a.prec == 2)
-            kt = rms ? k_gl4t<true, 2, CT, NCH, false, PF, NWV, WRES> : k_gl4t<false, 2, CT, NCH, false, PF, NWV, WRES>;
+            kt = rms ? k_gl4t<true, 2, CT, NCH, false, PF, NWV, WRES, RSTG, ILV> : k_gl4t<false, 2, CT, NCH, false, PF, NWV, WRES, RSTG, ILV>;
     }
     g_route_bits |= kRouteGemmTiled;
     hipLaunchKernelGGL(kt, grid, block, 0, s, a, ncg, ntile_r, yo);
@@ -1766,8 +1857,9 @@ static hipError_t launch_gl4t_v(const GLArgs& a, bool rms, int64_t ntile_r, cons
 
 template <int CT, int NCH, bool ROWMAJOR>
 static hipError_t launch_gl4t_ct(const GLArgs& a, bool rms, int64_t ntile_r, const YOut& yo, hipStream_t s) {
+    const int cfg = g_gl4t_cfg ? g_gl4t_cfg : g_gl4t_default;
     if constexpr (NCH == 12) {
-        switch (g_gl4t_cfg) {
+        switch (cfg) {
             case 1: return launch_gl4t_v<CT, NCH, ROWMAJOR, 4, false, 4>(a, rms, ntile_r, yo, s);
             case 2: return launch_gl4t_v<CT, NCH, ROWMAJOR, 4, true, 12>(a, rms, ntile_r, yo, s);
             case 3: return launch_gl4t_v<CT, NCH, ROWMAJOR, 8, true, 12>(a, rms, ntile_r, yo, s);
@@ -1775,6 +1867,8 @@ static hipError_t launch_gl4t_ct(const GLArgs& a, bool rms, int64_t ntile_r, con
             default: break;
         }
     }
+    if (cfg == 5) return launch_gl4t_v<CT, NCH, ROWMAJOR, 4, false, 2, true>(a, rms, ntile_r, yo, s);
+    if (cfg == 7) return launch_gl4t_v<CT, NCH, ROWMAJOR, 4, false, 2, false, true>(a, rms, ntile_r, yo, s);
     return launch_gl4t_v<CT, NCH, ROWMAJOR, 4, false>(a, rms, ntile_r, yo, s);
 }
 

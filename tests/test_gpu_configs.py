@@ -411,7 +411,7 @@ def test_two_default_plans_concurrently(cfg, batch, cuda):
     torch.cuda.synchronize()
     for k in ("a", "b"):
         assert torch.equal(res[k], solo[k]), (k, _max_err(res[k], solo[k]))
-    assert da.engine.get_option("last_chains") == (3 if rows > 640 else 2)  # auto row chains
+    assert da.engine.get_option("last_chains") == (3 if rows > 1200 else 2)  # auto row chains
 
 
 def test_graph_linear_rejects_aliased_output(cuda):

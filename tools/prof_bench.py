@@ -39,7 +39,7 @@ def kind(name):
     m = re.match(r"sd::k_gl4<(.*)>", n)
     if m:
         mode = int(m.group(1).split(",")[6]) if len(m.group(1).split(",")) > 6 else 0
-        return {0: "one_kernel", 1: "fused_attention", 2: "mix_phase", 3: "attn_phase"}[mode]
+        return {0: "one_kernel", 1: "fused_attention", 2: "mix_phase", 3: "attn_phase", 4: "one_kernel"}.get(mode, "other")
     if "k_update" in n:
         return "update"
     return "other"
