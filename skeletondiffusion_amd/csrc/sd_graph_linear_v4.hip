@@ -354,10 +354,16 @@ __device__ unsigned long long g_gl4t_chunk[8192 * 16];  // per workgroup: s_memr
 // for all CT tiles, then x_hi W_lo, then x_lo W_hi): each accumulator sees the same three products
 // in the same order (bitwise equal), but no tile waits on its own LDS read behind the previous
 // tile's MFMAs and consecutive MFMAs are independent
+// FF (the LDS-DMA ring with x by DMA only): fill(c + PF) issued right after chunk c's barrier,
+// before chunk c's LDS reads and MFMAs (its slot, chunk c - 1's, is free there), so PF chunks of
+// work cover each fill instead of PF - 1
+// LDW (with the ring, x by DMA): one extra loader wave issues every fill (the slice's weight pieces
+// and the NWV x images) PF chunks ahead and waits for them; the NWV compute waves issue no global
+// memory operation in the K loop (LDS reads and MFMAs only), one barrier per chunk for all
 template <bool RMS, int PREC, int CT, int NCH, bool ROWMAJOR, int PF = 2, int NWV = 4, bool WRES = false, bool RSTG = false,
-          bool ILV = false>
-__global__ __launch_bounds__(NWV * 64, WRES ? 1 : 2) void k_gl4t(const GLArgs p, int ncg, int64_t ntile_r, const YOut yo) {
-    constexpr int NT = NWV * 64;
+          bool ILV = false, bool FF = false, bool LDW = false>
+__global__ __launch_bounds__((NWV + (LDW ? 1 : 0)) * 64, WRES ? 1 : 2) void k_gl4t(const GLArgs p, int ncg, int64_t ntile_r, const YOut yo) {
+    constexpr int NT = NWV * 64;  // compute threads (the loader wave, LDW, is wave NWV)
     constexpr int TILE_H = PREC ? 512 : 1024;   // halves of one 32-column tile per chunk
     constexpr int PPT = TILE_H / 8;             // 16-B pieces per tile
     constexpr int NP = (CT * PPT + NT - 1) / NT;  // staged pieces per thread
@@ -397,7 +403,7 @@ __global__ __launch_bounds__(NWV * 64, WRES ? 1 : 2) void k_gl4t(const GLArgs p,
     const int j = (int)((u / ncg) / nrg);
     const int64_t rgi = (u / ncg) % nrg;
     const int64_t tr = rgi * NWV + wave;
-    const bool live = tr < ntile_r;  // wave-uniform; a dead wave still stages weights and joins barriers
+    const bool live = tr < ntile_r && !(LDW && wave == NWV);  // wave-uniform; a dead wave still joins barriers
     const int64_t row0 = (live ? tr : 0) * 32;
     constexpr int nchunk = NCH;
     const int64_t arow = row0 + l32;
@@ -656,9 +662,13 @@ __global__ __launch_bounds__(NWV * 64, WRES ? 1 : 2) void k_gl4t(const GLArgs p,
     };
     static_assert(PF >= 1 && PF <= 4 && OPA * (PF - 1) < 64, "vmcnt range");
     auto wait_chunk = [&](int younger) {  // all but the ops of `younger` later chunks done (folds per unrolled step)
+    // vmcnt(ops of the younger chunks) AND lgkmcnt(0): every LDS read this wave issued for the
+    // previous chunk has returned before it arrives, so a fill issued after the barrier into that
+    // chunk's slot cannot overtake a read still in flight (the compiler may schedule the last
+    // MFMAs' fragment waits past the barrier otherwise)
 #define SD_WAITN(n)                                                                     \
-    if (wa) __builtin_amdgcn_s_waitcnt(VmCnt4<OPA * (n)>::imm);                         \
-    else __builtin_amdgcn_s_waitcnt(VmCnt4<OPB * (n)>::imm);
+    if (wa) __builtin_amdgcn_s_waitcnt(VmCnt4<OPA * (n)>::imm & ~(0xF << 8));           \
+    else __builtin_amdgcn_s_waitcnt(VmCnt4<OPB * (n)>::imm & ~(0xF << 8));
         if (younger == 0) { SD_WAITN(0) }
         else if (younger == 1) { SD_WAITN(1) }
         else if (younger == 2) { SD_WAITN(2 < PF ? 2 : 0) }
@@ -669,6 +679,93 @@ __global__ __launch_bounds__(NWV * 64, WRES ? 1 : 2) void k_gl4t(const GLArgs p,
         asm volatile("" ::: "memory");
     };
     static_assert(NCH % PF == 0 && NCH >= 2 * PF, "ring positions fixed per unrolled step");
+    if constexpr (LDW && XDMA) {
+        // loader wave: every fill; compute waves: LDS and MFMA only.  Chunk c: the loader has
+        // waited for fill(c) (vmcnt = the ops of the younger fills in flight), every compute wave
+        // for its LDS reads of chunk c - 1 (lgkmcnt(0)); one barrier; the loader refills chunk
+        // c - 1's slot with chunk c + PF while the compute waves work on chunk c.
+        constexpr int OPL = NPC / 64 + 2 * NWV;  // DMA instructions per fill
+        static_assert(OPL * (PF - 1) < 64, "vmcnt range");
+        if (wave == NWV) {
+            const int64_t rg0 = rgi * NWV;
+            const float* lb1[NWV];
+            const float* lb2[NWV];
+#pragma unroll
+            for (int w = 0; w < NWV; ++w) {  // compute wave w's x bases (feature 4 h of chunk 0)
+                const int64_t ar = (rg0 + w < ntile_r ? rg0 + w : 0) * 32 + l32;
+                const int64_t a2 = ar < p.B ? ar : 0;
+                lb1[w] = p.x1_blk ? p.x1 + blk_off(ar, j, 4 * h, J, p.K1)
+                                  : p.x1 + ((a2 + p.x1_row0) / p.x1_div) * p.x1_rs + (int64_t)j * p.K1 + 4 * h;
+                lb2[w] = !p.K2 ? lb1[w]
+                               : p.x2_blk ? p.x2 + blk_off(ar, j, 4 * h, J, p.K2) : p.x2 + a2 * p.x2_rs + (int64_t)j * p.K2 + 4 * h;
+            }
+            auto lfill = [&](int c) {
+                _Float16* dst = sW[c % NS];
+#pragma unroll
+                for (int k = 0; k < NPC / 64; ++k) {
+                    const int q = 64 * k + lane;
+                    const _Float16* src = wt0 + ((int64_t)c * p.wsp_nct + q / PPT) * 1024 + (q % PPT) * 8;
+                    __builtin_amdgcn_global_load_lds((const void*)src, (lds_void*)(dst + (size_t)(64 * k) * 8), 16, 0, 0);
+                }
+                float* xslot = reinterpret_cast<float*>(smem_raw + NS * CT * TILE_H * 2) + (c % NS) * (NWV * 512);
+#pragma unroll
+                for (int w = 0; w < NWV; ++w) {
+                    // the two bases as values before the select (a select between the two array
+                    // elements' addresses kept the arrays on the stack: scratch loads, counted in vmcnt)
+                    const float* v1 = lb1[w];
+                    const float* v2 = lb2[w];
+                    asm volatile("" : "+v"(v1), "+v"(v2));
+                    const float* b = c < c1 ? v1 + (int64_t)c * cs1 : v2 + (int64_t)(c - c1) * cs2;
+                    const int ks = c < c1 ? ks1 : ks2;
+                    __builtin_amdgcn_global_load_lds((const void*)b, (lds_void*)(xslot + w * 512), 16, 0, 0);
+                    __builtin_amdgcn_global_load_lds((const void*)(b + ks), (lds_void*)(xslot + w * 512 + 256), 16, 0, 0);
+                }
+            };
+            auto lwait = [&](int younger) {
+                if (younger == 0) __builtin_amdgcn_s_waitcnt(VmCnt4<0>::imm);
+                else if (younger == 1) __builtin_amdgcn_s_waitcnt(VmCnt4<OPL>::imm);
+                else if (younger == 2) __builtin_amdgcn_s_waitcnt(VmCnt4<(2 < PF ? 2 : 0) * OPL>::imm);
+                else __builtin_amdgcn_s_waitcnt(VmCnt4<(3 < PF ? 3 : 0) * OPL>::imm);
+                asm volatile("" ::: "memory");
+                __builtin_amdgcn_s_barrier();
+                asm volatile("" ::: "memory");
+            };
+#pragma unroll
+            for (int i = 0; i < PF; ++i) lfill(i);
+#pragma nounroll
+            for (int c0 = 0; c0 < nchunk - PF; c0 += PF) {
+#pragma unroll
+                for (int i = 0; i < PF; ++i) {
+                    lwait(PF - 1);
+                    lfill(c0 + i + PF);
+                }
+            }
+#pragma unroll
+            for (int i = 0; i < PF; ++i) lwait(PF - 1 - i);
+            // the loader's share of the barrier after the K loop, then done: no accumulator is live
+            // on this path (the register allocator kept them, and spilled the loader's pointers)
+            __syncthreads();
+            return;
+        } else {
+            auto cwait = [&]() {
+                __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this wave's reads of the previous chunk returned
+                asm volatile("" ::: "memory");
+                __builtin_amdgcn_s_barrier();
+                asm volatile("" ::: "memory");
+            };
+#pragma nounroll
+            for (int c0 = 0; c0 < nchunk; c0 += PF) {
+#pragma unroll
+                for (int i = 0; i < PF; ++i) {
+                    const int c = c0 + i;
+                    cwait();
+                    x_lds(c);
+                    compute(c, 0, sW[c % NS]);
+                    asm volatile("" ::: "memory");
+                }
+            }
+        }
+    } else {
 #pragma unroll
     for (int i = 0; i < PF; ++i) {
         fill(i);
@@ -683,6 +780,13 @@ __global__ __launch_bounds__(NWV * 64, WRES ? 1 : 2) void k_gl4t(const GLArgs p,
 #ifdef SD_GL4T_STAMPS
             if (STAMP && tid == 0 && blockIdx.x < 8192 && c < 16) g_gl4t_chunk[blockIdx.x * 16 + c] = wall_clock64();
 #endif
+            if constexpr (XDMA && FF) {
+                fill(c + PF);
+                asm volatile("" ::: "memory");
+                x_lds(c);
+                compute(c, 0, sW[c % NS]);
+                continue;
+            }
             if constexpr (XDMA) {
                 x_lds(c);
                 compute(c, 0, sW[c % NS]);
@@ -706,6 +810,7 @@ __global__ __launch_bounds__(NWV * 64, WRES ? 1 : 2) void k_gl4t(const GLArgs p,
         }
         asm volatile("" ::: "memory");
     }
+    }  // loader-wave / plain ring
     }  // staged K loop
     __syncthreads();  // every wave past its last chunk: the stages become the output transposes
 #ifdef SD_GL4T_STAMPS
@@ -1831,24 +1936,26 @@ hipError_t launch_gemm_split(const GLArgs& a, bool rms, float* z, int64_t z_rs, 
 // k_gl4t's K loop (SKELDIFF_GL4T_CFG, read at load): 0 = the default form (g_gl4t_default);
 // 5 = the round-3 form (weights register-staged into two LDS stages one chunk ahead, x two chunks
 // ahead in registers; 24 KiB of LDS); 6 = the LDS-DMA ring (weights and x by LDS-DMA, 2 chunks
-// ahead; 60 KiB); 7 = 6 with the product-major MFMA order (ILV); K = 192 only: 1 = the ring 4 chunks ahead; 2 / 3 = resident weights, every x
+// ahead; 60 KiB); 7 = 6 with the product-major MFMA order (ILV); 8 = 6 with each fill issued before the chunk's work
+// (FF), 9 = 8 three chunks ahead; 10 = the ring filled by one loader wave (LDW); K = 192 only: 1 = the ring 4 chunks ahead; 2 / 3 = resident weights, every x
 // chunk in flight, 4 / 8 waves; 4 = resident weights, x 4 chunks ahead, 8 waves
 static int g_gl4t_cfg = [] {
     const char* e = getenv("SKELDIFF_GL4T_CFG");
     const int v = e ? atoi(e) : 0;
-    return (v >= 0 && v <= 7) ? v : 0;
+    return (v >= 0 && v <= 10) ? v : 0;
 }();
-static constexpr int g_gl4t_default = 6;
+static constexpr int g_gl4t_default = 8;
 
-template <int CT, int NCH, bool ROWMAJOR, int NWV, bool WRES, int PF = 2, bool RSTG = false, bool ILV = false>
+template <int CT, int NCH, bool ROWMAJOR, int NWV, bool WRES, int PF = 2, bool RSTG = false, bool ILV = false, bool FF = false,
+          bool LDW = false>
 static hipError_t launch_gl4t_v(const GLArgs& a, bool rms, int64_t ntile_r, const YOut& yo, hipStream_t s) {
     const int ncg = a.N / (32 * CT);
-    const dim3 grid((unsigned)(((ntile_r + NWV - 1) / NWV) * a.J * ncg)), block(NWV * 64);
-    auto kt = a.prec == 1 ? (rms ? k_gl4t<true, 1, CT, NCH, ROWMAJOR, PF, NWV, WRES, RSTG, ILV> : k_gl4t<false, 1, CT, NCH, ROWMAJOR, PF, NWV, WRES, RSTG, ILV>)
-                          : (rms ? k_gl4t<true, 0, CT, NCH, ROWMAJOR, PF, NWV, WRES, RSTG, ILV> : k_gl4t<false, 0, CT, NCH, ROWMAJOR, PF, NWV, WRES, RSTG, ILV>);
+    const dim3 grid((unsigned)(((ntile_r + NWV - 1) / NWV) * a.J * ncg)), block((NWV + (LDW && a.prec != 2 ? 1 : 0)) * 64);
+    auto kt = a.prec == 1 ? (rms ? k_gl4t<true, 1, CT, NCH, ROWMAJOR, PF, NWV, WRES, RSTG, ILV, FF, LDW> : k_gl4t<false, 1, CT, NCH, ROWMAJOR, PF, NWV, WRES, RSTG, ILV, FF, LDW>)
+                          : (rms ? k_gl4t<true, 0, CT, NCH, ROWMAJOR, PF, NWV, WRES, RSTG, ILV, FF, LDW> : k_gl4t<false, 0, CT, NCH, ROWMAJOR, PF, NWV, WRES, RSTG, ILV, FF, LDW>);
     if constexpr (!ROWMAJOR) {  // bf16 mode (precision 2): the split route's scratch output only
         if (a.prec == 2)
-            kt = rms ? k_gl4t<true, 2, CT, NCH, false, PF, NWV, WRES, RSTG, ILV> : k_gl4t<false, 2, CT, NCH, false, PF, NWV, WRES, RSTG, ILV>;
+            kt = rms ? k_gl4t<true, 2, CT, NCH, false, PF, NWV, WRES, RSTG, ILV, FF> : k_gl4t<false, 2, CT, NCH, false, PF, NWV, WRES, RSTG, ILV, FF>;
     }
     g_route_bits |= kRouteGemmTiled;
     hipLaunchKernelGGL(kt, grid, block, 0, s, a, ncg, ntile_r, yo);
@@ -1869,6 +1976,10 @@ static hipError_t launch_gl4t_ct(const GLArgs& a, bool rms, int64_t ntile_r, con
     }
     if (cfg == 5) return launch_gl4t_v<CT, NCH, ROWMAJOR, 4, false, 2, true>(a, rms, ntile_r, yo, s);
     if (cfg == 7) return launch_gl4t_v<CT, NCH, ROWMAJOR, 4, false, 2, false, true>(a, rms, ntile_r, yo, s);
+    if (cfg == 8) return launch_gl4t_v<CT, NCH, ROWMAJOR, 4, false, 2, false, false, true>(a, rms, ntile_r, yo, s);
+    if (cfg == 10) return launch_gl4t_v<CT, NCH, ROWMAJOR, 4, false, 2, false, false, false, true>(a, rms, ntile_r, yo, s);
+    if constexpr (NCH % 3 == 0)
+        if (cfg == 9) return launch_gl4t_v<CT, NCH, ROWMAJOR, 4, false, 3, false, false, true>(a, rms, ntile_r, yo, s);
     return launch_gl4t_v<CT, NCH, ROWMAJOR, 4, false>(a, rms, ntile_r, yo, s);
 }
 
