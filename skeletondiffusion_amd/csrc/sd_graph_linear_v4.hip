@@ -360,8 +360,13 @@ __device__ unsigned long long g_gl4t_chunk[8192 * 16];  // per workgroup: s_memr
 // LDW (with the ring, x by DMA): one extra loader wave issues every fill (the slice's weight pieces
 // and the NWV x images) PF chunks ahead and waits for them; the NWV compute waves issue no global
 // memory operation in the K loop (LDS reads and MFMAs only), one barrier per chunk for all
+// NU > 1 (the ring with x by DMA, fill first): each workgroup runs NU units -- NU consecutive
+// column groups of one (row group, node), i.e. the same x -- as one continuous ring of NU * NCH
+// chunks; a unit's Y leaves through its own LDS transposes right after its last chunk while the
+// next unit's first chunks are already in flight, so the store tail and the fill prologue of all
+// but the first unit overlap the K loop (to_qkv: 4 column groups per node)
 template <bool RMS, int PREC, int CT, int NCH, bool ROWMAJOR, int PF = 2, int NWV = 4, bool WRES = false, bool RSTG = false,
-          bool ILV = false, bool FF = false, bool LDW = false>
+          bool ILV = false, bool FF = false, bool LDW = false, int NU = 1>
 __global__ __launch_bounds__((NWV + (LDW ? 1 : 0)) * 64, WRES ? 1 : 2) void k_gl4t(const GLArgs p, int ncg, int64_t ntile_r, const YOut yo) {
     constexpr int NT = NWV * 64;  // compute threads (the loader wave, LDW, is wave NWV)
     constexpr int TILE_H = PREC ? 512 : 1024;   // halves of one 32-column tile per chunk
@@ -375,7 +380,9 @@ __global__ __launch_bounds__((NWV + (LDW ? 1 : 0)) * 64, WRES ? 1 : 2) void k_gl
     constexpr bool XDMA = !WRES && !RSTG && PREC != 2;
     constexpr int XSB = XDMA ? NS * NWV * 2048 : 0;  // bytes of the x slots (after the weight slots)
     constexpr int SBW = (WRES ? NCH : RSTG ? 2 : NS) * CT * TILE_H * 2 + XSB;
-    constexpr int SB = SBW > NWV * 32 * TS * 4 ? SBW : NWV * 32 * TS * 4;
+    // NU > 1: transposes of their own, then two 1-KiB bias slots (unit u's bias in slot u & 1)
+    constexpr int SBT = NU > 1 ? SBW + NWV * 32 * TS * 4 + 2048 : SBW;
+    constexpr int SB = SBT > NWV * 32 * TS * 4 ? SBT : NWV * 32 * TS * 4;
     static_assert(!WRES || SB <= 160 * 1024, "resident weight slice exceeds the LDS");
     __shared__ __attribute__((aligned(16))) char smem_raw[SB];  // weight stages, then the transposes
     _Float16(*sW)[CT * TILE_H] = reinterpret_cast<_Float16(*)[CT * TILE_H]>(smem_raw);
@@ -679,7 +686,102 @@ __global__ __launch_bounds__((NWV + (LDW ? 1 : 0)) * 64, WRES ? 1 : 2) void k_gl
         asm volatile("" ::: "memory");
     };
     static_assert(NCH % PF == 0 && NCH >= 2 * PF, "ring positions fixed per unrolled step");
-    if constexpr (LDW && XDMA) {
+    if constexpr (NU > 1) {
+        static_assert(XDMA && !LDW, "multi-unit workgroups: the ring with x by DMA");
+        constexpr int G = NU * NCH;
+        float* const sTd = reinterpret_cast<float*>(smem_raw + SBW) + wave * 32 * TS;
+        // the bias of a unit rides in with its first chunk (one 4-B LDS-DMA per wave: columns
+        // 64 w + lane, clamped): a register load of it in the epilogue would be the youngest
+        // vector-memory op, and waiting for it drained the ring (vmcnt(0) per tile)
+        float* const sBias = reinterpret_cast<float*>(smem_raw + SBW + NWV * 32 * TS * 4);
+        static_assert(CT * 32 <= NWV * 64 && NWV * 64 <= 256, "one bias slot: one 4-B DMA per wave");
+        const _Float16* const wtu = p.wsp + ((int64_t)p.ntype[j] * nchunk * p.wsp_nct + cg * NU * CT) * 1024;
+        auto gfill = [&](int g) {  // global chunk g = unit g / NCH, chunk g % NCH
+            const int uu = g / NCH, c = g - uu * NCH;
+            _Float16* dst = sW[g % NS];
+            const _Float16* w0 = wtu + (int64_t)uu * CT * 1024;
+#pragma unroll
+            for (int k = 0; k < (NPC / 64 + NWV - 1) / NWV; ++k) {
+                const int q0 = wave * 64 + NT * k;
+                if (q0 >= NPC) continue;  // wave-uniform
+                const int q = q0 + lane;
+                const _Float16* src = w0 + ((int64_t)c * p.wsp_nct + q / PPT) * 1024 + (q % PPT) * 8;
+                __builtin_amdgcn_global_load_lds((const void*)src, (lds_void*)(dst + (size_t)q0 * 8), 16, 0, 0);
+            }
+            float* xd = xs0 + (g % NS) * (NWV * 512);
+            __builtin_amdgcn_global_load_lds((const void*)xsrc(c, 0), (lds_void*)xd, 16, 0, 0);
+            __builtin_amdgcn_global_load_lds((const void*)xsrc(c, 1), (lds_void*)(xd + 256), 16, 0, 0);
+            if (c == 0 && p.bias) {  // wave-uniform; one more op on a unit's first chunk keeps every wait conservative
+                const int col = wave * 64 + lane;
+                const float* bs = p.bias + p.wrow[j] + (cg * NU + uu) * CT * 32 + (col < CT * 32 ? col : 0);
+                __builtin_amdgcn_global_load_lds((const void*)bs, (lds_void*)(sBias + (uu & 1) * 256 + wave * 64), 4, 0, 0);
+            }
+        };
+        auto gstep = [&](int g) {  // chunk g's work, then unit g / NCH's Y after its last chunk
+            const int uu = g / NCH, c = g - uu * NCH;
+            const float* xs = xs0 + (g % NS) * (NWV * 512) + h * 256 + l32 * 4;
+            xa[0] = *reinterpret_cast<const floatx4*>(xs);
+            xb[0] = *reinterpret_cast<const floatx4*>(xs + 128);
+            compute(c, 0, sW[g % NS]);
+            if (c != NCH - 1) return;  // wave-uniform
+            if (live) {
+                if (p.status && __builtin_amdgcn_ballot_w64(amx >= 65504.0f) != 0 && lane == 0) atomicOr(p.status, 1u);
+                float sc[16];
+#pragma unroll
+                for (int r = 0; r < 16; ++r) sc[r] = p.wsp_unscale;
+                if (RMS) {
+                    const float t = ss + __shfl_xor(ss, 32);
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) {
+                        const float n2 = __shfl(t, (r & 3) + 8 * (r >> 2) + 4 * h);
+                        sc[r] *= 1.0f / fmaxf(sqrtf(n2), 1e-12f);
+                    }
+                }
+                const int cgu = cg * NU + uu;
+                float* y = yo.y + tr * yo.y_ts + j * yo.y_js + (int64_t)cgu * CT * yo.y_cs;
+#pragma unroll
+                for (int ct = 0; ct < CT; ++ct) {
+                    const float bv = p.bias ? sBias[(uu & 1) * 256 + ct * 32 + l32] : 0.f;
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) sTd[((r & 3) + 8 * (r >> 2) + 4 * h) * TS + l32] = acc[ct][r] * sc[r] + bv;
+                    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) {
+                        const int row = 8 * q + (lane >> 3), c4 = (lane & 7) * 4;
+                        const floatx4 v = *reinterpret_cast<const floatx4*>(sTd + row * TS + c4);
+                        if (!ROWMAJOR || row0 + row < p.B)
+                            *reinterpret_cast<floatx4*>(y + (int64_t)row * yo.y_rs + ct * yo.y_cs + c4) = v;
+                    }
+                    __builtin_amdgcn_wave_barrier();
+                }
+            }
+#pragma unroll
+            for (int ct = 0; ct < CT; ++ct)
+#pragma unroll
+                for (int e = 0; e < 16; ++e) acc[ct][e] = 0.f;
+            ss = 0.f;
+            amx = 0.f;
+        };
+        // every wait counts only the younger fills; where a unit's stores were issued since (one
+        // chunk per unit), the wait also covers them -- a conservative, correct count
+#pragma unroll
+        for (int i = 0; i < PF; ++i) gfill(i);
+#pragma nounroll
+        for (int g = 0; g < G - PF; ++g) {
+            wait_chunk(PF - 1);
+            gfill(g + PF);
+            asm volatile("" ::: "memory");
+            gstep(g);
+            asm volatile("" ::: "memory");
+        }
+#pragma unroll
+        for (int i = 0; i < PF; ++i) {
+            wait_chunk(PF - 1 - i);
+            gstep(G - PF + i);
+            asm volatile("" ::: "memory");
+        }
+        return;
+    } else if constexpr (LDW && XDMA) {
         // loader wave: every fill; compute waves: LDS and MFMA only.  Chunk c: the loader has
         // waited for fill(c) (vmcnt = the ops of the younger fills in flight), every compute wave
         // for its LDS reads of chunk c - 1 (lgkmcnt(0)); one barrier; the loader refills chunk
@@ -1937,22 +2039,24 @@ hipError_t launch_gemm_split(const GLArgs& a, bool rms, float* z, int64_t z_rs, 
 // 5 = the round-3 form (weights register-staged into two LDS stages one chunk ahead, x two chunks
 // ahead in registers; 24 KiB of LDS); 6 = the LDS-DMA ring (weights and x by LDS-DMA, 2 chunks
 // ahead; 60 KiB); 7 = 6 with the product-major MFMA order (ILV); 8 = 6 with each fill issued before the chunk's work
-// (FF), 9 = 8 three chunks ahead; 10 = the ring filled by one loader wave (LDW); K = 192 only: 1 = the ring 4 chunks ahead; 2 / 3 = resident weights, every x
+// (FF), 9 = 8 three chunks ahead; 10 = the ring filled by one loader wave (LDW); 11 / 12 = 8 with
+// 2 / 4 units (column groups of one x tile) per workgroup where they divide (NU); K = 192 only: 1 = the ring 4 chunks ahead; 2 / 3 = resident weights, every x
 // chunk in flight, 4 / 8 waves; 4 = resident weights, x 4 chunks ahead, 8 waves
 static int g_gl4t_cfg = [] {
     const char* e = getenv("SKELDIFF_GL4T_CFG");
     const int v = e ? atoi(e) : 0;
-    return (v >= 0 && v <= 10) ? v : 0;
+    return (v >= 0 && v <= 12) ? v : 0;
 }();
 static constexpr int g_gl4t_default = 8;
 
 template <int CT, int NCH, bool ROWMAJOR, int NWV, bool WRES, int PF = 2, bool RSTG = false, bool ILV = false, bool FF = false,
-          bool LDW = false>
+          bool LDW = false, int NU = 1>
 static hipError_t launch_gl4t_v(const GLArgs& a, bool rms, int64_t ntile_r, const YOut& yo, hipStream_t s) {
-    const int ncg = a.N / (32 * CT);
+    if (NU > 1 && (a.prec == 2 || (a.N / (32 * CT)) % NU)) return hipErrorNotSupported;
+    const int ncg = a.N / (32 * CT) / NU;  // column groups of NU units each
     const dim3 grid((unsigned)(((ntile_r + NWV - 1) / NWV) * a.J * ncg)), block((NWV + (LDW && a.prec != 2 ? 1 : 0)) * 64);
-    auto kt = a.prec == 1 ? (rms ? k_gl4t<true, 1, CT, NCH, ROWMAJOR, PF, NWV, WRES, RSTG, ILV, FF, LDW> : k_gl4t<false, 1, CT, NCH, ROWMAJOR, PF, NWV, WRES, RSTG, ILV, FF, LDW>)
-                          : (rms ? k_gl4t<true, 0, CT, NCH, ROWMAJOR, PF, NWV, WRES, RSTG, ILV, FF, LDW> : k_gl4t<false, 0, CT, NCH, ROWMAJOR, PF, NWV, WRES, RSTG, ILV, FF, LDW>);
+    auto kt = a.prec == 1 ? (rms ? k_gl4t<true, 1, CT, NCH, ROWMAJOR, PF, NWV, WRES, RSTG, ILV, FF, LDW, NU> : k_gl4t<false, 1, CT, NCH, ROWMAJOR, PF, NWV, WRES, RSTG, ILV, FF, LDW, NU>)
+                          : (rms ? k_gl4t<true, 0, CT, NCH, ROWMAJOR, PF, NWV, WRES, RSTG, ILV, FF, LDW, NU> : k_gl4t<false, 0, CT, NCH, ROWMAJOR, PF, NWV, WRES, RSTG, ILV, FF, LDW, NU>);
     if constexpr (!ROWMAJOR) {  // bf16 mode (precision 2): the split route's scratch output only
         if (a.prec == 2)
             kt = rms ? k_gl4t<true, 2, CT, NCH, false, PF, NWV, WRES, RSTG, ILV, FF> : k_gl4t<false, 2, CT, NCH, false, PF, NWV, WRES, RSTG, ILV, FF>;
@@ -1978,6 +2082,14 @@ static hipError_t launch_gl4t_ct(const GLArgs& a, bool rms, int64_t ntile_r, con
     if (cfg == 7) return launch_gl4t_v<CT, NCH, ROWMAJOR, 4, false, 2, false, true>(a, rms, ntile_r, yo, s);
     if (cfg == 8) return launch_gl4t_v<CT, NCH, ROWMAJOR, 4, false, 2, false, false, true>(a, rms, ntile_r, yo, s);
     if (cfg == 10) return launch_gl4t_v<CT, NCH, ROWMAJOR, 4, false, 2, false, false, false, true>(a, rms, ntile_r, yo, s);
+    if (cfg == 11 || cfg == 12) {  // multi-unit workgroups where the column groups divide (to_qkv), else cfg 8
+        const int ncg0 = a.N / (32 * CT);
+        if (a.prec != 2 && cfg == 11 && ncg0 % 2 == 0)
+            return launch_gl4t_v<CT, NCH, ROWMAJOR, 4, false, 2, false, false, true, false, 2>(a, rms, ntile_r, yo, s);
+        if (a.prec != 2 && cfg == 12 && ncg0 % 4 == 0)
+            return launch_gl4t_v<CT, NCH, ROWMAJOR, 4, false, 2, false, false, true, false, 4>(a, rms, ntile_r, yo, s);
+        return launch_gl4t_v<CT, NCH, ROWMAJOR, 4, false, 2, false, false, true>(a, rms, ntile_r, yo, s);
+    }
     if constexpr (NCH % 3 == 0)
         if (cfg == 9) return launch_gl4t_v<CT, NCH, ROWMAJOR, 4, false, 3, false, false, true>(a, rms, ntile_r, yo, s);
     return launch_gl4t_v<CT, NCH, ROWMAJOR, 4, false>(a, rms, ntile_r, yo, s);
