@@ -286,6 +286,10 @@ __global__ __launch_bounds__(256) void k_gl4y(const GLArgs p, int ntile_c, int64
     // issues, a last round that never does.  (Round 4: the earlier `if (c + PF < nchunk) issue`
     // form made the waitcnt pass merge the paths and wait vmcnt(1-3) at every chunk, i.e. one
     // memory latency per chunk instead of one per launch.)
+    // the bias before the operand loads: loaded after the K loop it was the youngest memory op, and
+    // its vmcnt(0) put one more memory latency between the last MFMA and the stores
+    const int ncol = tc * 32 + l32;
+    const float bv = (p.bias && ncol < p.N) ? p.bias[p.wrow[j] + ncol] : 0.f;
 #pragma unroll
     for (int i = 0; i < PF; ++i) issue(i, i);
     for (int c0 = 0; c0 < nchunk - PF; c0 += PF) {
@@ -309,8 +313,6 @@ __global__ __launch_bounds__(256) void k_gl4y(const GLArgs p, int ntile_c, int64
             sc[r] *= 1.0f / fmaxf(sqrtf(n2), 1e-12f);
         }
     }
-    const int ncol = tc * 32 + l32;
-    const float bv = (p.bias && ncol < p.N) ? p.bias[p.wrow[j] + ncol] : 0.f;
     if constexpr (ROWMAJOR) {
         if (ncol >= p.N) return;
         float* y = yo.y + tr * yo.y_ts + j * yo.y_js + tc * yo.y_cs + l32;
@@ -450,6 +452,14 @@ __global__ __launch_bounds__((NWV + (LDW ? 1 : 0)) * 64, WRES ? 1 : 2) void k_gl
 #pragma unroll
         for (int e = 0; e < 16; ++e) acc[ct][e] = 0.f;
     float ss = 0.f, amx = 0.f;
+    // the epilogue's bias, loaded before the K loop: loaded per tile in the epilogue, each load was
+    // the youngest memory op and its vmcnt(0) also waited for the previous tile's stores -- CT
+    // serial memory round trips in the store tail (NU > 1 brings its units' bias by LDS-DMA)
+    float bvp[CT];
+    if constexpr (NU == 1) {
+#pragma unroll
+        for (int ct = 0; ct < CT; ++ct) bvp[ct] = p.bias ? p.bias[p.wrow[j] + (cg * CT + ct) * 32 + l32] : 0.f;
+    }
     auto compute = [&](int c, int sl, const _Float16* wst) {  // wst: the chunk's CT tiles in LDS
         if constexpr (PREC == 2) {  // bf16 mode: one bf16 product per k step (k_gl4 PREC 2's arithmetic)
             const bool bsrc = (c << 4) < p.K1 ? p.x1_bf16 : p.x2_bf16;  // wave-uniform
@@ -944,8 +954,7 @@ __global__ __launch_bounds__((NWV + (LDW ? 1 : 0)) * 64, WRES ? 1 : 2) void k_gl
     float* y = yo.y + tr * yo.y_ts + j * yo.y_js + (int64_t)cg * CT * yo.y_cs;  // YOut as k_gl4y's
 #pragma unroll
     for (int ct = 0; ct < CT; ++ct) {
-        const int ncol = (cg * CT + ct) * 32 + l32;
-        const float bv = p.bias ? p.bias[p.wrow[j] + ncol] : 0.f;
+        const float bv = bvp[ct];
 #pragma unroll
         for (int r = 0; r < 16; ++r) sT[((r & 3) + 8 * (r >> 2) + 4 * h) * TS + l32] = acc[ct][r] * sc[r] + bv;
         __builtin_amdgcn_wave_barrier();  // DS operations of one wave complete in order
