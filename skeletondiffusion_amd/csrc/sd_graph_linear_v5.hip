@@ -355,7 +355,6 @@ __global__ __launch_bounds__(256, 2) void k_gl5_mixd(const GLArgs p, const float
     const int SL = 4 * KS * 64;                   // floats per slab (4 KS rows x 64 columns)
     extern __shared__ __attribute__((aligned(16))) float s_m[];
     float* s_zr = s_m;                            // [NS][z | res][SL]
-    float* s_f = s_m + NS * (RES ? 2 : 1) * SL;   // FiLM (scale + 1 | shift)
     const int tid = threadIdx.x, lane = tid & 63, l16 = lane & 15, l4 = lane >> 4;
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int n0 = blockIdx.y * 64;
@@ -368,9 +367,24 @@ __global__ __launch_bounds__(256, 2) void k_gl5_mixd(const GLArgs p, const float
         const int j = 4 * s + l4;
         gb[s] = (s < KS && i < J && j < J) ? p.G[i * J + j] : 0.f;
     }
-    if (tid < 64) {
-        s_f[tid] = p.film ? p.film[n0 + tid] + 1.0f : 1.0f;
-        s_f[64 + tid] = p.film ? p.film[N + n0 + tid] : 0.0f;
+    // this lane's FiLM values (the same for every row) straight to registers, issued with G-hat's
+    // loads (one memory latency, waited at the first row's epilogue).  (Staged through LDS, they
+    // were read back after the fills, a read the waitcnt pass cannot tell apart from a DMA
+    // destination: vmcnt(0) -- the next rows' fills -- before every row's epilogue.)
+    float4 fa[4], fb[4];
+    if (p.film) {  // wave-uniform
+#pragma unroll
+        for (int cb = 0; cb < 4; ++cb) {
+            const float4 a = *reinterpret_cast<const float4*>(p.film + n0 + 16 * cb + 4 * l4);
+            fa[cb] = make_float4(a.x + 1.0f, a.y + 1.0f, a.z + 1.0f, a.w + 1.0f);
+            fb[cb] = *reinterpret_cast<const float4*>(p.film + N + n0 + 16 * cb + 4 * l4);
+        }
+    } else {
+#pragma unroll
+        for (int cb = 0; cb < 4; ++cb) {
+            fa[cb] = make_float4(1.0f, 1.0f, 1.0f, 1.0f);
+            fb[cb] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        }
     }
     // the k padding rows J .. 4 KS - 1 of every z slot stay zero (never a DMA destination)
     for (int q = tid; q < NS * (4 * KS - J) * 64; q += 256) {
@@ -423,7 +437,7 @@ __global__ __launch_bounds__(256, 2) void k_gl5_mixd(const GLArgs p, const float
         __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
     };
-    __syncthreads();  // the zero rows and FiLM before any DMA lands next to them
+    __syncthreads();  // the zero rows before any DMA lands next to them
 #pragma unroll
     for (int q = 0; q < PF; ++q) fill(q);  // rows 0 .. PF - 1 (clamped rows repeat a valid one)
     for (int r = 0; r < nrows; ++r) {
@@ -434,8 +448,23 @@ __global__ __launch_bounds__(256, 2) void k_gl5_mixd(const GLArgs p, const float
         const int yrows = (r - m0) + (r < PF ? (PF - 1 - r) : 0);   // later fills (incl. prologue ones)
         const int ystores = r - m0 + (r >= PF ? 1 : 0);
         wait_row(yrows, ystores);
-        fill(r + PF);  // slot (r + PF) % NS = (r - 1) % NS: read in row r - 1, before this barrier
         const float* zs = s_zr + (r % NS) * (RES ? 2 : 1) * SL;
+        // the row's residual out of LDS before the next fill is issued (read after it, the compiler
+        // drained vmcnt(0) -- that fill too -- before the read: it cannot tell the two apart)
+        // The reads are ds_read_b128 by inline asm: the waitcnt pass makes every LDS access it
+        // knows wait for all LDS-DMA in flight (it cannot tell fill(r + 1)'s slot from slot r), so a
+        // plain read here drained vmcnt(0) each row; wait_row already covers slot r, and the
+        // lgkmcnt(0) below covers the asm reads themselves
+        float4 rq[4];
+        if constexpr (RES) {
+#pragma unroll
+            for (int cb = 0; cb < 4; ++cb) {
+                const float* a = zs + SL + min(i, J - 1) * 64 + (((4 * cb + l4) ^ ((min(i, J - 1) & 1) << 2)) << 2);
+                asm volatile("ds_read_b128 %0, %1" : "=v"(rq[cb]) : "v"((uint32_t)(uintptr_t)a) : "memory");
+            }
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        }
+        fill(r + PF);  // slot (r + PF) % NS = (r - 1) % NS: read in row r - 1, before this barrier
         floatx4 acc[4];
 #pragma unroll
         for (int cb = 0; cb < 4; ++cb) {
@@ -454,14 +483,11 @@ __global__ __launch_bounds__(256, 2) void k_gl5_mixd(const GLArgs p, const float
 #pragma unroll
         for (int cb = 0; cb < 4; ++cb) {
             float v[4] = {acc[cb][0], acc[cb][1], acc[cb][2], acc[cb][3]};
-            const float4 fa = *reinterpret_cast<const float4*>(s_f + 16 * cb + 4 * l4);
-            const float4 fb = *reinterpret_cast<const float4*>(s_f + 64 + 16 * cb + 4 * l4);
-            const float fav[4] = {fa.x, fa.y, fa.z, fa.w};
-            const float fbv[4] = {fb.x, fb.y, fb.z, fb.w};
+            const float fav[4] = {fa[cb].x, fa[cb].y, fa[cb].z, fa[cb].w};
+            const float fbv[4] = {fb[cb].x, fb[cb].y, fb[cb].z, fb[cb].w};
             float rvv[4] = {0.f, 0.f, 0.f, 0.f};
             if constexpr (RES) {
-                const float4 rq = *reinterpret_cast<const float4*>(zs + SL + min(i, J - 1) * 64 + (((4 * cb + l4) ^ ((min(i, J - 1) & 1) << 2)) << 2));
-                rvv[0] = rq.x; rvv[1] = rq.y; rvv[2] = rq.z; rvv[3] = rq.w;
+                rvv[0] = rq[cb].x; rvv[1] = rq[cb].y; rvv[2] = rq[cb].z; rvv[3] = rq[cb].w;
             }
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
@@ -557,7 +583,7 @@ hipError_t launch_graph_linear_v5(const GLArgs& a, bool rms, hipStream_t s) {
         // the LDS-DMA form: slabs of 4 ceil(J / 4) rows, 3 slots (rows r, r + 1, r + 2 in flight)
         constexpr int R = 8, PF = 2;
         const int KS = (a.J + 3) / 4;
-        const size_t lds = ((size_t)(PF + 1) * (a.res ? 2 : 1) * 4 * KS * 64 + 128) * sizeof(float);
+        const size_t lds = (size_t)(PF + 1) * (a.res ? 2 : 1) * 4 * KS * 64 * sizeof(float);
         auto kt = a.res ? k_gl5_mixd<R, PF, true> : k_gl5_mixd<R, PF, false>;
         if (lds > 64 * 1024) {
             const hipError_t e = hipFuncSetAttribute((const void*)kt, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);

@@ -289,26 +289,59 @@ __global__ __launch_bounds__(256) void k_attention(const AttnArgs p) {
 #pragma unroll
         for (int c = 0; c < JT; ++c) S[a][c] = floatx4{0.f, 0.f, 0.f, 0.f};
 
-#pragma unroll
-    for (int cc = 0; cc < dh; cc += 16) {
-        floatx4 ka[JT], qv[JT];
-#pragma unroll
-        for (int t = 0; t < JT; ++t) {
-            const int j = t * 16 + lr;
-            ka[t] = (j < J) ? ld4(kb + j * rs + cc + 4 * lg) : floatx4{0.f, 0.f, 0.f, 0.f};
-            qv[t] = (j < J) ? ld4(qb + j * rs + cc + 4 * lg) * p.scale : floatx4{0.f, 0.f, 0.f, 0.f};
-        }
+    // unconditional loads from clamped nodes, padding zeroed after: a masked load beside a zero
+    // write of the same registers made the compiler wait vmcnt(0) per tile (one memory latency per
+    // 16 nodes).  DH = 32: both 16-wide chunks of K and Q and both of V are issued up front, so a
+    // wave pays one memory latency
+    constexpr int NCC = DH ? DH / 16 : 1;  // chunks loaded together
+    floatx4 vv[DH ? NCC : 1][JT];
+    auto load_v = [&](int dc, floatx4* v) {
 #pragma unroll
         for (int jt = 0; jt < JT; ++jt)
 #pragma unroll
-            for (int nt = 0; nt < JT; ++nt) {
-                floatx4 c = S[jt][nt];
-                c = mfma4(ka[jt].x, qv[nt].x, c);
-                c = mfma4(ka[jt].y, qv[nt].y, c);
-                c = mfma4(ka[jt].z, qv[nt].z, c);
-                c = mfma4(ka[jt].w, qv[nt].w, c);
-                S[jt][nt] = c;
+            for (int s4 = 0; s4 < 4; ++s4) v[jt][s4] = vb[min(jt * 16 + 4 * lg + s4, J - 1) * rs + dc + lr];
+    };
+    auto mask_v = [&](floatx4* v) {
+#pragma unroll
+        for (int jt = 0; jt < JT; ++jt)
+#pragma unroll
+            for (int s4 = 0; s4 < 4; ++s4) v[jt][s4] = jt * 16 + 4 * lg + s4 < J ? v[jt][s4] : 0.f;
+    };
+#pragma unroll
+    for (int cc0 = 0; cc0 < dh; cc0 += 16 * NCC) {
+        floatx4 ka[NCC][JT], qv[NCC][JT];
+#pragma unroll
+        for (int u = 0; u < NCC; ++u)
+#pragma unroll
+            for (int t = 0; t < JT; ++t) {
+                const int jc = min(t * 16 + lr, J - 1);
+                ka[u][t] = ld4(kb + jc * rs + cc0 + 16 * u + 4 * lg);
+                qv[u][t] = ld4(qb + jc * rs + cc0 + 16 * u + 4 * lg);
             }
+        if constexpr (DH != 0) {
+#pragma unroll
+            for (int u = 0; u < NCC; ++u) load_v(16 * u, vv[u]);
+        }
+#pragma unroll
+        for (int u = 0; u < NCC; ++u) {
+#pragma unroll
+            for (int t = 0; t < JT; ++t) {
+                const bool ok = t * 16 + lr < J;
+                ka[u][t] = ok ? ka[u][t] : floatx4{0.f, 0.f, 0.f, 0.f};
+                qv[u][t] = ok ? qv[u][t] * p.scale : floatx4{0.f, 0.f, 0.f, 0.f};
+            }
+#pragma unroll
+            for (int jt = 0; jt < JT; ++jt)
+#pragma unroll
+                for (int nt = 0; nt < JT; ++nt) {
+                    floatx4 c = S[jt][nt];
+                    c = mfma4(ka[u][jt].x, qv[u][nt].x, c);
+                    c = mfma4(ka[u][jt].y, qv[u][nt].y, c);
+                    c = mfma4(ka[u][jt].z, qv[u][nt].z, c);
+                    c = mfma4(ka[u][jt].w, qv[u][nt].w, c);
+                    S[jt][nt] = c;
+                }
+        }
     }
 
     // softmax over j (rows of S^T) for every query column n = nt*16 + lr
@@ -341,23 +374,18 @@ __global__ __launch_bounds__(256) void k_attention(const AttnArgs p) {
     // O^T[d][n] = sum_j V[j][d] P^T[j][n]
 #pragma unroll
     for (int dc = 0; dc < dh; dc += 16) {
-        floatx4 vv[JT];
-#pragma unroll
-        for (int jt = 0; jt < JT; ++jt)
-#pragma unroll
-            for (int s4 = 0; s4 < 4; ++s4) {
-                const int j = jt * 16 + 4 * lg + s4;
-                vv[jt][s4] = (j < J) ? vb[j * rs + dc + lr] : 0.f;
-            }
+        floatx4* v = vv[DH ? dc / 16 : 0];
+        if constexpr (DH == 0) load_v(dc, v);
+        mask_v(v);
 #pragma unroll
         for (int nt = 0; nt < JT; ++nt) {
             floatx4 o = floatx4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
             for (int jt = 0; jt < JT; ++jt) {
-                o = mfma4(vv[jt].x, S[jt][nt].x, o);
-                o = mfma4(vv[jt].y, S[jt][nt].y, o);
-                o = mfma4(vv[jt].z, S[jt][nt].z, o);
-                o = mfma4(vv[jt].w, S[jt][nt].w, o);
+                o = mfma4(v[jt].x, S[jt][nt].x, o);
+                o = mfma4(v[jt].y, S[jt][nt].y, o);
+                o = mfma4(v[jt].z, S[jt][nt].z, o);
+                o = mfma4(v[jt].w, S[jt][nt].w, o);
             }
             const int n = nt * 16 + lr;
             if (n < J) {
@@ -758,7 +786,9 @@ __global__ __launch_bounds__(256) void k_update_row(const UpdArgs p) {
 // contiguous bytes of one node), so one memory latency covers the whole workgroup; meanwhile the
 // tables go to LDS and phase A draws the rows' Philox normals (one 4x32 draw per 4 features, as
 // k_noise_fill) into LDS as sigma_j . eps; one barrier; then the MFMAs and the stores.
-template <int JP, int R, int MT>
+// BF: x0 / x_t may be bf16 (precision mode 2); the f32 form has no bf16 load path at all (a
+// per-operand branch around the loads left the waitcnt pass's merged counts at vmcnt(0))
+template <int JP, int R, int MT, bool BF = false>
 __global__ __launch_bounds__(256) void k_update_mfma(const UpdArgs p) {
     constexpr int KS = JP / 4, IB = JP / 16;
     // table rows JP + 2 floats apart: an A-fragment read (lanes 0-31 = rows i = l16, k columns l4 in
@@ -781,36 +811,63 @@ __global__ __launch_bounds__(256) void k_update_mfma(const UpdArgs p) {
     const int64_t rb = (live ? row : 0) * (int64_t)JD;
     const int l16 = lane & 15, l4 = lane >> 4;
     const int nct = D >> 4, ct0 = wave / R, cstep = 4 / R;
-    // the wave's x0 (activation + clamp) and x_t B fragments, all tiles in flight at once
-    float bx[MT][KS], bt[MT][KS];
-#pragma unroll
-    for (int q = 0; q < MT; ++q) {
-        const int ct = ct0 + q * cstep;
-        const int n = 16 * min(ct, nct - 1) + l16;
-#pragma unroll
-        for (int ks = 0; ks < KS; ++ks) {
-            const int jc = min(4 * ks + l4, J - 1);
-            bx[q][ks] = p.x0_bf16 ? (float)reinterpret_cast<const __bf16*>(p.x0)[rb + jc * D + n] : p.x0[rb + jc * D + n];
-            bt[q][ks] = p.xt_bf16 ? (float)reinterpret_cast<const __bf16*>(p.xt)[rb + jc * D + n] : p.xt[rb + jc * D + n];
-        }
-    }
-    {  // the three tables to LDS: every load of this thread issued before the first store (a
-       // load -> store loop waited out one memory latency per element: 48 per thread at JP = 64)
-        constexpr int TPT = (3 * JP * JP + 255) / 256;
-        float tv[TPT];
+    // Order of the prologue's loads (every load of a group issued before its first use: a load ->
+    // use loop waits out one memory latency per element).  JP <= 32: the tables, then sigma, then
+    // the x0 / x_t fragments, then the table stores (which wait for the tables alone), so the x
+    // loads stay in flight through phase A.  JP = 64 (48 table values per thread, which would not
+    // fit the registers beside the fragments): sigma, the fragments, then the tables loaded and stored.
+    constexpr int TPT = (3 * JP * JP + 255) / 256;
+    constexpr bool TFIRST = JP <= 32;
+    float tv[TPT];
+    auto load_tables = [&]() {
 #pragma unroll
         for (int k = 0; k < TPT; ++k) {
-            const int q = tid + 256 * k;
+            const int q = min(tid + 256 * k, 3 * JP * JP - 1);
             const int m = q / (JP * JP), ij = q % (JP * JP), i = ij / JP, j = ij % JP;
             const float* tab = m == 0 ? p.C1 : m == 1 ? p.C2 : p.U;
-            tv[k] = (q < 3 * JP * JP && i < J && j < J) ? tab[i * J + j] : 0.f;
+            tv[k] = tab[min(i, J - 1) * J + min(j, J - 1)];  // unconditional: padding zeroed at the store
         }
+    };
+    auto store_tables = [&]() {
 #pragma unroll
         for (int k = 0; k < TPT; ++k) {
             const int q = tid + 256 * k;
-            if (q < 3 * JP * JP) sTab[(q / JP) * TSJ + q % JP] = tv[k];
+            const int i = (q % (JP * JP)) / JP, j = q % JP;
+            if (q < 3 * JP * JP) sTab[(q / JP) * TSJ + q % JP] = (i < J && j < J) ? tv[k] : 0.f;
         }
+    };
+    if constexpr (TFIRST) load_tables();
+    // sigma_j of this thread's first SGP phase-A quads (unconditional, clamped node)
+    constexpr int SGP = 8;
+    float sgp[SGP];
+    if (p.noise_mode != 0) {  // wave-uniform
+#pragma unroll
+        for (int it = 0; it < SGP; ++it) sgp[it] = p.sig[min(((tid + 256 * it) % QPR) / (D >> 2), J - 1)];
     }
+    // the wave's x0 (activation + clamp) and x_t B fragments, all tiles in flight at once (BF: one
+    // uniform branch per operand around all of its loads; a per-element select between the bf16
+    // and the f32 load if-converted into both loads plus a merge that waited vmcnt(0) per element)
+    float bx[MT][KS], bt[MT][KS];
+    auto load_b = [&](const float* src, bool bf16, float (*dst)[KS]) {
+        if (BF && bf16) {  // wave-uniform
+            const __bf16* sb = reinterpret_cast<const __bf16*>(src);
+#pragma unroll
+            for (int q = 0; q < MT; ++q)
+#pragma unroll
+                for (int ks = 0; ks < KS; ++ks)
+                    dst[q][ks] = (float)sb[rb + min(4 * ks + l4, J - 1) * D + 16 * min(ct0 + q * cstep, nct - 1) + l16];
+        } else {
+#pragma unroll
+            for (int q = 0; q < MT; ++q)
+#pragma unroll
+                for (int ks = 0; ks < KS; ++ks)
+                    dst[q][ks] = src[rb + min(4 * ks + l4, J - 1) * D + 16 * min(ct0 + q * cstep, nct - 1) + l16];
+        }
+    };
+    load_b(p.x0, p.x0_bf16, bx);
+    load_b(p.xt, p.xt_bf16, bt);
+    if constexpr (!TFIRST) load_tables();
+    store_tables();
     uint64_t seed = p.seed;
     int64_t row0 = p.row0;
     if (p.noise_mode == 2 && p.rng_dev) {
@@ -818,11 +875,12 @@ __global__ __launch_bounds__(256) void k_update_mfma(const UpdArgs p) {
         row0 = (int64_t)p.rng_dev[1];
     }
     row0 += p.row_shift;
-    // phase A: sigma_j eps_j (and the raw eps record) for the workgroup's rows
-    for (int q = tid; q < R * QPR; q += 256) {
+    // phase A: sigma_j eps_j (and the raw eps record) for the workgroup's rows (the first SGP
+    // quads' sigma_j prefetched above: loaded in the loop, each was waited out right away)
+    auto phase_a = [&](int q, float sg) {
         const int rr = q / QPR, qq = q % QPR, j = qq / (D >> 2), d = 4 * (qq % (D >> 2));
         const int64_t rw = rowg + rr;
-        if (rw >= p.B) break;
+        if (rw >= p.B) return;
         floatx4 e = {0.f, 0.f, 0.f, 0.f};
         if (p.noise_mode == 1) {
             e = ld4(p.eps + rw * p.eps_rs + j * D + d);
@@ -832,10 +890,14 @@ __global__ __launch_bounds__(256) void k_update_mfma(const UpdArgs p) {
             e = floatx4{z0.x, z0.y, z1.x, z1.y};
         }
         if (p.noise_out) *reinterpret_cast<floatx4*>(p.noise_out + rw * p.noise_rs + j * D + d) = e;
-        if (p.noise_mode != 0) e *= p.sig[j];
+        if (p.noise_mode != 0) e *= sg;
         *reinterpret_cast<floatx4*>(sEv + (rr * J + j) * DS + d) = e;
         if (p.dump_ev) *reinterpret_cast<floatx4*>(p.dump_ev + rw * JD + j * D + d) = e;
-    }
+    };
+#pragma unroll
+    for (int it = 0; it < SGP; ++it)
+        if (tid + 256 * it < R * QPR) phase_a(tid + 256 * it, sgp[it]);
+    for (int q = tid + 256 * SGP; q < R * QPR; q += 256) phase_a(q, p.noise_mode != 0 ? p.sig[(q % QPR) / (D >> 2)] : 1.f);
     __syncthreads();
     if (!live) return;  // wave-uniform; no barrier follows
     // A fragments: lane (l16, l4) holds table[i = 16 ib + l16][j = 4 ks + l4]; JP <= 32: every
@@ -853,6 +915,17 @@ __global__ __launch_bounds__(256) void k_update_mfma(const UpdArgs p) {
 #pragma unroll
         for (int ib = 0; ib < IB; ++ib) load_a(ib, ib);
     }
+    // activation + clamp of every tile's x0 first: tanhf branches per lane, and with that
+    // divergent code between one tile's stores and the next tile's work the waitcnt pass drained
+    // vmcnt(0) -- the previous tile's stores -- once per tile
+#pragma unroll
+    for (int q = 0; q < MT; ++q)
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) {
+            float a = bx[q][ks];
+            if (p.act == 1) a = tanhf(a);
+            bx[q][ks] = fminf(fmaxf(a, -1.f), 1.f);
+        }
 #pragma unroll
     for (int q = 0; q < MT; ++q) {
         const int ct = ct0 + q * cstep;
@@ -863,9 +936,7 @@ __global__ __launch_bounds__(256) void k_update_mfma(const UpdArgs p) {
         for (int ks = 0; ks < KS; ++ks) {
             const int j = 4 * ks + l4;
             const bool ok = j < J;
-            float a = bx[q][ks];
-            if (p.act == 1) a = tanhf(a);
-            a = fminf(fmaxf(a, -1.f), 1.f);
+            const float a = bx[q][ks];
             bxa[ks] = ok ? a : 0.f;
             bta[ks] = ok ? bt[q][ks] : 0.f;
             be[ks] = ok ? sEv[(r * J + j) * DS + n] : 0.f;
@@ -925,12 +996,12 @@ hipError_t launch_update(const UpdArgs& a, hipStream_t s) {
         // J <= 64 (MANO J = 51 / 52): one row per workgroup, each wave at most two column tiles
         const size_t lds = (((3 * 64 * 66 + 3) & ~(size_t)3) + (size_t)a.J * (a.D + 16)) * sizeof(float);
         if (lds > 160 * 1024) return hipErrorNotSupported;
+        auto kern = (a.x0_bf16 || a.xt_bf16) ? k_update_mfma<64, 1, 2, true> : k_update_mfma<64, 1, 2>;
         if (lds > 64 * 1024) {
-            const hipError_t e = hipFuncSetAttribute((const void*)k_update_mfma<64, 1, 2>,
-                                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+            const hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
             if (e != hipSuccess) return e;
         }
-        hipLaunchKernelGGL((k_update_mfma<64, 1, 2>), dim3((unsigned)a.B), dim3(256), lds, s, a);
+        hipLaunchKernelGGL(kern, dim3((unsigned)a.B), dim3(256), lds, s, a);
         return hipGetLastError();
     }
     // the instantiations below cover MT column tiles per wave, cstep = 4 / R apart: R = 1 -> MT = 2
@@ -949,8 +1020,12 @@ hipError_t launch_update(const UpdArgs& a, hipStream_t s) {
             hipLaunchKernelGGL(kern, grid, dim3(256), lds, s, a);
             return hipGetLastError();
         };
-        if (a.J <= 16) return R == 1 ? go(k_update_mfma<16, 1, 2>, 16) : go(k_update_mfma<16, 4, 6>, 16);
-        return R == 1 ? go(k_update_mfma<32, 1, 2>, 32) : go(k_update_mfma<32, 4, 6>, 32);
+        const bool bf = a.x0_bf16 || a.xt_bf16;
+        if (a.J <= 16)
+            return R == 1 ? go(bf ? k_update_mfma<16, 1, 2, true> : k_update_mfma<16, 1, 2>, 16)
+                          : go(bf ? k_update_mfma<16, 4, 6, true> : k_update_mfma<16, 4, 6>, 16);
+        return R == 1 ? go(bf ? k_update_mfma<32, 1, 2, true> : k_update_mfma<32, 1, 2>, 32)
+                      : go(bf ? k_update_mfma<32, 4, 6, true> : k_update_mfma<32, 4, 6>, 32);
     }
     if (a.B <= g_update_rows && a.D % 2 == 0) {
         const size_t nt = a.iso ? 0 : 3 * (size_t)a.J * a.J + a.J;

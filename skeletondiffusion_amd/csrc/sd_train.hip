@@ -54,6 +54,18 @@ struct TileRegs {
     float a[TE], b[TE];
 };
 
+// ok ? v : 0 on a value already in registers (the asm pins it there: without it the select became
+// a load through a selected address -- the tile registers went to scratch)
+__device__ __forceinline__ float keep_or_zero(bool ok, float v) {
+    asm volatile("" : "+v"(v));
+    return ok ? v : 0.f;
+}
+__device__ __forceinline__ float4 keep_or_zero(bool ok, float4 v) {
+    f32x4 t = {v.x, v.y, v.z, v.w};
+    asm volatile("" : "+v"(t));
+    return ok ? make_float4(t[0], t[1], t[2], t[3]) : make_float4(0.f, 0.f, 0.f, 0.f);
+}
+
 __device__ __forceinline__ void load_tile(const GemmArgs& g, const float* A, const float* B, int m0, int n0, int k0,
                                           int kend, int tid, TileRegs& r) {
 #pragma unroll
@@ -62,11 +74,23 @@ __device__ __forceinline__ void load_tile(const GemmArgs& g, const float* A, con
         int mm, kk;
         if (g.am == 1) { mm = idx & 63; kk = idx >> 6; } else { kk = idx & (TK - 1); mm = idx / TK; }
         const int gm = m0 + mm, gk = k0 + kk;
-        r.a[q] = (gm < g.M && gk < kend) ? A[gm * g.am + (int64_t)gk * g.ak] : 0.f;
+        // unconditional loads from clamped indices (k0 < kend), out-of-range values zeroed after: a
+        // masked load beside a zero write of the same register waited vmcnt(0) per element
+        r.a[q] = A[min(gm, g.M - 1) * g.am + (int64_t)min(gk, kend - 1) * g.ak];
         int nn, kb;
         if (g.bn == 1) { nn = idx & 63; kb = idx >> 6; } else { kb = idx & (TK - 1); nn = idx / TK; }
         const int gn = n0 + nn, gkb = k0 + kb;
-        r.b[q] = (gn < g.N && gkb < kend) ? B[(int64_t)gkb * g.bk + gn * g.bn] : 0.f;
+        r.b[q] = B[(int64_t)min(gkb, kend - 1) * g.bk + min(gn, g.N - 1) * g.bn];
+    }
+#pragma unroll
+    for (int q = 0; q < TE; ++q) {
+        const int idx = tid + 256 * q;
+        int mm, kk;
+        if (g.am == 1) { mm = idx & 63; kk = idx >> 6; } else { kk = idx & (TK - 1); mm = idx / TK; }
+        r.a[q] = keep_or_zero(m0 + mm < g.M && k0 + kk < kend, r.a[q]);
+        int nn, kb;
+        if (g.bn == 1) { nn = idx & 63; kb = idx >> 6; } else { kb = idx & (TK - 1); nn = idx / TK; }
+        r.b[q] = keep_or_zero(n0 + nn < g.N && k0 + kb < kend, r.b[q]);
     }
 }
 
@@ -95,11 +119,25 @@ __device__ __forceinline__ void load_tile4(const GemmArgs& g, const float* A, co
         int mm, kk;
         if (g.ak == 1) { kk = 4 * (tid & 7); mm = (tid >> 3) + 32 * q; } else { mm = 4 * (tid & 15); kk = (tid >> 4) + 16 * q; }
         const int gm = m0 + mm, gk = k0 + kk;
-        r.a[q] = (gm < g.M && gk < kend) ? *reinterpret_cast<const float4*>(A + gm * g.am + (int64_t)gk * g.ak) : zero;
+        // unconditional 16-B loads from clamped pieces (the chunk's first k / the last full piece of
+        // the extent: a multiple of 4, gemm_vec_ok), out-of-range pieces zeroed after (a masked load
+        // beside a zero write of the same registers waited vmcnt(0) per piece)
+        const int gmc = gm < g.M ? gm : (g.am == 1 ? g.M - 4 : g.M - 1), gkc = gk < kend ? gk : k0;
+        r.a[q] = *reinterpret_cast<const float4*>(A + gmc * g.am + (int64_t)gkc * g.ak);
         int nn, kb;
         if (g.bk == 1) { kb = 4 * (tid & 7); nn = (tid >> 3) + 32 * q; } else { nn = 4 * (tid & 15); kb = (tid >> 4) + 16 * q; }
         const int gn = n0 + nn, gkb = k0 + kb;
-        r.b[q] = (gn < g.N && gkb < kend) ? *reinterpret_cast<const float4*>(B + (int64_t)gkb * g.bk + gn * g.bn) : zero;
+        const int gnc = gn < g.N ? gn : (g.bn == 1 ? g.N - 4 : g.N - 1), gkbc = gkb < kend ? gkb : k0;
+        r.b[q] = *reinterpret_cast<const float4*>(B + (int64_t)gkbc * g.bk + gnc * g.bn);
+    }
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+        int mm, kk;
+        if (g.ak == 1) { kk = 4 * (tid & 7); mm = (tid >> 3) + 32 * q; } else { mm = 4 * (tid & 15); kk = (tid >> 4) + 16 * q; }
+        r.a[q] = keep_or_zero(m0 + mm < g.M && k0 + kk < kend, r.a[q]);
+        int nn, kb;
+        if (g.bk == 1) { kb = 4 * (tid & 7); nn = (tid >> 3) + 32 * q; } else { nn = 4 * (tid & 15); kb = (tid >> 4) + 16 * q; }
+        r.b[q] = keep_or_zero(n0 + nn < g.N && k0 + kb < kend, r.b[q]);
     }
 }
 
@@ -183,6 +221,28 @@ __global__ __launch_bounds__(256) void k_gemm(GemmArgs g) {
     if (g.bias) {
         const int t = g.types ? (int)g.types[batch] : 0;
         bv = g.bias[t * g.bias_t + n];
+    }
+    // Every value and 32-bit byte offset first, pinned in registers, then the 16 stores (SGPR base +
+    // VGPR offset): the compiler waits vmcnt(0) before it overwrites a pending store's data or
+    // address registers, and reusing them per store waited out each store's completion in turn.
+    // (Offsets past 4 GiB: the plain loop.)
+    if ((int64_t)g.M * g.cm * 4 < 0xfffff000LL) {  // uniform
+        float o[16];
+        uint32_t off[16];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int m = m0 + wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+            o[r] = acc[r] + bv;
+            off[r] = (uint32_t)((m * g.cm + n) * 4);
+            asm volatile("" : "+v"(o[r]), "+v"(off[r]));
+        }
+        char* cb = reinterpret_cast<char*>(C);
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int m = m0 + wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+            if (m < g.M) *reinterpret_cast<float*>(cb + off[r]) = o[r];
+        }
+        return;
     }
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
