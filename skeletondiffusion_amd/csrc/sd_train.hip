@@ -67,40 +67,36 @@ __device__ __forceinline__ float4 keep_or_zero(bool ok, float4 v) {
 }
 
 __device__ __forceinline__ void load_tile(const GemmArgs& g, const float* A, const float* B, int m0, int n0, int k0,
-                                          int kend, int tid, TileRegs& r) {
+                                          int kend, int kval, int tid, TileRegs& r) {
+    // unconditional loads from clamped indices (kval: a valid k); the out-of-range values are
+    // zeroed at the LDS store (store_tile), when they have arrived: a masked load beside a zero
+    // write of the same register waited vmcnt(0) per element, and a select right after the load
+    // would wait for it there
 #pragma unroll
     for (int q = 0; q < TE; ++q) {
         const int idx = tid + 256 * q;
         int mm, kk;
         if (g.am == 1) { mm = idx & 63; kk = idx >> 6; } else { kk = idx & (TK - 1); mm = idx / TK; }
         const int gm = m0 + mm, gk = k0 + kk;
-        // unconditional loads from clamped indices (k0 < kend), out-of-range values zeroed after: a
-        // masked load beside a zero write of the same register waited vmcnt(0) per element
-        r.a[q] = A[min(gm, g.M - 1) * g.am + (int64_t)min(gk, kend - 1) * g.ak];
+        r.a[q] = A[min(gm, g.M - 1) * g.am + (int64_t)(gk < kend ? gk : kval) * g.ak];
         int nn, kb;
         if (g.bn == 1) { nn = idx & 63; kb = idx >> 6; } else { kb = idx & (TK - 1); nn = idx / TK; }
         const int gn = n0 + nn, gkb = k0 + kb;
-        r.b[q] = B[(int64_t)min(gkb, kend - 1) * g.bk + min(gn, g.N - 1) * g.bn];
+        r.b[q] = B[(int64_t)(gkb < kend ? gkb : kval) * g.bk + min(gn, g.N - 1) * g.bn];
     }
+}
+
+__device__ __forceinline__ void store_tile(const GemmArgs& g, float (*As)[TM + 4], float (*Bs)[TN + 4], int tid,
+                                           const TileRegs& r, int m0, int n0, int k0, int kend) {
 #pragma unroll
     for (int q = 0; q < TE; ++q) {
         const int idx = tid + 256 * q;
         int mm, kk;
         if (g.am == 1) { mm = idx & 63; kk = idx >> 6; } else { kk = idx & (TK - 1); mm = idx / TK; }
-        r.a[q] = keep_or_zero(m0 + mm < g.M && k0 + kk < kend, r.a[q]);
+        As[kk][mm] = keep_or_zero(m0 + mm < g.M && k0 + kk < kend, r.a[q]);
         int nn, kb;
         if (g.bn == 1) { nn = idx & 63; kb = idx >> 6; } else { kb = idx & (TK - 1); nn = idx / TK; }
-        r.b[q] = keep_or_zero(n0 + nn < g.N && k0 + kb < kend, r.b[q]);
-    }
-}
-
-__device__ __forceinline__ void store_tile(const GemmArgs& g, float (*As)[TM + 4], float (*Bs)[TN + 4], int tid,
-                                           const TileRegs& r) {
-#pragma unroll
-    for (int q = 0; q < TE; ++q) {
-        const int idx = tid + 256 * q;
-        if (g.am == 1) As[idx >> 6][idx & 63] = r.a[q]; else As[idx & (TK - 1)][idx / TK] = r.a[q];
-        if (g.bn == 1) Bs[idx >> 6][idx & 63] = r.b[q]; else Bs[idx & (TK - 1)][idx / TK] = r.b[q];
+        Bs[kb][nn] = keep_or_zero(n0 + nn < g.N && k0 + kb < kend, r.b[q]);
     }
 }
 
@@ -112,50 +108,43 @@ struct TileRegs4 {
 };
 
 __device__ __forceinline__ void load_tile4(const GemmArgs& g, const float* A, const float* B, int m0, int n0, int k0,
-                                           int kend, int tid, TileRegs4& r) {
-    const float4 zero = make_float4(0.f, 0.f, 0.f, 0.f);
+                                           int kend, int kval, int tid, TileRegs4& r) {
+    // unconditional 16-B loads from clamped pieces (kval: a valid k; the last full piece of the m /
+    // n extent, a multiple of 4: gemm_vec_ok); the out-of-range pieces are zeroed at the LDS store
 #pragma unroll
     for (int q = 0; q < 2; ++q) {
         int mm, kk;
         if (g.ak == 1) { kk = 4 * (tid & 7); mm = (tid >> 3) + 32 * q; } else { mm = 4 * (tid & 15); kk = (tid >> 4) + 16 * q; }
         const int gm = m0 + mm, gk = k0 + kk;
-        // unconditional 16-B loads from clamped pieces (the chunk's first k / the last full piece of
-        // the extent: a multiple of 4, gemm_vec_ok), out-of-range pieces zeroed after (a masked load
-        // beside a zero write of the same registers waited vmcnt(0) per piece)
-        const int gmc = gm < g.M ? gm : (g.am == 1 ? g.M - 4 : g.M - 1), gkc = gk < kend ? gk : k0;
+        const int gmc = gm < g.M ? gm : (g.am == 1 ? g.M - 4 : g.M - 1), gkc = gk < kend ? gk : kval;
         r.a[q] = *reinterpret_cast<const float4*>(A + gmc * g.am + (int64_t)gkc * g.ak);
         int nn, kb;
         if (g.bk == 1) { kb = 4 * (tid & 7); nn = (tid >> 3) + 32 * q; } else { nn = 4 * (tid & 15); kb = (tid >> 4) + 16 * q; }
         const int gn = n0 + nn, gkb = k0 + kb;
-        const int gnc = gn < g.N ? gn : (g.bn == 1 ? g.N - 4 : g.N - 1), gkbc = gkb < kend ? gkb : k0;
+        const int gnc = gn < g.N ? gn : (g.bn == 1 ? g.N - 4 : g.N - 1), gkbc = gkb < kend ? gkb : kval;
         r.b[q] = *reinterpret_cast<const float4*>(B + (int64_t)gkbc * g.bk + gnc * g.bn);
-    }
-#pragma unroll
-    for (int q = 0; q < 2; ++q) {
-        int mm, kk;
-        if (g.ak == 1) { kk = 4 * (tid & 7); mm = (tid >> 3) + 32 * q; } else { mm = 4 * (tid & 15); kk = (tid >> 4) + 16 * q; }
-        r.a[q] = keep_or_zero(m0 + mm < g.M && k0 + kk < kend, r.a[q]);
-        int nn, kb;
-        if (g.bk == 1) { kb = 4 * (tid & 7); nn = (tid >> 3) + 32 * q; } else { nn = 4 * (tid & 15); kb = (tid >> 4) + 16 * q; }
-        r.b[q] = keep_or_zero(n0 + nn < g.N && k0 + kb < kend, r.b[q]);
     }
 }
 
 __device__ __forceinline__ void store_tile4(const GemmArgs& g, float (*As)[TM + 4], float (*Bs)[TN + 4], int tid,
-                                            const TileRegs4& r) {
+                                            const TileRegs4& r, int m0, int n0, int k0, int kend) {
 #pragma unroll
     for (int q = 0; q < 2; ++q) {
+        int mm, kk;
+        if (g.ak == 1) { kk = 4 * (tid & 7); mm = (tid >> 3) + 32 * q; } else { mm = 4 * (tid & 15); kk = (tid >> 4) + 16 * q; }
+        const float4 a = keep_or_zero(m0 + mm < g.M && k0 + kk < kend, r.a[q]);
         if (g.ak == 1) {
-            const int kk = 4 * (tid & 7), mm = (tid >> 3) + 32 * q;
-            As[kk][mm] = r.a[q].x; As[kk + 1][mm] = r.a[q].y; As[kk + 2][mm] = r.a[q].z; As[kk + 3][mm] = r.a[q].w;
+            As[kk][mm] = a.x; As[kk + 1][mm] = a.y; As[kk + 2][mm] = a.z; As[kk + 3][mm] = a.w;
         } else {
-            *reinterpret_cast<float4*>(&As[(tid >> 4) + 16 * q][4 * (tid & 15)]) = r.a[q];
+            *reinterpret_cast<float4*>(&As[kk][mm]) = a;
         }
+        int nn, kb;
+        if (g.bk == 1) { kb = 4 * (tid & 7); nn = (tid >> 3) + 32 * q; } else { nn = 4 * (tid & 15); kb = (tid >> 4) + 16 * q; }
+        const float4 b = keep_or_zero(n0 + nn < g.N && k0 + kb < kend, r.b[q]);
         if (g.bk == 1) {
-            const int kb = 4 * (tid & 7), nn = (tid >> 3) + 32 * q;
-            Bs[kb][nn] = r.b[q].x; Bs[kb + 1][nn] = r.b[q].y; Bs[kb + 2][nn] = r.b[q].z; Bs[kb + 3][nn] = r.b[q].w;
+            Bs[kb][nn] = b.x; Bs[kb + 1][nn] = b.y; Bs[kb + 2][nn] = b.z; Bs[kb + 3][nn] = b.w;
         } else {
-            *reinterpret_cast<float4*>(&Bs[(tid >> 4) + 16 * q][4 * (tid & 15)]) = r.b[q];
+            *reinterpret_cast<float4*>(&Bs[kb][nn]) = b;
         }
     }
 }
@@ -182,32 +171,38 @@ __global__ __launch_bounds__(256) void k_gemm(GemmArgs g) {
         if (kbeg >= kend) continue;
         const float* A = g.A + j * g.aj + t * g.at;
         const float* B = g.B + j * g.bj + t * g.bt;
-        TileRegs r;
-        TileRegs4 r4;
-        if (VEC) {
-            load_tile4(g, A, B, m0, n0, kbeg, kend, tid, r4);
-            store_tile4(g, As[0], Bs[0], tid, r4);
-        } else {
-            load_tile(g, A, B, m0, n0, kbeg, kend, tid, r);
-            store_tile(g, As[0], Bs[0], tid, r);
-        }
-        __syncthreads();
-        int cur = 0;
-        for (int k0 = kbeg; k0 < kend; k0 += TK) {
-            const bool more = k0 + TK < kend;
-            if (more) {
-                if (VEC) load_tile4(g, A, B, m0, n0, k0 + TK, kend, tid, r4);
-                else load_tile(g, A, B, m0, n0, k0 + TK, kend, tid, r);
-            }
+        auto mfma_tile = [&](int cur) {
 #pragma unroll
             for (int kk = 0; kk < TK; kk += 2) {
                 const float a = As[cur][kk + (lane >> 5)][wm * 32 + (lane & 31)];
                 const float b = Bs[cur][kk + (lane >> 5)][wn * 32 + (lane & 31)];
                 acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, acc, 0, 0, 0);
             }
+        };
+        // the next tile's loads in registers while the MFMAs of this one run (one barrier per tile);
+        // a three-deep register ring measured no faster (30.2 vs 29.4 us at N = K = 192, 1,024 rows,
+        // with 180 VGPRs): the loop is not load-latency-bound
+        TileRegs r;
+        TileRegs4 r4;
+        if (VEC) {
+            load_tile4(g, A, B, m0, n0, kbeg, kend, kbeg, tid, r4);
+            store_tile4(g, As[0], Bs[0], tid, r4, m0, n0, kbeg, kend);
+        } else {
+            load_tile(g, A, B, m0, n0, kbeg, kend, kbeg, tid, r);
+            store_tile(g, As[0], Bs[0], tid, r, m0, n0, kbeg, kend);
+        }
+        __syncthreads();
+        int cur = 0;
+        for (int k0 = kbeg; k0 < kend; k0 += TK) {
+            const bool more = k0 + TK < kend;
             if (more) {
-                if (VEC) store_tile4(g, As[cur ^ 1], Bs[cur ^ 1], tid, r4);
-                else store_tile(g, As[cur ^ 1], Bs[cur ^ 1], tid, r);
+                if (VEC) load_tile4(g, A, B, m0, n0, k0 + TK, kend, kbeg, tid, r4);
+                else load_tile(g, A, B, m0, n0, k0 + TK, kend, kbeg, tid, r);
+            }
+            mfma_tile(cur);
+            if (more) {
+                if (VEC) store_tile4(g, As[cur ^ 1], Bs[cur ^ 1], tid, r4, m0, n0, k0 + TK, kend);
+                else store_tile(g, As[cur ^ 1], Bs[cur ^ 1], tid, r, m0, n0, k0 + TK, kend);
             }
             __syncthreads();
             cur ^= 1;
