@@ -267,21 +267,9 @@ __global__ __launch_bounds__(256) void k_mix(const float* __restrict__ in, const
         const int jj = e / (4 * RPT), i = e % (4 * RPT);
         s_mt[jj][i] = i < J ? (transpose ? ghat[jj * J + i] : ghat[i * J + jj]) : 0.f;
     }
-    // the J x 64 input slab: every load issued before the first LDS store (unconditional, clamped;
-    // out-of-range values zeroed at the store) -- a load -> store loop waited one memory latency
-    // per element
-    {
-        float v[16];  // J <= 64 (kMaxNodes)
-#pragma unroll
-        for (int k = 0; k < 16; ++k) {
-            const int e = min(tid + 256 * k, J * 64 - 1), j = e >> 6, c = e & 63;
-            v[k] = in[base + (int64_t)j * N + min(n0 + c, N - 1)];
-        }
-#pragma unroll
-        for (int k = 0; k < 16; ++k) {
-            const int e = tid + 256 * k, j = e >> 6, c = e & 63;
-            if (e < J * 64) s_in[j][c] = keep_or_zero(n0 + c < N, v[k]);
-        }
+    for (int e = tid; e < J * 64; e += 256) {
+        const int j = e >> 6, c = e & 63;
+        s_in[j][c] = (n0 + c < N) ? in[base + (int64_t)j * N + n0 + c] : 0.f;
     }
     __syncthreads();
     const int c = tid & 63, i0 = RPT * (tid >> 6);
@@ -456,24 +444,10 @@ __global__ __launch_bounds__(256) void k_dbias_part(const float* __restrict__ dz
     if (n >= N) return;
     const int64_t r0 = (int64_t)blockIdx.z * rows_per_chunk;
     const int64_t r1 = min(rows, r0 + rows_per_chunk);
-    // the (row, node) pairs in batches of 8 loads issued together (the one-load-then-add loop waited
-    // one memory latency per pair); the sum keeps the row-major, node-minor order
-    const int64_t total = (r1 - r0) * J;
     float acc = 0.f;
-    for (int64_t i0 = 0; i0 < total; i0 += 8) {
-        float v[8];
-#pragma unroll
-        for (int u = 0; u < 8; ++u) {
-            const int64_t i = min(i0 + u, total - 1);
-            v[u] = dz[((r0 + i / J) * J + i % J) * N + n];
-        }
-#pragma unroll
-        for (int u = 0; u < 8; ++u) {
-            const int64_t i = i0 + u;
-            const int j = (int)(i % J);
-            if (i < total && (types ? (int)types[j] : 0) == t) acc += v[u];
-        }
-    }
+    for (int64_t r = r0; r < r1; ++r)
+        for (int j = 0; j < J; ++j)
+            if ((types ? (int)types[j] : 0) == t) acc += dz[(r * J + j) * N + n];
     part[((int64_t)blockIdx.z * n_types + t) * N + n] = acc;
 }
 
