@@ -1,0 +1,103 @@
+"""CPU guard of the round-4 ISA audit: the shipped code objects of the hot kernels
+keep the memory-wait shape the audit fixed.  Each case disassembles one kernel symbol of the built
+libskeldiff.so (llvm-objdump --disassemble-symbols) and checks its s_waitcnt / load / store order:
+
+* k_gl4t (tiled GEMM phase, default fill-first ring): the bias is loaded before the K loop, so the
+  epilogue has no global load and no vmcnt wait between its stores; the K loop waits with counts
+  (vmcnt(5) at two chunks in flight), vmcnt(0) only for the last chunk;
+* k_attention<4, 32> (MANO attention): every K / Q / V load issued before the first vmcnt wait
+  (one memory round trip per wave, not one per 16-node tile);
+* k_gl5_mixd (MANO mixing pass): no vmcnt(0) between a row's fill and its stores;
+* k_update_mfma<16, 4, 6> f32 form: no bf16 (ushort) load path.
+"""
+import os
+import re
+import shutil
+import subprocess
+
+import pytest
+
+from conftest import REPO
+from skeletondiffusion_amd import isa_check
+
+LIB = os.path.join(REPO, "skeletondiffusion_amd", "libskeldiff.so")
+OBJDUMP = shutil.which("llvm-objdump") or "/opt/rocm/lib/llvm/bin/llvm-objdump"
+
+pytestmark = pytest.mark.skipif(not os.path.exists(OBJDUMP) or not os.path.exists(LIB), reason="no llvm-objdump / library")
+
+GL4T = "_ZN2sd6k_gl4tILb0ELi0ELi6ELi12ELb0ELi2ELi4ELb0ELb0ELb0ELb1ELb0ELi1EEEvNS_6GLArgsEilNS_4YOutE"
+ATTN = "_ZN2sd11k_attentionILi4ELi32EEEvNS_8AttnArgsE"
+MIXD = "_ZN2sd12_GLOBAL__N_110k_gl5_mixdILi8ELi2ELb0EEEvNS_6GLArgsEPKfl"
+UPD = "_ZN2sd13k_update_mfmaILi16ELi4ELi6ELb0EEEvNS_7UpdArgsE"
+
+_cache = {}
+
+
+def _objects(tmp_dir):
+    if "objs" not in _cache:
+        paths = []
+        for i, (_t, b) in enumerate(isa_check.code_objects(LIB)):
+            path = os.path.join(tmp_dir, f"co{i}.o")
+            with open(path, "wb") as f:
+                f.write(b)
+            paths.append(path)
+        _cache["objs"] = paths
+    return _cache["objs"]
+
+
+def _disasm(tmp_path_factory, sym):
+    """Instruction mnemonics + operands of one kernel symbol, in program order."""
+    d = str(tmp_path_factory.getbasetemp())
+    for path in _objects(d):
+        out = subprocess.run([OBJDUMP, "-d", "--mcpu=gfx950", f"--disassemble-symbols={sym}", path],
+                             capture_output=True, text=True).stdout
+        lines = [l.split("//")[0].strip() for l in out.splitlines()]
+        ins = [l for l in lines if l and not l.endswith(":") and not l.startswith(("Disassembly", "file format"))]
+        if any(re.match(r"s_endpgm", l) for l in ins):
+            return ins
+    pytest.fail(f"symbol {sym} not found in the shipped library")
+
+
+def _vmcnt(line):
+    m = re.match(r"s_waitcnt\b.*vmcnt\((\d+)\)", line)
+    return int(m.group(1)) if m else None
+
+
+def test_gl4t_store_tail_has_no_load_waits(tmp_path_factory):
+    ins = _disasm(tmp_path_factory, GL4T)
+    last_barrier = max(i for i, l in enumerate(ins) if l.startswith("s_barrier"))
+    tail = ins[last_barrier:]
+    assert not any(l.startswith("global_load") for l in tail), "a global load in the epilogue (bias?)"
+    first_store = next(i for i, l in enumerate(tail) if l.startswith("global_store"))
+    waits = [l for l in tail[first_store:] if _vmcnt(l) is not None]
+    assert waits == [], waits
+    counts = [_vmcnt(l) for l in ins if _vmcnt(l) is not None]
+    assert counts.count(0) <= 3 and any(c > 0 for c in counts), counts
+
+
+def test_attention_loads_issued_together(tmp_path_factory):
+    ins = _disasm(tmp_path_factory, ATTN)
+    first_wait = next(i for i, l in enumerate(ins) if _vmcnt(l) is not None)
+    loads = [i for i, l in enumerate(ins) if l.startswith("global_load")]
+    assert len(loads) >= 40 and max(loads) < first_wait, (len(loads), max(loads), first_wait)
+
+
+def test_mixd_rows_do_not_drain_fills(tmp_path_factory):
+    ins = _disasm(tmp_path_factory, MIXD)
+    # between a fill issued inside the row loop (after the first store) and the next store: no
+    # vmcnt(0) (the prologue's one wait before the loop precedes every store)
+    stores = [i for i, l in enumerate(ins) if l.startswith("buffer_store")]
+    fills = [i for i, l in enumerate(ins) if l.startswith("global_load_lds")]
+    in_loop_fills = [f for f in fills if f > stores[0]] if stores else []
+    assert in_loop_fills, "no fill inside the row loop"
+    for f in in_loop_fills:
+        nxt = next((s for s in stores if s > f), None)
+        if nxt is None:
+            continue
+        assert not any(_vmcnt(l) == 0 for l in ins[f:nxt]), ins[f:nxt]
+
+
+def test_update_f32_form_has_no_bf16_loads(tmp_path_factory):
+    ins = _disasm(tmp_path_factory, UPD)
+    assert any(l.startswith("global_load_dword") for l in ins)
+    assert not any(l.startswith(("global_load_ushort", "global_load_short")) for l in ins)
