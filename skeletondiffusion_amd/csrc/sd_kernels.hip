@@ -330,17 +330,15 @@ __global__ __launch_bounds__(256) void k_attention(const AttnArgs p) {
                 ka[u][t] = ok ? ka[u][t] : floatx4{0.f, 0.f, 0.f, 0.f};
                 qv[u][t] = ok ? qv[u][t] * p.scale : floatx4{0.f, 0.f, 0.f, 0.f};
             }
+            // component-major over the JT x JT tiles: consecutive MFMAs are independent (tile by
+            // tile, each waited for the previous one's result); every tile still accumulates its
+            // k steps x, y, z, w in order, so the sums are bit-identical
 #pragma unroll
-            for (int jt = 0; jt < JT; ++jt)
+            for (int e = 0; e < 4; ++e)
 #pragma unroll
-                for (int nt = 0; nt < JT; ++nt) {
-                    floatx4 c = S[jt][nt];
-                    c = mfma4(ka[u][jt].x, qv[u][nt].x, c);
-                    c = mfma4(ka[u][jt].y, qv[u][nt].y, c);
-                    c = mfma4(ka[u][jt].z, qv[u][nt].z, c);
-                    c = mfma4(ka[u][jt].w, qv[u][nt].w, c);
-                    S[jt][nt] = c;
-                }
+                for (int jt = 0; jt < JT; ++jt)
+#pragma unroll
+                    for (int nt = 0; nt < JT; ++nt) S[jt][nt] = mfma4(ka[u][jt][e], qv[u][nt][e], S[jt][nt]);
         }
     }
 
@@ -377,20 +375,22 @@ __global__ __launch_bounds__(256) void k_attention(const AttnArgs p) {
         floatx4* v = vv[DH ? dc / 16 : 0];
         if constexpr (DH == 0) load_v(dc, v);
         mask_v(v);
+        // the JT output tiles' chains interleaved (each still sums jt-major, x y z w minor)
+        floatx4 o[JT];
+#pragma unroll
+        for (int nt = 0; nt < JT; ++nt) o[nt] = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int jt = 0; jt < JT; ++jt)
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+#pragma unroll
+                for (int nt = 0; nt < JT; ++nt) o[nt] = mfma4(v[jt][e], S[jt][nt][e], o[nt]);
 #pragma unroll
         for (int nt = 0; nt < JT; ++nt) {
-            floatx4 o = floatx4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-            for (int jt = 0; jt < JT; ++jt) {
-                o = mfma4(v[jt].x, S[jt][nt].x, o);
-                o = mfma4(v[jt].y, S[jt][nt].y, o);
-                o = mfma4(v[jt].z, S[jt][nt].z, o);
-                o = mfma4(v[jt].w, S[jt][nt].w, o);
-            }
             const int n = nt * 16 + lr;
             if (n < J) {
                 float* ob = p.out + (b * J + n) * hid + h * dh + dc + 4 * lg;
-                *reinterpret_cast<floatx4*>(ob) = o;
+                *reinterpret_cast<floatx4*>(ob) = o[nt];
             }
         }
     }
