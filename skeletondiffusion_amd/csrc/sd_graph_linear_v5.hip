@@ -465,19 +465,21 @@ __global__ __launch_bounds__(256, 2) void k_gl5_mixd(const GLArgs p, const float
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         }
         fill(r + PF);  // slot (r + PF) % NS = (r - 1) % NS: read in row r - 1, before this barrier
+        // the four column blocks' chains interleaved (k step outer): consecutive MFMAs are
+        // independent; each block still sums its k steps in order (bit-identical)
         floatx4 acc[4];
 #pragma unroll
-        for (int cb = 0; cb < 4; ++cb) {
-            floatx4 t = {0.f, 0.f, 0.f, 0.f};
+        for (int cb = 0; cb < 4; ++cb) acc[cb] = floatx4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-            for (int s = 0; s < 16; ++s) {
-                if (s < KS) {  // wave-uniform
-                    const int row = 4 * s + l4;
+        for (int s = 0; s < 16; ++s) {
+            if (s < KS) {  // wave-uniform
+                const int row = 4 * s + l4;
+#pragma unroll
+                for (int cb = 0; cb < 4; ++cb) {
                     const float a = zs[row * 64 + ((((16 * cb + l16) >> 2) ^ ((l4 & 1) << 2)) << 2) + (l16 & 3)];
-                    t = __builtin_amdgcn_mfma_f32_16x16x4f32(a, gb[s], t, 0, 0, 0);
+                    acc[cb] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, gb[s], acc[cb], 0, 0, 0);
                 }
             }
-            acc[cb] = t;
         }
         const bool live = i < J;
 #pragma unroll
