@@ -2111,12 +2111,24 @@ static int g_gl4t_ct3 = [] {
     return e ? atoi(e) : 0;
 }();
 
+// to_qkv (N = 768, K = 192) on 256-column workgroups (3 column groups of 8 tiles instead of 4 of 6:
+// 0.75 of the x re-reads, 24 MFMAs per chunk and wave).  Default on the row-major v5 path (MANO
+// J = 51: 3,757 / 3,766 vs 3,729 / 3,727 futures/s), off on the tiled split route (config 2:
+// 16,104 / 16,353 vs 16,498 / 16,375), profiles/r04_ab/gl4t_ct8.txt.  SKELDIFF_GL4T_CT8 at load:
+// -1 (unset) that default, 0 never, 1 always.
+static int g_gl4t_ct8 = [] {
+    const char* e = getenv("SKELDIFF_GL4T_CT8");
+    return e ? atoi(e) : -1;
+}();
+
 // the release Denoiser's shapes: K = 192 (12 chunks), 256 (to_out, 16) or 384 (24), N a multiple
 // of 96 (192 wide layers, 768 to_qkv, 96 final_glin); hipErrorNotSupported otherwise (k_gl4y)
 template <bool ROWMAJOR>
 static hipError_t launch_gl4t(const GLArgs& a, bool rms, int64_t ntile_r, const YOut& yo, hipStream_t s) {
     const int K = a.K1 + a.K2;
     if (a.K1 % 16 || (a.x1_div != 1 && a.x1_blk)) return hipErrorNotSupported;
+    if ((g_gl4t_ct8 == 1 || (g_gl4t_ct8 < 0 && ROWMAJOR)) && a.N % 256 == 0 && K == 192 && a.prec != 2)
+        return launch_gl4t_v<8, 12, ROWMAJOR, 4, false, 2, false, false, true>(a, rms, ntile_r, yo, s);
     if (a.N % 192 == 0 && !(g_gl4t_ct3 && a.N == 192 && K == 192)) {
         if (K == 192) return launch_gl4t_ct<6, 12, ROWMAJOR>(a, rms, ntile_r, yo, s);
         if (K == 256) return launch_gl4t_ct<6, 16, ROWMAJOR>(a, rms, ntile_r, yo, s);
