@@ -41,7 +41,10 @@
 extern "C" {
 #endif
 
-#define SD_ABI_VERSION 1
+/* ABI history: 1 (rounds 1-3); 2 (round 5) -- sd_mahalanobis_loss_forward / _backward take T,
+ * sd_set_kernel_variant / sd_set_row_chains / sd_set_update_kernel / sd_set_v5_mix removed
+ * (per-plan options instead), sd_test_set_split_route added.  Bindings check it at load. */
+#define SD_ABI_VERSION 2
 
 enum {
     SD_OK = 0,
@@ -260,6 +263,11 @@ int sd_test_qkv_attention(const float* x, int32_t K, const float* W, const int64
  * -1 leaves it.  Returns the previous gl_variant, or -1 for an invalid one (nothing changed);
  * gl_variant = -1 only queries (returns the current value). */
 int sd_test_set_kernel_variant(int32_t gl_variant, int32_t gl4_tile);
+/* Test hook: the v4 split route of the sd_test_graph_linear* entry points ONLY (as
+ * SD_OPT_SPLIT_ROUTE: 0 auto, 1 never, 2 k_gl4y GEMM phase, 3 k_gl4t GEMM phase, 5 fused small
+ * tile; 2 / 3 / 5 allocate the pre-mix scratch per call).  Returns the previous route, or -1 for an
+ * invalid one; route = -1 only queries. */
+int sd_test_set_split_route(int32_t route);
 
 /* Per-plan kernel options (read by the launches recorded after the call; part of the graph
  * cache key).  There is no process-wide kernel state: a plan starts from the SKELDIFF_*

@@ -15,6 +15,11 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 # SKELDIFF_LIB: load another build of the library (e.g. the libskeldiff_dbg.so diagnostic variant)
 LIB_PATH = os.environ.get("SKELDIFF_LIB") or os.path.join(HERE, "libskeldiff.so")
 
+# include/skeldiff.h SD_ABI_VERSION: a library of another ABI is refused at load (round 4 changed
+# signatures under the same number; a client built against the old header would pass shifted
+# arguments instead of failing cleanly)
+SD_ABI_VERSION = 2
+
 SD_FLAG_GRAPH = 1
 SD_FLAG_DEVICE_START = 2
 SD_FLAG_DEVICE_NOISE = 4
@@ -34,7 +39,7 @@ EXPORTED = (
     "sd_attn_train_backward", "sd_film_tanh_forward", "sd_film_tanh_backward", "sd_l1norm_rows_forward",
     "sd_l1norm_rows_backward", "sd_rmsnorm_workspace_bytes", "sd_rmsnorm_forward", "sd_rmsnorm_backward",
     "sd_mahalanobis_loss_forward", "sd_mahalanobis_loss_backward", "sd_best_of_k", "sd_best_of_k_backward",
-    "sd_pose_loss",
+    "sd_pose_loss", "sd_test_set_split_route",
 )
 
 # sd_plan_set_option keys (include/skeldiff.h)
@@ -113,6 +118,7 @@ def _declare(lib: ctypes.CDLL) -> None:
                                                 vp, i32, vp, vp, i64, i32, i32, i32, vp]),
         "sd_test_attention": (ctypes.c_int, [vp, vp, i64, i32, i32, i32, vp]),
         "sd_test_set_kernel_variant": (ctypes.c_int, [i32, i32]),
+        "sd_test_set_split_route": (ctypes.c_int, [i32]),
         "sd_plan_set_precision": (ctypes.c_int, [vp, i32]),
         "sd_plan_set_option": (ctypes.c_int, [vp, i32, i64]),
         "sd_plan_get_option": (ctypes.c_int, [vp, i32, ctypes.POINTER(ctypes.c_int64)]),
@@ -169,6 +175,10 @@ def lib() -> ctypes.CDLL:
                     "(hipcc --offload-arch=gfx950).  There is no CPU fallback for sampling.")
             handle = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
             _declare(handle)
+            abi = handle.sd_abi_version()
+            if abi != SD_ABI_VERSION:
+                raise SkelDiffError(f"{LIB_PATH} has ABI version {abi}, this binding needs {SD_ABI_VERSION}: "
+                                    "rebuild it with skeletondiffusion_amd.build.build_library()")
             info = handle.sd_build_info().decode()
             # the product library is built without packed-FP32 instructions; a
             # diagnostic build is loaded only when named explicitly through SKELDIFF_LIB

@@ -9,14 +9,12 @@ stays on torch ops so that it keeps autograd.
 from __future__ import annotations
 
 import math
-import warnings
 from typing import Dict, Optional
 
 import torch
 import torch.nn.functional as F
 from torch import nn
 
-from ... import _lib
 from ... import engine as _engine
 
 __all__ = ["LatentDiffusion", "extract", "default", "exists", "identity", "linear_beta_schedule",
@@ -268,13 +266,14 @@ class LatentDiffusion(nn.Module):
     @torch.no_grad()
     def p_sample_loop(self, shape, x_cond=None, start_noise=None, sampling_noise=None,
                       return_sampling_noise=False, return_timages=False, if_interpolate=False,
-                      noise2interpolate=None, interpolation_kwargs=None, seed=None, row0=0, **kwargs):
+                      noise2interpolate=None, interpolation_kwargs=None, seed=None, row0=0, out=None, **kwargs):
         """Reverse chain t = T-1 .. 0 (base.py:343-390) on the HIP engine.
 
         Engine extensions (keyword-only, optional): `seed` fixes the device Philox stream used
         when start/sampling noise is not supplied (default: drawn from torch's global RNG, so
         torch.manual_seed controls it); `row0` is the global index of the first row, which makes
-        device noise independent of how rows are split over launches or GPUs."""
+        device noise independent of how rows are split over launches or GPUs; `out` (rows, J, D)
+        fp32 receives the latents (reusing it keeps a captured hipGraph valid across calls)."""
         if start_noise is not None:
             assert tuple(start_noise.shape) == tuple(shape), f"Shape mismatch: {start_noise.shape} != {shape}"
         if sampling_noise is not None:
@@ -290,31 +289,12 @@ class LatentDiffusion(nn.Module):
         if seed is None and (start_noise is None or sampling_noise is None):
             seed = int(torch.randint(0, 2 ** 62, (1,)).item())  # fixed, so a re-run draws the same noise
 
-        def run():
-            return self.engine.sample_loop(shape[0], x_cond=x_cond, start_noise=start_noise,
-                                           sampling_noise=sampling_noise,
-                                           record=(return_sampling_noise, return_timages),
-                                           seed=seed, row0=row0)
-
-        res = run()
-        # the f16 range guard, only where a kernel can set it (the split-f16 graph-linear tiles):
-        # deferred by default (an async copy of the status word, read at a later call: sample()
-        # stays asynchronous); engine.range_guard = "sync" waits and re-runs a hit on exact f32
-        mode = self.engine.range_guard_mode()
-        if mode == "deferred":
-            self.engine.check_range_guard()
-            self.engine.defer_status(shape[0])
-        elif mode == "sync" and self.engine.status(shape[0]) & _lib.SD_STATUS_F16_RANGE:
-            # an activation left the f16 range of the split-f16 kernels: the whole chain again on
-            # the exact-f32 kernels (same seed / noise, so the same sample)
-            warnings.warn("activation outside the f16 range of the split-f16 kernels: re-sampling with the "
-                          "exact-f32 kernels (kernel_variant=3)")
-            old = self.engine.get_option("kernel_variant")
-            self.engine.set_option("kernel_variant", 3)
-            try:
-                res = run()
-            finally:
-                self.engine.set_option("kernel_variant", old)
+        # no host-side range check: a split-f16 tile whose operands leave the f16 range is
+        # recomputed on exact-f32 MFMA inside the kernel (engine.py, exact_tile_f32)
+        res = self.engine.sample_loop(shape[0], x_cond=x_cond, start_noise=start_noise,
+                                      sampling_noise=sampling_noise,
+                                      record=(return_sampling_noise, return_timages), seed=seed, row0=row0,
+                                      out=out)
         img, start, noise_t, mean_t, imgs = res
         noise = start
         if return_sampling_noise:

@@ -220,6 +220,58 @@ __device__ __forceinline__ int64_t zs_off(int64_t row, int j, int n, int J, int 
     return ((((row >> 5) * (N >> 5) + (n >> 5)) * J + j) << 10) + ((row & 31) << 5) + (n & 31);
 }
 
+// f16 range fallback (round 5; was a host-side re-run of the whole call): a wave whose split-f16
+// operands reached |x| >= 65504 (x_hi would be inf) recomputes its 32 x 32 tile -- rows row0 ..
+// row0 + 31, node j, columns col0 .. col0 + 31 -- on exact-f32 MFMA (v_mfma_f32_32x32x2_f32)
+// straight from memory: the x operand as the split kernels address it (row-major with the x_cond
+// row division and the tail rows clamped to row 0, or row-blocked), the plan's f32 weights p.W
+// (types, N, K).  The sum is scaled by 1 / wsp_unscale (a power of two: exact), so the caller's
+// epilogue (acc * unscale * rms + bias) is unchanged and the tile is f32-accurate for any finite
+// input.  Taken only by the waves whose operands left the f16 range (wave-uniform ballot), so
+// the in-range path keeps its arithmetic and its bitwise route equalities.
+// Placement matters: run while the accumulators are live (before the epilogue), its loop raised the
+// register count of every caller (k_gl4t 163 -> 235 VGPRs; the one-kernel J = 17 / 21 tiles
+// spilled 4-8x more), as a call with acc live too (the live values move to callee-saved
+// registers).  So the callers run it AFTER their normal stores, in a rolled loop over the tiles,
+// inlined (no call frame, no scratch), and store the exact tile over the first.
+__device__ __forceinline__ floatx16 exact_tile_f32_impl(const float* x1, int64_t x1_rs, int K1, int x1_div,
+                                                                  int64_t x1_row0, int x1_blk, const float* x2,
+                                                                  int64_t x2_rs, int K2, int x2_blk, int64_t B, int J,
+                                                                  const float* W, int wrow, int N, float unscale,
+                                                                  int64_t row0, int j, int col0) {
+    const int lane = threadIdx.x & 63, l32 = lane & 31, h = lane >> 5;
+    const int K = K1 + K2;
+    const int col = col0 + l32;
+    const float* wr = W + (int64_t)(wrow + (col < N ? col : 0)) * K + 4 * h;
+    const int64_t row = row0 + l32, ac = row < B ? row : 0;
+    // lane (l32, h) row `row`, features k0 + 4h .. + 3 (16-B pieces: K1, K2 multiples of 16)
+    const float* xr1 = x1 + (x1_blk ? blk_off(row, j, 4 * h, J, K1) : ((ac + x1_row0) / x1_div) * x1_rs + (int64_t)j * K1 + 4 * h);
+    const float* xr2 = !K2 ? xr1 : x2 + (x2_blk ? blk_off(row, j, 4 * h, J, K2) : ac * x2_rs + (int64_t)j * K2 + 4 * h);
+    floatx16 c;
+#pragma unroll
+    for (int e = 0; e < 16; ++e) c[e] = 0.f;
+#pragma nounroll
+    for (int k0 = 0; k0 < K; k0 += 8) {  // A[row l32][k0 + 4h + i], B[k0 + 4h + i][col l32]
+        // row-blocked: features f and f + 8 are 256 floats apart, row-major 8
+        const float* xp = k0 < K1 ? xr1 + (x1_blk ? (k0 >> 3) * 256 : k0) : xr2 + (x2_blk ? ((k0 - K1) >> 3) * 256 : k0 - K1);
+        const float4 xv = *reinterpret_cast<const float4*>(xp);
+        float4 wv = *reinterpret_cast<const float4*>(wr + k0);
+        if (col >= N) wv = float4{0.f, 0.f, 0.f, 0.f};
+        c = __builtin_amdgcn_mfma_f32_32x32x2f32(xv.x, wv.x, c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_32x32x2f32(xv.y, wv.y, c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_32x32x2f32(xv.z, wv.z, c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_32x32x2f32(xv.w, wv.w, c, 0, 0, 0);
+    }
+    const float up = 1.0f / unscale;
+#pragma unroll
+    for (int e = 0; e < 16; ++e) c[e] *= up;
+    return c;
+}
+__device__ __forceinline__ floatx16 exact_tile_f32(const GLArgs& p, int64_t row0, int j, int col0) {
+    return exact_tile_f32_impl(p.x1, p.x1_rs, p.K1, p.x1_div, p.x1_row0, p.x1_blk, p.x2, p.x2_rs, p.K2, p.x2_blk, p.B,
+                               p.J, p.W, p.wrow[j], p.N, p.wsp_unscale, row0, j, col0);
+}
+
 template <bool RMS, int PREC, bool ROWMAJOR, int PF = 8>  // PF: chunks in flight
 __global__ __launch_bounds__(256) void k_gl4y(const GLArgs p, int ntile_c, int64_t ntile_r, const YOut yo) {
     const int lane = threadIdx.x & 63, l32 = lane & 31, h = lane >> 5;
@@ -301,7 +353,7 @@ __global__ __launch_bounds__(256) void k_gl4y(const GLArgs p, int ntile_c, int64
     }
 #pragma unroll
     for (int i = 0; i < PF; ++i) compute(nchunk - PF + i, i);
-    if (p.status && __builtin_amdgcn_ballot_w64(amx >= 65504.0f) != 0 && lane == 0) atomicOr(p.status, 1u);
+    const bool oor = __builtin_amdgcn_ballot_w64(amx >= 65504.0f) != 0;  // wave-uniform
     float sc[16];
 #pragma unroll
     for (int r = 0; r < 16; ++r) sc[r] = p.wsp_unscale;
@@ -313,18 +365,28 @@ __global__ __launch_bounds__(256) void k_gl4y(const GLArgs p, int ntile_c, int64
             sc[r] *= 1.0f / fmaxf(sqrtf(n2), 1e-12f);
         }
     }
-    if constexpr (ROWMAJOR) {
-        if (ncol >= p.N) return;
-        float* y = yo.y + tr * yo.y_ts + j * yo.y_js + tc * yo.y_cs + l32;
+    auto store = [&](const floatx16& v) {
+        if constexpr (ROWMAJOR) {
+            if (ncol < p.N) {
+                float* y = yo.y + tr * yo.y_ts + j * yo.y_js + tc * yo.y_cs + l32;
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            const int rr = (r & 3) + 8 * (r >> 2) + 4 * h;
-            if (row0 + rr < p.B) y[rr * yo.y_rs] = acc[r] * sc[r] + bv;
+                for (int r = 0; r < 16; ++r) {
+                    const int rr = (r & 3) + 8 * (r >> 2) + 4 * h;
+                    if (row0 + rr < p.B) y[rr * yo.y_rs] = v[r] * sc[r] + bv;
+                }
+            }
+        } else {  // the split route's column-tiled scratch: every row of the tile, N % 32 == 0
+            float* y = p.zs + zs_off(row0, j, tc * 32, J, p.N) + l32;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) y[((r & 3) + 8 * (r >> 2) + 4 * h) << 5] = v[r] * sc[r] + bv;
         }
-    } else {  // the split route's column-tiled scratch: every row of the tile, N % 32 == 0
-        float* y = p.zs + zs_off(row0, j, tc * 32, J, p.N) + l32;
-#pragma unroll
-        for (int r = 0; r < 16; ++r) y[((r & 3) + 8 * (r >> 2) + 4 * h) << 5] = acc[r] * sc[r] + bv;
+    };
+    store(acc);
+    // f16 range left: the tile again on exact-f32 MFMA, stored over the first (same lanes, same
+    // addresses: program order); after the stores, so no accumulator is live across the call
+    if (oor) {
+        if (p.status && lane == 0) atomicOr(p.status, 1u);
+        store(exact_tile_f32(p, row0, j, tc * 32));
     }
 }
 
@@ -735,7 +797,7 @@ __global__ __launch_bounds__((NWV + (LDW ? 1 : 0)) * 64, WRES ? 1 : 2) void k_gl
             compute(c, 0, sW[g % NS]);
             if (c != NCH - 1) return;  // wave-uniform
             if (live) {
-                if (p.status && __builtin_amdgcn_ballot_w64(amx >= 65504.0f) != 0 && lane == 0) atomicOr(p.status, 1u);
+                const bool oor = __builtin_amdgcn_ballot_w64(amx >= 65504.0f) != 0;  // wave-uniform
                 float sc[16];
 #pragma unroll
                 for (int r = 0; r < 16; ++r) sc[r] = p.wsp_unscale;
@@ -749,20 +811,26 @@ __global__ __launch_bounds__((NWV + (LDW ? 1 : 0)) * 64, WRES ? 1 : 2) void k_gl
                 }
                 const int cgu = cg * NU + uu;
                 float* y = yo.y + tr * yo.y_ts + j * yo.y_js + (int64_t)cgu * CT * yo.y_cs;
+                auto store_tile = [&](int ct, const floatx16& v) {
+                    const float bv = p.bias ? sBias[(uu & 1) * 256 + ct * 32 + l32] : 0.f;  // LDS: any ct
 #pragma unroll
-                for (int ct = 0; ct < CT; ++ct) {
-                    const float bv = p.bias ? sBias[(uu & 1) * 256 + ct * 32 + l32] : 0.f;
-#pragma unroll
-                    for (int r = 0; r < 16; ++r) sTd[((r & 3) + 8 * (r >> 2) + 4 * h) * TS + l32] = acc[ct][r] * sc[r] + bv;
+                    for (int r = 0; r < 16; ++r) sTd[((r & 3) + 8 * (r >> 2) + 4 * h) * TS + l32] = v[r] * sc[r] + bv;
                     __builtin_amdgcn_wave_barrier();
 #pragma unroll
                     for (int q = 0; q < 4; ++q) {
                         const int row = 8 * q + (lane >> 3), c4 = (lane & 7) * 4;
-                        const floatx4 v = *reinterpret_cast<const floatx4*>(sTd + row * TS + c4);
+                        const floatx4 o = *reinterpret_cast<const floatx4*>(sTd + row * TS + c4);
                         if (!ROWMAJOR || row0 + row < p.B)
-                            *reinterpret_cast<floatx4*>(y + (int64_t)row * yo.y_rs + ct * yo.y_cs + c4) = v;
+                            *reinterpret_cast<floatx4*>(y + (int64_t)row * yo.y_rs + ct * yo.y_cs + c4) = o;
                     }
                     __builtin_amdgcn_wave_barrier();
+                };
+#pragma unroll
+                for (int ct = 0; ct < CT; ++ct) store_tile(ct, acc[ct]);
+                if (oor) {  // f16 range left: the unit's tiles again on exact-f32 MFMA (as the main epilogue)
+                    if (p.status && lane == 0) atomicOr(p.status, 1u);
+#pragma nounroll
+                    for (int ct = 0; ct < CT; ++ct) store_tile(ct, exact_tile_f32(p, row0, j, (cgu * CT + ct) * 32));
                 }
             }
 #pragma unroll
@@ -935,7 +1003,7 @@ __global__ __launch_bounds__((NWV + (LDW ? 1 : 0)) * 64, WRES ? 1 : 2) void k_gl
     }
 #endif
     if (!live) return;
-    if (p.status && __builtin_amdgcn_ballot_w64(amx >= 65504.0f) != 0 && lane == 0) atomicOr(p.status, 1u);
+    const bool oor = PREC != 2 && __builtin_amdgcn_ballot_w64(amx >= 65504.0f) != 0;  // wave-uniform
     float sc[16];
 #pragma unroll
     for (int r = 0; r < 16; ++r) sc[r] = p.wsp_unscale;
@@ -952,20 +1020,30 @@ __global__ __launch_bounds__((NWV + (LDW ? 1 : 0)) * 64, WRES ? 1 : 2) void k_gl
     // per tile.  Launch shapes: N a multiple of 32 CT (launch_gl4t), so every column is real.
     float* sT = reinterpret_cast<float*>(smem_raw) + wave * 32 * TS;
     float* y = yo.y + tr * yo.y_ts + j * yo.y_js + (int64_t)cg * CT * yo.y_cs;  // YOut as k_gl4y's
+    auto store_tile = [&](int ct, const floatx16& v, float bv) {
 #pragma unroll
-    for (int ct = 0; ct < CT; ++ct) {
-        const float bv = bvp[ct];
-#pragma unroll
-        for (int r = 0; r < 16; ++r) sT[((r & 3) + 8 * (r >> 2) + 4 * h) * TS + l32] = acc[ct][r] * sc[r] + bv;
+        for (int r = 0; r < 16; ++r) sT[((r & 3) + 8 * (r >> 2) + 4 * h) * TS + l32] = v[r] * sc[r] + bv;
         __builtin_amdgcn_wave_barrier();  // DS operations of one wave complete in order
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
             const int row = 8 * q + (lane >> 3), c4 = (lane & 7) * 4;
-            const floatx4 v = *reinterpret_cast<const floatx4*>(sT + row * TS + c4);
+            const floatx4 o = *reinterpret_cast<const floatx4*>(sT + row * TS + c4);
             if (!ROWMAJOR || row0 + row < p.B)  // row-major z holds rows < B only
-                *reinterpret_cast<floatx4*>(y + (int64_t)row * yo.y_rs + ct * yo.y_cs + c4) = v;
+                *reinterpret_cast<floatx4*>(y + (int64_t)row * yo.y_rs + ct * yo.y_cs + c4) = o;
         }
         __builtin_amdgcn_wave_barrier();
+    };
+#pragma unroll
+    for (int ct = 0; ct < CT; ++ct) store_tile(ct, acc[ct], bvp[ct]);
+    // f16 range left: every tile of the wave again on exact-f32 MFMA, stored over the first (same
+    // lanes, same addresses: program order) -- after the stores, with the accumulators dead
+    if (oor) {
+        if (p.status && lane == 0) atomicOr(p.status, 1u);
+#pragma nounroll
+        for (int ct = 0; ct < CT; ++ct) {
+            const int col = (cg * CT + ct) * 32;
+            store_tile(ct, exact_tile_f32(p, row0, j, col), p.bias ? p.bias[p.wrow[j] + col + l32] : 0.f);
+        }
     }
 #ifdef SD_GL4T_STAMPS
     if (STAMP && lane == 0 && blockIdx.x < 8192) {
@@ -1728,8 +1806,11 @@ __global__ __launch_bounds__(NW * 64, 1) void k_gl4(const GLArgs p) {
     }
     if (DBG == 6) ts[7] = clock64();
     if (DBG == 6) ts[2] = wall_clock64();
-    // f16 range guard: an activation the split cannot represent (the caller re-runs on the
-    // exact-f32 kernels, engine.py); one atomic per wave at most, none in range
+    // f16 range guard: an activation the split cannot represent.  The one-kernel tiles (MODE 0 / 1
+    // / 4: J <= 21 on SD_OPT_SPLIT_ROUTE 1 / 5, half precision's J = 16 full-batch default) only
+    // report it in the status word -- their accumulators stay live into the mixing epilogue, and a
+    // recompute here (inline or called) raised their register counts / spills severalfold; the
+    // split-route GEMM phases k_gl4t / k_gl4y recompute such tiles in exact f32 (exact_tile_f32)
     if (p.status && __builtin_amdgcn_ballot_w64(amx >= 65504.0f) != 0 && lane == 0) atomicOr(p.status, 1u);
 
     // ---- unscale, RMS, bias in the accumulator layout:
@@ -2012,16 +2093,21 @@ template <bool ROWMAJOR>
 static hipError_t launch_gl4y(const GLArgs& a, bool rms, int ntc, int64_t ntile_r, const YOut& yo, hipStream_t s) {
     const int64_t units = ntile_r * a.J * ntc;
     const dim3 grid((unsigned)((units + 3) / 4));
-    const int nchunk = (a.K1 + a.K2) / 16;  // even (launch_graph_linear_v4)
+    // any chunk count: the v5 GEMM phase (launch_gemm_split) passes K = 16 / 48 (odd nchunk) too
+    const int nchunk = (a.K1 + a.K2) / 16;
+    if (nchunk < 1 || (a.K1 + a.K2) % 16) return hipErrorNotSupported;
     g_route_bits |= kRouteGemmWave;
-    // chunks in flight: a divisor of nchunk (the K loop's rounds); every chunk of a K = 192 layer
-    // in flight on grids of at most one workgroup per CU
+    // chunks in flight: a divisor of nchunk (the K loop's rounds: the loop issues unconditionally,
+    // so PF must divide nchunk); every chunk of a K = 192 layer in flight on grids of at most one
+    // workgroup per CU
     if (g_gl4y_pf == 12 && grid.x <= 256 && a.prec == 0 && nchunk % 12 == 0)
         launch_gl4y_pf<ROWMAJOR, 12>(a, rms, ntc, ntile_r, yo, grid, s);
     else if (nchunk % 8 == 0) launch_gl4y_pf<ROWMAJOR, 8>(a, rms, ntc, ntile_r, yo, grid, s);
     else if (nchunk % 6 == 0) launch_gl4y_pf<ROWMAJOR, 6>(a, rms, ntc, ntile_r, yo, grid, s);
     else if (nchunk % 4 == 0) launch_gl4y_pf<ROWMAJOR, 4>(a, rms, ntc, ntile_r, yo, grid, s);
-    else launch_gl4y_pf<ROWMAJOR, 2>(a, rms, ntc, ntile_r, yo, grid, s);
+    else if (nchunk % 3 == 0) launch_gl4y_pf<ROWMAJOR, 3>(a, rms, ntc, ntile_r, yo, grid, s);
+    else if (nchunk % 2 == 0) launch_gl4y_pf<ROWMAJOR, 2>(a, rms, ntc, ntile_r, yo, grid, s);
+    else launch_gl4y_pf<ROWMAJOR, 1>(a, rms, ntc, ntile_r, yo, grid, s);
     return hipGetLastError();
 }
 

@@ -1341,6 +1341,17 @@ static int g_test_variant = -1, g_test_tile = -1;  // -1: the process defaults (
 static int test_variant() { return g_test_variant >= 0 ? g_test_variant : sd::graph_linear_variant(); }
 static int test_tile() { return g_test_tile >= 0 ? g_test_tile : sd::gl4_tile_default(); }
 
+// split route of the test entry points (GLArgs::split: 0 auto, 1 never, 2 k_gl4y, 3 k_gl4t, 5
+// the fused small tile); 2 / 3 / 5 give sd_test_graph_linear* a scratch of its own for the pre-mix Y
+static int g_test_split = 0;
+int sd_test_set_split_route(int32_t route) {
+    if (route == -1) return g_test_split;  // query
+    if (route < 0 || route > 5) return fail(SD_E_INVALID, "split route out of range");
+    const int old = g_test_split;
+    g_test_split = route;
+    return old;
+}
+
 int sd_test_set_kernel_variant(int32_t gl_variant, int32_t gl4_tile) {
     if (gl_variant == -1) return test_variant();  // query
     if (gl_variant < 0 || gl_variant > 5) return fail(SD_E_INVALID, "gl_variant out of range");
@@ -1502,10 +1513,18 @@ int sd_test_graph_linear_layout(const float* x1, int32_t K1, int64_t x1_div, con
         a.wsp_nct = sw.nct;
         a.wsp_unscale = sw.unscale;
     }
+    a.split = g_test_split;
+    float* zs = nullptr;
+    if (a.split >= 2 && rows > 0) {  // the split route's pre-mix Y scratch (zs_off layout)
+        a.zs_cap = (rows + 31) / 32 * 32 * (int64_t)J * N;
+        SD_HIP(hipMalloc(&zs, a.zs_cap * sizeof(float)));
+        a.zs = zs;
+    }
     const hipError_t e = sd::launch_graph_linear(a, rms != 0, (hipStream_t)stream);
-    if (sw.w && !cache) {
+    if ((sw.w && !cache) || zs) {
         (void)hipStreamSynchronize((hipStream_t)stream);
-        (void)hipFree(sw.w);
+        if (sw.w && !cache) (void)hipFree(sw.w);
+        if (zs) (void)hipFree(zs);
     }
     SD_HIP(e);
     return SD_OK;

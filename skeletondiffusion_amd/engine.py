@@ -11,7 +11,6 @@ from __future__ import annotations
 
 import ctypes
 import threading
-import warnings
 from typing import Optional, Tuple
 
 import torch
@@ -36,7 +35,6 @@ class SamplingEngine:
         self._graph = False
         self._precision = 0
         self._options = {}  # sd_plan_set_option values, re-applied when the plan is rebuilt
-        self._pending = []  # deferred range-guard reads: (pinned host word, event)
 
     # ---------------------------------------------------------------------------------------
     def __del__(self):
@@ -119,59 +117,11 @@ class SamplingEngine:
                "last_route": _lib.SD_OPT_LAST_ROUTE, "update_kernel": _lib.SD_OPT_UPDATE_KERNEL,
                "v5_mix": _lib.SD_OPT_V5_MIX}
     READ_ONLY = ("last_chains", "last_route")
-    # sample()'s f16 range guard (SD_STATUS_F16_RANGE, set on the device by a split-f16 launch
-    # whose input reached |x| >= 65504):
-    #   "deferred" (default) -- the call stays asynchronous: the workspace status word is copied
-    #       to pinned host memory behind it on the same stream and read at the next sample() or
-    #       check_range_guard(); a hit warns that that call's latents are not f32-accurate;
-    #   "sync" -- wait for the status after each call and re-run a hit on the exact-f32 kernels;
-    #   "off" -- not checked.
-    range_guard = "deferred"
-
-    def range_guard_mode(self) -> str:
-        """"deferred" / "sync" / "off" where the plan's graph-linear kernels can raise
-        SD_STATUS_F16_RANGE (the split-f16 tiles, kernel variant 0 / 4, in f32 or half
-        precision); "off" for the exact-f32 kernels and the bf16 mode, which never do."""
-        mode = {True: "sync", False: "off", None: "off"}.get(self.range_guard, self.range_guard)
-        if mode not in ("deferred", "sync", "off"):
-            raise SkelDiffError(f"range_guard must be 'deferred', 'sync' or 'off', got {self.range_guard!r}")
-        if self._precision == self.PRECISIONS["bf16"] or self._options.get("kernel_variant", 0) not in (0, 4):
-            return "off"
-        return mode
-
-    def defer_status(self, rows: int) -> None:
-        """Queue an asynchronous copy of the `rows`-row workspace's status word (behind the work
-        already on torch's current stream) for check_range_guard()."""
-        ws, _ = self.workspace(rows)
-        host = torch.empty(1, dtype=torch.int32, pin_memory=True)
-        host.copy_(ws[32:36].view(torch.int32), non_blocking=True)  # sd_workspace_status's word
-        ev = torch.cuda.Event()
-        ev.record(torch.cuda.current_stream(self._device))
-        with self._ws_lock:
-            self._pending.append((host, ev))
-            del self._pending[:-64]  # bounded: the oldest unchecked calls are dropped
-
-    def check_range_guard(self, wait: bool = False) -> bool:
-        """Read the deferred status of earlier calls whose copies have landed (all of them, waiting,
-        when `wait`); warn and return True if any of them left the f16 range."""
-        with self._ws_lock:
-            pend, self._pending = self._pending, []
-        hit, keep = False, []
-        for host, ev in pend:
-            if wait:
-                ev.synchronize()
-            elif not ev.query():
-                keep.append((host, ev))
-                continue
-            hit = hit or bool(int(host.item()) & _lib.SD_STATUS_F16_RANGE)
-        if keep:
-            with self._ws_lock:
-                self._pending[:0] = keep
-        if hit:
-            warnings.warn("an earlier sample() call had activations outside the f16 range of the split-f16 kernels: "
-                          "its latents are not f32-accurate (set engine.range_guard = 'sync' to re-run such calls "
-                          "on the exact-f32 kernels, or kernel_variant=3)")
-        return hit
+    # The split-f16 graph-linear tiles need |x| < 65504.  A wave whose operands leave that range
+    # recomputes its tiles on exact-f32 MFMA inside the kernel (sd_graph_linear_v4.hip:
+    # exact_tile_f32) and sets SD_STATUS_F16_RANGE in the workspace status word for information
+    # (status()); sample() needs no host check, no re-run and no warning: its latents are
+    # f32-accurate for any finite input.
 
     def set_option(self, name: str, value: int) -> None:
         """Per-plan kernel option (sd_plan_set_option): "kernel_variant" (0 auto, 1..5),
@@ -356,15 +306,20 @@ class SamplingEngine:
         ws, _ = self.workspace(rows)
         # through the torch.library op skeldiff::sample_loop (ops.py): shape / dtype / device
         # validation against the plan, then sd_sample_loop on torch's current stream
-        torch.ops.skeldiff.sample_loop(plan.value, xc, rep, start, samp, seed, int(row0), out, noise_t, mean_t, imgs,
-                                       start_out, ws, flags)
+        # the op's schema int is signed int64: a uint64 seed >= 2^63 travels as its two's
+        # complement and the op masks it back to uint64 (ops.py)
+        seed = int(seed) & (2 ** 64 - 1)
+        seed_i64 = seed - 2 ** 64 if seed >= 2 ** 63 else seed
+        torch.ops.skeldiff.sample_loop(plan.value, xc, rep, start, samp, seed_i64, int(row0), out, noise_t, mean_t,
+                                       imgs, start_out, ws, flags)
         start_ret = start.clone() if start is not None else start_out
         return out, start_ret, noise_t, mean_t, imgs
 
     def status(self, rows: int) -> int:
         """Flags of the last sample_loop / denoiser_forward on the `rows`-row workspace
         (sd_workspace_status; synchronises the current stream): SD_STATUS_F16_RANGE = an
-        activation left the f16 range of the split-f16 products."""
+        activation left the f16 range of the split-f16 products and its tiles were recomputed on
+        exact-f32 MFMA in the kernel (informational: the results are f32-accurate either way)."""
         ws, nb = self.workspace(rows)
         v = ctypes.c_uint32()
         check(_lib.lib().sd_workspace_status(self.plan(), ptr(ws), nb, ctypes.byref(v), _stream(self._device)))

@@ -77,6 +77,39 @@ def scan(so_path: str) -> dict:
     return res
 
 
+# kernel-level keys of amdhsa.kernels: a kernel's map starts with "  - ." and its own keys sit at
+# 4 columns (its .args entries deeper)
+_NOTE_KEY = re.compile(r"^(  - |    )\.(name|vgpr_count|agpr_count|sgpr_count|private_segment_fixed_size|"
+                       r"group_segment_fixed_size|vgpr_spill_count|sgpr_spill_count):\s*(\S+)\s*$")
+
+
+def resources(so_path: str) -> dict:
+    """{kernel symbol: {'vgpr_count', 'agpr_count', 'sgpr_count', 'private_segment_fixed_size'
+    (scratch bytes per lane), 'group_segment_fixed_size' (static LDS), 'vgpr_spill_count', ...}}
+    from the AMDGPU metadata notes of every device code object (`llvm-readelf --notes`)."""
+    out = {}
+    with tempfile.TemporaryDirectory() as td:
+        for i, (_, blob) in enumerate(code_objects(so_path)):
+            path = os.path.join(td, f"co{i}.o")
+            with open(path, "wb") as f:
+                f.write(blob)
+            notes = subprocess.run([_tool("llvm-readelf"), "--notes", path], check=True, capture_output=True,
+                                   text=True).stdout
+            cur = {}
+            for line in notes.splitlines():
+                if line.startswith("  - "):  # a new kernel's map begins
+                    if ".name" in cur:
+                        out[cur.pop(".name")] = cur
+                    cur = {}
+                m = _NOTE_KEY.match(line)
+                if m:
+                    _, k, v = m.groups()
+                    cur["." + k if k == "name" else k] = v if k == "name" else int(v)
+            if ".name" in cur:
+                out[cur.pop(".name")] = cur
+    return out
+
+
 def check(so_path: str) -> dict:
     """Raise RuntimeError unless every code object is gfx950 code without packed-FP32 instructions."""
     r = scan(so_path)

@@ -136,6 +136,52 @@ def test_config2_as_benched(cuda):
         assert _max_err(imgs[sel, k], x) < TOL, (k, _max_err(imgs[sel, k], x))
 
 
+@pytest.mark.config_parity
+def test_config3_as_benched(cuda):
+    """BASELINE config 3's per-rank shard exactly as `bench.py --config mano51` times it (AMASS-MANO
+    J = 51, 64 sequences x 50 futures = 3,200 rows, T = 100, default plan options: v5 with the
+    split-f16 k_gl4t GEMM phase -- to_qkv on the 8-tile CT8 workgroups -- the k_gl5_mixd LDS-DMA
+    mixing ring and k_attention, on 3 row chains sharing CUs, hipGraph, device noise, reused
+    output buffer): every per-step record of the whole chain bitwise equal to one chain run
+    eagerly; the first 3 steps against the oracle on the rows either side of each chain boundary."""
+    from bench import build_config
+
+    d, x_cond, rows = build_config("mano51", cuda, T=100)
+    J, D, T = d.channels, d.seq_length, d.num_timesteps
+    assert (rows, J, T) == (3200, 51, 100)
+    eng, seed = d.engine, 20261018
+    out = torch.empty((rows, J, D), device=cuda)
+    a = eng.sample_loop(rows, x_cond=x_cond, seed=seed, graph=True, out=out, record=(True, True))
+    a = [t.clone() for t in (a[0], a[1], a[2], a[4])]  # img, start, noise_t, imgs
+    assert eng.get_option("last_chains") == 3  # auto at 3,200 rows
+    bits = eng.get_option("last_route")
+    assert bits & 8 and bits & 32 and bits & 128, bits  # k_gl4t GEMM phase, v5 mixing, k_attention
+    eng.set_option("row_chains", 1)
+    b = eng.sample_loop(rows, x_cond=x_cond, seed=seed, graph=False, record=(True, True))
+    b = [b[0], b[1], b[2], b[4]]
+    assert eng.get_option("last_chains") == 1
+    eng.set_option("row_chains", 0)
+    c = eng.sample_loop(rows, x_cond=x_cond, seed=seed, graph=True, out=out, keep_start=False)[0]
+    assert eng.get_option("last_chains") == 3
+    torch.cuda.synchronize()
+    for x, y in zip(a, b):
+        assert torch.equal(x, y)
+    assert torch.equal(c, a[0])
+    img, start, imgs = a[0], a[1], a[3]
+    assert torch.isfinite(img).all() and img.abs().max() <= 1.0 + 1e-6
+    assert eng.status(rows) == 0
+    # 3 chains of a 3,200-row call start at rows 0, 1056, 2112 (multiples of 32)
+    sel = np.concatenate([np.arange(0, 8), np.arange(1048, 1064), np.arange(2104, 2120), np.arange(3192, 3200)])
+    sd, cfg, bufs = _oracle_setup(d)
+    xc = x_cond.cpu().repeat_interleave(rows // x_cond.shape[0], 0)[sel]
+    x = _device_normals(seed, sel, T, J, D)
+    assert _max_err(start[sel], x) < 2e-5
+    for k in range(3):
+        t = T - 1 - k
+        x, _ = O.p_sample_step(sd, cfg, bufs, x, t, _device_normals(seed, sel, t, J, D), x_cond=xc)
+        assert _max_err(imgs[sel, k], x) < TOL, (k, _max_err(imgs[sel, k], x))
+
+
 @pytest.mark.parametrize("route,staging", [(1, 0), (1, 1), (3, 0), (2, 0)])
 def test_row_chains_share_cus_bitwise(route, staging, cuda):
     """Row chains whose kernels share CUs (no whole-CU reservations) on each route
@@ -431,46 +477,33 @@ def test_graph_linear_rejects_aliased_output(cuda):
     assert rc != 0 and b"invalid" in L.sd_last_error().lower()
 
 
-def test_f16_range_guard_falls_back_to_exact_f32(cuda):
-    """Activations the split-f16 products cannot represent (|x| >= 65504) set the workspace status
-    (sd_workspace_status); sample() then re-runs the chain on the exact-f32 kernels, so the
-    result equals an exact-f32 plan's."""
-    z = golden("release_h36m16_T10")
-    d = build_release_diffusion(z, cuda)
-    d.engine.range_guard = "sync"  # opt-in: wait for the status after each call, re-run a hit
-    xcs, fu, start, samp = release_inputs(z)
-    kw = dict(batch_size=start.shape[0], start_noise=start.to(cuda), sampling_noise=samp.to(cuda))
-    d.sample(x_cond=xcs.to(cuda), **kw)
-    assert d.engine.status(start.shape[0]) == 0
-    big = xcs.to(cuda) * 1e5
-    with pytest.warns(UserWarning, match="f16 range"):
-        img = d.sample(x_cond=big, **kw)[0]
-    assert d.engine.get_option("kernel_variant") == 0  # restored after the fallback
-    ref = build_release_diffusion(z, cuda)
-    ref.engine.set_option("kernel_variant", 3)
-    img_ref = ref.sample(x_cond=big, **kw)[0]
-    assert torch.equal(img, img_ref)
-
-
-def test_f16_range_guard_deferred_by_default(cuda):
-    """The default sample() does not wait for the range guard: the status word is copied behind
-    the call and read later (check_range_guard / the next sample()); a hit warns that the earlier
-    call's latents are not f32-accurate, a clean call does not."""
+@pytest.mark.parametrize("route", [0, 1, 2, 3])
+def test_f16_range_exact_in_kernel(route, cuda):
+    """Activations the split-f16 products cannot represent (|x| >= 65504; conditioning latents
+    scaled by 1e5) on each split-f16 route -- auto, one-kernel k_gl4, k_gl4y + MODE 2 / 3, tiled
+    k_gl4t + MODE 2 / 3 -- with default options: the waves that leave the range recompute their
+    tiles on exact-f32 MFMA in the kernel (exact_tile_f32), so sample() returns latents within the
+    1e-4 parity bar of an exact-f32 plan's, with no warning and no host re-run; the status word
+    records that the fallback ran.  In range, the status stays clear."""
     import warnings
 
     z = golden("release_h36m16_T10")
     d = build_release_diffusion(z, cuda)
-    assert d.engine.range_guard_mode() == "deferred"
+    if route:
+        d.engine.set_option("split_route", route)
     xcs, fu, start, samp = release_inputs(z)
     kw = dict(batch_size=start.shape[0], start_noise=start.to(cuda), sampling_noise=samp.to(cuda))
     d.sample(x_cond=xcs.to(cuda), **kw)
-    with warnings.catch_warnings():
-        warnings.simplefilter("error")
-        assert d.engine.check_range_guard(wait=True) is False
-    d.sample(x_cond=xcs.to(cuda) * 1e5, **kw)
-    assert len(d.engine._pending) == 1  # queued, not yet read
-    with pytest.warns(UserWarning, match="f16 range"):
-        assert d.engine.check_range_guard(wait=True) is True
-    assert d.engine._pending == []
-    d.engine.set_option("kernel_variant", 3)  # the exact-f32 kernels never raise it
-    assert d.engine.range_guard_mode() == "off"
+    assert d.engine.status(start.shape[0]) == 0
+    ref = build_release_diffusion(z, cuda)
+    ref.engine.set_option("kernel_variant", 3)
+    for scale in (1e5, 3e9):
+        big = xcs.to(cuda) * scale
+        with warnings.catch_warnings():
+            warnings.simplefilter("error")
+            img = d.sample(x_cond=big, **kw)[0]
+            torch.cuda.synchronize()
+        assert d.engine.status(start.shape[0]) & _lib.SD_STATUS_F16_RANGE
+        img_ref = ref.sample(x_cond=big, **kw)[0]
+        assert torch.isfinite(img).all()
+        assert _max_err(img, img_ref) < TOL, (route, scale, _max_err(img, img_ref))

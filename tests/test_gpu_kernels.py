@@ -91,6 +91,10 @@ CASES = [  # (J, n_types, K1, K2, N, div, bias, film, act, res, rms)
     (5, 3, 96, 0, 96, 1, True, False, 0, False, False),       # generic JM=8 path
     (12, 4, 192, 0, 192, 1, True, True, 1, True, True),       # generic JM=16 path, everything on
     (33, 7, 96, 0, 192, 1, True, False, 1, False, False),     # generic JM=64 path
+    # J > 21 (v5's split GEMM phase) with an odd chunk count: latent_dim 16 / 48, cond_dim 0
+    (33, 7, 16, 0, 96, 1, True, False, 0, False, False),
+    (33, 7, 48, 0, 96, 1, True, False, 0, False, False),
+    (51, 43, 48, 0, 192, 1, True, False, 1, True, False),
 ]
 
 
@@ -128,6 +132,64 @@ def test_graph_linear_v5(case, kernel_variant, cuda):
     """v5 (node-batched GEMM + mixing pass; the default for J > 21) forced on every shape."""
     kernel_variant(5, 0)
     _check_gl(*case, 67, cuda)
+
+
+@pytest.fixture
+def split_route():
+    """Select the split route of the sd_test_graph_linear* hooks for one test, restoring auto."""
+    L = _lib.lib()
+
+    def set_(route):
+        assert L.sd_test_set_split_route(route) >= 0
+
+    yield set_
+    L.sd_test_set_split_route(0)
+
+
+@pytest.mark.parametrize("route", [2, 3])
+def test_split_route_hook_matches_reference(route, split_route, cuda):
+    """sd_test_set_split_route: the J <= 21 split routes (k_gl4y / k_gl4t GEMM phase + k_gl4 MODE 2)
+    through the kernel test hook, against the float64 reference."""
+    split_route(route)
+    for case in [c for c in CASES if c[0] in (16, 17, 21) and c[4] % 32 == 0]:
+        _check_gl(*case, 67, cuda)
+
+
+@pytest.mark.parametrize("J,nty,K1,K2,N,has_res,rms", [(16, 10, 192, 0, 192, True, False), (16, 10, 96, 96, 192, False, False),
+                                                       (16, 10, 192, 0, 768, False, True), (17, 9, 192, 0, 192, False, False),
+                                                       (51, 43, 192, 0, 192, True, False), (51, 43, 192, 0, 768, False, True)])
+@pytest.mark.parametrize("route", [2, 3])
+def test_graph_linear_out_of_f16_range(J, nty, K1, K2, N, has_res, rms, route, split_route, cuda):
+    """Operands the split-f16 products cannot represent (|x| >= 65504: rows scaled by 1e5 and
+    1e12): the waves holding them recompute their tiles on exact-f32 MFMA (exact_tile_f32), so
+    every row stays within 2e-5 of the float64 reference relative to that row's magnitude; the
+    in-range rows of the same launch keep the absolute 2e-5.  J <= 21: the split routes' GEMM
+    phases k_gl4y (route 2) and k_gl4t (route 3) + the MODE 2 mixing phase; J = 51: v5, whose GEMM
+    phase is k_gl4t / k_gl4y row-major (the route setting does not apply).  The one-kernel tiles
+    only flag SD_STATUS_F16_RANGE."""
+    if J > 21 and route == 3:
+        pytest.skip("v5 picks its GEMM phase itself")
+    split_route(route)
+    B = 67
+    g = torch.Generator().manual_seed(J + N + K1 + K2)
+    r = lambda *s: torch.rand(*s, generator=g) * 2 - 1  # noqa: E731
+    x1 = r(B, J, K1)
+    x1[5] *= 1e5
+    x1[40, 3] *= 1e12
+    x2 = r(B, J, K2) if K2 else None
+    if x2 is not None:
+        x2[33, :, 7] = 7e4
+    W = r(nty, N, K1 + K2) / (K1 + K2) ** 0.5
+    types = torch.arange(J) % nty
+    bias = r(nty, N) * 0.1
+    ghat = F.normalize(torch.eye(J) + torch.rand(J, J, generator=g) * 0.1, p=1.0, dim=1)
+    res = r(B, J, N) if has_res else None
+    got = _run_gl(cuda, x1, x2, W, bias, types, ghat, None, 0, res, rms, 1)
+    ref = _gl_reference(x1, x2, W, bias, types, ghat, None, 0, res, rms, 1)
+    assert torch.isfinite(got).all()
+    scale = ref.abs().amax(dim=(1, 2)).clamp_min(1.0)  # per row
+    err = ((got - ref).abs().amax(dim=(1, 2)) / scale).max().item()
+    assert err < 2e-5, err
 
 
 def test_kernel_variant_rejects_bad_value():

@@ -9,6 +9,18 @@ libskeldiff.so (llvm-objdump --disassemble-symbols) and checks its s_waitcnt / l
   (one memory round trip per wave, not one per 16-node tile);
 * k_gl5_mixd (MANO mixing pass): no vmcnt(0) between a row's fill and its stores;
 * k_update_mfma<16, 4, 6> f32 form: no bf16 (ushort) load path.
+
+Safety waits (round 5) -- the correctness of two hand-counted rings rests on
+waits the compiler's waitcnt pass does not place by itself:
+
+* k_gl4t's LDS-DMA ring: every s_barrier is directly preceded by an s_waitcnt that drains
+  lgkmcnt(0), so no wave reaches the barrier with an LDS read of the previous chunk in flight (the
+  fill issued after the barrier into that slot raced such a read in the round-4 first cut:
+  test_row_chains_share_cus_bitwise[3-0] 6.6e-5 off);
+* k_gl5_mixd<8, 2, true>: the residual of row r is read by inline-asm ds_read_b128 that the
+  waitcnt pass cannot see; each such read group follows an s_barrier that follows the row's
+  counted vmcnt wait, with no LDS-DMA issued in between, and an lgkmcnt(0) drains the reads before
+  the next fill is issued.
 """
 import os
 import re
@@ -28,6 +40,7 @@ pytestmark = pytest.mark.skipif(not os.path.exists(OBJDUMP) or not os.path.exist
 GL4T = "_ZN2sd6k_gl4tILb0ELi0ELi6ELi12ELb0ELi2ELi4ELb0ELb0ELb0ELb1ELb0ELi1EEEvNS_6GLArgsEilNS_4YOutE"
 ATTN = "_ZN2sd11k_attentionILi4ELi32EEEvNS_8AttnArgsE"
 MIXD = "_ZN2sd12_GLOBAL__N_110k_gl5_mixdILi8ELi2ELb0EEEvNS_6GLArgsEPKfl"
+MIXD_RES = "_ZN2sd12_GLOBAL__N_110k_gl5_mixdILi8ELi2ELb1EEEvNS_6GLArgsEPKfl"
 UPD = "_ZN2sd13k_update_mfmaILi16ELi4ELi6ELb0EEEvNS_7UpdArgsE"
 
 _cache = {}
@@ -67,11 +80,17 @@ def test_gl4t_store_tail_has_no_load_waits(tmp_path_factory):
     ins = _disasm(tmp_path_factory, GL4T)
     last_barrier = max(i for i, l in enumerate(ins) if l.startswith("s_barrier"))
     tail = ins[last_barrier:]
+    # the normal store tail: 6 tiles x 4 dwordx4 stores; after it only the f16-range fallback
+    # (exact_tile_f32, its own loads and waits, taken by out-of-range waves alone)
+    stores = [i for i, l in enumerate(tail) if l.startswith("global_store")]
+    assert len(stores) >= 24, len(stores)
+    tail = tail[:stores[23] + 1]
     assert not any(l.startswith("global_load") for l in tail), "a global load in the epilogue (bias?)"
     first_store = next(i for i, l in enumerate(tail) if l.startswith("global_store"))
     waits = [l for l in tail[first_store:] if _vmcnt(l) is not None]
     assert waits == [], waits
-    counts = [_vmcnt(l) for l in ins if _vmcnt(l) is not None]
+    # up to the last normal store (the out-of-range fallback after it waits for its own loads)
+    counts = [_vmcnt(l) for l in ins[:last_barrier + len(tail)] if _vmcnt(l) is not None]
     assert counts.count(0) <= 3 and any(c > 0 for c in counts), counts
 
 
@@ -101,3 +120,35 @@ def test_update_f32_form_has_no_bf16_loads(tmp_path_factory):
     ins = _disasm(tmp_path_factory, UPD)
     assert any(l.startswith("global_load_dword") for l in ins)
     assert not any(l.startswith(("global_load_ushort", "global_load_short")) for l in ins)
+
+
+def test_gl4t_ring_barriers_drain_lds_reads(tmp_path_factory):
+    ins = _disasm(tmp_path_factory, GL4T)
+    bars = [i for i, l in enumerate(ins) if l.startswith("s_barrier")]
+    assert len(bars) >= 4, len(bars)  # the unrolled ring steps (PF = 2) + the last chunks + the epilogue
+    for i in bars:
+        prev = ins[i - 1]
+        assert prev.startswith("s_waitcnt") and "lgkmcnt(0)" in prev, (i, ins[i - 3:i + 1])
+    ring = [i for i in bars if _vmcnt(ins[i - 1]) is not None]
+    assert len(ring) >= 3, [ins[i - 1] for i in bars]  # ring waits: counted vmcnt AND lgkmcnt(0)
+
+
+def test_mixd_residual_reads_follow_the_row_wait(tmp_path_factory):
+    ins = _disasm(tmp_path_factory, MIXD_RES)
+    groups = []  # runs of consecutive-ish ds_read_b128 (the asm residual reads of one row)
+    for i, l in enumerate(ins):
+        if l.startswith("ds_read_b128"):
+            if groups and i - groups[-1][-1] <= 4:
+                groups[-1].append(i)
+            else:
+                groups.append([i])
+    groups = [g for g in groups if len(g) == 4]
+    assert groups, "no residual read group (4 x ds_read_b128)"
+    for g in groups:
+        bar = max(i for i in range(g[0]) if ins[i].startswith("s_barrier"))
+        assert not any(l.startswith("global_load_lds") for l in ins[bar:g[0]]), "a fill between the barrier and the reads"
+        prev_issue = max((i for i in range(bar) if ins[i].startswith(("global_load_lds", "buffer_store"))), default=-1)
+        assert any(_vmcnt(l) is not None for l in ins[prev_issue + 1:bar]), "no vmcnt wait before the row's barrier"
+        nxt = next((i for i in range(g[-1], len(ins)) if ins[i].startswith("global_load_lds")), len(ins))
+        assert any(l.startswith("s_waitcnt") and "lgkmcnt(0)" in l for l in ins[g[-1]:nxt]), \
+            "the asm reads are not drained before the next fill"
