@@ -320,7 +320,7 @@ def denoiser_forward(sd: Dict[str, torch.Tensor], cfg: DenoiserConfig, x: torch.
     x = net.graph_linear("init_lin", x)
     r = x.clone()
     hdim = cfg.dim + cfg.cond_dim
-    temb = sinusoidal_embedding(t, hdim, cfg.theta)
+    temb = sinusoidal_embedding(t, hdim, cfg.theta).to(x.dtype)  # no-op in f32 (a float64 run: tests)
     temb = net.linear("time_mlp.1", temb)
     temb = F.gelu(temb)
     temb = net.linear("time_mlp.3", temb)

@@ -477,14 +477,17 @@ def test_graph_linear_rejects_aliased_output(cuda):
     assert rc != 0 and b"invalid" in L.sd_last_error().lower()
 
 
-@pytest.mark.parametrize("route", [0, 1, 2, 3])
+@pytest.mark.parametrize("route", [0, 2, 3])
 def test_f16_range_exact_in_kernel(route, cuda):
     """Activations the split-f16 products cannot represent (|x| >= 65504; conditioning latents
-    scaled by 1e5) on each split-f16 route -- auto, one-kernel k_gl4, k_gl4y + MODE 2 / 3, tiled
-    k_gl4t + MODE 2 / 3 -- with default options: the waves that leave the range recompute their
-    tiles on exact-f32 MFMA in the kernel (exact_tile_f32), so sample() returns latents within the
-    1e-4 parity bar of an exact-f32 plan's, with no warning and no host re-run; the status word
-    records that the fallback ran.  In range, the status stays clear."""
+    scaled by 1e5 and 3e9) on each default-capable split-f16 route -- auto, k_gl4y + MODE 2 / 3,
+    tiled k_gl4t + MODE 2 / 3 -- with default options: the waves that leave the range recompute
+    their tiles on exact-f32 MFMA in the kernel (exact_tile_f32), with no warning and no host
+    re-run; the status word records that the fallback ran (in range it stays clear).
+    Accuracy: at these magnitudes any f32 evaluation order moves the latents by ~1e-3 (an f32 ulp
+    of a 1e5 activation is 8e-3, and x0 = clamp(out) passes the rows near +-1 through), so the
+    bar is the float64 oracle: sample()'s deviation from it must stay within that of an exact-f32
+    plan (kernel variant 3), i.e. f32-accurate.  In range the 1e-4 latent bar holds (goldens)."""
     import warnings
 
     z = golden("release_h36m16_T10")
@@ -497,13 +500,18 @@ def test_f16_range_exact_in_kernel(route, cuda):
     assert d.engine.status(start.shape[0]) == 0
     ref = build_release_diffusion(z, cuda)
     ref.engine.set_option("kernel_variant", 3)
+    sd, cfg, bufs = _oracle_setup(d)
+    sd64 = {k: v.double() if v.is_floating_point() else v for k, v in sd.items()}
+    bufs64 = {k: v.double() if v.is_floating_point() else v for k, v in bufs.items()}
     for scale in (1e5, 3e9):
-        big = xcs.to(cuda) * scale
+        big = xcs * scale
         with warnings.catch_warnings():
             warnings.simplefilter("error")
-            img = d.sample(x_cond=big, **kw)[0]
+            img = d.sample(x_cond=big.to(cuda), **kw)[0]
             torch.cuda.synchronize()
         assert d.engine.status(start.shape[0]) & _lib.SD_STATUS_F16_RANGE
-        img_ref = ref.sample(x_cond=big, **kw)[0]
+        img_exact = ref.sample(x_cond=big.to(cuda), **kw)[0]
+        img64, _ = O.p_sample_loop(sd64, cfg, bufs64, start.double(), samp.double(), x_cond=big.double())
         assert torch.isfinite(img).all()
-        assert _max_err(img, img_ref) < TOL, (route, scale, _max_err(img, img_ref))
+        err, err_exact = _max_err(img, img64), _max_err(img_exact, img64)
+        assert err <= max(1.5 * err_exact, TOL), (route, scale, err, err_exact)
