@@ -121,10 +121,13 @@ int sd_denoiser_forward(const sd_plan* plan, const float* x_t, const float* x_co
 
 /* Status of the last sd_sample_loop / sd_denoiser_forward / sd_denoiser_trace on `workspace`
  * (synchronises `stream`): flags bit 0 (SD_STATUS_F16_RANGE) = an activation reached |x| >= 65504,
- * outside the f16 range of the split-f16 (v4) products, so the results are not f32-accurate; run
- * again with SD_OPT_KERNEL_VARIANT = 3 (exact f32).  The word is cleared at the start of each
- * of those calls. */
-enum { SD_STATUS_F16_RANGE = 1 };
+ * outside the f16 range of the split-f16 (v4) products: informational on the split routes (their
+ * GEMM phases recomputed those tiles on exact-f32 MFMA), and on the one-kernel route
+ * (SD_OPT_SPLIT_ROUTE 1 / 5) the results are not f32-accurate -- run again with
+ * SD_OPT_KERNEL_VARIANT = 3.  Bit 1 (SD_STATUS_FUSE_TIMEOUT) = a wait of the fused layer kernel
+ * (SD_OPT_SPLIT_ROUTE 6) gave up: the results are invalid (never expected; bounded instead of a
+ * hang).  The word is cleared at the start of each of those calls. */
+enum { SD_STATUS_F16_RANGE = 1, SD_STATUS_FUSE_TIMEOUT = 2 };
 int sd_workspace_status(const sd_plan* plan, const void* workspace, size_t workspace_bytes, uint32_t* flags,
                         void* stream);
 
@@ -264,7 +267,7 @@ int sd_test_qkv_attention(const float* x, int32_t K, const float* W, const int64
  * gl_variant = -1 only queries (returns the current value). */
 int sd_test_set_kernel_variant(int32_t gl_variant, int32_t gl4_tile);
 /* Test hook: the v4 split route of the sd_test_graph_linear* entry points ONLY (as
- * SD_OPT_SPLIT_ROUTE: 0 auto, 1 never, 2 k_gl4y GEMM phase, 3 k_gl4t GEMM phase, 5 fused small
+ * SD_OPT_SPLIT_ROUTE: 0 auto, 1 never, 2 k_gl4y GEMM phase, 3 k_gl4t GEMM phase, 6 k_gl4t + k_gl4f, 5 fused small
  * tile; 2 / 3 / 5 allocate the pre-mix scratch per call).  Returns the previous route, or -1 for an
  * invalid one; route = -1 only queries. */
 int sd_test_set_split_route(int32_t route);
@@ -290,7 +293,11 @@ enum {
                                    GEMM phase except for to_qkv + attention (one-kernel fused
                                    tile), 5 the small-batch fused tile (one launch per plain
                                    graph-linear, J = 16 f32 / half; auto at <= SKELDIFF_SMALL_ROWS
-                                   rows) with the k_gl4y split route for to_qkv + attention */
+                                   rows) with the k_gl4y split route for to_qkv + attention, 6 the
+                                   tiled route with every plain J = 16 layer (N = 192) on the fused
+                                   layer kernel k_gl4f: GEMM and mixing phase in one persistent
+                                   launch, Y mixed out of the L2 of the XCD that wrote it
+                                   (auto where SKELDIFF_FUSED=1) */
     SD_OPT_LAST_CHAINS = 7,     /* read-only: row chains the plan's last sd_sample_loop ran (the
                                    SD_OPT_ROW_CHAINS value, fewer for batches of fewer than n
                                    32-row units, a ragged last unit counting; auto: 1 at <= 128

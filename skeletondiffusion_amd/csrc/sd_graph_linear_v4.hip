@@ -429,9 +429,26 @@ __device__ unsigned long long g_gl4t_chunk[8192 * 16];  // per workgroup: s_memr
 // chunks; a unit's Y leaves through its own LDS transposes right after its last chunk while the
 // next unit's first chunks are already in flight, so the store tail and the fill prologue of all
 // but the first unit overlap the K loop (to_qkv: 4 column groups per node)
+// LDS bytes of one k_gl4t workgroup (the fused layer kernel k_gl4f carves two of them)
+template <int PREC, int CT, int NCH, int PF, int NWV, bool WRES, bool RSTG, int NU>
+constexpr int gl4t_smem_bytes() {
+    constexpr int TILE_H = PREC ? 512 : 1024, TS = 36, NS = PF + 1;
+    constexpr bool XDMA = !WRES && !RSTG && PREC != 2;
+    constexpr int XSB = XDMA ? NS * NWV * 2048 : 0;
+    constexpr int SBW = (WRES ? NCH : RSTG ? 2 : NS) * CT * TILE_H * 2 + XSB;
+    constexpr int SBT = NU > 1 ? SBW + NWV * 32 * TS * 4 + 2048 : SBW;
+    return SBT > NWV * 32 * TS * 4 ? SBT : NWV * 32 * TS * 4;
+}
+
+// The workgroup's work: unit u = (node j, row group, column group), tid = thread within the
+// workgroup's NWV (+ LDW) waves, smem_raw = its gl4t_smem_bytes of LDS.  k_gl4t derives u from
+// blockIdx; k_gl4f (the fused layer) runs two such bodies side by side in one 8-wave workgroup --
+// every barrier below is reached the same number of times by both halves (same template, same
+// chunk count; dead waves join barriers).
 template <bool RMS, int PREC, int CT, int NCH, bool ROWMAJOR, int PF = 2, int NWV = 4, bool WRES = false, bool RSTG = false,
           bool ILV = false, bool FF = false, bool LDW = false, int NU = 1>
-__global__ __launch_bounds__((NWV + (LDW ? 1 : 0)) * 64, WRES ? 1 : 2) void k_gl4t(const GLArgs p, int ncg, int64_t ntile_r, const YOut yo) {
+__device__ __forceinline__ void gl4t_body(const GLArgs& p, int ncg, int64_t ntile_r, const YOut& yo, const int64_t u,
+                                          const int tid, char* __restrict__ smem_raw) {
     constexpr int NT = NWV * 64;  // compute threads (the loader wave, LDW, is wave NWV)
     constexpr int TILE_H = PREC ? 512 : 1024;   // halves of one 32-column tile per chunk
     constexpr int PPT = TILE_H / 8;             // 16-B pieces per tile
@@ -448,9 +465,9 @@ __global__ __launch_bounds__((NWV + (LDW ? 1 : 0)) * 64, WRES ? 1 : 2) void k_gl
     constexpr int SBT = NU > 1 ? SBW + NWV * 32 * TS * 4 + 2048 : SBW;
     constexpr int SB = SBT > NWV * 32 * TS * 4 ? SBT : NWV * 32 * TS * 4;
     static_assert(!WRES || SB <= 160 * 1024, "resident weight slice exceeds the LDS");
-    __shared__ __attribute__((aligned(16))) char smem_raw[SB];  // weight stages, then the transposes
+    static_assert(SB == gl4t_smem_bytes<PREC, CT, NCH, PF, NWV, WRES, RSTG, NU>(), "LDS carve");
     _Float16(*sW)[CT * TILE_H] = reinterpret_cast<_Float16(*)[CT * TILE_H]>(smem_raw);
-    const int tid = threadIdx.x, lane = tid & 63, l32 = lane & 31, h = lane >> 5;
+    const int lane = tid & 63, l32 = lane & 31, h = lane >> 5;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int J = p.J;
 #ifdef SD_GL4T_STAMPS
@@ -461,10 +478,6 @@ __global__ __launch_bounds__((NWV + (LDW ? 1 : 0)) * 64, WRES ? 1 : 2) void k_gl
         ck0 = clock64();
     }
 #endif
-    // XCD-aware order (k_gl4's): consecutive u -- the column groups of one (row group, node), which
-    // read the same x -- on one XCD (blocks b, b + 8, ... share one), so x reaches that L2 once
-    const int nwg = gridDim.x, xcd = blockIdx.x & 7, q8 = nwg >> 3, r8 = nwg & 7;
-    const int64_t u = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (blockIdx.x >> 3);
     // node-major order: column group fastest (the ncg workgroups sharing one x tile), then row
     // groups, then nodes, so an XCD's contiguous share of u holds one or two nodes' weights
     // (N = 768: 5.9 MB of split weights for all 10 types did not fit a 4 MB L2 when every XCD
@@ -1053,6 +1066,18 @@ __global__ __launch_bounds__((NWV + (LDW ? 1 : 0)) * 64, WRES ? 1 : 2) void k_gl
 #endif
 }
 
+template <bool RMS, int PREC, int CT, int NCH, bool ROWMAJOR, int PF = 2, int NWV = 4, bool WRES = false, bool RSTG = false,
+          bool ILV = false, bool FF = false, bool LDW = false, int NU = 1>
+__global__ __launch_bounds__((NWV + (LDW ? 1 : 0)) * 64, WRES ? 1 : 2) void k_gl4t(const GLArgs p, int ncg, int64_t ntile_r, const YOut yo) {
+    __shared__ __attribute__((aligned(16))) char smem_raw[gl4t_smem_bytes<PREC, CT, NCH, PF, NWV, WRES, RSTG, NU>()];
+    // XCD-aware order (k_gl4's): consecutive u -- the column groups of one (row group, node), which
+    // read the same x -- on one XCD (blocks b, b + 8, ... share one), so x reaches that L2 once
+    const int nwg = gridDim.x, xcd = blockIdx.x & 7, q8 = nwg >> 3, r8 = nwg & 7;
+    const int64_t u = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (blockIdx.x >> 3);
+    gl4t_body<RMS, PREC, CT, NCH, ROWMAJOR, PF, NWV, WRES, RSTG, ILV, FF, LDW, NU>(p, ncg, ntile_r, yo, u, threadIdx.x,
+                                                                                 smem_raw);
+}
+
 // Epilogue of the fused to_qkv + Attention kernel (MODE 1), J <= 32, dh = 32, 8 waves, a
 // 32-row tile.  Per 8-row slab: the mixed-in q|k|v (Z = G-hat Y) goes to LDS as [row][node][96],
 // then wave w runs the attention of row 8*slab + w exactly as k_attention<JT> does (same f32 MFMA
@@ -1242,8 +1267,12 @@ __device__ __forceinline__ void attention_epilogue(const GLArgs& p, floatx16 (&a
 //   LDS, no barriers), then the MODE 0 mixing / FiLM / tanh / residual epilogue.  One launch and
 //   no scratch round trip per layer instead of the split route's two; every output element sees
 //   the same products in the same order, so it is bitwise equal to MODE 0 and the split routes.
-template <int J, int NW, int RT, int CT, bool RMS, int DBG = 0, int MODE = 0, int XP = 0, int PREC = 0, int STG = 0>
-__global__ __launch_bounds__(NW * 64, 1) void k_gl4(const GLArgs p) {
+// The workgroup's work for virtual block index bx of a grid of nwg (k_gl4 passes blockIdx.x /
+// gridDim.x); smem = its dynamic LDS.  YSC1 (MODE 2 inside the fused layer k_gl4f): the pre-mix Y
+// is read with sc1 loads (past this CU's L1, from the XCD's L2 where the same launch wrote it).
+template <int J, int NW, int RT, int CT, bool RMS, int DBG = 0, int MODE = 0, int XP = 0, int PREC = 0, int STG = 0,
+          bool YSC1 = false>
+__device__ __forceinline__ void gl4_body(const GLArgs& p, const int bx, const int nwg, float* __restrict__ smem) {
     static_assert(MODE == 0 || MODE == 2 || MODE == 4 || (CT == 3 && RT == 1 && J <= 32 && NW == 8),
                   "attention mode: 32 x (q|k|v)");
     static_assert(MODE < 2 || (RT == 1 && XP == 0 && STG == 0 && DBG == 0), "split-route phase 2: one 32-row tile");
@@ -1257,7 +1286,6 @@ __global__ __launch_bounds__(NW * 64, 1) void k_gl4(const GLArgs p) {
     constexpr int YS = 16 * YR + 16;        // floats per node in a 16-row Y slab (+16: bank shift)
     constexpr int NTH = NW * 64;
     constexpr int BPW = (COLS + NW - 1) / NW;  // 16-wide mixing blocks per wave per slab
-    extern __shared__ __attribute__((aligned(16))) float smem[];
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int l32 = lane & 31, h = lane >> 5, lr = lane & 15, lg = lane >> 4;
@@ -1275,17 +1303,17 @@ __global__ __launch_bounds__(NW * 64, 1) void k_gl4(const GLArgs p) {
     float* sF = sG + J * J;  // FiLM (scale + 1 | shift) for this workgroup's columns
 
     const int ntile_c = ATT ? p.attn_heads : (p.N + COLS - 1) / COLS;
-    const int nwg = gridDim.x, xcd = blockIdx.x & 7, q8 = nwg >> 3, r8 = nwg & 7;
+    const int xcd = bx & 7, q8 = nwg >> 3, r8 = nwg & 7;
     // XCD-aware order: consecutive L (the column tiles of one row tile) on one XCD, so x is
     // fetched into that XCD's L2 once.  attn_order 1 (fused attention): L = blockIdx, i.e. head
     // h = blockIdx % heads runs on XCD h % 8 and each XCD's L2 keeps only its heads' weights.
     // Split-route phase 2: workgroup = (tile, 16-row slab) in MODE 2, (tile, 8-row slab) in MODE 3.
-    const int L = MODE == 2   ? (int)(blockIdx.x >> 1)
-                  : MODE == 3 ? (int)(blockIdx.x >> 2)
+    const int L = MODE == 2   ? (int)(bx >> 1)
+                  : MODE == 3 ? (int)(bx >> 2)
                   : (MODE == 1 && p.attn_order == 1)
-                      ? (int)blockIdx.x
-                      : (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (blockIdx.x >> 3);
-    const int slab = MODE == 2 ? (int)(blockIdx.x & 1) : MODE == 3 ? (int)(blockIdx.x & 3) : 0;
+                      ? (int)bx
+                      : (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bx >> 3);
+    const int slab = MODE == 2 ? (int)(bx & 1) : MODE == 3 ? (int)(bx & 3) : 0;
     const int ctile = L % ntile_c;
     const int64_t row0 = (int64_t)(L / ntile_c) * (32 * RT);
     const int c0 = ctile * COLS;
@@ -1391,11 +1419,18 @@ __global__ __launch_bounds__(NW * 64, 1) void k_gl4(const GLArgs p) {
         floatx4 yv[NYL];
         float gv[NGL];
         float f0 = 1.0f, f1 = 0.0f;
+        [[maybe_unused]] const __amdgpu_buffer_rsrc_t zrsrc = __builtin_amdgcn_make_buffer_rsrc(p.zs, 0, 0x7fffffff, 0x00020000);
 #pragma unroll
         for (int k = 0; k < NYL; ++k) {
             const int q = tid + k * NTH;
             float* d;
-            if (q < YQ) yv[k] = g4(ysrc(q, d));
+            if (q < YQ) {
+                if constexpr (YSC1)  // aux 16 = sc1: past this CU's L1 (k_gl4f; zs < 2 GiB, checked at launch)
+                    yv[k] = __builtin_bit_cast(floatx4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                            zrsrc, (int)((ysrc(q, d) - p.zs) * 4), 0, 16));
+                else
+                    yv[k] = g4(ysrc(q, d));
+            }
         }
         if constexpr (MODE == 2 && RES_EARLY)  // the residual in flight with the slab (one memory latency)
             if (p.res) load_res(slab, 0, BPW);
@@ -1954,16 +1989,22 @@ __global__ __launch_bounds__(NW * 64, 1) void k_gl4(const GLArgs p) {
         __syncthreads();
         ts[5] = wall_clock64();
         if (lane == 0) {  // per wave: chunk-5 phase cycles at out[(nwg * 8) + (blockIdx * NW + wave) * 4]
-            unsigned* q = reinterpret_cast<unsigned*>(p.out) + (size_t)gridDim.x * 8 + ((size_t)blockIdx.x * NW + wave) * 4;
+            unsigned* q = reinterpret_cast<unsigned*>(p.out) + (size_t)nwg * 8 + ((size_t)bx * NW + wave) * 4;
             for (int i = 0; i < 4; ++i) q[i] = (unsigned)(cs[i + 1] - cs[i]);
         }
         if (tid == 0) {
-            unsigned* o = reinterpret_cast<unsigned*>(p.out) + (size_t)blockIdx.x * 8;
+            unsigned* o = reinterpret_cast<unsigned*>(p.out) + (size_t)bx * 8;
             for (int i = 0; i < 6; ++i) o[i] = (unsigned)ts[i];
             o[6] = __smid();
             o[7] = (unsigned)(ts[7] - ts[6]);  // shader-clock cycles of chunks 2 .. end
         }
     }
+}
+
+template <int J, int NW, int RT, int CT, bool RMS, int DBG = 0, int MODE = 0, int XP = 0, int PREC = 0, int STG = 0>
+__global__ __launch_bounds__(NW * 64, 1) void k_gl4(const GLArgs p) {
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    gl4_body<J, NW, RT, CT, RMS, DBG, MODE, XP, PREC, STG>(p, blockIdx.x, gridDim.x, smem);
 }
 
 // v4 weight staging (GLArgs::gl4_stage): 0 = LDS-DMA stages, 1 = register-staged stages (2, a
@@ -2054,7 +2095,7 @@ static int split_route(const GLArgs& a, bool attn) {
     if (a.zs == a.out || a.zs == a.x1 || a.zs == a.x2 || a.zs == a.res) return 0;
     if (attn && (a.attn_heads * 96 != a.N)) return 0;
     if (a.split == 2 || a.split == 5) return a.prec == 2 ? 0 : 1;
-    if (a.split == 3) return 2;
+    if (a.split == 3 || a.split == 6) return 2;
     if (a.split == 4) return attn ? 0 : 2;  // tiled GEMM phase; to_qkv + attention on the one-kernel tile
     if (a.gl4_cfg != 0) return 0;
     const int64_t rows = a.route_rows > 0 ? a.route_rows : a.B;
@@ -2226,11 +2267,178 @@ static hipError_t launch_gl4t(const GLArgs& a, bool rms, int64_t ntile_r, const 
     return hipErrorNotSupported;
 }
 
+// ---- the fused layer kernel k_gl4f (round 5) --------------------------------
+// One launch for a plain J = 16 graph-linear layer of the tiled split route: the GEMM phase
+// (gl4t_body, k_gl4t's K loop and epilogue) and the mixing phase (gl4_body MODE 2, k_gl4's) as
+// work items of one persistent grid, so each 128-row group's pre-mix Y is mixed straight out of
+// the L2 of the XCD that wrote it, and the mixing of one row group overlaps the GEMMs of the next
+// instead of waiting for a kernel boundary.  Same functions, same arithmetic: bitwise equal to
+// the tiled split route.
+//   Work items: per row group rg (128 rows), 8 GEMM items (a node pair: the two 4-wave halves of
+//   the 8-wave workgroup each run one node's 128 x 192 k_gl4t tile, with their own LDS) and 48
+//   mixing items (MODE 2 units: 32-row tile x 16-row slab x 32-column tile).
+//   Queues: one per XCD (the workgroup reads its s_getreg XCC_ID).  XCD x's item stream is slot
+//   after slot: [8 GEMM items of slot s][48 mixing items of slot s - 1]; the workgroup that takes
+//   the first GEMM item of a slot claims the next row group for it (one global counter), so every
+//   item of a row group runs on one XCD, and XCDs that run faster claim more row groups.
+//   Hand-off: the GEMM items store Y plainly (it stays in the XCD's L2), every wave drains its
+//   stores (vmcnt(0)), one agent-scope add per item on the row group's counter; a mixing item
+//   polls that counter (relaxed agent-scope loads) until all 8 are in, then reads Y with sc1 loads
+//   (past its CU's L1).  tools/handoff_probe.hip: plain stores + sc1 loads inside one XCD, 0 stale
+//   words in 2,000 rounds (and every word stale across XCDs -- hence the per-XCD queues).
+//   Progress: a mixing item waits only for GEMM items taken earlier from the same stream, which
+//   never wait (a slot claim waits for the claimant, which took its item earlier) -- no deadlock
+//   whatever the residency; every spin is bounded (SD_STATUS_FUSE_TIMEOUT, then the item is
+//   dropped rather than hang).  The last workgroup out zeroes the queue block for the next launch.
+constexpr int kFusePer = 8 + 48;   // items per slot
+constexpr unsigned kFuseNone = 0xffffffffu;
+typedef __attribute__((address_space(1))) unsigned fgu32;
+
+__device__ __forceinline__ unsigned fq_load(const unsigned* q) {
+    return __hip_atomic_load((fgu32*)q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void fq_store(unsigned* q, unsigned v) {
+    __hip_atomic_store((fgu32*)q, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ unsigned fq_add(unsigned* q, unsigned v) {
+    return __hip_atomic_fetch_add((fgu32*)q, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// poll until pred(value) (bounded: ~2^24 polls with s_sleep, seconds); returns the value, or
+// kFuseNone with the timeout flag set
+template <typename P>
+__device__ __forceinline__ unsigned fq_wait(const unsigned* q, P pred, unsigned* status) {
+    for (unsigned i = 0; i < (1u << 24); ++i) {
+        const unsigned v = fq_load(q);
+        if (pred(v)) return v;
+        __builtin_amdgcn_s_sleep(2);
+    }
+    if (status) atomicOr(status, 2u);  // SD_STATUS_FUSE_TIMEOUT
+    return kFuseNone;
+}
+
+template <int NCH, int PREC>
+__global__ __launch_bounds__(512, 1) void k_gl4f(const GLArgs p, int64_t ntile_r, const YOut yo) {
+    constexpr int SBH = gl4t_smem_bytes<PREC, 6, NCH, 2, 4, false, false, 1>();  // LDS of one half
+    extern __shared__ __attribute__((aligned(16))) float smem_f[];  // (one extern name, one type: k_gl4's)
+    char* const smem = reinterpret_cast<char*>(smem_f);
+    unsigned* const sq = reinterpret_cast<unsigned*>(smem + 2 * SBH);  // item, row group broadcast
+    const int tid = threadIdx.x, half = tid >> 8;
+    unsigned xcc;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+    xcc &= 7;
+    const int nrg = (int)((ntile_r + 3) / 4);  // 128-row groups
+    const int S = nrg + 2;                     // slots per XCD stream (all row groups + the end)
+    unsigned* const head = p.fq + 32 * xcc;
+    unsigned* const slot_rg = p.fq + kFqSlot + xcc * S;
+    unsigned* const gdone = p.fq + kFqSlot + 8 * S;
+    for (;;) {
+        if (tid == 0) sq[0] = fq_add(head, 1u);
+        __syncthreads();
+        const unsigned it = sq[0];
+        const int slot = (int)(it / kFusePer), w = (int)(it % kFusePer);
+        if (slot >= S) break;  // past the end of the stream (every slot's row group settled)
+        if (w < 8) {  // GEMM item: node pair w of slot `slot`
+            if (tid == 0) {
+                unsigned v;
+                if (w == 0) {  // claim the next row group for this slot
+                    const unsigned r = fq_add(p.fq + kFqNext, 1u);
+                    v = r < (unsigned)nrg ? r + 1 : kFuseNone;
+                    fq_store(slot_rg + slot, v);
+                } else {
+                    v = fq_wait(slot_rg + slot, [](unsigned x) { return x != 0u; }, p.status);
+                }
+                sq[1] = v;
+            }
+            __syncthreads();
+            const unsigned v = sq[1];
+            if (v != kFuseNone) {
+                const int64_t rg = v - 1;
+                const int64_t u = (int64_t)(2 * w + half) * nrg + rg;  // k_gl4t's (node, row group), ncg = 1
+                gl4t_body<false, PREC, 6, NCH, false, 2, 4, false, false, false, true, false, 1>(
+                    p, 1, ntile_r, yo, u, tid & 255, smem + half * SBH);
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's Y stores are in L2
+                __syncthreads();
+                if (tid == 0) fq_add(gdone + rg, 1u);
+            }
+        } else {  // mixing item w - 8 of slot - 1
+            if (tid == 0) {
+                unsigned v = kFuseNone;
+                if (slot > 0) {
+                    v = fq_wait(slot_rg + slot - 1, [](unsigned x) { return x != 0u; }, p.status);
+                    if (v != kFuseNone &&
+                        fq_wait(gdone + (v - 1), [](unsigned x) { return x >= 8u; }, p.status) == kFuseNone)
+                        v = kFuseNone;
+                }
+                sq[1] = v;
+            }
+            __syncthreads();
+            const unsigned v = sq[1];
+            if (v == kFuseNone) break;  // slot - 1 had no row group: the stream is done
+            const int m = w - 8, tl = m / 12, rem = m % 12;
+            const int64_t tile = (int64_t)(v - 1) * 4 + tl;
+            if (tile < ntile_r) {
+                const int bx = (int)(((tile * 6 + (rem >> 1)) << 1) | (rem & 1));  // k_gl4 MODE 2's block index
+                gl4_body<16, 8, 1, 1, false, 0, 2, 0, 0, 0, true>(p, bx, 0, reinterpret_cast<float*>(smem));
+            }
+        }
+        __syncthreads();  // LDS and sq reused by the next item
+    }
+    // the last workgroup out zeroes the block for the next launch (all others are past their last
+    // access: each adds to the exit counter after it)
+    if (tid == 0) {
+        const unsigned n = __hip_atomic_fetch_add((fgu32*)(p.fq + kFqExit), 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+        sq[2] = n == gridDim.x - 1;
+    }
+    __syncthreads();
+    if (sq[2]) {
+        for (int i = tid; i < 8; i += 512) fq_store(p.fq + 32 * i, 0u);
+        for (int i = tid; i < 8 * S + nrg; i += 512) fq_store(p.fq + kFqSlot + i, 0u);
+        if (tid == 0) {
+            fq_store(p.fq + kFqNext, 0u);
+            fq_store(p.fq + kFqExit, 0u);
+        }
+    }
+}
+
+// k_gl4f eligibility: J = 16 plain (non-RMS, non-attention) layers of N = 192 on split-f16 (f32 or
+// half) products, K = 192 / 256 / 384, the column-tiled scratch; route 6 forces it, the auto
+// route takes it where SKELDIFF_FUSED (process default of new plans' g_fused) says
+static int g_fused = [] {
+    const char* e = getenv("SKELDIFF_FUSED");
+    return e ? atoi(e) : 0;
+}();
+template <int NCH>
+static hipError_t launch_gl4f_n(const GLArgs& a, int64_t ntile_r, const YOut& yo, hipStream_t s) {
+    constexpr int SBH = gl4t_smem_bytes<0, 6, NCH, 2, 4, false, false, 1>();
+    const size_t lds = 2 * SBH + 64;
+    auto kt = a.prec == 1 ? k_gl4f<NCH, 1> : k_gl4f<NCH, 0>;
+    hipError_t e = hipFuncSetAttribute((const void*)kt, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return e;
+    g_route_bits |= kRouteGemmTiled | kRouteMixPhase | kRouteFusedLayer;
+    hipLaunchKernelGGL(kt, dim3(256), dim3(512), lds, s, a, ntile_r, yo);  // one workgroup per CU
+    return hipGetLastError();
+}
+static hipError_t launch_gl4f(const GLArgs& a, int64_t ntile_r, const YOut& yo, hipStream_t s) {
+    const int K = a.K1 + a.K2;
+    if (K == 192) return launch_gl4f_n<12>(a, ntile_r, yo, s);
+    if (K == 256) return launch_gl4f_n<16>(a, ntile_r, yo, s);
+    return launch_gl4f_n<24>(a, ntile_r, yo, s);
+}
+static bool fused_ok(const GLArgs& a, bool rms, bool attn) {
+    if (!a.fq || rms || attn || a.J != 16 || a.prec == 2 || a.N != 192 || a.x2_blk != a.x1_blk) return false;
+    if (!(a.split == 6 || (a.split == 0 && g_fused))) return false;
+    const int K = a.K1 + a.K2;
+    if (!(K == 192 || K == 256 || K == 384) || a.K1 % 16 || (a.x1_div != 1 && a.x1_blk)) return false;
+    if ((int64_t)(a.B + 31) / 32 * 32 * a.J * a.N * 4 >= 0x7fffffffLL) return false;  // sc1 loads: 32-bit offsets
+    return true;
+}
+
 template <int J>
 static hipError_t gl4_split(const GLArgs& a, bool rms, bool attn, int route, hipStream_t s) {
     const int64_t ntile_r = (a.B + 31) / 32;
     const int ntc = a.N / 32;
     const YOut yo{a.zs, 32, 1024, (int64_t)(a.N / 32) * J * 1024, (int64_t)J * 1024};  // column-tiled (zs_off)
+    if (route == 2 && fused_ok(a, rms, attn)) return launch_gl4f(a, ntile_r, yo, s);
     hipError_t e = route == 2 ? launch_gl4t<false>(a, rms, ntile_r, yo, s) : hipErrorNotSupported;
     if (e == hipErrorNotSupported) {
         if (a.prec == 2) return hipErrorNotSupported;  // k_gl4y has no bf16 form
@@ -2255,7 +2463,7 @@ static int64_t g_small_rows = [] {
     return e ? (int64_t)atoll(e) : (int64_t)0;
 }();
 static bool small_fused(const GLArgs& a) {
-    if (a.J != 16 || a.prec == 2 || a.split == 1 || a.split == 2 || a.split == 3 || a.split == 4) return false;
+    if (a.J != 16 || a.prec == 2 || a.split == 1 || a.split == 2 || a.split == 3 || a.split == 4 || a.split == 6) return false;
     if ((a.K1 + a.K2) % 64) return false;  // MODE 4's K loop: chunks in rounds of 4
     if (a.split == 5) return true;
     if (a.gl4_cfg != 0) return false;

@@ -70,7 +70,16 @@ struct GLArgs {
     // bf16 storage of operands / result (precision mode 2): the tensor
     // holds bf16 elements at the same element offsets (row-major only)
     int x1_bf16, x2_bf16, res_bf16, out_bf16;
+    // the fused layer kernel k_gl4f (split route 6 / auto): this launch's work-queue block in the
+    // workspace (fq_words(rows) words, zeroed before the first launch of a call; every launch
+    // leaves it zeroed), or null = k_gl4f unavailable
+    unsigned* fq;
 };
+// k_gl4f work-queue block: 8 per-XCD item heads (own 128-B lines), the row-group claim counter,
+// the exit counter, per XCD the row group of each slot, per row group its finished GEMM items
+constexpr int kFqNext = 256, kFqExit = 288, kFqSlot = 320, kFqRows = 128;
+inline int64_t fq_rgs(int64_t rows) { return (rows + kFqRows - 1) / kFqRows; }
+inline int64_t fq_words(int64_t rows) { return (kFqSlot + 8 * (fq_rgs(rows) + 2) + fq_rgs(rows) + 63) / 64 * 64; }
 int diag_flags();  // SKELDIFF_DIAG (sd_plan.hip)
 
 // Kernels a sampling call launched (SD_OPT_LAST_ROUTE): every graph-linear / attention launch site
@@ -84,7 +93,8 @@ enum RouteBits : unsigned {
     kRouteV5Mix = 32,      // k_gl5_gemm / k_gl5_mix (J > 21)
     kRouteExact = 64,      // exact-f32 generations v1-v3
     kRouteAttention = 128,  // k_attention: the separate attention kernel (J > 21, unfused routes)
-    kRouteFusedSmall = 256  // k_gl4 MODE 4: small-batch fused graph-linear tile
+    kRouteFusedSmall = 256,  // k_gl4 MODE 4: small-batch fused graph-linear tile
+    kRouteFusedLayer = 512   // k_gl4f: GEMM + mixing phase of a plain layer in one launch
 };
 extern thread_local unsigned g_route_bits;
 

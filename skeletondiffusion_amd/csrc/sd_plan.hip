@@ -251,6 +251,8 @@ int dalloc(sd_plan* p, T** out, size_t n) {
 // workspace carve (all offsets 256-B aligned)
 struct WS {
     uint64_t* rng;      // {seed, row0} of the device noise (graph replays); rng + 4: status word
+    unsigned* fq;       // k_gl4f work-queue blocks: one of sd::fq_words(rows) words per row chain
+    int64_t fq_stride;  // words per block
     float *x, *r, *h, *qkv, *o, *res, *x0, *img0, *img1;
 };
 
@@ -272,6 +274,8 @@ size_t carve(const sd_plan* p, int64_t rows, char* base, WS* w) {
     WS tmp;
     WS& W = w ? *w : tmp;
     W.rng = (uint64_t*)take(64);
+    W.fq_stride = sd::fq_words(rows);
+    W.fq = (unsigned*)take((size_t)sd_plan::kMaxChains * W.fq_stride * sizeof(unsigned));
     W.x = (float*)take(nH);
     W.r = (float*)take(nH);
     W.h = (float*)take(nH);
@@ -286,6 +290,13 @@ size_t carve(const sd_plan* p, int64_t rows, char* base, WS* w) {
 
 // the workspace's status word (range-guard flags, sd_workspace_status)
 unsigned* ws_status(const WS& w) { return reinterpret_cast<unsigned*>(w.rng + 4); }
+// entry points zero the status word and every row chain's k_gl4f queue block (each fused launch
+// leaves its block zeroed again, so one memset per call covers all of its launches)
+int ws_reset(const WS& w, hipStream_t s) {
+    SD_HIP(hipMemsetAsync(ws_status(w), 0, sizeof(unsigned), s));
+    SD_HIP(hipMemsetAsync(w.fq, 0, (size_t)sd_plan::kMaxChains * w.fq_stride * sizeof(unsigned), s));
+    return SD_OK;
+}
 
 sd::GLArgs gl_args(const sd_plan* p, const GL& g, const float* x1, int x1_div, const float* x2,
                    const float* film, const float* res, float* out, int64_t rows) {
@@ -410,6 +421,7 @@ int run_denoiser(const sd_plan* p, const float* x_t, const float* x_cond, int64_
     const int64_t zs_cap = (rows + 31) / 32 * 32 * p->J * (int64_t)(p->d.use_attention ? 3 * p->hid : p->H);
     auto lay = [B, tile_hint, &w, zs_cap, &bfl, route_rows](sd::GLArgs& g, int in, int res, int out) {
         g.status = ws_status(w);
+        g.fq = w.fq;
         g.route_rows = route_rows;
         g.zs = w.qkv;
         g.zs_cap = zs_cap;
@@ -898,7 +910,7 @@ int sd_denoiser_forward(const sd_plan* p, const float* x_t, const float* x_cond,
     if (!x_t || !x0_out) return fail(SD_E_INVALID, "null tensor");
     if (p->C > 0 && !x_cond) return fail(SD_E_INVALID, "x_cond is required (diffusion_conditioning)");
     if (cond_repeat < 1) return fail(SD_E_INVALID, "cond_repeat must be >= 1");
-    SD_HIP(hipMemsetAsync(ws_status(w), 0, sizeof(unsigned), (hipStream_t)stream));
+    if ((rc = ws_reset(w, (hipStream_t)stream))) return rc;
     return run_denoiser(p, x_t, x_cond, cond_repeat, t, x0_out, rows, w, (hipStream_t)stream);
 }
 
@@ -927,7 +939,7 @@ int sd_denoiser_trace(const sd_plan* p, const float* x_t, const float* x_cond, i
         if (!acts[i]) return fail(SD_E_INVALID, "null activation buffer");
     if (p->C > 0 && !x_cond) return fail(SD_E_INVALID, "x_cond is required (diffusion_conditioning)");
     if (cond_repeat < 1) return fail(SD_E_INVALID, "cond_repeat must be >= 1");
-    SD_HIP(hipMemsetAsync(ws_status(w), 0, sizeof(unsigned), (hipStream_t)stream));
+    if ((rc = ws_reset(w, (hipStream_t)stream))) return rc;
     return run_denoiser(p, x_t, x_cond, cond_repeat, t, x0_out, rows, w, (hipStream_t)stream, nullptr, 0, 0, acts);
 }
 
@@ -945,8 +957,9 @@ int sd_p_sample_update(const sd_plan* p, const float* x0_raw, const float* x_t, 
                       noise_out ? noise_rs : JD, rows, (hipStream_t)stream);
 }
 
-static WS shift_ws(const sd_plan* p, const WS& w, int64_t r0) {
+static WS shift_ws(const sd_plan* p, const WS& w, int64_t r0, int chain) {
     WS o = w;
+    o.fq += chain * w.fq_stride;  // a queue block per row chain (chains run concurrently)
     const int64_t J = p->J;
     o.x += r0 * J * p->H;
     o.r += r0 * J * p->H;
@@ -1040,7 +1053,7 @@ static int record_loop(const sd_plan* p, const float* x_T, const float* x_cond, 
         Chain& c = ch[i];
         c.r0 = chain_row(i, nch, rows, unit);
         c.n = chain_row(i + 1, nch, rows, unit) - c.r0;
-        c.w = shift_ws(p, w, c.r0);
+        c.w = shift_ws(p, w, c.r0, i);
         c.cur = (dev_start || bf) ? c.w.img1 : x_T + c.r0 * JD;
         if (dev_start) SD_HIP(sd::launch_noise_fill(c.w.img1, c.n, JD, seed, row0, T, rng, cs[i], c.r0, bf));
         else if (bf)  // bf16 latents: the caller's f32 start noise rounded once
@@ -1122,7 +1135,7 @@ int sd_sample_loop(const sd_plan* p, const float* x_T, const float* x_cond, int6
     if (rows == 0) return SD_OK;
     hipStream_t s = (hipStream_t)stream;
     sd_plan* mp = const_cast<sd_plan*>(p);
-    SD_HIP(hipMemsetAsync(ws_status(w), 0, sizeof(unsigned), s));
+    if ((rc = ws_reset(w, s))) return rc;
     int64_t unit = 32;
     const int nch = chain_count(p, rows, cond_repeat, &unit);
     mp->last_chains.store(nch);
@@ -1247,6 +1260,7 @@ int sd_profile_step(const sd_plan* p, const float* x_t, const float* x_cond, int
     if (t < 0 || t >= p->T) return fail(SD_E_INVALID, "t out of range");
     if (p->C > 0 && !x_cond) return fail(SD_E_INVALID, "x_cond is required (diffusion_conditioning)");
     hipStream_t s = (hipStream_t)stream;
+    if ((rc = ws_reset(w, s))) return rc;
     double acc[4] = {0, 0, 0, 0};
     int32_t counts[3] = {0, 0, 0};
     for (int r = 0; r < reps; ++r) {
@@ -1387,9 +1401,10 @@ int sd_plan_set_option(sd_plan* p, int32_t option, int64_t value) {
         case SD_OPT_LAST_CHAINS:
         case SD_OPT_LAST_ROUTE: return fail(SD_E_INVALID, "SD_OPT_LAST_CHAINS / SD_OPT_LAST_ROUTE are read-only");
         case SD_OPT_SPLIT_ROUTE:
-            if (value < 0 || value > 5)
+            if (value < 0 || value > 6)
                 return fail(SD_E_INVALID, "split route must be 0 (auto), 1 (never), 2 (always), 3 (always, tiled phase 1), "
-                                          "4 (tiled phase 1 except to_qkv + attention) or 5 (small-batch fused tile)");
+                                          "4 (tiled phase 1 except to_qkv + attention), 5 (small-batch fused tile) or "
+                                          "6 (tiled, plain layers on the fused layer kernel k_gl4f)");
             p->split = (int)value;
             return SD_OK;
         case SD_OPT_UPDATE_KERNEL:

@@ -288,6 +288,32 @@ def test_tiled_split_route_bitwise(cfg, batch, T, prec, cuda):
     assert eng.status(rows) == 0
 
 
+@pytest.mark.parametrize("batch,T,chains,prec", [(64, 4, 1, "f32"), (64, 4, 3, "f32"), (3, 10, 1, "f32"), (5, 10, 2, "f32"),
+                                                  (32, 4, 3, "half")])
+def test_fused_layer_route_bitwise(batch, T, chains, prec, cuda):
+    """SD_OPT_SPLIT_ROUTE = 6: every plain J = 16 layer on the fused layer kernel
+    k_gl4f (GEMM and mixing phase of a layer as work items of one persistent launch, per-XCD work
+    queues, Y handed over inside the XCD's L2) is bitwise equal to the tiled split route (k_gl4t +
+    k_gl4 MODE 2 launches), graph and eager, on 1-3 row chains and at ragged row groups (150 / 250
+    rows); the fused kernel ran (route bit 512) and no wait timed out (status clear)."""
+    from bench import build_config
+
+    d, x_cond, rows = build_config("amass16", cuda, T=T, batch=batch)
+    eng = d.engine
+    eng.set_precision(prec)
+    eng.set_option("row_chains", chains)
+    eng.set_option("split_route", 3)
+    ref = eng.sample_loop(rows, x_cond=x_cond, seed=31, record=(False, True))
+    ref = [ref[0].clone(), ref[4].clone()]
+    eng.set_option("split_route", 6)
+    for graph in (False, True, True):
+        got = eng.sample_loop(rows, x_cond=x_cond, seed=31, graph=graph, record=(False, True))
+        torch.cuda.synchronize()
+        assert eng.get_option("last_route") & 512, eng.get_option("last_route")
+        assert torch.equal(got[0], ref[0]) and torch.equal(got[4], ref[1]), (batch, chains, graph, _max_err(got[0], ref[0]))
+    assert eng.status(rows) == 0
+
+
 def test_split_route_shard_equals_full_batch(cuda):
     """A shard small enough for the split route (400 rows at row0 = 1600, as one rank of an
     8-GPU strong-scaling run of config 2) reproduces those rows of the full 3,200-row batch on
