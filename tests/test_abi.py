@@ -87,10 +87,10 @@ def test_plan_options_validated_on_host():
     assert lib.sd_plan_create(ctypes.byref(h), ctypes.byref(d)) == 0, lib.sd_last_error()
     try:
         v = ctypes.c_int64()
-        for value in (0, 1, 2, 3, 4, 5):
+        for value in (0, 1, 2, 3, 4, 5, 6):
             assert lib.sd_plan_set_option(h, _lib.SD_OPT_SPLIT_ROUTE, value) == 0
             assert lib.sd_plan_get_option(h, _lib.SD_OPT_SPLIT_ROUTE, ctypes.byref(v)) == 0 and v.value == value
-        assert lib.sd_plan_set_option(h, _lib.SD_OPT_SPLIT_ROUTE, 6) == -1
+        assert lib.sd_plan_set_option(h, _lib.SD_OPT_SPLIT_ROUTE, 7) == -1
         assert b"split route" in lib.sd_last_error()
         assert lib.sd_plan_set_option(h, _lib.SD_OPT_ROW_CHAINS, -1) == -1
         assert lib.sd_plan_set_option(h, _lib.SD_OPT_ROW_CHAINS, 0) == 0  # auto
