@@ -43,7 +43,8 @@ extern "C" {
 
 /* ABI history: 1 (rounds 1-3); 2 (round 5) -- sd_mahalanobis_loss_forward / _backward take T,
  * sd_set_kernel_variant / sd_set_row_chains / sd_set_update_kernel / sd_set_v5_mix removed
- * (per-plan options instead), sd_test_set_split_route added.  Bindings check it at load. */
+ * (per-plan options instead), sd_test_set_split_route and sd_plan_desc::objective added.
+ * Bindings check it at load. */
 #define SD_ABI_VERSION 2
 
 enum {
@@ -81,6 +82,8 @@ typedef struct sd_plan_desc {
     int32_t isotropic;        /* 1: IsotropicGaussianDiffusion posterior (scalar coefficients) */
     int32_t activation;       /* diffusion_activation: 0 identity, 1 tanh */
     float sinusoidal_theta;   /* SinusoidalPosEmb theta (10000) */
+    int32_t objective;        /* 0 pred_x0 (release configs); isotropic only: 1 pred_noise, 2 pred_v
+                                 (x0 = a[t] x_t - b[t] act(model_out): isotropic.py:48-70) */
 } sd_plan_desc;
 
 int32_t sd_abi_version(void);

@@ -356,7 +356,8 @@ def p_sample_loop(sd, cfg: DenoiserConfig, bufs: Dict[str, torch.Tensor], start_
                   sampling_noise: Optional[torch.Tensor], x_cond: Optional[torch.Tensor] = None,
                   isotropic: bool = False, activation: str = "identity", record_means: bool = False,
                   steps: Optional[int] = None, record_imgs: bool = False,
-                  noise2interpolate: Optional[torch.Tensor] = None, interpolate_funct=None):
+                  noise2interpolate: Optional[torch.Tensor] = None, interpolate_funct=None,
+                  objective: str = "pred_x0"):
     """Reverse diffusion with host-supplied noise.  Returns (img, [mean_t for t=T-1..1]), or
     (img, means, [x_t for t=T-1..1]) with `record_imgs` (return_timages, base.py:371-389).
 
@@ -376,6 +377,10 @@ def p_sample_loop(sd, cfg: DenoiserConfig, bufs: Dict[str, torch.Tensor], start_
         tt = torch.full((B,), t, dtype=torch.long)
         out = denoiser_forward(sd, cfg, img, tt, x_cond)
         x0 = torch.tanh(out) if activation == "tanh" else out
+        if objective == "pred_noise":  # model_predictions, base.py:219-241 -> isotropic.py:48-52
+            x0 = bufs["sqrt_recip_alphas_cumprod"][t] * img - bufs["sqrt_recipm1_alphas_cumprod"][t] * x0
+        elif objective == "pred_v":    # isotropic.py:66-70
+            x0 = bufs["sqrt_alphas_cumprod"][t] * img - bufs["sqrt_one_minus_alphas_cumprod"][t] * x0
         x0 = x0.clamp(-1.0, 1.0)
         if isotropic:
             mean = bufs["posterior_mean_coef1"][t] * x0 + bufs["posterior_mean_coef2"][t] * img

@@ -72,6 +72,7 @@ class SDPlanDesc(ctypes.Structure):
         ("isotropic", ctypes.c_int32),
         ("activation", ctypes.c_int32),
         ("sinusoidal_theta", ctypes.c_float),
+        ("objective", ctypes.c_int32),
     ]
 
 

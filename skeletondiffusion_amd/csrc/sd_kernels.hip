@@ -598,6 +598,12 @@ hipError_t launch_copy_rows(float* dst, int64_t dst_rs, const float* src, int64_
 // wave-uniform broadcasts.  HBM-bound: 4 * J * D * 4 B per row (x0, x_t, eps in; x_{t-1} out).
 // =============================================================================================
 
+// isotropic pred_noise / pred_v (isotropic.py:48-70): x0 = a[t] x_t - b[t] act(model_out), each
+// product rounded before the difference, as the reference's two tensor products and subtraction
+__device__ __forceinline__ floatx2 start_from_pred(const UpdArgs& p, floatx2 xt, floatx2 m) {
+    return floatx2{__fmul_rn(p.xa, xt.x) - __fmul_rn(p.xb, m.x), __fmul_rn(p.xa, xt.y) - __fmul_rn(p.xb, m.y)};
+}
+
 template <int JM, bool EXACT>
 __global__ __launch_bounds__(256) void k_update(const UpdArgs p) {
     const int J = EXACT ? JM : p.J;
@@ -636,8 +642,9 @@ __global__ __launch_bounds__(256) void k_update(const UpdArgs p) {
             a.x = tanhf(a.x);
             a.y = tanhf(a.y);
         }
-        x0v[j] = floatx2{fminf(fmaxf(a.x, -1.f), 1.f), fminf(fmaxf(a.y, -1.f), 1.f)};
         xtv[j] = ld2x(p.xt, rb + j * D + d, p.xt_bf16);
+        if (p.obj) a = start_from_pred(p, xtv[j], a);
+        x0v[j] = floatx2{fminf(fmaxf(a.x, -1.f), 1.f), fminf(fmaxf(a.y, -1.f), 1.f)};
         if (p.noise_mode == 1)
             ev[j] = ld2(p.eps + row * p.eps_rs + j * D + d);
         else if (p.noise_mode == 2)
@@ -741,8 +748,10 @@ __global__ __launch_bounds__(256) void k_update_row(const UpdArgs p) {
             a.x = tanhf(a.x);
             a.y = tanhf(a.y);
         }
+        const floatx2 xt = ld2x(p.xt, rb + o, p.xt_bf16);
+        if (p.obj) a = start_from_pred(p, xt, a);
         st2(sx0 + o, floatx2{fminf(fmaxf(a.x, -1.f), 1.f), fminf(fmaxf(a.y, -1.f), 1.f)});
-        st2(sxt + o, ld2x(p.xt, rb + o, p.xt_bf16));
+        st2(sxt + o, xt);
         floatx2 e;
         if (p.noise_mode == 1) e = ld2(p.eps + row * p.eps_rs + o);
         else if (p.noise_mode == 2) e = noise_pair(seed, (uint64_t)(row0 + row), p.step, (uint32_t)o);

@@ -178,6 +178,8 @@ struct sd_plan {
     float* film = nullptr;  // (nres, T, 2H) raw Linear(tanh(temb)) outputs
     float* sig = nullptr;   // (T, J) or (T)
     std::vector<float> iso_c1, iso_c2, iso_sig;  // host copies of the scalar tables (isotropic)
+    std::vector<float> iso_xa, iso_xb;           // pred_noise / pred_v: x0 = xa[t] x_t - xb[t] act(out)
+    int s_xa = -1, s_xb = -1;
 
     std::mutex gmu;
     std::map<GraphKey, std::shared_ptr<GraphSet>> graphs;  // one graph per row chain
@@ -236,6 +238,10 @@ int check_dims(const sd_plan_desc* d) {
         return fail(SD_E_INVALID, "attn_dim_head must be a positive multiple of 16");
     if (d->timesteps < 1) return fail(SD_E_INVALID, "timesteps must be >= 1");
     if (d->activation != 0 && d->activation != 1) return fail(SD_E_INVALID, "activation must be 0 (identity) or 1 (tanh)");
+    if (d->objective < 0 || d->objective > 2) return fail(SD_E_INVALID, "objective must be 0 (pred_x0), 1 (pred_noise) or 2 (pred_v)");
+    if (d->objective != 0 && !d->isotropic)
+        return fail(SD_E_INVALID, "the nonisotropic sampler supports objective pred_x0 only (the release configs; "
+                                  "pred_v is not implemented in the reference, nonisotropic.py:122-124)");
     return SD_OK;
 }
 
@@ -583,6 +589,11 @@ int run_update(const sd_plan* p, const float* x0, const float* xt, const float* 
         u.c1s = p->iso_c1[t];
         u.c2s = p->iso_c2[t];
         u.sigs = p->iso_sig[t];
+        if (p->d.objective) {
+            u.obj = 1;
+            u.xa = p->iso_xa[t];
+            u.xb = p->iso_xb[t];
+        }
     } else {
         const size_t JJ = (size_t)p->J * p->J;
         u.C1 = p->ptr(p->s_c1) + t * JJ;
@@ -735,6 +746,13 @@ int sd_plan_create(sd_plan** out, const sd_plan_desc* desc) {
         p->s_c1 = p->add("posterior_mean_coef1", p->T);
         p->s_c2 = p->add("posterior_mean_coef2", p->T);
         p->s_lv = p->add("posterior_log_variance_clipped", p->T);
+        if (desc->objective == 1) {  // predict_start_from_noise (isotropic.py:48-52)
+            p->s_xa = p->add("sqrt_recip_alphas_cumprod", p->T);
+            p->s_xb = p->add("sqrt_recipm1_alphas_cumprod", p->T);
+        } else if (desc->objective == 2) {  // predict_start_from_v (isotropic.py:66-70)
+            p->s_xa = p->add("sqrt_alphas_cumprod", p->T);
+            p->s_xb = p->add("sqrt_one_minus_alphas_cumprod", p->T);
+        }
     } else {
         p->s_c1 = p->add("posterior_mean_coef1_x0", (int64_t)p->T * J * J);
         p->s_c2 = p->add("posterior_mean_coef2_xt", (int64_t)p->T * J * J);
@@ -858,6 +876,12 @@ int sd_plan_finalize(sd_plan* p, void* stream_) {
         SD_HIP(hipMemcpyAsync(p->iso_c1.data(), p->ptr(p->s_c1), T * sizeof(float), hipMemcpyDeviceToHost, s));
         SD_HIP(hipMemcpyAsync(p->iso_c2.data(), p->ptr(p->s_c2), T * sizeof(float), hipMemcpyDeviceToHost, s));
         SD_HIP(hipMemcpyAsync(lv.data(), p->ptr(p->s_lv), T * sizeof(float), hipMemcpyDeviceToHost, s));
+        if (p->d.objective) {
+            p->iso_xa.resize(T);
+            p->iso_xb.resize(T);
+            SD_HIP(hipMemcpyAsync(p->iso_xa.data(), p->ptr(p->s_xa), T * sizeof(float), hipMemcpyDeviceToHost, s));
+            SD_HIP(hipMemcpyAsync(p->iso_xb.data(), p->ptr(p->s_xb), T * sizeof(float), hipMemcpyDeviceToHost, s));
+        }
         SD_HIP(hipStreamSynchronize(s));
         for (int t = 0; t < T; ++t) p->iso_sig[t] = std::exp(0.5f * lv[t]);
     } else {

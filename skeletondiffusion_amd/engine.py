@@ -68,8 +68,11 @@ class SamplingEngine:
             unsupported.append("self_condition")
         if m.graph_kwargs.get("norm_type", "none") != "none":
             unsupported.append("norm_type != 'none'")
-        if self.diff.objective != "pred_x0":
-            unsupported.append(f"objective {self.diff.objective!r} (the reference samples pred_x0)")
+        objectives = {"pred_x0": 0, "pred_noise": 1, "pred_v": 2}
+        iso = not hasattr(self.diff, "posterior_mean_coef1_x0")
+        if self.diff.objective not in objectives or (self.diff.objective != "pred_x0" and not iso):
+            unsupported.append(f"objective {self.diff.objective!r} on the nonisotropic sampler (pred_x0 only; the "
+                               "isotropic sampler also takes pred_noise / pred_v)")
         if unsupported:
             raise SkelDiffError("sampling engine does not support: " + ", ".join(unsupported))
         d.num_nodes = m.channels
@@ -95,6 +98,7 @@ class SamplingEngine:
         d.isotropic = int(not hasattr(self.diff, "posterior_mean_coef1_x0"))
         d.activation = 1 if self.diff.diffusion_activation == "tanh" else 0
         d.sinusoidal_theta = float(m.sinusoidal_pos_emb_theta)
+        d.objective = objectives.get(self.diff.objective, 0)
         return d
 
     PRECISIONS = {"f32": 0, "half": 1, "bf16": 2}
@@ -269,6 +273,11 @@ class SamplingEngine:
         check(L.sd_p_sample_update(plan, ptr(x0_raw), ptr(x), ptr(eps), JD, seed, 0, int(t), ptr(out),
                                    ptr(mean), JD, ptr(noise_used), JD, rows, _stream(self._device)))
         x0 = torch.tanh(x0_raw) if self.diff.diffusion_activation == "tanh" else x0_raw
+        obj = self.diff.objective
+        if obj == "pred_noise":    # isotropic.py:48-52 (the update kernel does the same)
+            x0 = self.diff.sqrt_recip_alphas_cumprod[t] * x - self.diff.sqrt_recipm1_alphas_cumprod[t] * x0
+        elif obj == "pred_v":      # isotropic.py:66-70
+            x0 = self.diff.sqrt_alphas_cumprod[t] * x - self.diff.sqrt_one_minus_alphas_cumprod[t] * x0
         return out, x0.clamp_(-1.0, 1.0), (noise_used if t > 0 else 0.0), mean
 
     def sample_loop(self, rows: int, x_cond=None, start_noise=None, sampling_noise=None,

@@ -222,6 +222,29 @@ def gen_readme():
     _save("readme16_T10", **out)
 
 
+def gen_iso_objectives():
+    """IsotropicGaussianDiffusion sampled with the pred_noise and pred_v objectives (x0 from
+    predict_start_from_noise / _from_v, isotropic.py:48-70; base.py:219-241), README Denoiser,
+    J=16, T=10, identity and tanh diffusion activation (round 5)."""
+    J, B, T = 16, 4, 10
+    start = torch.from_numpy(synthetic.normal((B, J, 96), seed=11))
+    samp = torch.from_numpy(synthetic.normal((B, T - 1, J, 96), seed=12))
+    out = {}
+    for obj in ("pred_noise", "pred_v"):
+        for act in ("identity", "tanh"):
+            model = Denoiser(dim=96, cond_dim=0, out_dim=96, channels=J, num_nodes=J)
+            synthetic.fill_module_(model, WEIGHT_SEED)
+            diff = IsotropicGaussianDiffusion(model=model, diffusion_timesteps=T, diffusion_objective=obj,
+                                              diffusion_activation=act).eval()
+            with torch.no_grad():
+                img, (noise0, noise_t, mean_t) = diff.sample(batch_size=B, start_noise=start.clone(),
+                                                             sampling_noise=samp.clone(), return_sampling_noise=True)
+            out[f"{obj}_{act}_img"] = img
+            out[f"{obj}_{act}_mean_t"] = mean_t
+    out["start"], out["samp"] = start, samp
+    _save("iso_objectives_T10", **out)
+
+
 def gen_release(skel_key, T, B_seq, futures, with_acts, steps_to_keep=None, tag=None,
                 final_scale=1.0):
     sk, corr, node_types, diff = build_release(skel_key, T, final_scale=final_scale)
@@ -429,6 +452,9 @@ def gen_best_of_k():
 
 
 def main():
+    if sys.argv[1:] == ["iso_obj"]:
+        gen_iso_objectives()
+        return
     if sys.argv[1:] == ["best_of_k"]:
         gen_best_of_k()
         return
@@ -460,6 +486,7 @@ def main():
     gen_hip_included()
     gen_new_r03()
     gen_best_of_k()
+    gen_iso_objectives()
 
 
 if __name__ == "__main__":

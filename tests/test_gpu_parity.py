@@ -81,6 +81,43 @@ def test_readme_config_matches_reference(mode, cuda):
     assert _max_err(mean_t, z[f"{mode}_mean_t"]) < TOL
 
 
+@pytest.mark.parametrize("obj", ["pred_noise", "pred_v"])
+@pytest.mark.parametrize("act", ["identity", "tanh"])
+def test_isotropic_objectives_match_reference(obj, act, cuda):
+    """IsotropicGaussianDiffusion sampled with the pred_noise / pred_v objectives (isotropic.py:48-70,
+    base.py:219-241): the update kernel forms x0 = a[t] x_t - b[t] act(model_out) before the clamp;
+    sample() and p_sample() against the reference's own outputs (tests/golden/iso_objectives_T10.npz)."""
+    from skeletondiffusion_amd import synthetic
+    from skeletondiffusion_amd.core.diffusion import IsotropicGaussianDiffusion
+    from skeletondiffusion_amd.core.network import Denoiser
+
+    z = golden("iso_objectives_T10")
+    m = Denoiser(dim=96, cond_dim=0, out_dim=96, channels=16, num_nodes=16)
+    synthetic.fill_module_(m, WEIGHT_SEED)
+    d = IsotropicGaussianDiffusion(model=m, diffusion_timesteps=10, diffusion_objective=obj,
+                                   diffusion_activation=act).to(cuda).eval()
+    start = torch.from_numpy(z["start"]).to(cuda)
+    samp = torch.from_numpy(z["samp"]).to(cuda)
+    img, (_, _, mean_t) = d.sample(batch_size=4, start_noise=start, sampling_noise=samp, return_sampling_noise=True)
+    assert _max_err(img, z[f"{obj}_{act}_img"]) < TOL
+    assert _max_err(mean_t, z[f"{obj}_{act}_mean_t"]) < TOL
+    # one p_sample step (its x_start return is the predicted start, clamped)
+    x, x_start, _, mean = d.p_sample(start, 9, sampling_noise=samp)
+    assert _max_err(mean, z[f"{obj}_{act}_mean_t"][:, 0]) < TOL
+    assert float(x_start.abs().max()) <= 1.0
+
+
+def test_nonisotropic_objective_refusal_text(cuda):
+    """The nonisotropic sampler takes pred_x0 only (the release configs; the reference's pred_v is
+    'Not implemented', nonisotropic.py:122-124): the engine refuses others with a pinned message."""
+    from skeletondiffusion_amd._lib import SkelDiffError
+
+    d = build_readme_diffusion("noniso", cuda)
+    d.objective = "pred_noise"
+    with pytest.raises(SkelDiffError, match="objective 'pred_noise' on the nonisotropic sampler"):
+        d.sample(batch_size=2)
+
+
 def test_philox_device_stream_bit_exact(cuda):
     L = _lib.lib()
     rows, quads, seed, row0, step = 37, 24, 0x123456789ABCDEF, 1 << 33, 7
