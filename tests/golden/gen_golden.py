@@ -451,7 +451,31 @@ def gen_best_of_k():
           pose_l1=pl1, pose_mse=pmse)
 
 
+def gen_best_of_k_metric():
+    """Best-of-k in `metric_space` (trainer.py:193-198 + 213-214) on the fixture gen_best_of_k wrote:
+    the reference skeleton of the release task config (SkeletonRescalePose, if_consider_hip False,
+    pose_box_size 1.5: configs/config_train_autoencoder/task/hmp.yaml) maps the decoded samples and
+    the future to metric space; the similarity is the per-sample L2 over the flattened joints, mean
+    over frames; the selection is trainer.py:218-220 (restated: trainer.py imports ignite, absent)."""
+    from src.data.skeleton.motion.rescalepose import SkeletonRescalePose
+
+    z = np.load(os.path.join(HERE, "best_of_k.npz"))
+    sk = SkeletonRescalePose(if_consider_hip=False, pose_box_size=1.5, obs_length=30, pred_length=int(z["ph"]))
+    out, fut = torch.from_numpy(z["decoded"]), torch.from_numpy(z["fut"])
+    loss = torch.from_numpy(z["loss"])
+    b, k = out.shape[:2]
+    out_c = sk.transform_to_metric_space(out).flatten(start_dim=3)
+    fut_c = sk.transform_to_metric_space(fut).unsqueeze(1).flatten(start_dim=3).repeat_interleave(k, dim=1)
+    sim = torch.linalg.norm(out_c - fut_c, axis=-1).mean(axis=-1)
+    idx = sim.view(b, -1).min(axis=-1).indices
+    sel = torch.gather(loss.view(b, -1), dim=1, index=idx.unsqueeze(1)).squeeze(-1)
+    _save("best_of_k_metric", out_c=out_c, fut_c=fut_c, sim=sim, idx=idx, sel=sel, pose_box_size=1.5)
+
+
 def main():
+    if sys.argv[1:] == ["best_of_k_metric"]:
+        gen_best_of_k_metric()
+        return
     if sys.argv[1:] == ["iso_obj"]:
         gen_iso_objectives()
         return

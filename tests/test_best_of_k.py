@@ -45,27 +45,53 @@ def _autoencoder(device):
     return m.to(device)
 
 
+def _to_metric_space(kpts, box=1.5):
+    """The release task's skeleton (SkeletonRescalePose, if_consider_hip False, pose_box_size 1.5;
+    reference rescalepose.py:29-39 via base.py:69-86): the pose scaled back out of the unit box."""
+    return kpts * box
+
+
+def test_metric_space_selection_matches_reference():
+    """metric_space (trainer.py:193-198, 213-214) restated on the fixture's decoded samples against
+    tests/golden/best_of_k_metric.npz (gen_golden.py:gen_best_of_k_metric, the reference skeleton)."""
+    z, m = golden("best_of_k"), golden("best_of_k_metric")
+    assert float(m["pose_box_size"]) == 1.5
+    k = int(z["k"])
+    out_c = _to_metric_space(torch.from_numpy(z["decoded"])).flatten(start_dim=3)
+    fut_c = _to_metric_space(torch.from_numpy(z["fut"])).unsqueeze(1).flatten(start_dim=3).repeat_interleave(k, 1)
+    np.testing.assert_array_equal(out_c.numpy(), m["out_c"])
+    np.testing.assert_array_equal(fut_c.numpy(), m["fut_c"])
+    sim = torch.linalg.norm(out_c - fut_c, dim=-1).mean(dim=-1)
+    np.testing.assert_allclose(sim.numpy(), m["sim"], rtol=1e-6, atol=1e-8)
+    sel, idx = O.best_of_k(torch.from_numpy(z["loss"]), k, sim.reshape(-1))
+    np.testing.assert_array_equal(idx.numpy(), m["idx"])
+    np.testing.assert_array_equal(sel.numpy(), m["sel"])
+
+
 @pytest.mark.gpu
-@pytest.mark.parametrize("space", ["input_space", "latent_space"])
+@pytest.mark.parametrize("space", ["input_space", "metric_space", "latent_space"])
 def test_hip_best_of_k_matches_reference(space, cuda):
-    """p_losses(n_train_samples=k) on the HIP training kernels, the HIP decoder, sd_pose_loss and
-    sd_best_of_k: the selected indices equal the reference's, the selected losses and the trainer's
-    scalar within 1e-5, and the gradient reaches only the selected samples' rows."""
+    """p_losses(n_train_samples=k) on the HIP training kernels, the HIP decoder, sd_pose_loss /
+    sd_ade_fde and sd_best_of_k: the selected indices equal the reference's, the selected losses and
+    the trainer's scalar within 1e-5, and the gradient reaches only the selected samples' rows."""
     from skeletondiffusion_amd.core import best_of_k as B
 
     z = golden("best_of_k")
+    m = golden("best_of_k_metric")
     d = build_release_diffusion(golden("release_h36m16_T10"), cuda)
     d.train()
     ae = _autoencoder(cuda)
     k, ph = int(z["k"]), int(z["ph"])
     dev = lambda n: torch.from_numpy(z[n]).to(cuda)  # noqa: E731
+    dev_m = lambda n: torch.from_numpy(m[n]).to(cuda)  # noqa: E731
     data, x_cond, t, noise, past, fut = (dev(n) for n in ("data", "x_cond", "t", "noise", "past", "fut"))
     loss, w, samples = d.p_losses(data, t, noise=noise, x_cond=x_cond, n_train_samples=k)
     assert float((loss - dev("loss")).abs().max()) < 1e-5
     out_c, fut_c = B.to_comparison_space_train(samples.detach(), diff_input=data, past_seq=past, autoencoder=ae,
-                                               fut_seq=fut, space=space, x_cond=x_cond, prediction_horizon=ph)
+                                               fut_seq=fut, space=space, x_cond=x_cond, prediction_horizon=ph,
+                                               transform_to_metric_space=_to_metric_space)
     sel, idx = B.get_ksimilarity_loss(loss, out_c, fut_c, similarity_space=space, autoencoder=ae)
-    want = z["idx"] if space == "input_space" else z["idx_latent"]
+    want = {"input_space": z["idx"], "metric_space": m["idx"], "latent_space": z["idx_latent"]}[space]
     np.testing.assert_array_equal(idx.cpu().numpy(), want)
     ref_sel = torch.gather(dev("loss").view(3, -1), 1, torch.from_numpy(want).to(cuda).unsqueeze(1)).squeeze(1)
     assert float((sel - ref_sel).abs().max()) < 1e-5
@@ -73,6 +99,10 @@ def test_hip_best_of_k_matches_reference(space, cuda):
         assert float((out_c - dev("decoded")).abs().max()) < 1e-4
         final = (sel * w).mean()
         assert abs(float(final) - float(z["final"])) < 1e-5
+    if space == "metric_space":
+        assert float((out_c - dev_m("out_c")).abs().max()) < 1.5e-4  # the decoder's 1e-4, scaled by the box
+        sim = B._metrics.ade(fut_c[:, 0], out_c, reduction="none")
+        assert float((sim - dev_m("sim")).abs().max()) < 1e-4
     g = torch.autograd.grad(sel.sum(), samples, retain_graph=False)[0]
     torch.cuda.synchronize()
     rows = torch.arange(3, device=cuda) * k + idx

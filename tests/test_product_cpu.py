@@ -1,6 +1,7 @@
 """Host-side product logic on CPU: the reference API surface (constructors, attributes,
 state_dict, buffers, training forward) against the reference's own outputs, and the
 no-CPU-sampling rule."""
+import re
 import numpy as np
 import pytest
 import torch
@@ -86,6 +87,27 @@ def test_sample_on_cpu_raises():
     d = build_readme_diffusion("noniso")
     with pytest.raises(SkelDiffError, match="HIP engine"):
         d.sample(batch_size=2)
+
+
+@pytest.mark.parametrize("kw, reason", [
+    (dict(norm_type="layer"), "norm_type != 'none'"),
+    (dict(self_condition=True), "self_condition"),
+    (dict(learned_variance=True), "learned_variance"),
+    (dict(learned_sinusoidal_cond=True), "learned/random sinusoidal time embedding"),
+    (dict(random_fourier_features=True), "learned/random sinusoidal time embedding"),
+])
+def test_non_release_denoiser_options_refused_with_reason(kw, reason):
+    """Denoiser options no release config uses (attention.py:55-60, generator.py:16-45,80,88) build
+    as torch modules like the reference's, and the sampling engine refuses them by name at plan
+    time instead of sampling something else (engine.py:_desc)."""
+    from skeletondiffusion_amd.core.diffusion import NonisotropicGaussianDiffusion, get_cov_from_corr
+    from skeletondiffusion_amd.core.network import Denoiser
+
+    m = Denoiser(dim=96, cond_dim=0, out_dim=96, channels=16, num_nodes=16, **kw)
+    S, L, U = get_cov_from_corr(torch.eye(16))
+    d = NonisotropicGaussianDiffusion(Sigma_N=S, Lambda_N=L, U=U, model=m, diffusion_timesteps=10)
+    with pytest.raises(SkelDiffError, match="sampling engine does not support: " + re.escape(reason)):
+        d.engine._desc()
 
 
 def test_unknown_kwargs_are_swallowed():
