@@ -314,9 +314,12 @@ enum {
     SD_OPT_UPDATE_KERNEL = 9,   /* posterior update: 0 (default) the J x J projections on
                                    v_mfma_f32_16x16x4_f32 where they apply (nonisotropic, J <= 64),
                                    1 the element-per-thread forms; both give the same bits */
-    SD_OPT_V5_MIX = 10          /* J > 21 mixing pass (v5): 0 (default) G-hat mixing on
+    SD_OPT_V5_MIX = 10,         /* J > 21 mixing pass (v5): 0 (default) G-hat mixing on
                                    v_mfma_f32_16x16x4_f32 (k_gl5_mixm), 1 the VALU form (k_gl5_mix);
                                    the same j-ordered fmaf chains */
+    SD_OPT_ATTENTION = 11       /* separate attention kernel at 49 <= J <= 52 (MANO): 0 (default)
+                                   48 nodes on the MFMAs + the last J - 48 on an fmaf chain in the
+                                   MFMA's k order, 1 the form padded to 64 nodes; the same bits */
 };
 int sd_plan_set_option(sd_plan* plan, int32_t option, int64_t value);
 int sd_plan_get_option(const sd_plan* plan, int32_t option, int64_t* value);

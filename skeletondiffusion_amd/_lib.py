@@ -44,7 +44,8 @@ EXPORTED = (
 
 # sd_plan_set_option keys (include/skeldiff.h)
 (SD_OPT_KERNEL_VARIANT, SD_OPT_GL4_TILE, SD_OPT_ROW_CHAINS, SD_OPT_PRECISION, SD_OPT_GL4_STAGING,
- SD_OPT_SPLIT_ROUTE, SD_OPT_LAST_CHAINS, SD_OPT_LAST_ROUTE, SD_OPT_UPDATE_KERNEL, SD_OPT_V5_MIX) = range(1, 11)
+ SD_OPT_SPLIT_ROUTE, SD_OPT_LAST_CHAINS, SD_OPT_LAST_ROUTE, SD_OPT_UPDATE_KERNEL, SD_OPT_V5_MIX,
+ SD_OPT_ATTENTION) = range(1, 12)
 # SD_OPT_LAST_ROUTE bits (sd::RouteBits)
 ROUTE_BITS = {1: "k_gl4 one-kernel", 2: "k_gl4 fused to_qkv+attention", 4: "k_gl4y GEMM phase",
               8: "k_gl4t GEMM phase", 16: "k_gl4 MODE 2/3 mixing phase", 32: "v5 k_gl5 mixing", 64: "exact-f32 kernels",

@@ -268,8 +268,18 @@ hipError_t launch_graph_linear_v1(const GLArgs& a, bool rms, hipStream_t s) {
 
 // DH: the head width at compile time (32, the release model: both 16-wide chunks' loads are
 // issued together and the V loads with them, so a wave pays one memory latency), 0 = runtime.
-template <int JT, int DH = 0>
+// TAIL (JT = 4, DH = 32, 48 < J <= 52: MANO J = 51 / 52): the last node tile has only J - 48 real
+// rows, so its key rows j = 48 .. J-1 of S^T and its value rows of O^T leave the MFMAs (12 of 16
+// S tiles, 3 of 4 k tiles of O) for an fmaf chain on the VALU in the MFMA's own k order -- the
+// f32 MFMA sums its k = 4 products as an fmaf chain, and the padded rows added exact zeros -- so
+// the result is the padded form's bit for bit (test_attention_tail_bitwise):
+//   S^T[48 + r][n] (lane n): sum over d in the (u, e, g) order of the QK MFMAs of
+//     K[48 + r][d] (read from the key fragments with v_readlane) * Q[n][d] scale (the lane's row);
+//   O^T[d][n] += V[48 + r][d] P^T[48 + r][n] after the 12 PV k tiles, r = 0 .. J - 49 in order.
+template <int JT, int DH = 0, bool TAIL = false>
 __global__ __launch_bounds__(256) void k_attention(const AttnArgs p) {
+    static_assert(!TAIL || (JT == 4 && DH == 32), "the tail form is the MANO J = 49..52 kernel");
+    constexpr int JA = TAIL ? JT - 1 : JT;  // node tiles on the MFMAs as keys / values
     const int lane = threadIdx.x & 63;
     const int lr = lane & 15, lg = lane >> 4;
     const int64_t pair = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -297,13 +307,26 @@ __global__ __launch_bounds__(256) void k_attention(const AttnArgs p) {
     floatx4 vv[DH ? NCC : 1][JT];
     auto load_v = [&](int dc, floatx4* v) {
 #pragma unroll
-        for (int jt = 0; jt < JT; ++jt)
+        for (int jt = 0; jt < JA; ++jt)
 #pragma unroll
             for (int s4 = 0; s4 < 4; ++s4) v[jt][s4] = vb[min(jt * 16 + 4 * lg + s4, J - 1) * rs + dc + lr];
     };
+    // TAIL: this lane's query row (n = lane, scaled as the B fragments) and the tail value rows
+    // V[48 + r][dc + 4 lg .. + 3] for both 16-wide chunks, issued with the fragment loads
+    constexpr int QW = TAIL ? 8 : 1;
+    floatx4 qrow[QW], vt[TAIL ? 2 : 1][TAIL ? 4 : 1];
+    if constexpr (TAIL) {
+#pragma unroll
+        for (int c = 0; c < 8; ++c) qrow[c] = ld4(qb + min(lane, J - 1) * rs + 4 * c);
+#pragma unroll
+        for (int u = 0; u < 2; ++u)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) vt[u][r] = ld4(vb + min(48 + r, J - 1) * rs + 16 * u + 4 * lg);
+    }
+    float tl[4] = {0.f, 0.f, 0.f, 0.f};  // TAIL: S^T[48 + r][n = lane]
     auto mask_v = [&](floatx4* v) {
 #pragma unroll
-        for (int jt = 0; jt < JT; ++jt)
+        for (int jt = 0; jt < JA; ++jt)
 #pragma unroll
             for (int s4 = 0; s4 < 4; ++s4) v[jt][s4] = jt * 16 + 4 * lg + s4 < J ? v[jt][s4] : 0.f;
     };
@@ -336,10 +359,36 @@ __global__ __launch_bounds__(256) void k_attention(const AttnArgs p) {
 #pragma unroll
             for (int e = 0; e < 4; ++e)
 #pragma unroll
-                for (int jt = 0; jt < JT; ++jt)
+                for (int jt = 0; jt < JA; ++jt)
 #pragma unroll
                     for (int nt = 0; nt < JT; ++nt) S[jt][nt] = mfma4(ka[u][jt][e], qv[u][nt][e], S[jt][nt]);
+            if constexpr (TAIL) {  // key rows 48 + r: the MFMA's chain order, k = (e, g), d = 16 u + 4 g + e
+#pragma unroll
+                for (int e = 0; e < 4; ++e)
+#pragma unroll
+                    for (int g = 0; g < 4; ++g) {
+                        const float q = qrow[4 * u + g][e] * p.scale;
+                        // the element through a scalar first: __builtin_bit_cast of a vector-element
+                        // subscript (ka[..][e]) reads element 0 for every e with this compiler
+                        // (found here: tools/readlane_probe.hip)
+                        const float ke = ka[u][JT - 1][e];
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) {
+                            const float k = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(ke), 16 * g + r));
+                            tl[r] = fmaf(k, q, tl[r]);
+                        }
+                    }
+            }
         }
+    }
+    if constexpr (TAIL) {  // S^T[48 + 4 lg + i][nt 16 + lr] in the MFMA layout: rows 48 + i at lg = 0, zero rows beyond
+#pragma unroll
+        for (int nt = 0; nt < JT; ++nt)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const float t = __shfl(tl[i], nt * 16 + lr);
+                S[JT - 1][nt][i] = (lg == 0 && 48 + i < J) ? t : 0.f;
+            }
     }
 
     // softmax over j (rows of S^T) for every query column n = nt*16 + lr
@@ -380,11 +429,23 @@ __global__ __launch_bounds__(256) void k_attention(const AttnArgs p) {
 #pragma unroll
         for (int nt = 0; nt < JT; ++nt) o[nt] = floatx4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int jt = 0; jt < JT; ++jt)
+        for (int jt = 0; jt < JA; ++jt)
 #pragma unroll
             for (int e = 0; e < 4; ++e)
 #pragma unroll
                 for (int nt = 0; nt < JT; ++nt) o[nt] = mfma4(v[jt][e], S[jt][nt][e], o[nt]);
+        if constexpr (TAIL) {  // value rows 48 + r, last in the chain as in the padded k tile
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                if (48 + r >= J) break;  // wave-uniform
+#pragma unroll
+                for (int nt = 0; nt < JT; ++nt) {
+                    const float pr = __shfl(S[JT - 1][nt][r], lr);  // P^T[48 + r][nt 16 + lr] from lane (lr, 0)
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) o[nt][i] = fmaf(vt[dc / 16][r][i], pr, o[nt][i]);
+                }
+            }
+        }
 #pragma unroll
         for (int nt = 0; nt < JT; ++nt) {
             const int n = nt * 16 + lr;
@@ -405,6 +466,7 @@ hipError_t launch_attention(const AttnArgs& a, hipStream_t s) {
         if (a.J <= 16) hipLaunchKernelGGL((k_attention<1, 32>), grid, dim3(256), 0, s, a);
         else if (a.J <= 32) hipLaunchKernelGGL((k_attention<2, 32>), grid, dim3(256), 0, s, a);
         else if (a.J <= 48) hipLaunchKernelGGL((k_attention<3, 32>), grid, dim3(256), 0, s, a);
+        else if (a.J <= 52 && !a.padded) hipLaunchKernelGGL((k_attention<4, 32, true>), grid, dim3(256), 0, s, a);
         else hipLaunchKernelGGL((k_attention<4, 32>), grid, dim3(256), 0, s, a);
         return hipGetLastError();
     }
@@ -885,28 +947,38 @@ __global__ __launch_bounds__(256) void k_update_mfma(const UpdArgs p) {
     }
     row0 += p.row_shift;
     // phase A: sigma_j eps_j (and the raw eps record) for the workgroup's rows (the first SGP
-    // quads' sigma_j prefetched above: loaded in the loop, each was waited out right away)
-    auto phase_a = [&](int q, float sg) {
+    // quads' sigma_j prefetched above: loaded in the loop, each was waited out right away).  One
+    // loop per noise mode (a wave-uniform branch around whole loops): with the given-noise load and
+    // the Philox draw as two arms of one body, the waitcnt pass merged the arms and waited
+    // vmcnt(0) -- every x0 / x_t fragment load above -- before the first draw was even scaled
+    auto phase_a = [&](auto nm, int q, float sg) {
+        constexpr int NM = decltype(nm)::value;
         const int rr = q / QPR, qq = q % QPR, j = qq / (D >> 2), d = 4 * (qq % (D >> 2));
         const int64_t rw = rowg + rr;
         if (rw >= p.B) return;
         floatx4 e = {0.f, 0.f, 0.f, 0.f};
-        if (p.noise_mode == 1) {
+        if constexpr (NM == 1) {
             e = ld4(p.eps + rw * p.eps_rs + j * D + d);
-        } else if (p.noise_mode == 2) {
+        } else if constexpr (NM == 2) {
             const uint4 x = philox_at(seed, (uint64_t)(row0 + rw), p.step, (uint32_t)qq);
             const floatx2 z0 = box_muller(x.x, x.y), z1 = box_muller(x.z, x.w);
             e = floatx4{z0.x, z0.y, z1.x, z1.y};
         }
         if (p.noise_out) *reinterpret_cast<floatx4*>(p.noise_out + rw * p.noise_rs + j * D + d) = e;
-        if (p.noise_mode != 0) e *= sg;
+        if constexpr (NM != 0) e *= sg;
         *reinterpret_cast<floatx4*>(sEv + (rr * J + j) * DS + d) = e;
         if (p.dump_ev) *reinterpret_cast<floatx4*>(p.dump_ev + rw * JD + j * D + d) = e;
     };
+    auto run_a = [&](auto nm) {
 #pragma unroll
-    for (int it = 0; it < SGP; ++it)
-        if (tid + 256 * it < R * QPR) phase_a(tid + 256 * it, sgp[it]);
-    for (int q = tid + 256 * SGP; q < R * QPR; q += 256) phase_a(q, p.noise_mode != 0 ? p.sig[(q % QPR) / (D >> 2)] : 1.f);
+        for (int it = 0; it < SGP; ++it)
+            if (tid + 256 * it < R * QPR) phase_a(nm, tid + 256 * it, sgp[it]);
+        for (int q = tid + 256 * SGP; q < R * QPR; q += 256)
+            phase_a(nm, q, decltype(nm)::value != 0 ? p.sig[(q % QPR) / (D >> 2)] : 1.f);
+    };
+    if (p.noise_mode == 2) run_a(std::integral_constant<int, 2>{});
+    else if (p.noise_mode == 1) run_a(std::integral_constant<int, 1>{});
+    else run_a(std::integral_constant<int, 0>{});
     __syncthreads();
     if (!live) return;  // wave-uniform; no barrier follows
     // A fragments: lane (l16, l4) holds table[i = 16 ib + l16][j = 4 ks + l4]; JP <= 32: every
@@ -935,6 +1007,24 @@ __global__ __launch_bounds__(256) void k_update_mfma(const UpdArgs p) {
             if (p.act == 1) a = tanhf(a);
             bx[q][ks] = fminf(fmaxf(a, -1.f), 1.f);
         }
+    if (p.dump_x0) {  // diagnostics (sd_debug_update_dump), apart from the tile loop (wave-uniform)
+#pragma unroll
+        for (int q = 0; q < MT; ++q) {
+            const int ct = ct0 + q * cstep;
+#pragma unroll
+            for (int ks = 0; ks < KS; ++ks) {
+                const int j = 4 * ks + l4;
+                if (ct < nct && j < J) {
+                    p.dump_x0[rb + j * D + 16 * ct + l16] = bx[q][ks];
+                    p.dump_xt[rb + j * D + 16 * ct + l16] = bt[q][ks];
+                }
+            }
+        }
+    }
+    // every tile's result first, then the stores back to back: with a tile's stores between its
+    // MFMAs and the next tile's, the next tile reused the pending stores' data / address registers
+    // and the waitcnt pass drained vmcnt(0) -- one store round trip -- per tile (15 such waits)
+    floatx4 vres[MT][IB];
 #pragma unroll
     for (int q = 0; q < MT; ++q) {
         const int ct = ct0 + q * cstep;
@@ -945,14 +1035,9 @@ __global__ __launch_bounds__(256) void k_update_mfma(const UpdArgs p) {
         for (int ks = 0; ks < KS; ++ks) {
             const int j = 4 * ks + l4;
             const bool ok = j < J;
-            const float a = bx[q][ks];
-            bxa[ks] = ok ? a : 0.f;
+            bxa[ks] = ok ? bx[q][ks] : 0.f;
             bta[ks] = ok ? bt[q][ks] : 0.f;
             be[ks] = ok ? sEv[(r * J + j) * DS + n] : 0.f;
-            if (p.dump_x0 && ok) {
-                p.dump_x0[rb + j * D + n] = a;
-                p.dump_xt[rb + j * D + n] = bt[q][ks];
-            }
         }
 #pragma unroll
         for (int ib = 0; ib < IB; ++ib) {
@@ -969,11 +1054,23 @@ __global__ __launch_bounds__(256) void k_update_mfma(const UpdArgs p) {
                 m2 = __builtin_amdgcn_mfma_f32_16x16x4f32(bta[ks], A[1][sl][ks], m2, 0, 0, 0);
                 nz = __builtin_amdgcn_mfma_f32_16x16x4f32(be[ks], A[2][sl][ks], nz, 0, 0, 0);
             }
-            const int i = 16 * ib + l16;
-            if (i >= J) continue;
-            const int n4 = 16 * ct + 4 * l4;
             const floatx4 mean = m1 + m2;
-            const floatx4 v = (p.noise_mode != 0) ? mean + nz : mean;
+            vres[q][ib] = (p.noise_mode != 0) ? mean + nz : mean;
+            const int i = 16 * ib + l16;
+            if (p.mean_out && i < J)  // records only (the mean_t record of sample_loop)
+                *reinterpret_cast<floatx4*>(p.mean_out + row * p.mean_rs + i * D + 16 * ct + 4 * l4) = mean;
+        }
+    }
+#pragma unroll
+    for (int q = 0; q < MT; ++q) {
+        const int ct = ct0 + q * cstep;
+        if (ct >= nct) continue;  // wave-uniform
+        const int n4 = 16 * ct + 4 * l4;
+#pragma unroll
+        for (int ib = 0; ib < IB; ++ib) {
+            const int i = 16 * ib + l16;
+            if (16 * ib >= J || i >= J) continue;
+            const floatx4 v = vres[q][ib];
             const int64_t o = rb + i * D + n4;
             if (p.out_bf16) {
                 const bf16x4 vb = __builtin_convertvector(v, bf16x4);
@@ -983,7 +1080,6 @@ __global__ __launch_bounds__(256) void k_update_mfma(const UpdArgs p) {
                 *reinterpret_cast<floatx4*>(p.out + o) = v;
                 if (p.out2) *reinterpret_cast<floatx4*>(p.out2 + row * p.out2_rs + i * D + n4) = v;
             }
-            if (p.mean_out) *reinterpret_cast<floatx4*>(p.mean_out + row * p.mean_rs + i * D + n4) = mean;
         }
     }
 }

@@ -119,7 +119,7 @@ class SamplingEngine:
                "row_chains": _lib.SD_OPT_ROW_CHAINS, "gl4_staging": _lib.SD_OPT_GL4_STAGING,
                "split_route": _lib.SD_OPT_SPLIT_ROUTE, "last_chains": _lib.SD_OPT_LAST_CHAINS,
                "last_route": _lib.SD_OPT_LAST_ROUTE, "update_kernel": _lib.SD_OPT_UPDATE_KERNEL,
-               "v5_mix": _lib.SD_OPT_V5_MIX}
+               "v5_mix": _lib.SD_OPT_V5_MIX, "attention": _lib.SD_OPT_ATTENTION}
     READ_ONLY = ("last_chains", "last_route")
     # The split-f16 graph-linear tiles need |x| < 65504.  A wave whose operands leave that range
     # recomputes its tiles on exact-f32 MFMA inside the kernel (sd_graph_linear_v4.hip:

@@ -97,6 +97,11 @@ def test_plan_options_validated_on_host():
         assert lib.sd_plan_set_option(h, _lib.SD_OPT_ROW_CHAINS, 8) == 0
         assert lib.sd_plan_set_option(h, _lib.SD_OPT_GL4_STAGING, 3) == -1
         assert lib.sd_plan_set_option(h, 99, 0) == -1
+        for opt in (_lib.SD_OPT_UPDATE_KERNEL, _lib.SD_OPT_V5_MIX, _lib.SD_OPT_ATTENTION):  # 0 / 1 switches
+            assert lib.sd_plan_get_option(h, opt, ctypes.byref(v)) == 0 and v.value == 0
+            assert lib.sd_plan_set_option(h, opt, 1) == 0
+            assert lib.sd_plan_get_option(h, opt, ctypes.byref(v)) == 0 and v.value == 1
+            assert lib.sd_plan_set_option(h, opt, 2) == -1 and lib.sd_plan_set_option(h, opt, 0) == 0
         # SD_OPT_LAST_CHAINS: read-only, 0 before the plan's first sampling call
         assert lib.sd_plan_get_option(h, _lib.SD_OPT_LAST_CHAINS, ctypes.byref(v)) == 0 and v.value == 0
         assert lib.sd_plan_set_option(h, _lib.SD_OPT_LAST_CHAINS, 1) == -1

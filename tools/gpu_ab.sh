@@ -11,6 +11,6 @@ for i in $(seq ${REPS:-2}); do
   for run in "$@"; do
     cfg=${run%%|*}; opts=${run#*|}
     env ${ENVS:-X=1} timeout -k 10 300 python bench.py --config $cfg $B $opts > $OUT/b.json 2>> $OUT/b.err || { echo "bench failed: $run"; exit 1; }
-    python3 -c "import json;d=json.load(open('$OUT/b.json'));print('$cfg [$opts]', round(d['value'],1), 'futures/s', round(d['ms_per_step'],1), 'ms/step')"
+    python3 -c "import json;d=json.load(open('$OUT/b.json'));print('$cfg [$opts]', round(d['value'],1), 'futures/s', round(d['ms_per_step'],1), 'ms/step', 'update', round(d['update_kernel']['avg_launch_ms']*1e3,1), 'us')"
   done
 done
