@@ -318,8 +318,9 @@ enum {
                                    v_mfma_f32_16x16x4_f32 (k_gl5_mixm), 1 the VALU form (k_gl5_mix);
                                    the same j-ordered fmaf chains */
     SD_OPT_ATTENTION = 11       /* separate attention kernel at 49 <= J <= 52 (MANO): 0 (default)
-                                   48 nodes on the MFMAs + the last J - 48 on an fmaf chain in the
-                                   MFMA's k order, 1 the form padded to 64 nodes; the same bits */
+                                   the form padded to 64 nodes, 1 48 nodes on the MFMAs + the last
+                                   J - 48 on an fmaf chain in the MFMA's k order (the same bits;
+                                   measured 1 % slower on config 3) */
 };
 int sd_plan_set_option(sd_plan* plan, int32_t option, int64_t value);
 int sd_plan_get_option(const sd_plan* plan, int32_t option, int64_t* value);

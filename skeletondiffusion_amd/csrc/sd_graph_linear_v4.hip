@@ -2360,9 +2360,9 @@ __global__ __launch_bounds__(512, 1) void k_gl4f(const GLArgs p, int64_t ntile_r
                 __syncthreads();
                 if (tid == 0) fq_add(gdone + rg, 1u);
             }
-        } else {  // mixing item w - 8 of slot - 1
+        } else {  // mixing item w - 8 of slot - 1 (slot 0: no previous slot, nothing to mix)
             if (tid == 0) {
-                unsigned v = kFuseNone;
+                unsigned v = 0u;  // 0: skip this item
                 if (slot > 0) {
                     v = fq_wait(slot_rg + slot - 1, [](unsigned x) { return x != 0u; }, p.status);
                     if (v != kFuseNone &&
@@ -2376,7 +2376,7 @@ __global__ __launch_bounds__(512, 1) void k_gl4f(const GLArgs p, int64_t ntile_r
             if (v == kFuseNone) break;  // slot - 1 had no row group: the stream is done
             const int m = w - 8, tl = m / 12, rem = m % 12;
             const int64_t tile = (int64_t)(v - 1) * 4 + tl;
-            if (tile < ntile_r) {
+            if (v != 0u && tile < ntile_r) {
                 const int bx = (int)(((tile * 6 + (rem >> 1)) << 1) | (rem & 1));  // k_gl4 MODE 2's block index
                 gl4_body<16, 8, 1, 1, false, 0, 2, 0, 0, 0, true>(p, bx, 0, reinterpret_cast<float*>(smem));
             }

@@ -112,7 +112,7 @@ hipError_t make_bf16_weights(const float* W, int ntypes, int N, int K, SplitW* o
 // Multi-head attention over joints (attention.py:122-136) from a (B, J, 3*heads*dh) qkv buffer.
 struct AttnArgs {
     const float* qkv; float* out; int64_t B; int J; int heads; int dh; float scale;
-    int padded = 0;  // SD_OPT_ATTENTION 1: the padded k_attention form at 49 <= J <= 52
+    int tail = 0;  // SD_OPT_ATTENTION 1: k_attention's tail form at 49 <= J <= 52 (default: padded)
 };
 
 // Posterior mean + correlated noise step (nonisotropic.py:196-210 / isotropic.py:85-95).

@@ -272,7 +272,10 @@ hipError_t launch_graph_linear_v1(const GLArgs& a, bool rms, hipStream_t s) {
 // rows, so its key rows j = 48 .. J-1 of S^T and its value rows of O^T leave the MFMAs (12 of 16
 // S tiles, 3 of 4 k tiles of O) for an fmaf chain on the VALU in the MFMA's own k order -- the
 // f32 MFMA sums its k = 4 products as an fmaf chain, and the padded rows added exact zeros -- so
-// the result is the padded form's bit for bit (test_attention_tail_bitwise):
+// the result is the padded form's bit for bit (test_attention_tail_bitwise_vs_padded).  Plan option
+// SD_OPT_ATTENTION 1; not the default: config 3 measured 3,641 vs 3,677 futures/s for the padded form
+// (the kernel is not MFMA-bound at 2 waves / SIMD, and the tail adds ~400 VALU / readlane / shuffle
+// instructions per wave to its critical path):
 //   S^T[48 + r][n] (lane n): sum over d in the (u, e, g) order of the QK MFMAs of
 //     K[48 + r][d] (read from the key fragments with v_readlane) * Q[n][d] scale (the lane's row);
 //   O^T[d][n] += V[48 + r][d] P^T[48 + r][n] after the 12 PV k tiles, r = 0 .. J - 49 in order.
@@ -466,7 +469,7 @@ hipError_t launch_attention(const AttnArgs& a, hipStream_t s) {
         if (a.J <= 16) hipLaunchKernelGGL((k_attention<1, 32>), grid, dim3(256), 0, s, a);
         else if (a.J <= 32) hipLaunchKernelGGL((k_attention<2, 32>), grid, dim3(256), 0, s, a);
         else if (a.J <= 48) hipLaunchKernelGGL((k_attention<3, 32>), grid, dim3(256), 0, s, a);
-        else if (a.J <= 52 && !a.padded) hipLaunchKernelGGL((k_attention<4, 32, true>), grid, dim3(256), 0, s, a);
+        else if (a.J <= 52 && a.tail) hipLaunchKernelGGL((k_attention<4, 32, true>), grid, dim3(256), 0, s, a);
         else hipLaunchKernelGGL((k_attention<4, 32>), grid, dim3(256), 0, s, a);
         return hipGetLastError();
     }

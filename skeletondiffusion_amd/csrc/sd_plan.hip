@@ -85,7 +85,7 @@ struct GraphKey {
     int32_t flags;
     int32_t chains;
     int32_t prec;
-    int32_t variant, gl4_cfg, gl4_stage, split, upd_elem, v5_valu, attn_pad;  // the plan's kernel options at capture time
+    int32_t variant, gl4_cfg, gl4_stage, split, upd_elem, v5_valu, attn_tail;  // the plan's kernel options at capture time
     void* stream;
     bool operator<(const GraphKey& o) const { return std::memcmp(this, &o, sizeof(GraphKey)) < 0; }
 };
@@ -162,7 +162,7 @@ struct sd_plan {
     int variant = 0, gl4_cfg = 0, gl4_stage = 0, split = 0, chains = 0;
     int upd_elem = 0;  // SD_OPT_UPDATE_KERNEL: 1 = the element-per-thread update forms
     int v5_valu = 0;   // SD_OPT_V5_MIX: 1 = the VALU mixing pass of v5
-    int attn_pad = 0;  // SD_OPT_ATTENTION: 1 = the padded k_attention form at 49 <= J <= 52
+    int attn_tail = 0;  // SD_OPT_ATTENTION: 1 = k_attention's tail form at 49 <= J <= 52
     bool fuse_attention_now() const { return fuse_ok && (variant == 0 || variant == 4); }
     bool blocked_now() const { return blk_ok && fuse_attention_now() && prec != 2; }
     std::vector<void*> allocs;
@@ -501,7 +501,7 @@ int run_denoiser(const sd_plan* p, const float* x_t, const float* x_cond, int64_
                 lay(a, 0, 0, 0);
                 SD_LAUNCH(prof, 0, sd::launch_graph_linear(a, true, s));
                 if ((rc = snap(a))) return rc;
-                sd::AttnArgs aa{w.qkv, w.o, rows, p->J, p->d.attn_heads, p->d.attn_dim_head, qscale, p->attn_pad};
+                sd::AttnArgs aa{w.qkv, w.o, rows, p->J, p->d.attn_heads, p->d.attn_dim_head, qscale, p->attn_tail};
                 SD_LAUNCH(prof, 1, sd::launch_attention(aa, s));
             }
             a = gl_args(p, p->outp[l], w.o, 1, nullptr, nullptr, w.x, w.x, rows);
@@ -1202,7 +1202,7 @@ int sd_sample_loop(const sd_plan* p, const float* x_T, const float* x_cond, int6
     key.split = p->split;
     key.upd_elem = p->upd_elem;
     key.v5_valu = p->v5_valu;
-    key.attn_pad = p->attn_pad;
+    key.attn_tail = p->attn_tail;
     key.stream = stream;
     SD_HIP(sd::launch_set_rng(w.rng, seed, row0, s));
     std::shared_ptr<GraphSet> set;
@@ -1444,8 +1444,8 @@ int sd_plan_set_option(sd_plan* p, int32_t option, int64_t value) {
             return SD_OK;
         case SD_OPT_ATTENTION:
             if (value != 0 && value != 1)
-                return fail(SD_E_INVALID, "attention must be 0 (tail form where it applies) or 1 (padded form)");
-            p->attn_pad = (int)value;
+                return fail(SD_E_INVALID, "attention must be 0 (padded form) or 1 (tail form at 49 <= J <= 52)");
+            p->attn_tail = (int)value;
             return SD_OK;
         default: return fail(SD_E_INVALID, "unknown option " + std::to_string(option));
     }
@@ -1464,7 +1464,7 @@ int sd_plan_get_option(const sd_plan* p, int32_t option, int64_t* value) {
         case SD_OPT_LAST_ROUTE: *value = p->last_route.load(); return SD_OK;
         case SD_OPT_UPDATE_KERNEL: *value = p->upd_elem; return SD_OK;
         case SD_OPT_V5_MIX: *value = p->v5_valu; return SD_OK;
-        case SD_OPT_ATTENTION: *value = p->attn_pad; return SD_OK;
+        case SD_OPT_ATTENTION: *value = p->attn_tail; return SD_OK;
         default: return fail(SD_E_INVALID, "unknown option " + std::to_string(option));
     }
 }

@@ -41,7 +41,7 @@ def test_attention_tail_bitwise_vs_padded(cfg, batch, cuda):
     d, x_cond, rows = build_config(cfg, cuda, T=10 if batch < 64 else 3, batch=batch)
     eng = d.engine
     res = {}
-    for v in (1, 0):  # SD_OPT_ATTENTION: 1 the padded form, 0 (default) the tail form
+    for v in (1, 0):  # SD_OPT_ATTENTION: 1 the tail form, 0 (default) the padded form
         eng.set_option("attention", v)
         a = eng.sample_loop(rows, x_cond=x_cond, seed=6, record=(True, False), graph=batch >= 64)
         torch.cuda.synchronize()

@@ -1,14 +1,25 @@
-"""Summarise tools/pmc_gl.sh output: MFMA utilisation, stall split, instruction mix."""
+"""Summarise tools/pmc_gl.sh / tools/pmc_kernel.sh output: MFMA utilisation, stall split,
+instruction mix, LDS bank conflicts.
+usage: python tools/pmc_report.py [--kernel REGEX] [--dir PATTERN] tag [tag ...]
+(defaults: the graph-linear kernels, gpurun_out/pmc_gl_<tag>)"""
+import argparse
 import collections
 import csv
 import glob
-import sys
+import re
 
-for tag in sys.argv[1:]:
+ap = argparse.ArgumentParser()
+ap.add_argument("--kernel", default=r"k_gl|k_graph_linear")
+ap.add_argument("--dir", default="gpurun_out/pmc_gl_{tag}")
+ap.add_argument("tags", nargs="+")
+args = ap.parse_args()
+kpat = re.compile(args.kernel)
+
+for tag in args.tags:
     vals = collections.defaultdict(list)
-    for f in sorted(glob.glob(f"gpurun_out/pmc_gl_{tag}/p*/run_counter_collection.csv")):
+    for f in sorted(glob.glob(args.dir.format(tag=tag) + "/p*/run_counter_collection.csv")):
         for r in csv.DictReader(open(f)):
-            if "k_gl" not in r["Kernel_Name"] and "k_graph_linear" not in r["Kernel_Name"]:
+            if not kpat.search(r["Kernel_Name"]):
                 continue
             vals[r["Counter_Name"]].append(float(r["Counter_Value"]))
     a = {k: sum(v) / len(v) for k, v in vals.items()}
@@ -22,6 +33,10 @@ for tag in sys.argv[1:]:
     print(f"  insts VALU {a.get('SQ_INSTS_VALU', 0):,.0f} LDS {a.get('SQ_INSTS_LDS', 0):,.0f} VMEM "
           f"{a.get('SQ_INSTS_VMEM', 0):,.0f} SALU {a.get('SQ_INSTS_SALU', 0):,.0f}  LDS bank conflicts "
           f"{a.get('SQ_LDS_BANK_CONFLICT', 0):,.0f}  L2 hit {hit * 100:.1f}%")
+    if "SQ_LDS_IDX_ACTIVE" in a or "SQ_INSTS_MFMA" in a:
+        print(f"  LDS array cycles {a.get('SQ_LDS_IDX_ACTIVE', 0):,.0f} (bank-conflict share "
+              f"{a.get('SQ_LDS_BANK_CONFLICT', 0) / max(a.get('SQ_LDS_IDX_ACTIVE', 0), 1) * 100:.1f}%)  LDS-issue stall "
+              f"{a.get('SQ_WAIT_INST_LDS', 0) / w * 100:.1f}% of wave cycles  MFMA insts {a.get('SQ_INSTS_MFMA', 0):,.0f}")
     if "FETCH_SIZE" in a:
         print(f"  HBM/MALL bytes per launch: fetch {2 * a['FETCH_SIZE'] * 1024 / 1e6:.1f} MB (2x FETCH_SIZE, gfx950)"
               f"  write {a.get('WRITE_SIZE', 0) * 1024 / 1e6:.1f} MB")
