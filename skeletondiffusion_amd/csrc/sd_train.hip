@@ -66,6 +66,14 @@ __device__ __forceinline__ float4 keep_or_zero(bool ok, float4 v) {
     return ok ? make_float4(t[0], t[1], t[2], t[3]) : make_float4(0.f, 0.f, 0.f, 0.f);
 }
 
+// LDS column swizzle of the k_gemm operand tiles: column m of k row k is stored at m ^ 4 ((k >> 2) & 7)
+// (bits 2-4 only: 16-B pieces stay whole and aligned, a row's 32-column halves stay put).  The
+// transposed stores of a k-contiguous operand (store_tile4, ak / bk == 1: a thread writes k rows
+// kk .. kk + 3 of one column, lanes 8 apart in kk) hit 8 of the 32 banks at the 68-float row stride
+// -- 4-way conflicts, 33 % of k_gemm's LDS cycles (profiles/r05d/pmc_kgemm.txt); swizzled they hit
+// all 32, and the MFMA reads (32 consecutive columns of one k row) stay conflict-free
+__device__ __forceinline__ int swz(int k, int m) { return m ^ (((k >> 2) & 7) << 2); }
+
 __device__ __forceinline__ void load_tile(const GemmArgs& g, const float* A, const float* B, int m0, int n0, int k0,
                                           int kend, int kval, int tid, TileRegs& r) {
     // unconditional loads from clamped indices (kval: a valid k); the out-of-range values are
@@ -93,10 +101,10 @@ __device__ __forceinline__ void store_tile(const GemmArgs& g, float (*As)[TM + 4
         const int idx = tid + 256 * q;
         int mm, kk;
         if (g.am == 1) { mm = idx & 63; kk = idx >> 6; } else { kk = idx & (TK - 1); mm = idx / TK; }
-        As[kk][mm] = keep_or_zero(m0 + mm < g.M && k0 + kk < kend, r.a[q]);
+        As[kk][swz(kk, mm)] = keep_or_zero(m0 + mm < g.M && k0 + kk < kend, r.a[q]);
         int nn, kb;
         if (g.bn == 1) { nn = idx & 63; kb = idx >> 6; } else { kb = idx & (TK - 1); nn = idx / TK; }
-        Bs[kb][nn] = keep_or_zero(n0 + nn < g.N && k0 + kb < kend, r.b[q]);
+        Bs[kb][swz(kb, nn)] = keep_or_zero(n0 + nn < g.N && k0 + kb < kend, r.b[q]);
     }
 }
 
@@ -134,17 +142,19 @@ __device__ __forceinline__ void store_tile4(const GemmArgs& g, float (*As)[TM + 
         if (g.ak == 1) { kk = 4 * (tid & 7); mm = (tid >> 3) + 32 * q; } else { mm = 4 * (tid & 15); kk = (tid >> 4) + 16 * q; }
         const float4 a = keep_or_zero(m0 + mm < g.M && k0 + kk < kend, r.a[q]);
         if (g.ak == 1) {
-            As[kk][mm] = a.x; As[kk + 1][mm] = a.y; As[kk + 2][mm] = a.z; As[kk + 3][mm] = a.w;
+            As[kk][swz(kk, mm)] = a.x; As[kk + 1][swz(kk + 1, mm)] = a.y;
+            As[kk + 2][swz(kk + 2, mm)] = a.z; As[kk + 3][swz(kk + 3, mm)] = a.w;
         } else {
-            *reinterpret_cast<float4*>(&As[kk][mm]) = a;
+            *reinterpret_cast<float4*>(&As[kk][swz(kk, mm)]) = a;
         }
         int nn, kb;
         if (g.bk == 1) { kb = 4 * (tid & 7); nn = (tid >> 3) + 32 * q; } else { nn = 4 * (tid & 15); kb = (tid >> 4) + 16 * q; }
         const float4 b = keep_or_zero(n0 + nn < g.N && k0 + kb < kend, r.b[q]);
         if (g.bk == 1) {
-            Bs[kb][nn] = b.x; Bs[kb + 1][nn] = b.y; Bs[kb + 2][nn] = b.z; Bs[kb + 3][nn] = b.w;
+            Bs[kb][swz(kb, nn)] = b.x; Bs[kb + 1][swz(kb + 1, nn)] = b.y;
+            Bs[kb + 2][swz(kb + 2, nn)] = b.z; Bs[kb + 3][swz(kb + 3, nn)] = b.w;
         } else {
-            *reinterpret_cast<float4*>(&Bs[kb][nn]) = b;
+            *reinterpret_cast<float4*>(&Bs[kb][swz(kb, nn)]) = b;
         }
     }
 }
@@ -174,8 +184,9 @@ __global__ __launch_bounds__(256) void k_gemm(GemmArgs g) {
         auto mfma_tile = [&](int cur) {
 #pragma unroll
             for (int kk = 0; kk < TK; kk += 2) {
-                const float a = As[cur][kk + (lane >> 5)][wm * 32 + (lane & 31)];
-                const float b = Bs[cur][kk + (lane >> 5)][wn * 32 + (lane & 31)];
+                const int k = kk + (lane >> 5);
+                const float a = As[cur][k][swz(k, wm * 32 + (lane & 31))];
+                const float b = Bs[cur][k][swz(k, wn * 32 + (lane & 31))];
                 acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, acc, 0, 0, 0);
             }
         };
