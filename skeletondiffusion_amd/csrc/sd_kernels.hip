@@ -1087,10 +1087,184 @@ __global__ __launch_bounds__(256) void k_update_mfma(const UpdArgs p) {
     }
 }
 
+// k_update_mfma's arithmetic on a persistent, software-pipelined grid (full batches, f32 latents).
+// k_update_mfma gives every 4-row group its own workgroup; at 3,200 rows all 800 are resident at
+// once and walk load -> Philox -> barrier -> MFMA -> store in lockstep, so the phases, each bound by
+// a different unit, never overlap (26 us alone, the same with given noise, i.e. not the Philox:
+// profiles/r05d/update_probe.txt).  Here a workgroup walks groups g = blockIdx, + gridDim, ... of
+// R rows: group g + gridDim's x0 / x_t fragments are issued before group g's phase A, so the next
+// group's loads stream under this group's Philox, MFMAs and stores; the tables are loaded once per
+// workgroup; sigma . eps is double-buffered in LDS (one barrier per group).  Each row's products,
+// sums and stores are k_update_mfma's: bitwise equal (test_update_mfma_bitwise_vs_elementwise).
+template <int JP, int R, int MT, int NG>
+__global__ __launch_bounds__(256, 2) void k_update_pipe(const UpdArgs p) {
+    constexpr int KS = JP / 4, IB = JP / 16, TSJ = JP + 2;
+    static_assert(JP == 16 && 4 % R == 0, "J <= 16 (NG register sets of B fragments)");
+    const int J = p.J, D = p.D, JD = J * D, QPR = J * (D >> 2);
+    extern __shared__ __attribute__((aligned(16))) float sm[];
+    float* sTab = sm;
+    const int DS = D + 16, EVS = R * J * DS;  // floats per sigma . eps buffer
+    float* sSig = sm + 3 * JP * TSJ;          // sigma_j
+    float* sEv0 = sm + ((3 * JP * TSJ + JP + 3) & ~3);
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int r = wave % R, l16 = lane & 15, l4 = lane >> 4;
+    const int nct = D >> 4, ct0 = wave / R, cstep = 4 / R;
+    const int64_t ngroups = (p.B + R - 1) / R;
+    constexpr int TPT = (3 * JP * JP + 255) / 256;
+    float tv[TPT];
+#pragma unroll
+    for (int k = 0; k < TPT; ++k) {
+        const int q = min(tid + 256 * k, 3 * JP * JP - 1);
+        const int m = q / (JP * JP), ij = q % (JP * JP), i = ij / JP, j = ij % JP;
+        const float* tab = m == 0 ? p.C1 : m == 1 ? p.C2 : p.U;
+        tv[k] = tab[min(i, J - 1) * J + min(j, J - 1)];
+    }
+    float sgv = 1.f;
+    if (tid < J && p.noise_mode != 0) sgv = p.sig[tid];  // before the fragments: its wait leaves them in flight
+    auto load_b = [&](int64_t g, const float* src, float (*dst)[KS]) {
+        const int64_t row = min(g * R + r, p.B - 1);  // clamped: a dead row loads a valid one
+        const float* base = src + row * (int64_t)JD;
+#pragma unroll
+        for (int q = 0; q < MT; ++q)
+#pragma unroll
+            for (int ks = 0; ks < KS; ++ks)
+                dst[q][ks] = base[min(4 * ks + l4, J - 1) * D + 16 * min(ct0 + q * cstep, nct - 1) + l16];
+    };
+    // NG groups per workgroup, g_k = blockIdx + k gridDim; set k holds group k's fragments, issued
+    // one group ahead (straight-line code: no loop-carried register sets for the waitcnt pass)
+    float bx[NG][MT][KS], bt[NG][MT][KS];
+    load_b(blockIdx.x, p.x0, bx[0]);
+    load_b(blockIdx.x, p.xt, bt[0]);
+#pragma unroll
+    for (int k = 0; k < TPT; ++k) {
+        const int q = tid + 256 * k;
+        const int i = (q % (JP * JP)) / JP, j = q % JP;
+        if (q < 3 * JP * JP) sTab[(q / JP) * TSJ + q % JP] = (i < J && j < J) ? tv[k] : 0.f;
+    }
+    if (tid < J) sSig[tid] = sgv;
+    uint64_t seed = p.seed;
+    int64_t row0 = p.row0;
+    if (p.noise_mode == 2 && p.rng_dev) {
+        seed = p.rng_dev[0];
+        row0 = (int64_t)p.rng_dev[1];
+    }
+    row0 += p.row_shift;
+    __syncthreads();  // the tables and sigma
+    float A[3][IB][KS];
+#pragma unroll
+    for (int m = 0; m < 3; ++m)
+#pragma unroll
+        for (int ib = 0; ib < IB; ++ib)
+#pragma unroll
+            for (int ks = 0; ks < KS; ++ks) A[m][ib][ks] = sTab[(m * JP + 16 * ib + l16) * TSJ + 4 * ks + l4];
+    // phase A of group gg into buffer ev (noise mode as a template constant: see k_update_mfma)
+    auto phase_a = [&](auto nm, int64_t gg, float* ev) {
+        constexpr int NM = decltype(nm)::value;
+        // straight-line (J <= 16, D <= 96: at most R * 384 quads): with a runtime trip count the
+        // register allocator split the live in-flight fragments around the loop (vmcnt(0) on entry)
+        constexpr int NQ = (R * JP * 24 + 255) / 256;
+#pragma unroll
+        for (int it = 0; it < NQ; ++it) {
+            const int q = tid + 256 * it;
+            if (q >= R * QPR) continue;
+            const int rr = q / QPR, qq = q - rr * QPR, j = qq / (D >> 2), d = 4 * (qq - j * (D >> 2));
+            const int64_t rw = gg * R + rr;
+            if (rw >= p.B) continue;
+            floatx4 e = {0.f, 0.f, 0.f, 0.f};
+            if constexpr (NM == 1) {
+                e = ld4(p.eps + rw * p.eps_rs + j * D + d);
+            } else if constexpr (NM == 2) {
+                const uint4 x = philox_at(seed, (uint64_t)(row0 + rw), p.step, (uint32_t)qq);
+                const floatx2 z0 = box_muller(x.x, x.y), z1 = box_muller(x.z, x.w);
+                e = floatx4{z0.x, z0.y, z1.x, z1.y};
+            }
+            if (p.noise_out) *reinterpret_cast<floatx4*>(p.noise_out + rw * p.noise_rs + j * D + d) = e;
+            if constexpr (NM != 0) e *= sSig[j];
+            *reinterpret_cast<floatx4*>(ev + (rr * J + j) * DS + d) = e;
+        }
+    };
+#pragma unroll
+    for (int k = 0; k < NG; ++k) {
+        const int64_t gg = blockIdx.x + (int64_t)k * gridDim.x;
+        if (gg >= ngroups) break;  // uniform
+        if (k + 1 < NG && gg + gridDim.x < ngroups) {  // the next group's fragments first
+            load_b(gg + gridDim.x, p.x0, bx[k + 1 < NG ? k + 1 : k]);
+            load_b(gg + gridDim.x, p.xt, bt[k + 1 < NG ? k + 1 : k]);
+        }
+        float* ev = sEv0 + (k & 1) * EVS;  // double-buffered: one barrier per group
+        if (p.noise_mode == 2) phase_a(std::integral_constant<int, 2>{}, gg, ev);
+        else if (p.noise_mode == 1) phase_a(std::integral_constant<int, 1>{}, gg, ev);
+        else phase_a(std::integral_constant<int, 0>{}, gg, ev);
+        __syncthreads();
+        const int64_t row = gg * R + r;
+        if (row >= p.B) continue;  // wave-uniform: the ragged last group (no later group: no later barrier)
+        const int64_t rb = row * (int64_t)JD;
+#pragma unroll
+        for (int q = 0; q < MT; ++q)
+#pragma unroll
+            for (int ks = 0; ks < KS; ++ks) {
+                float a = bx[k][q][ks];
+                if (p.act == 1) a = tanhf(a);
+                bx[k][q][ks] = fminf(fmaxf(a, -1.f), 1.f);
+            }
+        floatx4 vres[MT][IB];
+#pragma unroll
+        for (int q = 0; q < MT; ++q) {
+            const int ct = ct0 + q * cstep;
+            if (ct >= nct) continue;  // wave-uniform
+            const int n = 16 * ct + l16;
+            float bxa[KS], bta[KS], be[KS];
+#pragma unroll
+            for (int ks = 0; ks < KS; ++ks) {
+                const int j = 4 * ks + l4;
+                const bool ok = j < J;
+                bxa[ks] = ok ? bx[k][q][ks] : 0.f;
+                bta[ks] = ok ? bt[k][q][ks] : 0.f;
+                be[ks] = ok ? ev[(r * J + j) * DS + n] : 0.f;
+            }
+#pragma unroll
+            for (int ib = 0; ib < IB; ++ib) {
+                if (16 * ib >= J) continue;
+                floatx4 m1 = {0.f, 0.f, 0.f, 0.f}, m2 = m1, nz = m1;
+#pragma unroll
+                for (int ks = 0; ks < KS; ++ks) {
+                    m1 = __builtin_amdgcn_mfma_f32_16x16x4f32(bxa[ks], A[0][ib][ks], m1, 0, 0, 0);
+                    m2 = __builtin_amdgcn_mfma_f32_16x16x4f32(bta[ks], A[1][ib][ks], m2, 0, 0, 0);
+                    nz = __builtin_amdgcn_mfma_f32_16x16x4f32(be[ks], A[2][ib][ks], nz, 0, 0, 0);
+                }
+                const floatx4 mean = m1 + m2;
+                vres[q][ib] = (p.noise_mode != 0) ? mean + nz : mean;
+                const int i = 16 * ib + l16;
+                if (p.mean_out && i < J)
+                    *reinterpret_cast<floatx4*>(p.mean_out + row * p.mean_rs + i * D + 16 * ct + 4 * l4) = mean;
+            }
+        }
+#pragma unroll
+        for (int q = 0; q < MT; ++q) {
+            const int ct = ct0 + q * cstep;
+            if (ct >= nct) continue;
+            const int n4 = 16 * ct + 4 * l4;
+#pragma unroll
+            for (int ib = 0; ib < IB; ++ib) {
+                const int i = 16 * ib + l16;
+                if (16 * ib >= J || i >= J) continue;
+                *reinterpret_cast<floatx4*>(p.out + rb + i * D + n4) = vres[q][ib];
+                if (p.out2) *reinterpret_cast<floatx4*>(p.out2 + row * p.out2_rs + i * D + n4) = vres[q][ib];
+            }
+        }
+    }
+}
+
 // rows at or below which launch_update runs k_update_row (process default SKELDIFF_UPDATE_ROWS)
 static int64_t g_update_rows = [] {
     const char* e = getenv("SKELDIFF_UPDATE_ROWS");
     return e ? (int64_t)atoll(e) : (int64_t)1024;
+}();
+// SKELDIFF_UPDATE_PIPE=0 at load: full batches on k_update_mfma instead of k_update_pipe (A/B)
+static int g_update_pipe = [] {
+    const char* e = getenv("SKELDIFF_UPDATE_PIPE");
+    return e ? atoi(e) : 1;
 }();
 
 hipError_t launch_update(const UpdArgs& a, hipStream_t s) {
@@ -1111,6 +1285,23 @@ hipError_t launch_update(const UpdArgs& a, hipStream_t s) {
         }
         hipLaunchKernelGGL(kern, dim3((unsigned)a.B), dim3(256), lds, s, a);
         return hipGetLastError();
+    }
+    // full batches of f32 latents: the persistent pipelined form (2-row groups, 2 workgroups per CU)
+    if (g_update_mfma && g_update_pipe && !a.iso && a.J <= 16 && a.D % 16 == 0 && a.D / 16 <= 6 && a.B > g_update_rows &&
+        !a.x0_bf16 && !a.xt_bf16 && !a.out_bf16 && !a.dump_x0 && !a.dump_ev) {
+        constexpr int NG = 3;  // groups per workgroup
+        const int64_t groups = (a.B + 1) / 2;
+        const dim3 grid((unsigned)((groups + NG - 1) / NG));
+        auto go = [&](auto kern, int JP) -> hipError_t {
+            const size_t lds = (((3 * (size_t)JP * (JP + 2) + JP + 3) & ~(size_t)3) + 2 * 2 * (size_t)a.J * (a.D + 16)) * sizeof(float);
+            if (lds > 64 * 1024) {
+                const hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+                if (e != hipSuccess) return e;
+            }
+            hipLaunchKernelGGL(kern, grid, dim3(256), lds, s, a);
+            return hipGetLastError();
+        };
+        return go(k_update_pipe<16, 2, 3, NG>, 16);
     }
     // the instantiations below cover MT column tiles per wave, cstep = 4 / R apart: R = 1 -> MT = 2
     // (tiles w, w + 4: D <= 128), R = 4 -> MT = 6 (tiles 0..5: D <= 96); wider rows take the forms below
