@@ -1089,9 +1089,9 @@ __global__ __launch_bounds__(256) void k_update_mfma(const UpdArgs p) {
 
 // k_update_mfma's arithmetic on a persistent, software-pipelined grid (full batches, f32 latents).
 // k_update_mfma gives every 4-row group its own workgroup; at 3,200 rows all 800 are resident at
-// once and walk load -> Philox -> barrier -> MFMA -> store in lockstep, so the phases, each bound by
-// a different unit, never overlap (26 us alone, the same with given noise, i.e. not the Philox:
-// profiles/r05d/update_probe.txt).  Here a workgroup walks groups g = blockIdx, + gridDim, ... of
+// once and walk load -> Philox -> barrier -> MFMA -> store in lockstep -- the hypothesis this form
+// tested (26 us alone, the same with given noise, i.e. not the Philox: profiles/r05d/update_probe.txt);
+// it measured no faster (plan option SD_OPT_UPDATE_KERNEL 2, not the default).  Here a workgroup walks groups g = blockIdx, + gridDim, ... of
 // R rows: group g + gridDim's x0 / x_t fragments are issued before group g's phase A, so the next
 // group's loads stream under this group's Philox, MFMAs and stores; the tables are loaded once per
 // workgroup; sigma . eps is double-buffered in LDS (one barrier per group).  Each row's products,
@@ -1261,11 +1261,7 @@ static int64_t g_update_rows = [] {
     const char* e = getenv("SKELDIFF_UPDATE_ROWS");
     return e ? (int64_t)atoll(e) : (int64_t)1024;
 }();
-// SKELDIFF_UPDATE_PIPE=0 at load: full batches on k_update_mfma instead of k_update_pipe (A/B)
-static int g_update_pipe = [] {
-    const char* e = getenv("SKELDIFF_UPDATE_PIPE");
-    return e ? atoi(e) : 1;
-}();
+
 
 hipError_t launch_update(const UpdArgs& a, hipStream_t s) {
     if (a.B <= 0) return hipSuccess;
@@ -1287,7 +1283,9 @@ hipError_t launch_update(const UpdArgs& a, hipStream_t s) {
         return hipGetLastError();
     }
     // full batches of f32 latents: the persistent pipelined form (2-row groups, 2 workgroups per CU)
-    if (g_update_mfma && g_update_pipe && !a.iso && a.J <= 16 && a.D % 16 == 0 && a.D / 16 <= 6 && a.B > g_update_rows &&
+    // (plan option SD_OPT_UPDATE_KERNEL 2 only: measured no faster -- 27.7 vs 27.1 us with device noise,
+    // 26.5 vs 25.5 with given noise, alone at 3,200 rows; profiles/r05d/update_probe.txt)
+    if (a.pipe && !a.iso && a.J <= 16 && a.D % 16 == 0 && a.D / 16 <= 6 && a.B > g_update_rows &&
         !a.x0_bf16 && !a.xt_bf16 && !a.out_bf16 && !a.dump_x0 && !a.dump_ev) {
         constexpr int NG = 3;  // groups per workgroup
         const int64_t groups = (a.B + 1) / 2;

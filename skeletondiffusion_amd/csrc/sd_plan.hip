@@ -160,7 +160,7 @@ struct sd_plan {
     int prec = 0;          // sd_plan_set_precision: 0 f32-accurate, 1 half (f16 products)
     // kernel options (sd_plan_set_option), initialised from the process defaults at creation
     int variant = 0, gl4_cfg = 0, gl4_stage = 0, split = 0, chains = 0;
-    int upd_elem = 0;  // SD_OPT_UPDATE_KERNEL: 1 = the element-per-thread update forms
+    int upd_elem = 0;  // SD_OPT_UPDATE_KERNEL: 1 = the element-per-thread update forms, 2 = k_update_pipe
     int v5_valu = 0;   // SD_OPT_V5_MIX: 1 = the VALU mixing pass of v5
     int attn_tail = 0;  // SD_OPT_ATTENTION: 1 = k_attention's tail form at 49 <= J <= 52
     bool fuse_attention_now() const { return fuse_ok && (variant == 0 || variant == 4); }
@@ -579,7 +579,8 @@ int run_update(const sd_plan* p, const float* x0, const float* xt, const float* 
     u.B = rows;
     u.J = p->J;
     u.D = p->D;
-    u.elementwise = p->upd_elem;
+    u.elementwise = p->upd_elem == 1;
+    u.pipe = p->upd_elem == 2;
 #ifdef SD_DEBUG_LDS
     u.dbg = sd::debug_counters();
 #endif
@@ -1434,8 +1435,9 @@ int sd_plan_set_option(sd_plan* p, int32_t option, int64_t value) {
             p->split = (int)value;
             return SD_OK;
         case SD_OPT_UPDATE_KERNEL:
-            if (value != 0 && value != 1)
-                return fail(SD_E_INVALID, "update kernel must be 0 (matrix cores where they apply) or 1 (element-per-thread)");
+            if (value < 0 || value > 2)
+                return fail(SD_E_INVALID, "update kernel must be 0 (matrix cores where they apply), 1 (element-per-thread) "
+                                          "or 2 (the pipelined matrix-core form for full J <= 16 batches)");
             p->upd_elem = (int)value;
             return SD_OK;
         case SD_OPT_V5_MIX:

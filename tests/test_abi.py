@@ -97,7 +97,13 @@ def test_plan_options_validated_on_host():
         assert lib.sd_plan_set_option(h, _lib.SD_OPT_ROW_CHAINS, 8) == 0
         assert lib.sd_plan_set_option(h, _lib.SD_OPT_GL4_STAGING, 3) == -1
         assert lib.sd_plan_set_option(h, 99, 0) == -1
-        for opt in (_lib.SD_OPT_UPDATE_KERNEL, _lib.SD_OPT_V5_MIX, _lib.SD_OPT_ATTENTION):  # 0 / 1 switches
+        assert lib.sd_plan_set_option(h, _lib.SD_OPT_UPDATE_KERNEL, 2) == 0  # the pipelined form
+        assert lib.sd_plan_set_option(h, _lib.SD_OPT_UPDATE_KERNEL, 3) == -1
+        assert lib.sd_plan_set_option(h, _lib.SD_OPT_UPDATE_KERNEL, 0) == 0
+        assert lib.sd_plan_set_option(h, _lib.SD_OPT_UPDATE_KERNEL, 1) == 0
+        assert lib.sd_plan_get_option(h, _lib.SD_OPT_UPDATE_KERNEL, ctypes.byref(v)) == 0 and v.value == 1
+        assert lib.sd_plan_set_option(h, _lib.SD_OPT_UPDATE_KERNEL, 0) == 0
+        for opt in (_lib.SD_OPT_V5_MIX, _lib.SD_OPT_ATTENTION):  # 0 / 1 switches
             assert lib.sd_plan_get_option(h, opt, ctypes.byref(v)) == 0 and v.value == 0
             assert lib.sd_plan_set_option(h, opt, 1) == 0
             assert lib.sd_plan_get_option(h, opt, ctypes.byref(v)) == 0 and v.value == 1
