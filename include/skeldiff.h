@@ -315,7 +315,8 @@ enum {
                                    v_mfma_f32_16x16x4_f32 where they apply (nonisotropic, J <= 64),
                                    1 the element-per-thread forms, 2 the persistent pipelined
                                    matrix-core form for full batches of J <= 16 (A/B: measured no
-                                   faster); all give the same bits */
+                                   faster), 3 that form's arithmetic on 8-B fragment
+                                   loads (A/B); all give the same bits */
     SD_OPT_V5_MIX = 10,         /* J > 21 mixing pass (v5): 0 (default) G-hat mixing on
                                    v_mfma_f32_16x16x4_f32 (k_gl5_mixm), 1 the VALU form (k_gl5_mix);
                                    the same j-ordered fmaf chains */

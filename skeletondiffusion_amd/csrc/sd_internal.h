@@ -132,6 +132,7 @@ struct UpdArgs {
     int x0_bf16, xt_bf16, out_bf16;  // bf16 latents (precision mode 2); out2 / records stay f32
     int elementwise;  // SD_OPT_UPDATE_KERNEL: 0 k_update_mfma where it applies, 1 the element-per-thread forms
     int pipe;         // SD_OPT_UPDATE_KERNEL 2: k_update_pipe for full batches of J <= 16 (A/B)
+    int v2;           // SD_OPT_UPDATE_KERNEL 3: k_update_v2 (8-B fragment loads) for full batches of J <= 16 (A/B)
     // diagnostics only (sd_debug_update_dump): the J values of x0 (activation + clamp applied),
     // x_t and sigma eps each thread computed from, stored after its outputs; null = off
     float* dump_x0; float* dump_xt; float* dump_ev;

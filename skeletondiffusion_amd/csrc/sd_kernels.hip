@@ -1256,6 +1256,161 @@ __global__ __launch_bounds__(256, 2) void k_update_pipe(const UpdArgs p) {
     }
 }
 
+// k_update_mfma (R = 4, J <= 16) with 8-B fragment loads: one wave per row, its 96 columns as three
+// 32-column groups of two "virtual" 16-column tiles.  Lane (l16, l4) loads x[j = 4 ks + l4][32 g +
+// 2 l16 .. + 1] (16 lanes: 128 contiguous bytes, a whole line) and feeds element e of it as the A row
+// l16 of virtual tile (g, e) -- columns 32 g + 2 l16 + e.  The MFMA output row rho = 4 l4 + rr of tile
+// (g, e) is column 32 g + 8 l4 + 2 rr + e, so a lane holds 8 consecutive columns of its node after
+// both tiles: two 16-B stores.  Half the load instructions of k_update_mfma (whose 16 lanes read 64-B
+// half lines) for the same products in the same k order: bitwise equal.  SD_OPT_UPDATE_KERNEL 3.
+template <int JP>
+__global__ __launch_bounds__(256) void k_update_v2(const UpdArgs p) {
+    constexpr int R = 4, KS = JP / 4, TSJ = JP + 2, NG = 3;
+    static_assert(JP == 16, "one 16-node output block");
+    const int J = p.J, D = p.D, JD = J * D, QPR = J * (D >> 2), ng = D >> 5;
+    extern __shared__ __attribute__((aligned(16))) float sm[];
+    float* sTab = sm;
+    const int DS = D + 16;
+    float* sEv = sm + ((3 * JP * TSJ + 3) & ~3);
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int64_t rowg = (int64_t)blockIdx.x * R;
+    const int64_t row = rowg + wave;
+    const bool live = row < p.B;
+    const int64_t rb = (live ? row : 0) * (int64_t)JD;
+    const int l16 = lane & 15, l4 = lane >> 4;
+    constexpr int TPT = (3 * JP * JP + 255) / 256;
+    float tv[TPT];
+#pragma unroll
+    for (int k = 0; k < TPT; ++k) {
+        const int q = min(tid + 256 * k, 3 * JP * JP - 1);
+        const int m = q / (JP * JP), ij = q % (JP * JP), i = ij / JP, j = ij % JP;
+        const float* tab = m == 0 ? p.C1 : m == 1 ? p.C2 : p.U;
+        tv[k] = tab[min(i, J - 1) * J + min(j, J - 1)];
+    }
+    constexpr int SGP = 8;
+    float sgp[SGP];
+    if (p.noise_mode != 0) {
+#pragma unroll
+        for (int it = 0; it < SGP; ++it) sgp[it] = p.sig[min(((tid + 256 * it) % QPR) / (D >> 2), J - 1)];
+    }
+    floatx2 bx[NG][KS], bt[NG][KS];
+#pragma unroll
+    for (int g = 0; g < NG; ++g)
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) {
+            const int64_t o = rb + min(4 * ks + l4, J - 1) * D + 32 * min(g, ng - 1) + 2 * l16;
+            bx[g][ks] = ld2(p.x0 + o);
+            bt[g][ks] = ld2(p.xt + o);
+        }
+#pragma unroll
+    for (int k = 0; k < TPT; ++k) {
+        const int q = tid + 256 * k;
+        const int i = (q % (JP * JP)) / JP, j = q % JP;
+        if (q < 3 * JP * JP) sTab[(q / JP) * TSJ + q % JP] = (i < J && j < J) ? tv[k] : 0.f;
+    }
+    uint64_t seed = p.seed;
+    int64_t row0 = p.row0;
+    if (p.noise_mode == 2 && p.rng_dev) {
+        seed = p.rng_dev[0];
+        row0 = (int64_t)p.rng_dev[1];
+    }
+    row0 += p.row_shift;
+    auto phase_a = [&](auto nm, int q, float sg) {
+        constexpr int NM = decltype(nm)::value;
+        const int rr = q / QPR, qq = q % QPR, j = qq / (D >> 2), d = 4 * (qq % (D >> 2));
+        const int64_t rw = rowg + rr;
+        if (rw >= p.B) return;
+        floatx4 e = {0.f, 0.f, 0.f, 0.f};
+        if constexpr (NM == 1) {
+            e = ld4(p.eps + rw * p.eps_rs + j * D + d);
+        } else if constexpr (NM == 2) {
+            const uint4 x = philox_at(seed, (uint64_t)(row0 + rw), p.step, (uint32_t)qq);
+            const floatx2 z0 = box_muller(x.x, x.y), z1 = box_muller(x.z, x.w);
+            e = floatx4{z0.x, z0.y, z1.x, z1.y};
+        }
+        if (p.noise_out) *reinterpret_cast<floatx4*>(p.noise_out + rw * p.noise_rs + j * D + d) = e;
+        if constexpr (NM != 0) e *= sg;
+        *reinterpret_cast<floatx4*>(sEv + (rr * J + j) * DS + d) = e;
+    };
+    auto run_a = [&](auto nm) {
+#pragma unroll
+        for (int it = 0; it < SGP; ++it)
+            if (tid + 256 * it < R * QPR) phase_a(nm, tid + 256 * it, sgp[it]);
+        for (int q = tid + 256 * SGP; q < R * QPR; q += 256)
+            phase_a(nm, q, decltype(nm)::value != 0 ? p.sig[(q % QPR) / (D >> 2)] : 1.f);
+    };
+    if (p.noise_mode == 2) run_a(std::integral_constant<int, 2>{});
+    else if (p.noise_mode == 1) run_a(std::integral_constant<int, 1>{});
+    else run_a(std::integral_constant<int, 0>{});
+    __syncthreads();
+    if (!live) return;
+    float A[3][KS];
+#pragma unroll
+    for (int m = 0; m < 3; ++m)
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) A[m][ks] = sTab[(m * JP + l16) * TSJ + 4 * ks + l4];
+#pragma unroll
+    for (int g = 0; g < NG; ++g)
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) {
+            floatx2 a = bx[g][ks];
+            if (p.act == 1) {
+                a.x = tanhf(a.x);
+                a.y = tanhf(a.y);
+            }
+            bx[g][ks] = floatx2{fminf(fmaxf(a.x, -1.f), 1.f), fminf(fmaxf(a.y, -1.f), 1.f)};
+        }
+    floatx4 vres[NG][2], mres[NG][2];
+#pragma unroll
+    for (int g = 0; g < NG; ++g) {
+        if (g >= ng) continue;  // wave-uniform
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+            const int n = 32 * g + 2 * l16 + e;
+            float bxa[KS], bta[KS], be[KS];
+#pragma unroll
+            for (int ks = 0; ks < KS; ++ks) {
+                const int j = 4 * ks + l4;
+                const bool ok = j < J;
+                bxa[ks] = ok ? bx[g][ks][e] : 0.f;
+                bta[ks] = ok ? bt[g][ks][e] : 0.f;
+                be[ks] = ok ? sEv[(wave * J + j) * DS + n] : 0.f;
+            }
+            floatx4 m1 = {0.f, 0.f, 0.f, 0.f}, m2 = m1, nz = m1;
+#pragma unroll
+            for (int ks = 0; ks < KS; ++ks) {
+                m1 = __builtin_amdgcn_mfma_f32_16x16x4f32(bxa[ks], A[0][ks], m1, 0, 0, 0);
+                m2 = __builtin_amdgcn_mfma_f32_16x16x4f32(bta[ks], A[1][ks], m2, 0, 0, 0);
+                nz = __builtin_amdgcn_mfma_f32_16x16x4f32(be[ks], A[2][ks], nz, 0, 0, 0);
+            }
+            mres[g][e] = m1 + m2;
+            vres[g][e] = (p.noise_mode != 0) ? mres[g][e] + nz : mres[g][e];
+        }
+    }
+    const int i = l16;
+    if (i >= J) return;
+#pragma unroll
+    for (int g = 0; g < NG; ++g) {
+        if (g >= ng) continue;
+        const int n0 = 32 * g + 8 * l4;
+        const floatx4 v0 = {vres[g][0][0], vres[g][1][0], vres[g][0][1], vres[g][1][1]};
+        const floatx4 v1 = {vres[g][0][2], vres[g][1][2], vres[g][0][3], vres[g][1][3]};
+        *reinterpret_cast<floatx4*>(p.out + rb + i * D + n0) = v0;
+        *reinterpret_cast<floatx4*>(p.out + rb + i * D + n0 + 4) = v1;
+        if (p.out2) {
+            *reinterpret_cast<floatx4*>(p.out2 + row * p.out2_rs + i * D + n0) = v0;
+            *reinterpret_cast<floatx4*>(p.out2 + row * p.out2_rs + i * D + n0 + 4) = v1;
+        }
+        if (p.mean_out) {
+            *reinterpret_cast<floatx4*>(p.mean_out + row * p.mean_rs + i * D + n0) =
+                floatx4{mres[g][0][0], mres[g][1][0], mres[g][0][1], mres[g][1][1]};
+            *reinterpret_cast<floatx4*>(p.mean_out + row * p.mean_rs + i * D + n0 + 4) =
+                floatx4{mres[g][0][2], mres[g][1][2], mres[g][0][3], mres[g][1][3]};
+        }
+    }
+}
+
 // rows at or below which launch_update runs k_update_row (process default SKELDIFF_UPDATE_ROWS)
 static int64_t g_update_rows = [] {
     const char* e = getenv("SKELDIFF_UPDATE_ROWS");
@@ -1280,6 +1435,13 @@ hipError_t launch_update(const UpdArgs& a, hipStream_t s) {
             if (e != hipSuccess) return e;
         }
         hipLaunchKernelGGL(kern, dim3((unsigned)a.B), dim3(256), lds, s, a);
+        return hipGetLastError();
+    }
+    // SD_OPT_UPDATE_KERNEL 3: 8-B fragment loads (A/B), full batches of f32 latents, J <= 16, D 32 .. 96
+    if (a.v2 && !a.iso && a.J <= 16 && a.D % 32 == 0 && a.D <= 96 && a.B > g_update_rows && !a.x0_bf16 && !a.xt_bf16 &&
+        !a.out_bf16 && !a.dump_x0 && !a.dump_ev) {
+        const size_t lds = (((3 * 16 * 18 + 3) & ~(size_t)3) + 4 * (size_t)a.J * (a.D + 16)) * sizeof(float);
+        hipLaunchKernelGGL(k_update_v2<16>, dim3((unsigned)((a.B + 3) / 4)), dim3(256), lds, s, a);
         return hipGetLastError();
     }
     // full batches of f32 latents: the persistent pipelined form (2-row groups, 2 workgroups per CU)

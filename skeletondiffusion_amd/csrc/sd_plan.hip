@@ -581,6 +581,7 @@ int run_update(const sd_plan* p, const float* x0, const float* xt, const float* 
     u.D = p->D;
     u.elementwise = p->upd_elem == 1;
     u.pipe = p->upd_elem == 2;
+    u.v2 = p->upd_elem == 3;
 #ifdef SD_DEBUG_LDS
     u.dbg = sd::debug_counters();
 #endif
@@ -1435,9 +1436,9 @@ int sd_plan_set_option(sd_plan* p, int32_t option, int64_t value) {
             p->split = (int)value;
             return SD_OK;
         case SD_OPT_UPDATE_KERNEL:
-            if (value < 0 || value > 2)
-                return fail(SD_E_INVALID, "update kernel must be 0 (matrix cores where they apply), 1 (element-per-thread) "
-                                          "or 2 (the pipelined matrix-core form for full J <= 16 batches)");
+            if (value < 0 || value > 3)
+                return fail(SD_E_INVALID, "update kernel must be 0 (matrix cores where they apply), 1 (element-per-thread), "
+                                          "2 (the pipelined matrix-core form for full J <= 16 batches) or 3 (its 8-B-load form)");
             p->upd_elem = (int)value;
             return SD_OK;
         case SD_OPT_V5_MIX:

@@ -98,7 +98,8 @@ def test_plan_options_validated_on_host():
         assert lib.sd_plan_set_option(h, _lib.SD_OPT_GL4_STAGING, 3) == -1
         assert lib.sd_plan_set_option(h, 99, 0) == -1
         assert lib.sd_plan_set_option(h, _lib.SD_OPT_UPDATE_KERNEL, 2) == 0  # the pipelined form
-        assert lib.sd_plan_set_option(h, _lib.SD_OPT_UPDATE_KERNEL, 3) == -1
+        assert lib.sd_plan_set_option(h, _lib.SD_OPT_UPDATE_KERNEL, 3) == 0  # its 8-B-load form
+        assert lib.sd_plan_set_option(h, _lib.SD_OPT_UPDATE_KERNEL, 4) == -1
         assert lib.sd_plan_set_option(h, _lib.SD_OPT_UPDATE_KERNEL, 0) == 0
         assert lib.sd_plan_set_option(h, _lib.SD_OPT_UPDATE_KERNEL, 1) == 0
         assert lib.sd_plan_get_option(h, _lib.SD_OPT_UPDATE_KERNEL, ctypes.byref(v)) == 0 and v.value == 1
