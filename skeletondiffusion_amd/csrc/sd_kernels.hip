@@ -862,6 +862,16 @@ __global__ __launch_bounds__(256) void k_update_row(const UpdArgs p) {
 // k_noise_fill) into LDS as sigma_j . eps; one barrier; then the MFMAs and the stores.
 // BF: x0 / x_t may be bf16 (precision mode 2); the f32 form has no bf16 load path at all (a
 // per-operand branch around the loads left the waitcnt pass's merged counts at vmcnt(0))
+#ifdef SD_UPD_STAMPS
+// diagnostic build only (tools/update_stamps.py): per workgroup of the full-batch k_update_mfma form,
+// thread 0's s_memrealtime at entry, after its loads are issued (tables stored), after phase A,
+// after the barrier, after the x0 prepass (its fragments arrived), after the MFMAs, after its stores
+// completed, and its CU id; overwritten by every launch (the last one of a call is read back)
+__device__ unsigned long long g_upd_stamps[4096 * 8];
+#define SD_UPD_STAMP(k, v) do { if (R == 4 && threadIdx.x == 0 && blockIdx.x < 4096) g_upd_stamps[blockIdx.x * 8 + (k)] = (v); } while (0)
+#else
+#define SD_UPD_STAMP(k, v) do { } while (0)
+#endif
 template <int JP, int R, int MT, bool BF = false>
 __global__ __launch_bounds__(256) void k_update_mfma(const UpdArgs p) {
     constexpr int KS = JP / 4, IB = JP / 16;
@@ -869,6 +879,7 @@ __global__ __launch_bounds__(256) void k_update_mfma(const UpdArgs p) {
     // {0, 1}) then hits 32 distinct banks; at a JP stride the 16 rows shared one or two banks (16-way
     // conflicts on every ds_read_b32 of the J <= 64 form, which re-reads its fragments per tile)
     constexpr int TSJ = JP + 2;
+    SD_UPD_STAMP(0, wall_clock64());
     const int J = p.J, D = p.D, JD = J * D, QPR = J * (D >> 2);  // quads per row
     extern __shared__ __attribute__((aligned(16))) float sm[];
     float* sTab = sm;                        // [3][JP][TSJ] zero-padded C1, C2, U
@@ -942,6 +953,7 @@ __global__ __launch_bounds__(256) void k_update_mfma(const UpdArgs p) {
     load_b(p.xt, p.xt_bf16, bt);
     if constexpr (!TFIRST) load_tables();
     store_tables();
+    SD_UPD_STAMP(1, wall_clock64());
     uint64_t seed = p.seed;
     int64_t row0 = p.row0;
     if (p.noise_mode == 2 && p.rng_dev) {
@@ -982,7 +994,9 @@ __global__ __launch_bounds__(256) void k_update_mfma(const UpdArgs p) {
     if (p.noise_mode == 2) run_a(std::integral_constant<int, 2>{});
     else if (p.noise_mode == 1) run_a(std::integral_constant<int, 1>{});
     else run_a(std::integral_constant<int, 0>{});
+    SD_UPD_STAMP(2, wall_clock64());
     __syncthreads();
+    SD_UPD_STAMP(3, wall_clock64());
     if (!live) return;  // wave-uniform; no barrier follows
     // A fragments: lane (l16, l4) holds table[i = 16 ib + l16][j = 4 ks + l4]; JP <= 32: every
     // output block's fragments in registers for the whole row, JP = 64 (J <= 64): one block's at a
@@ -1010,6 +1024,16 @@ __global__ __launch_bounds__(256) void k_update_mfma(const UpdArgs p) {
             if (p.act == 1) a = tanhf(a);
             bx[q][ks] = fminf(fmaxf(a, -1.f), 1.f);
         }
+#ifdef SD_UPD_STAMPS
+    {  // the prepass's values in use: the x0 fragments have arrived
+        float chk = 0.f;
+#pragma unroll
+        for (int q = 0; q < MT; ++q)
+#pragma unroll
+            for (int ks = 0; ks < KS; ++ks) chk += bx[q][ks];
+        SD_UPD_STAMP(4, wall_clock64() + (chk == 12345.f ? 1 : 0));
+    }
+#endif
     if (p.dump_x0) {  // diagnostics (sd_debug_update_dump), apart from the tile loop (wave-uniform)
 #pragma unroll
         for (int q = 0; q < MT; ++q) {
@@ -1064,6 +1088,16 @@ __global__ __launch_bounds__(256) void k_update_mfma(const UpdArgs p) {
                 *reinterpret_cast<floatx4*>(p.mean_out + row * p.mean_rs + i * D + 16 * ct + 4 * l4) = mean;
         }
     }
+#ifdef SD_UPD_STAMPS
+    {
+        float chk = 0.f;
+#pragma unroll
+        for (int q = 0; q < MT; ++q)
+#pragma unroll
+            for (int ib = 0; ib < IB; ++ib) chk += vres[q][ib][0];
+        SD_UPD_STAMP(5, wall_clock64() + (chk == 12345.f ? 1 : 0));
+    }
+#endif
 #pragma unroll
     for (int q = 0; q < MT; ++q) {
         const int ct = ct0 + q * cstep;
@@ -1085,6 +1119,11 @@ __global__ __launch_bounds__(256) void k_update_mfma(const UpdArgs p) {
             }
         }
     }
+#ifdef SD_UPD_STAMPS
+    __builtin_amdgcn_s_waitcnt(0);  // this wave's stores acknowledged
+    SD_UPD_STAMP(6, wall_clock64());
+    SD_UPD_STAMP(7, (unsigned long long)__smid());
+#endif
 }
 
 // k_update_mfma's arithmetic on a persistent, software-pipelined grid (full batches, f32 latents).
@@ -1599,3 +1638,15 @@ hipError_t launch_sigma(const float* logvar, float* sig, int64_t n, hipStream_t 
 }
 
 }  // namespace sd
+
+#ifdef SD_UPD_STAMPS
+extern "C" int sd_debug_update_stamps(unsigned long long* host, int nwg, int reset) {
+    if (reset) {
+        static unsigned long long zeros[4096 * 8] = {};
+        return hipMemcpyToSymbol(HIP_SYMBOL(sd::g_upd_stamps), zeros, sizeof(zeros)) == hipSuccess ? 0 : -3;
+    }
+    if (nwg < 0 || nwg > 4096) return -1;
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(sd::g_upd_stamps), (size_t)nwg * 8 * sizeof(unsigned long long)) ==
+                   hipSuccess ? 0 : -3;
+}
+#endif
