@@ -952,8 +952,6 @@ __global__ __launch_bounds__(256) void k_update_mfma(const UpdArgs p) {
     load_b(p.x0, p.x0_bf16, bx);
     load_b(p.xt, p.xt_bf16, bt);
     if constexpr (!TFIRST) load_tables();
-    store_tables();
-    SD_UPD_STAMP(1, wall_clock64());
     uint64_t seed = p.seed;
     int64_t row0 = p.row0;
     if (p.noise_mode == 2 && p.rng_dev) {
@@ -961,12 +959,31 @@ __global__ __launch_bounds__(256) void k_update_mfma(const UpdArgs p) {
         row0 = (int64_t)p.rng_dev[1];
     }
     row0 += p.row_shift;
+    // device noise: the thread's first EPRE draws into registers BEFORE the table stores.  The table
+    // stores wait for the table loads, and with every workgroup's fragment loads in flight those took
+    // ~4 us (stamps, profiles/r05d/update_stamps.txt) -- the Philox work (~3 us) now runs under that wait
+    // instead of after it.  Same draws, same scaling below: the same bits.
+    constexpr int EPRE = (R * JP * 24 + 255) / 256 < SGP ? (R * JP * 24 + 255) / 256 : SGP;
+    floatx4 epre[EPRE];
+    if (p.noise_mode == 2) {  // wave-uniform
+#pragma unroll
+        for (int it = 0; it < EPRE; ++it) {
+            const int q = min(tid + 256 * it, R * QPR - 1);  // clamped: a spare draw is never used
+            const int rr = q / QPR, qq = q % QPR;
+            const uint4 x = philox_at(seed, (uint64_t)(row0 + rowg + rr), p.step, (uint32_t)qq);
+            const floatx2 z0 = box_muller(x.x, x.y), z1 = box_muller(x.z, x.w);
+            epre[it] = floatx4{z0.x, z0.y, z1.x, z1.y};
+        }
+    }
+    store_tables();
+    SD_UPD_STAMP(1, wall_clock64());
     // phase A: sigma_j eps_j (and the raw eps record) for the workgroup's rows (the first SGP
     // quads' sigma_j prefetched above: loaded in the loop, each was waited out right away).  One
     // loop per noise mode (a wave-uniform branch around whole loops): with the given-noise load and
     // the Philox draw as two arms of one body, the waitcnt pass merged the arms and waited
     // vmcnt(0) -- every x0 / x_t fragment load above -- before the first draw was even scaled
-    auto phase_a = [&](auto nm, int q, float sg) {
+    // it: the item's index among this thread's first SGP items (its draw may be in epre), -1 beyond
+    auto phase_a = [&](auto nm, int q, float sg, int it) {
         constexpr int NM = decltype(nm)::value;
         const int rr = q / QPR, qq = q % QPR, j = qq / (D >> 2), d = 4 * (qq % (D >> 2));
         const int64_t rw = rowg + rr;
@@ -975,9 +992,13 @@ __global__ __launch_bounds__(256) void k_update_mfma(const UpdArgs p) {
         if constexpr (NM == 1) {
             e = ld4(p.eps + rw * p.eps_rs + j * D + d);
         } else if constexpr (NM == 2) {
-            const uint4 x = philox_at(seed, (uint64_t)(row0 + rw), p.step, (uint32_t)qq);
-            const floatx2 z0 = box_muller(x.x, x.y), z1 = box_muller(x.z, x.w);
-            e = floatx4{z0.x, z0.y, z1.x, z1.y};
+            if (it >= 0 && it < EPRE) {  // compile-time after unrolling
+                e = epre[it < EPRE ? it : 0];
+            } else {
+                const uint4 x = philox_at(seed, (uint64_t)(row0 + rw), p.step, (uint32_t)qq);
+                const floatx2 z0 = box_muller(x.x, x.y), z1 = box_muller(x.z, x.w);
+                e = floatx4{z0.x, z0.y, z1.x, z1.y};
+            }
         }
         if (p.noise_out) *reinterpret_cast<floatx4*>(p.noise_out + rw * p.noise_rs + j * D + d) = e;
         if constexpr (NM != 0) e *= sg;
@@ -987,9 +1008,9 @@ __global__ __launch_bounds__(256) void k_update_mfma(const UpdArgs p) {
     auto run_a = [&](auto nm) {
 #pragma unroll
         for (int it = 0; it < SGP; ++it)
-            if (tid + 256 * it < R * QPR) phase_a(nm, tid + 256 * it, sgp[it]);
+            if (tid + 256 * it < R * QPR) phase_a(nm, tid + 256 * it, sgp[it], it);
         for (int q = tid + 256 * SGP; q < R * QPR; q += 256)
-            phase_a(nm, q, decltype(nm)::value != 0 ? p.sig[(q % QPR) / (D >> 2)] : 1.f);
+            phase_a(nm, q, decltype(nm)::value != 0 ? p.sig[(q % QPR) / (D >> 2)] : 1.f, -1);
     };
     if (p.noise_mode == 2) run_a(std::integral_constant<int, 2>{});
     else if (p.noise_mode == 1) run_a(std::integral_constant<int, 1>{});
