@@ -11,6 +11,7 @@ import re
 ap = argparse.ArgumentParser()
 ap.add_argument("--kernel", default=r"k_gl|k_graph_linear")
 ap.add_argument("--dir", default="gpurun_out/pmc_gl_{tag}")
+ap.add_argument("--raw", action="store_true", help="also print every counter's per-dispatch average")
 ap.add_argument("tags", nargs="+")
 args = ap.parse_args()
 kpat = re.compile(args.kernel)
@@ -37,6 +38,10 @@ for tag in args.tags:
         print(f"  LDS array cycles {a.get('SQ_LDS_IDX_ACTIVE', 0):,.0f} (bank-conflict share "
               f"{a.get('SQ_LDS_BANK_CONFLICT', 0) / max(a.get('SQ_LDS_IDX_ACTIVE', 0), 1) * 100:.1f}%)  LDS-issue stall "
               f"{a.get('SQ_WAIT_INST_LDS', 0) / w * 100:.1f}% of wave cycles  MFMA insts {a.get('SQ_INSTS_MFMA', 0):,.0f}")
+    if args.raw:
+        for k in sorted(a):
+            print(f"    {k:32s} {a[k]:16,.0f}  ({a[k] / w * 100:6.1f}% of wave cycles)" if k.startswith("SQ_")
+                  else f"    {k:32s} {a[k]:16,.0f}")
     if "FETCH_SIZE" in a:
         print(f"  HBM/MALL bytes per launch: fetch {2 * a['FETCH_SIZE'] * 1024 / 1e6:.1f} MB (2x FETCH_SIZE, gfx950)"
               f"  write {a.get('WRITE_SIZE', 0) * 1024 / 1e6:.1f} MB")
