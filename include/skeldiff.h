@@ -320,10 +320,13 @@ enum {
     SD_OPT_V5_MIX = 10,         /* J > 21 mixing pass (v5): 0 (default) G-hat mixing on
                                    v_mfma_f32_16x16x4_f32 (k_gl5_mixm), 1 the VALU form (k_gl5_mix);
                                    the same j-ordered fmaf chains */
-    SD_OPT_ATTENTION = 11       /* separate attention kernel at 49 <= J <= 52 (MANO): 0 (default)
-                                   the form padded to 64 nodes, 1 48 nodes on the MFMAs + the last
-                                   J - 48 on an fmaf chain in the MFMA's k order (the same bits;
-                                   measured 1 % slower on config 3) */
+    SD_OPT_ATTENTION = 11       /* separate attention kernel at 49 <= J <= 52 (MANO), all forms
+                                   the same bits: 0 (default) auto = 2; 1 after the mixing pass, 48
+                                   nodes on the MFMAs + the last J - 48 on an fmaf chain in the
+                                   MFMA's k order (1 % slower on config 3); 2 the to_qkv layer's
+                                   G-hat mixing inside the attention kernel, its pre-mix Y in the
+                                   qkv buffer (k_attention_mix, 5 % faster); 3 after the mixing
+                                   pass, padded to 64 nodes */
 };
 int sd_plan_set_option(sd_plan* plan, int32_t option, int64_t value);
 int sd_plan_get_option(const sd_plan* plan, int32_t option, int64_t* value);

@@ -576,6 +576,7 @@ hipError_t launch_graph_linear_v5(const GLArgs& a, bool rms, hipStream_t s) {
         e = hipGetLastError();
     }
     if (e != hipSuccess) return e;
+    if (a.skip_mix) return z == a.out ? hipSuccess : hipErrorNotSupported;  // the pre-mix Y in out
     const int vec = ((uintptr_t)z & 15) == 0 && (a.N & 3) == 0 && (z_rs & 3) == 0;
     g_route_bits |= kRouteV5Mix;
     // the matrix-core mixing pass: 64-column blocks, 16-B z / residual / output pieces

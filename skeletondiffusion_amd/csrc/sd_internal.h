@@ -74,6 +74,9 @@ struct GLArgs {
     // workspace (fq_words(rows) words, zeroed before the first launch of a call; every launch
     // leaves it zeroed), or null = k_gl4f unavailable
     unsigned* fq;
+    // v5 only (J > 21): run the GEMM phase alone and leave the pre-mix Y in `out` (k_attention_mix
+    // mixes the to_qkv layer); hipErrorNotSupported where the route cannot
+    int skip_mix = 0;
 };
 // k_gl4f work-queue block: 8 per-XCD item heads (own 128-B lines), the row-group claim counter,
 // the exit counter, per XCD the row group of each slot, per row group its finished GEMM items
@@ -113,6 +116,9 @@ hipError_t make_bf16_weights(const float* W, int ntypes, int N, int K, SplitW* o
 struct AttnArgs {
     const float* qkv; float* out; int64_t B; int J; int heads; int dh; float scale;
     int tail = 0;  // SD_OPT_ATTENTION 1: k_attention's tail form at 49 <= J <= 52 (default: padded)
+    // SD_OPT_ATTENTION 2: qkv holds the to_qkv layer's PRE-mix Y and the kernel mixes it with this
+    // (J, J) G-hat first (k_attention_mix, 49 <= J <= 52, dh 32); null: qkv is mixed
+    const float* G = nullptr;
 };
 
 // Posterior mean + correlated noise step (nonisotropic.py:196-210 / isotropic.py:85-95).

@@ -223,6 +223,7 @@ hipError_t launch_graph_linear(const GLArgs& a, bool rms, hipStream_t s) {
     // every generation computes a column tile from the whole K extent of its rows: an input that
     // aliases the output would be overwritten by sibling column tiles while still being read
     if (a.B > 0 && (a.x1 == a.out || (a.x2 && a.x2 == a.out))) return hipErrorInvalidValue;
+    if (a.skip_mix) return (v == 0 || v == 5) && a.J > 21 && a.prec != 2 ? launch_graph_linear_v5(a, rms, s) : hipErrorNotSupported;
     if (v == 1) return launch_graph_linear_v1(a, rms, s);
     if (v == 4 || v == 0) {
         const hipError_t e = launch_graph_linear_v4(a, rms, s);
@@ -279,22 +280,35 @@ hipError_t launch_graph_linear_v1(const GLArgs& a, bool rms, hipStream_t s) {
 //   S^T[48 + r][n] (lane n): sum over d in the (u, e, g) order of the QK MFMAs of
 //     K[48 + r][d] (read from the key fragments with v_readlane) * Q[n][d] scale (the lane's row);
 //   O^T[d][n] += V[48 + r][d] P^T[48 + r][n] after the 12 PV k tiles, r = 0 .. J - 49 in order.
-template <int JT, int DH = 0, bool TAIL = false>
-__global__ __launch_bounds__(256) void k_attention(const AttnArgs p) {
+// Where the attention reads q / k / v: the (B, J, 3 hid) qkv rows in HBM (k_attention), or one
+// head's mixed q | k | v in the wave's LDS region (k_attention_mix).  c: a column of the head
+// (0 .. dh - 1), a multiple of 4 for the 16-B forms.
+struct AttnSrcG {
+    const float* qb; const float* kb; const float* vb; int64_t rs;
+    __device__ __forceinline__ floatx4 q4(int j, int c) const { return ld4(qb + j * rs + c); }
+    __device__ __forceinline__ floatx4 k4(int j, int c) const { return ld4(kb + j * rs + c); }
+    __device__ __forceinline__ floatx4 v4(int j, int c) const { return ld4(vb + j * rs + c); }
+    __device__ __forceinline__ float v(int j, int c) const { return vb[j * rs + c]; }
+};
+// k_attention_mix's region: node j's 96 columns (q | k | v, 32 each) as 24 16-B pieces, piece q at
+// q ^ (j & 7) (within its aligned group of 8, so q, k and v stay in their 32-column parts): the
+// 16-B reads of 8 consecutive nodes hit 8 different bank groups at the 384-B row stride
+struct AttnSrcL {
+    const float* s;
+    static __device__ __forceinline__ int at(int j, int c) { return j * 96 + (((c >> 2) ^ (j & 7)) << 2) + (c & 3); }
+    __device__ __forceinline__ floatx4 q4(int j, int c) const { return ld4(s + at(j, c)); }
+    __device__ __forceinline__ floatx4 k4(int j, int c) const { return ld4(s + at(j, 32 + c)); }
+    __device__ __forceinline__ floatx4 v4(int j, int c) const { return ld4(s + at(j, 64 + c)); }
+    __device__ __forceinline__ float v(int j, int c) const { return s[at(j, 64 + c)]; }
+};
+
+// One wave's attention of (row b, head h) from `src` (k_attention's math; every caller the same bits)
+template <int JT, int DH, bool TAIL, class Src>
+__device__ __forceinline__ void attention_body(const AttnArgs& p, const Src& src, int64_t b, int h, int lane) {
     static_assert(!TAIL || (JT == 4 && DH == 32), "the tail form is the MANO J = 49..52 kernel");
     constexpr int JA = TAIL ? JT - 1 : JT;  // node tiles on the MFMAs as keys / values
-    const int lane = threadIdx.x & 63;
     const int lr = lane & 15, lg = lane >> 4;
-    const int64_t pair = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (pair >= p.B * p.heads) return;
-    const int64_t b = pair / p.heads;
-    const int h = (int)(pair % p.heads);
     const int J = p.J, dh = DH ? DH : p.dh, hid = p.heads * dh;
-    const int64_t rs = 3 * (int64_t)hid;
-    const float* base = p.qkv + b * J * rs;
-    const float* qb = base + h * dh;
-    const float* kb = base + hid + h * dh;
-    const float* vb = base + 2 * hid + h * dh;
 
     floatx4 S[JT][JT];
 #pragma unroll
@@ -312,7 +326,7 @@ __global__ __launch_bounds__(256) void k_attention(const AttnArgs p) {
 #pragma unroll
         for (int jt = 0; jt < JA; ++jt)
 #pragma unroll
-            for (int s4 = 0; s4 < 4; ++s4) v[jt][s4] = vb[min(jt * 16 + 4 * lg + s4, J - 1) * rs + dc + lr];
+            for (int s4 = 0; s4 < 4; ++s4) v[jt][s4] = src.v(min(jt * 16 + 4 * lg + s4, J - 1), dc + lr);
     };
     // TAIL: this lane's query row (n = lane, scaled as the B fragments) and the tail value rows
     // V[48 + r][dc + 4 lg .. + 3] for both 16-wide chunks, issued with the fragment loads
@@ -320,11 +334,11 @@ __global__ __launch_bounds__(256) void k_attention(const AttnArgs p) {
     floatx4 qrow[QW], vt[TAIL ? 2 : 1][TAIL ? 4 : 1];
     if constexpr (TAIL) {
 #pragma unroll
-        for (int c = 0; c < 8; ++c) qrow[c] = ld4(qb + min(lane, J - 1) * rs + 4 * c);
+        for (int c = 0; c < 8; ++c) qrow[c] = src.q4(min(lane, J - 1), 4 * c);
 #pragma unroll
         for (int u = 0; u < 2; ++u)
 #pragma unroll
-            for (int r = 0; r < 4; ++r) vt[u][r] = ld4(vb + min(48 + r, J - 1) * rs + 16 * u + 4 * lg);
+            for (int r = 0; r < 4; ++r) vt[u][r] = src.v4(min(48 + r, J - 1), 16 * u + 4 * lg);
     }
     float tl[4] = {0.f, 0.f, 0.f, 0.f};  // TAIL: S^T[48 + r][n = lane]
     auto mask_v = [&](floatx4* v) {
@@ -341,8 +355,8 @@ __global__ __launch_bounds__(256) void k_attention(const AttnArgs p) {
 #pragma unroll
             for (int t = 0; t < JT; ++t) {
                 const int jc = min(t * 16 + lr, J - 1);
-                ka[u][t] = ld4(kb + jc * rs + cc0 + 16 * u + 4 * lg);
-                qv[u][t] = ld4(qb + jc * rs + cc0 + 16 * u + 4 * lg);
+                ka[u][t] = src.k4(jc, cc0 + 16 * u + 4 * lg);
+                qv[u][t] = src.q4(jc, cc0 + 16 * u + 4 * lg);
             }
         if constexpr (DH != 0) {
 #pragma unroll
@@ -460,11 +474,113 @@ __global__ __launch_bounds__(256) void k_attention(const AttnArgs p) {
     }
 }
 
+
+template <int JT, int DH = 0, bool TAIL = false>
+__global__ __launch_bounds__(256) void k_attention(const AttnArgs p) {
+    const int lane = threadIdx.x & 63;
+    const int64_t pair = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (pair >= p.B * p.heads) return;
+    const int64_t b = pair / p.heads;
+    const int h = (int)(pair % p.heads);
+    const int J = p.J, dh = DH ? DH : p.dh, hid = p.heads * dh;
+    const int64_t rs = 3 * (int64_t)hid;
+    const float* base = p.qkv + b * J * rs;
+    const AttnSrcG src{base + h * dh, base + hid + h * dh, base + 2 * hid + h * dh, rs};
+    attention_body<JT, DH, TAIL>(p, src, b, h, lane);
+}
+
+// k_attention_mix (SD_OPT_ATTENTION 2; 49 <= J <= 52, dh = 32: MANO): the to_qkv layer's node mixing
+// (its k_gl5_mixd pass) moved into the attention kernel, so the mixed q / k / v never reach HBM --
+// the plan's to_qkv launch writes only its pre-mix Y (GLArgs::skip_mix).  Per wave (row b, head h):
+//   1. the head's pre-mix Y (J nodes x 96 columns q | k | v) to the wave's LDS region (AttnSrcL),
+//      rows J .. 51 zero (k_gl5_mixd's padding rows);
+//   2. out[i][c] = sum_j G-hat[i][j] Y[j][c] on v_mfma_f32_16x16x4_f32 with k_gl5_mixd's operands
+//      (A = Y^T: 16 columns x 4 nodes, B = G-hat^T fragments, k steps in j order from a zero
+//      accumulator, + 0.f as its epilogue adds the absent residual): the same bits;
+//   3. the results to the region (all of this wave's Y reads are behind them: the region is the
+//      wave's own, no barrier), then k_attention's padded-form body reads q / k / v from it.
+// 4 waves x 52 x 96 floats = 78 KiB per workgroup: 2 workgroups per CU.
+constexpr int kAttnMixRows = 52;  // 4 ceil(J / 4) at J <= 52
+template <int DH>
+__global__ __launch_bounds__(256, 2) void k_attention_mix(const AttnArgs p) {
+    static_assert(DH == 32, "the MANO head width");
+    constexpr int KS = kAttnMixRows / 4, NPC = (kAttnMixRows * 24 + 63) / 64;
+    __shared__ __attribute__((aligned(16))) float s_y[4][kAttnMixRows * 96];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int l16 = lane & 15, l4 = lane >> 4;
+    const int64_t pair = (int64_t)blockIdx.x * 4 + wv;
+    if (pair >= p.B * p.heads) return;
+    const int64_t b = pair / p.heads;
+    const int h = (int)(pair % p.heads);
+    const int J = p.J, hid = p.heads * DH;
+    const int64_t rs = 3 * (int64_t)hid;
+    float* sy = s_y[wv];
+    // 1. piece idx = 24 j + q of the region: node j, part q / 8 (q, k, v), columns 4 (q % 8) ..;
+    // unconditional loads from clamped nodes, the padding rows zeroed at the LDS store
+    const float* yb = p.qkv + b * J * rs + h * DH;
+    floatx4 yv[NPC];
+#pragma unroll
+    for (int e = 0; e < NPC; ++e) {
+        const int idx = min(lane + 64 * e, kAttnMixRows * 24 - 1), j = idx / 24, q = idx % 24;
+        yv[e] = ld4(yb + min(j, J - 1) * rs + (q >> 3) * hid + 4 * (q & 7));
+    }
+    float gb[4][KS];  // G-hat[16 ib + l16][4 s + l4] (k_gl5_mixd's B fragments), 0 outside J x J
+#pragma unroll
+    for (int ib = 0; ib < 4; ++ib)
+#pragma unroll
+        for (int s = 0; s < KS; ++s) gb[ib][s] = p.G[min(16 * ib + l16, J - 1) * J + min(4 * s + l4, J - 1)];
+#pragma unroll
+    for (int e = 0; e < NPC; ++e) {
+        const int idx = lane + 64 * e, j = idx / 24, q = idx % 24;
+        if (idx < kAttnMixRows * 24)
+            *reinterpret_cast<floatx4*>(sy + AttnSrcL::at(j, 4 * q)) = j < J ? yv[e] : floatx4{0.f, 0.f, 0.f, 0.f};
+    }
+    // the clamped G-hat loads zeroed outside J x J once they have landed (a select right behind
+    // each load -- or a masked load -- waited for it there)
+#pragma unroll
+    for (int ib = 0; ib < 4; ++ib)
+#pragma unroll
+        for (int s = 0; s < KS; ++s) {
+            float g = gb[ib][s];
+            asm volatile("" : "+v"(g));
+            gb[ib][s] = (16 * ib + l16 < J && 4 * s + l4 < J) ? g : 0.f;
+        }
+    // 2. the mixing, 6 column blocks of 16 x 4 node blocks; per accumulator k_gl5_mixd's chain
+    floatx4 mo[6][4];
+#pragma unroll
+    for (int cb = 0; cb < 6; ++cb) {
+#pragma unroll
+        for (int ib = 0; ib < 4; ++ib) mo[cb][ib] = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int s = 0; s < KS; ++s) {
+            const float a = sy[AttnSrcL::at(4 * s + l4, 16 * cb + l16)];
+#pragma unroll
+            for (int ib = 0; ib < 4; ++ib) mo[cb][ib] = mfma4(a, gb[ib][s], mo[cb][ib]);
+        }
+    }
+    // 3. lane (l16, l4) holds out[i = 16 ib + l16][16 cb + 4 l4 + r]
+#pragma unroll
+    for (int ib = 0; ib < 4; ++ib) {
+        const int i = 16 * ib + l16;
+        if (i < J) {
+#pragma unroll
+            for (int cb = 0; cb < 6; ++cb)
+                *reinterpret_cast<floatx4*>(sy + AttnSrcL::at(i, 16 * cb + 4 * l4)) = mo[cb][ib] + 0.f;
+        }
+    }
+    attention_body<4, DH, false>(p, AttnSrcL{sy}, b, h, lane);
+}
+
 hipError_t launch_attention(const AttnArgs& a, hipStream_t s) {
     if (a.B <= 0) return hipSuccess;
     const int64_t waves = a.B * a.heads;
     const dim3 grid((unsigned)((waves + 3) / 4));
     g_route_bits |= kRouteAttention;
+    if (a.G) {  // the to_qkv mixing in this kernel (k_attention_mix)
+        if (a.dh != 32 || a.J < 49 || a.J > kAttnMixRows) return hipErrorNotSupported;
+        hipLaunchKernelGGL((k_attention_mix<32>), grid, dim3(256), 0, s, a);
+        return hipGetLastError();
+    }
     if (a.dh == 32) {  // the release head width: every load of a wave issued up front
         if (a.J <= 16) hipLaunchKernelGGL((k_attention<1, 32>), grid, dim3(256), 0, s, a);
         else if (a.J <= 32) hipLaunchKernelGGL((k_attention<2, 32>), grid, dim3(256), 0, s, a);

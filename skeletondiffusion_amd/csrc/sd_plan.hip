@@ -162,8 +162,12 @@ struct sd_plan {
     int variant = 0, gl4_cfg = 0, gl4_stage = 0, split = 0, chains = 0;
     int upd_elem = 0;  // SD_OPT_UPDATE_KERNEL: 1 = the element-per-thread update forms, 2 = k_update_pipe
     int v5_valu = 0;   // SD_OPT_V5_MIX: 1 = the VALU mixing pass of v5
-    int attn_tail = 0;  // SD_OPT_ATTENTION: 1 = k_attention's tail form at 49 <= J <= 52
+    int attn_tail = 0;  // SD_OPT_ATTENTION: 0 auto (= 2 where it applies), 1 tail form, 2 k_attention_mix, 3 padded
     bool fuse_attention_now() const { return fuse_ok && (variant == 0 || variant == 4); }
+    // SD_OPT_ATTENTION 2 where it applies: the v5 route's to_qkv mixing inside the attention kernel
+    bool attn_mix_now() const {
+        return (attn_tail == 0 || attn_tail == 2) && J >= 49 && J <= 52 && d.attn_dim_head == 32 && (variant == 0 || variant == 5) && prec != 2;
+    }
     bool blocked_now() const { return blk_ok && fuse_attention_now() && prec != 2; }
     std::vector<void*> allocs;
 
@@ -499,9 +503,20 @@ int run_denoiser(const sd_plan* p, const float* x_t, const float* x_cond, int64_
                 if (B) return fail(SD_E_INTERNAL, "row-blocked plan without the fused attention kernel");
                 a = gl_args(p, p->qkv[l], w.x, 1, nullptr, nullptr, nullptr, w.qkv, rows);
                 lay(a, 0, 0, 0);
-                SD_LAUNCH(prof, 0, sd::launch_graph_linear(a, true, s));
+                // SD_OPT_ATTENTION 2: the GEMM phase alone, k_attention_mix mixes (else, or where
+                // the route cannot leave the pre-mix Y in qkv, the whole layer)
+                a.skip_mix = p->attn_mix_now() ? 1 : 0;
+                if (prof && prof->pre(0, s)) return fail(SD_E_HIP, "hipEventRecord failed");
+                hipError_t ge = sd::launch_graph_linear(a, true, s);
+                if (ge == hipErrorNotSupported && a.skip_mix) {
+                    a.skip_mix = 0;
+                    ge = sd::launch_graph_linear(a, true, s);
+                }
+                SD_HIP(ge);
+                if (prof && prof->post(s)) return fail(SD_E_HIP, "hipEventRecord failed");
                 if ((rc = snap(a))) return rc;
-                sd::AttnArgs aa{w.qkv, w.o, rows, p->J, p->d.attn_heads, p->d.attn_dim_head, qscale, p->attn_tail};
+                sd::AttnArgs aa{w.qkv, w.o, rows, p->J, p->d.attn_heads, p->d.attn_dim_head, qscale, p->attn_tail == 1 ? 1 : 0,
+                                a.skip_mix ? a.G : nullptr};
                 SD_LAUNCH(prof, 1, sd::launch_attention(aa, s));
             }
             a = gl_args(p, p->outp[l], w.o, 1, nullptr, nullptr, w.x, w.x, rows);
@@ -1446,8 +1461,10 @@ int sd_plan_set_option(sd_plan* p, int32_t option, int64_t value) {
             p->v5_valu = (int)value;
             return SD_OK;
         case SD_OPT_ATTENTION:
-            if (value != 0 && value != 1)
-                return fail(SD_E_INVALID, "attention must be 0 (padded form) or 1 (tail form at 49 <= J <= 52)");
+            if (value < 0 || value > 3)
+                return fail(SD_E_INVALID, "attention must be 0 (auto: 2 where it applies), 1 (tail form at 49 <= J <= 52), "
+                                          "2 (to_qkv mixing inside the attention kernel at 49 <= J <= 52) or 3 (padded form "
+                                          "after the separate mixing pass)");
             p->attn_tail = (int)value;
             return SD_OK;
         default: return fail(SD_E_INVALID, "unknown option " + std::to_string(option));

@@ -131,7 +131,8 @@ class SamplingEngine:
         """Per-plan kernel option (sd_plan_set_option): "kernel_variant" (0 auto, 1..5),
         "gl4_tile" (<waves><row tiles><col tiles>, 0 auto), "row_chains" (1..8), "gl4_staging"
         (0 LDS-DMA, 1 register-staged), "split_route" (0 auto, 1 never, 2 k_gl4y, 3 k_gl4t),
-        "update_kernel" (0 matrix cores, 1 element-per-thread, 2 pipelined), "attention" (0 padded, 1 tail form), "v5_mix" (0 matrix cores, 1 VALU);
+        "update_kernel" (0 matrix cores, 1 element-per-thread, 2 pipelined), "attention" (0 auto,
+        1 tail form, 2 to_qkv mixing in the attention kernel, 3 padded), "v5_mix" (0 matrix cores, 1 VALU);
         get_option("last_chains") reads the row chains the last sample_loop ran.  Kept across plan rebuilds;
         other engines (plans) in the process are unaffected."""
         if name not in self.OPTIONS or name in self.READ_ONLY:

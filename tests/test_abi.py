@@ -104,11 +104,12 @@ def test_plan_options_validated_on_host():
         assert lib.sd_plan_set_option(h, _lib.SD_OPT_UPDATE_KERNEL, 1) == 0
         assert lib.sd_plan_get_option(h, _lib.SD_OPT_UPDATE_KERNEL, ctypes.byref(v)) == 0 and v.value == 1
         assert lib.sd_plan_set_option(h, _lib.SD_OPT_UPDATE_KERNEL, 0) == 0
-        for opt in (_lib.SD_OPT_V5_MIX, _lib.SD_OPT_ATTENTION):  # 0 / 1 switches
+        for opt, top in ((_lib.SD_OPT_V5_MIX, 1), (_lib.SD_OPT_ATTENTION, 3)):  # 0 .. top
             assert lib.sd_plan_get_option(h, opt, ctypes.byref(v)) == 0 and v.value == 0
-            assert lib.sd_plan_set_option(h, opt, 1) == 0
-            assert lib.sd_plan_get_option(h, opt, ctypes.byref(v)) == 0 and v.value == 1
-            assert lib.sd_plan_set_option(h, opt, 2) == -1 and lib.sd_plan_set_option(h, opt, 0) == 0
+            for x in range(1, top + 1):
+                assert lib.sd_plan_set_option(h, opt, x) == 0
+                assert lib.sd_plan_get_option(h, opt, ctypes.byref(v)) == 0 and v.value == x
+            assert lib.sd_plan_set_option(h, opt, top + 1) == -1 and lib.sd_plan_set_option(h, opt, 0) == 0
         # SD_OPT_LAST_CHAINS: read-only, 0 before the plan's first sampling call
         assert lib.sd_plan_get_option(h, _lib.SD_OPT_LAST_CHAINS, ctypes.byref(v)) == 0 and v.value == 0
         assert lib.sd_plan_set_option(h, _lib.SD_OPT_LAST_CHAINS, 1) == -1

@@ -34,21 +34,24 @@ def test_v5_mix_mfma_bitwise_vs_valu(cfg, batch, cuda):
 def test_attention_tail_bitwise_vs_padded(cfg, batch, cuda):
     """k_attention at J = 51 / 52 (sd_kernels.hip, TAIL form): 48 nodes on the MFMAs and the last
     J - 48 on fmaf chains in the MFMA's own k order, against the form padded to 64 nodes, over
-    whole sampling chains (reference op: attention.py:122-136) -- bitwise; 64 sequences = the
-    config-3 batch (3,200 rows, three row chains, hipGraph) as benched."""
+    whole sampling chains (reference op: attention.py:122-136) -- bitwise; and k_attention_mix
+    (option 2: the to_qkv layer's G-hat mixing inside the attention kernel, the pre-mix Y in the
+    qkv buffer, graph_structural.py:30-43) -- bitwise too.  64 sequences = the config-3 batch
+    (3,200 rows, three row chains, hipGraph) as benched."""
     from bench import build_config
 
     d, x_cond, rows = build_config(cfg, cuda, T=10 if batch < 64 else 3, batch=batch)
     eng = d.engine
     res = {}
-    for v in (1, 0):  # SD_OPT_ATTENTION: 1 the tail form, 0 (default) the padded form
+    for v in (1, 2, 3, 0):  # SD_OPT_ATTENTION: 1 tail, 2 mixing in the kernel, 3 padded, 0 auto (2)
         eng.set_option("attention", v)
         a = eng.sample_loop(rows, x_cond=x_cond, seed=6, record=(True, False), graph=batch >= 64)
         torch.cuda.synchronize()
         res[v] = [t.clone() for t in (a[0], a[3])]  # img, mean_t
     assert eng.get_option("last_route") & 128, "the separate k_attention did not run"
-    for name, x, y in zip(("img", "mean_t"), res[0], res[1]):
-        assert torch.equal(x, y), (name, float((x - y).abs().max()))
+    for v in (1, 2, 3):
+        for name, x, y in zip(("img", "mean_t"), res[0], res[v]):
+            assert torch.equal(x, y), (v, name, float((x - y).abs().max()))
     assert eng.get_option("attention") == 0
     with pytest.raises(_lib.SkelDiffError):
-        eng.set_option("attention", 2)
+        eng.set_option("attention", 4)
