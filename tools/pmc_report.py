@@ -24,7 +24,7 @@ for tag in args.tags:
                 continue
             vals[r["Counter_Name"]].append(float(r["Counter_Value"]))
     a = {k: sum(v) / len(v) for k, v in vals.items()}
-    w = a.get("SQ_WAVE_CYCLES", 1)
+    w = a.get("SQ_WAVE_CYCLES", float("nan"))  # percentages of wave cycles: nan without that counter
     gui = a.get("GRBM_GUI_ACTIVE", 8) / 8          # summed over the 8 XCDs
     print(f"===== {tag}: kernel {gui / 2.4e3:.1f} us (at 2.4 GHz)  MFMA util "
           f"{a.get('SQ_VALU_MFMA_BUSY_CYCLES', 0) / (gui * 1024) * 100:.1f}%  waves/SIMD {w * 4 / (gui * 1024):.2f}")
