@@ -365,15 +365,20 @@ def main():
     route = ("tiled split (k_gl4t + k_gl4 MODE 2/3)" if tiled and not route_bits & (1 | 2) else
              "tiled split + one-kernel fused attention" if tiled else
              "small-batch split (k_gl4y + k_gl4 MODE 2/3)" if small else
-             "v5 (k_gl4t + k_gl5_mixm + k_attention)" if route_bits & 32 and split else
+             "v5 (k_gl4t + k_gl5_mixd + k_attention_mix)" if route_bits & 32 and route_bits & 1024 and split else
+             "v5 (k_gl4t + k_gl5_mixd + k_attention)" if route_bits & 32 and split else
              "one-kernel (k_gl4)" if split else "exact f32")
     half = split and eng.precision in ("half", "bf16")
-    fused_attn = ms[1] == 0.0 and cnt[1] == 0   # attention ran inside the graph-linear launches
+    # the to_qkv layer's mixing inside the attention launch (k_attention_mix): to_qkv + attention
+    # count as one fused layer (its bytes, FLOPs and both launches' time), as on the fused routes
+    attn_mix = bool(route_bits & 1024)
+    fused_attn = (ms[1] == 0.0 and cnt[1] == 0) or attn_mix  # attention inside the layer's launches
+    gl_ms = ms[0] + (ms[1] if attn_mix else 0.0)
     gl_flops = fl[0] + (fl[1] if fused_attn else 0.0)
-    gl_tflops = gl_flops / (ms[0] * 1e-3) / 1e12
+    gl_tflops = gl_flops / (gl_ms * 1e-3) / 1e12
     peak = F16_MFMA_PEAK_TFLOPS if half else F16_MFMA_PEAK_TFLOPS / 3.0 if split else FP32_PEAK_TFLOPS
     gl_bytes = graph_linear_bytes(d, rows, fused_attn)
-    gl_gbs = gl_bytes / (ms[0] * 1e-3) / 1e9
+    gl_gbs = gl_bytes / (gl_ms * 1e-3) / 1e9
     launches = max(cnt[0], 1)
     upd_bytes = 3.0 * rows * J * D * 4        # x0, x_t in, x_{t-1} out (device Philox noise)
     upd_gbs = upd_bytes / (ms[2] * 1e-3) / 1e9
@@ -431,7 +436,7 @@ def main():
                       "attention fused); per-launch average over the layers of one denoise step",
             "achieved": gl_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": gl_gbs / HBM_PEAK_GBS,
             "traffic": traffic, "traffic_source": traffic_note,
-            "algorithmic_bytes_per_launch": gl_bytes / launches, "avg_launch_ms": ms[0] / launches,
+            "algorithmic_bytes_per_launch": gl_bytes / launches, "avg_launch_ms": gl_ms / launches,
             "launches_per_denoise_step": cnt[0],
             "measured_on": ("HIP events on the launch stream around each layer, one denoise step at the full "
                             "batch on one stream (sd_profile_step, kernels alone on the GPU), "

@@ -97,7 +97,8 @@ enum RouteBits : unsigned {
     kRouteExact = 64,      // exact-f32 generations v1-v3
     kRouteAttention = 128,  // k_attention: the separate attention kernel (J > 21, unfused routes)
     kRouteFusedSmall = 256,  // k_gl4 MODE 4: small-batch fused graph-linear tile
-    kRouteFusedLayer = 512   // k_gl4f: GEMM + mixing phase of a plain layer in one launch
+    kRouteFusedLayer = 512,  // k_gl4f: GEMM + mixing phase of a plain layer in one launch
+    kRouteAttnMix = 1024     // k_attention_mix: the to_qkv layer's mixing inside the attention kernel
 };
 extern thread_local unsigned g_route_bits;
 

@@ -578,6 +578,7 @@ hipError_t launch_attention(const AttnArgs& a, hipStream_t s) {
     g_route_bits |= kRouteAttention;
     if (a.G) {  // the to_qkv mixing in this kernel (k_attention_mix)
         if (a.dh != 32 || a.J < 49 || a.J > kAttnMixRows) return hipErrorNotSupported;
+        g_route_bits |= kRouteAttnMix;
         hipLaunchKernelGGL((k_attention_mix<32>), grid, dim3(256), 0, s, a);
         return hipGetLastError();
     }

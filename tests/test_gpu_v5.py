@@ -48,6 +48,7 @@ def test_attention_tail_bitwise_vs_padded(cfg, batch, cuda):
         a = eng.sample_loop(rows, x_cond=x_cond, seed=6, record=(True, False), graph=batch >= 64)
         torch.cuda.synchronize()
         res[v] = [t.clone() for t in (a[0], a[3])]  # img, mean_t
+        assert bool(eng.get_option("last_route") & 1024) == (v in (0, 2)), (v, "k_attention_mix")
     assert eng.get_option("last_route") & 128, "the separate k_attention did not run"
     for v in (1, 2, 3):
         for name, x, y in zip(("img", "mean_t"), res[0], res[v]):
