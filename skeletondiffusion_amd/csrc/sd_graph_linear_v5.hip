@@ -514,6 +514,10 @@ static const int g_mix_mfma = [] {
     // 3 (default): k_gl5_mixd (LDS-DMA ring); 1: k_gl5_mixm; 2: its two-deep register ring (A/B)
     return e ? std::min(std::max(atoi(e), 0), 3) : 3;
 }();
+static const int g_mixd_cfg = [] {
+    const char* e = getenv("SKELDIFF_V5_MIXD");
+    return e ? atoi(e) : 0;
+}();
 // rows per k_gl5_mixm workgroup (SKELDIFF_V5_ROWS at load: 4, 8 or 16)
 static int g_mix_rows = [] {
     const char* e = getenv("SKELDIFF_V5_ROWS");
@@ -583,18 +587,24 @@ hipError_t launch_graph_linear_v5(const GLArgs& a, bool rms, hipStream_t s) {
     const bool mfma = g_mix_mfma && !a.v5_valu && vec && a.N % 64 == 0 && ((uintptr_t)a.out & 15) == 0 && (a.out_rs & 3) == 0 &&
                       (!a.res || (((uintptr_t)a.res & 15) == 0 && (a.res_rs & 3) == 0)) && a.B / 8 < 0x7fffffff;
     if (mfma && g_mix_mfma == 3 && (int64_t)a.B * a.out_rs * 4 < 0x7fffffff && (!a.res || a.res_rs % 4 == 0)) {
-        // the LDS-DMA form: slabs of 4 ceil(J / 4) rows, 3 slots (rows r, r + 1, r + 2 in flight)
-        constexpr int R = 8, PF = 2;
+        // the LDS-DMA form: slabs of 4 ceil(J / 4) rows, 2 slots (row r + 1 in flight while row r is
+        // mixed): 53 KiB of LDS at J = 51 with the residual, 3 workgroups per CU -- config 3 4,193 /
+        // 4,195 vs 4,070 / 4,068 futures/s for 3 slots (2 workgroups per CU), profiles/r05k/ab_mixd.txt.
+        // SKELDIFF_V5_MIXD (A/B at load): 1 = 4 rows per workgroup with 3 slots, 3 = 3 slots
         const int KS = (a.J + 3) / 4;
-        const size_t lds = (size_t)(PF + 1) * (a.res ? 2 : 1) * 4 * KS * 64 * sizeof(float);
-        auto kt = a.res ? k_gl5_mixd<R, PF, true> : k_gl5_mixd<R, PF, false>;
-        if (lds > 64 * 1024) {
-            const hipError_t e = hipFuncSetAttribute((const void*)kt, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-            if (e != hipSuccess) return e;
-        }
-        hipLaunchKernelGGL(kt, dim3((unsigned)((a.B + R - 1) / R), (unsigned)(a.N / 64)), dim3(256), lds, s, a,
-                           (const float*)z, z_rs);
-        return hipGetLastError();
+        auto launch = [&](auto kt, int R, int PF) -> hipError_t {
+            const size_t lds = (size_t)(PF + 1) * (a.res ? 2 : 1) * 4 * KS * 64 * sizeof(float);
+            if (lds > 64 * 1024) {
+                const hipError_t e = hipFuncSetAttribute((const void*)kt, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+                if (e != hipSuccess) return e;
+            }
+            hipLaunchKernelGGL(kt, dim3((unsigned)((a.B + R - 1) / R), (unsigned)(a.N / 64)), dim3(256), lds, s, a,
+                               (const float*)z, z_rs);
+            return hipGetLastError();
+        };
+        if (g_mixd_cfg == 1) return a.res ? launch(k_gl5_mixd<4, 2, true>, 4, 2) : launch(k_gl5_mixd<4, 2, false>, 4, 2);
+        if (g_mixd_cfg == 3) return a.res ? launch(k_gl5_mixd<8, 2, true>, 8, 2) : launch(k_gl5_mixd<8, 2, false>, 8, 2);
+        return a.res ? launch(k_gl5_mixd<8, 1, true>, 8, 1) : launch(k_gl5_mixd<8, 1, false>, 8, 1);
     }
     if (mfma) {
         const dim3 blk(256);

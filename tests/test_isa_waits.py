@@ -17,7 +17,7 @@ waits the compiler's waitcnt pass does not place by itself:
   lgkmcnt(0), so no wave reaches the barrier with an LDS read of the previous chunk in flight (the
   fill issued after the barrier into that slot raced such a read in the round-4 first cut:
   test_row_chains_share_cus_bitwise[3-0] 6.6e-5 off);
-* k_gl5_mixd<8, 2, true>: the residual of row r is read by inline-asm ds_read_b128 that the
+* k_gl5_mixd<8, 1, true>: the residual of row r is read by inline-asm ds_read_b128 that the
   waitcnt pass cannot see; each such read group follows an s_barrier that follows the row's
   counted vmcnt wait, with no LDS-DMA issued in between, and an lgkmcnt(0) drains the reads before
   the next fill is issued.
@@ -40,8 +40,8 @@ pytestmark = pytest.mark.skipif(not os.path.exists(OBJDUMP) or not os.path.exist
 GL4T = "_ZN2sd6k_gl4tILb0ELi0ELi6ELi12ELb0ELi2ELi4ELb0ELb0ELb0ELb1ELb0ELi1EEEvNS_6GLArgsEilNS_4YOutE"
 ATTN = "_ZN2sd11k_attentionILi4ELi32ELb0EEEvNS_8AttnArgsE"
 ATTN_TAIL = "_ZN2sd11k_attentionILi4ELi32ELb1EEEvNS_8AttnArgsE"  # J = 49..52 tail form
-MIXD = "_ZN2sd12_GLOBAL__N_110k_gl5_mixdILi8ELi2ELb0EEEvNS_6GLArgsEPKfl"
-MIXD_RES = "_ZN2sd12_GLOBAL__N_110k_gl5_mixdILi8ELi2ELb1EEEvNS_6GLArgsEPKfl"
+MIXD = "_ZN2sd12_GLOBAL__N_110k_gl5_mixdILi8ELi1ELb0EEEvNS_6GLArgsEPKfl"
+MIXD_RES = "_ZN2sd12_GLOBAL__N_110k_gl5_mixdILi8ELi1ELb1EEEvNS_6GLArgsEPKfl"
 UPD = "_ZN2sd13k_update_mfmaILi16ELi4ELi6ELb0EEEvNS_7UpdArgsE"
 
 _cache = {}
