@@ -590,7 +590,8 @@ hipError_t launch_graph_linear_v5(const GLArgs& a, bool rms, hipStream_t s) {
         // the LDS-DMA form: slabs of 4 ceil(J / 4) rows, 2 slots (row r + 1 in flight while row r is
         // mixed): 53 KiB of LDS at J = 51 with the residual, 3 workgroups per CU -- config 3 4,193 /
         // 4,195 vs 4,070 / 4,068 futures/s for 3 slots (2 workgroups per CU), profiles/r05k/ab_mixd.txt.
-        // SKELDIFF_V5_MIXD (A/B at load): 1 = 4 rows per workgroup with 3 slots, 3 = 3 slots
+        // SKELDIFF_V5_MIXD (A/B at load): 1 = 4 rows per workgroup with 3 slots, 3 = 3 slots,
+        // 4 / 5 = 16 / 4 rows per workgroup with 2 slots
         const int KS = (a.J + 3) / 4;
         auto launch = [&](auto kt, int R, int PF) -> hipError_t {
             const size_t lds = (size_t)(PF + 1) * (a.res ? 2 : 1) * 4 * KS * 64 * sizeof(float);
@@ -604,6 +605,8 @@ hipError_t launch_graph_linear_v5(const GLArgs& a, bool rms, hipStream_t s) {
         };
         if (g_mixd_cfg == 1) return a.res ? launch(k_gl5_mixd<4, 2, true>, 4, 2) : launch(k_gl5_mixd<4, 2, false>, 4, 2);
         if (g_mixd_cfg == 3) return a.res ? launch(k_gl5_mixd<8, 2, true>, 8, 2) : launch(k_gl5_mixd<8, 2, false>, 8, 2);
+        if (g_mixd_cfg == 4) return a.res ? launch(k_gl5_mixd<16, 1, true>, 16, 1) : launch(k_gl5_mixd<16, 1, false>, 16, 1);
+        if (g_mixd_cfg == 5) return a.res ? launch(k_gl5_mixd<4, 1, true>, 4, 1) : launch(k_gl5_mixd<4, 1, false>, 4, 1);
         return a.res ? launch(k_gl5_mixd<8, 1, true>, 8, 1) : launch(k_gl5_mixd<8, 1, false>, 8, 1);
     }
     if (mfma) {
