@@ -43,9 +43,10 @@ extern "C" {
 
 /* ABI history: 1 (rounds 1-3); 2 (round 5) -- sd_mahalanobis_loss_forward / _backward take T,
  * sd_set_kernel_variant / sd_set_row_chains / sd_set_update_kernel / sd_set_v5_mix removed
- * (per-plan options instead), sd_test_set_split_route and sd_plan_desc::objective added.
- * Bindings check it at load. */
-#define SD_ABI_VERSION 2
+ * (per-plan options instead), sd_test_set_split_route and sd_plan_desc::objective added;
+ * 3 (round 6) -- SD_FLAG_NO_CLIP (p_sample's clip_denoised = False), sd_p_sample_update takes
+ * flags.  Bindings check it at load. */
+#define SD_ABI_VERSION 3
 
 enum {
     SD_OK = 0,
@@ -60,7 +61,10 @@ enum {
 enum {
     SD_FLAG_GRAPH = 1,          /* capture the whole T-step chain in a hipGraph, cache, replay */
     SD_FLAG_DEVICE_START = 2,   /* x_T drawn on device (Philox, step index T) instead of x_T arg */
-    SD_FLAG_DEVICE_NOISE = 4    /* per-step noise drawn on device instead of eps_all */
+    SD_FLAG_DEVICE_NOISE = 4,   /* per-step noise drawn on device instead of eps_all */
+    SD_FLAG_NO_CLIP = 8         /* x0 is not clamped to [-1, 1] (p_sample / p_mean_variance with
+                                   clip_denoised = False, base.py:314-328; the flag also applies to
+                                   sd_p_sample_update) */
 };
 
 typedef struct sd_plan sd_plan;
@@ -144,7 +148,7 @@ int sd_denoiser_trace(const sd_plan* plan, const float* x_t, const float* x_cond
                       float* const* acts, int32_t nacts, void* stream);
 
 /* One reverse step for B rows at time t:
- *   x0 = clamp(act(x0_raw), -1, 1); mean = C1[t] x0 + C2[t] x_t;
+ *   x0 = clamp(act(x0_raw), -1, 1) (no clamp with SD_FLAG_NO_CLIP in flags); mean = C1[t] x0 + C2[t] x_t;
  *   x_prev = mean + U (sigma_t * eps)   (nonisotropic)   |  c1 x0 + c2 x_t + sigma_t eps (iso)
  * eps: (B, J, D) rows `eps_row_stride` floats apart, or NULL for device Philox noise
  * (seed, global row row0 + b, step t).  t == 0 adds no noise.  mean_out / noise_out are
@@ -152,7 +156,8 @@ int sd_denoiser_trace(const sd_plan* plan, const float* x_t, const float* x_cond
 int sd_p_sample_update(const sd_plan* plan, const float* x0_raw, const float* x_t,
                        const float* eps, int64_t eps_row_stride, uint64_t seed, int64_t row0,
                        int32_t t, float* x_prev, float* mean_out, int64_t mean_row_stride,
-                       float* noise_out, int64_t noise_row_stride, int64_t rows, void* stream);
+                       float* noise_out, int64_t noise_row_stride, int64_t rows, int32_t flags,
+                       void* stream);
 
 /* The full reverse chain t = T-1 .. 0 (base.py:365-367).
  *   x_T     : (B,J,D) start noise, or ignored with SD_FLAG_DEVICE_START

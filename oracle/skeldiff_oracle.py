@@ -34,7 +34,7 @@ import torch.nn.functional as F
 __all__ = [
     "beta_schedule", "schedule_buffers", "covariance_diagonals", "nonisotropic_buffers",
     "isotropic_buffers", "get_cov_from_corr", "DenoiserConfig", "denoiser_forward",
-    "sinusoidal_embedding", "p_sample_loop", "p_sample_step", "philox4x32_10", "philox_normal",
+    "sinusoidal_embedding", "p_sample_loop", "p_sample_step", "p_mean_variance", "philox4x32_10", "philox_normal",
     "device_noise", "ORACLE_IS_TEST_INFRASTRUCTURE",
 ]
 
@@ -352,19 +352,50 @@ def p_sample_step(sd, cfg: DenoiserConfig, bufs: Dict[str, torch.Tensor], img: t
     return mean + bufs["U"] @ ((0.5 * lv).exp() * noise), mean
 
 
+def p_mean_variance(sd, cfg: DenoiserConfig, bufs: Dict[str, torch.Tensor], x: torch.Tensor, t: int,
+                    x_cond: Optional[torch.Tensor] = None, isotropic: bool = False, activation: str = "identity",
+                    objective: str = "pred_x0", clip: bool = True):
+    """base.py:314-322 with model_predictions (:219-241) and feed_model (:243-255): x0 from the
+    Denoiser output per objective (isotropic.py:48-70), clamped unless clip=False, then q_posterior
+    (nonisotropic.py:196-206 / isotropic.py:85-92).  Returns (mean, var, logvar, x0) with the
+    reference's broadcast shapes ((B, J, 1) nonisotropic, (B, 1, 1) isotropic)."""
+    B = x.shape[0]
+    if x_cond is not None and B > x_cond.shape[0]:
+        x_cond = x_cond.repeat_interleave(B // x_cond.shape[0], 0)
+    out = denoiser_forward(sd, cfg, x, torch.full((B,), t, dtype=torch.long), x_cond)
+    x0 = torch.tanh(out) if activation == "tanh" else out
+    if objective == "pred_noise":
+        x0 = bufs["sqrt_recip_alphas_cumprod"][t] * x - bufs["sqrt_recipm1_alphas_cumprod"][t] * x0
+    elif objective == "pred_v":
+        x0 = bufs["sqrt_alphas_cumprod"][t] * x - bufs["sqrt_one_minus_alphas_cumprod"][t] * x0
+    if clip:
+        x0 = x0.clamp(-1.0, 1.0)
+    if isotropic:
+        mean = bufs["posterior_mean_coef1"][t] * x0 + bufs["posterior_mean_coef2"][t] * x
+        var = bufs["posterior_variance"][t].expand(B, 1, 1)
+        lv = bufs["posterior_log_variance_clipped"][t].expand(B, 1, 1)
+    else:
+        mean = bufs["posterior_mean_coef1_x0"][t] @ x0 + bufs["posterior_mean_coef2_xt"][t] @ x
+        var = bufs["Lambda_posterior"][t].unsqueeze(-1).expand(B, -1, 1)
+        lv = bufs["Lambda_posterior_log_variance_clipped"][t].unsqueeze(-1).expand(B, -1, 1)
+    return mean, var, lv, x0
+
+
 def p_sample_loop(sd, cfg: DenoiserConfig, bufs: Dict[str, torch.Tensor], start_noise: torch.Tensor,
                   sampling_noise: Optional[torch.Tensor], x_cond: Optional[torch.Tensor] = None,
                   isotropic: bool = False, activation: str = "identity", record_means: bool = False,
                   steps: Optional[int] = None, record_imgs: bool = False,
                   noise2interpolate: Optional[torch.Tensor] = None, interpolate_funct=None,
-                  objective: str = "pred_x0"):
+                  objective: str = "pred_x0", clip: bool = True):
     """Reverse diffusion with host-supplied noise.  Returns (img, [mean_t for t=T-1..1]), or
     (img, means, [x_t for t=T-1..1]) with `record_imgs` (return_timages, base.py:371-389).
 
     `steps` runs only the first `steps` iterations (t = T-1 .. T-steps) for bounded CPU
     baselines; the per-step cost is constant in t.
     `noise2interpolate` + `interpolate_funct`: the reference's noise interpolation
-    (base.py:335-338; nonisotropic.py:218-227): x = mean + f(U(s*n1), U(s*n2))."""
+    (base.py:335-338; nonisotropic.py:218-227): x = mean + f(U(s*n1), U(s*n2)); isotropic
+    (isotropic.py:97-103): x = mean + s * f(n1, n2).
+    `clip=False`: p_sample's clip_denoised=False (base.py:318-319 skipped)."""
     T = bufs["betas"].shape[0]
     img = start_noise.clone()
     B = img.shape[0]
@@ -381,7 +412,8 @@ def p_sample_loop(sd, cfg: DenoiserConfig, bufs: Dict[str, torch.Tensor], start_
             x0 = bufs["sqrt_recip_alphas_cumprod"][t] * img - bufs["sqrt_recipm1_alphas_cumprod"][t] * x0
         elif objective == "pred_v":    # isotropic.py:66-70
             x0 = bufs["sqrt_alphas_cumprod"][t] * img - bufs["sqrt_one_minus_alphas_cumprod"][t] * x0
-        x0 = x0.clamp(-1.0, 1.0)
+        if clip:
+            x0 = x0.clamp(-1.0, 1.0)
         if isotropic:
             mean = bufs["posterior_mean_coef1"][t] * x0 + bufs["posterior_mean_coef2"][t] * img
             lv = bufs["posterior_log_variance_clipped"][t]
@@ -396,7 +428,10 @@ def p_sample_loop(sd, cfg: DenoiserConfig, bufs: Dict[str, torch.Tensor], start_
         if noise2interpolate is not None and t > 0:  # base.py:335-338, nonisotropic.py:218-227
             n2 = noise2interpolate[:, sampling_noise.shape[1] - t]
             s = (0.5 * lv).exp()
-            img = mean + interpolate_funct(bufs["U"] @ (s * noise), bufs["U"] @ (s * n2))
+            if isotropic:
+                img = mean + s * interpolate_funct(noise, n2)
+            else:
+                img = mean + interpolate_funct(bufs["U"] @ (s * noise), bufs["U"] @ (s * n2))
         elif isotropic:
             img = mean + (0.5 * lv).exp() * noise
         else:

@@ -18,11 +18,12 @@ LIB_PATH = os.environ.get("SKELDIFF_LIB") or os.path.join(HERE, "libskeldiff.so"
 # include/skeldiff.h SD_ABI_VERSION: a library of another ABI is refused at load (round 4 changed
 # signatures under the same number; a client built against the old header would pass shifted
 # arguments instead of failing cleanly)
-SD_ABI_VERSION = 2
+SD_ABI_VERSION = 3
 
 SD_FLAG_GRAPH = 1
 SD_FLAG_DEVICE_START = 2
 SD_FLAG_DEVICE_NOISE = 4
+SD_FLAG_NO_CLIP = 8
 
 # every symbol include/skeldiff.h declares (checked by tests/test_abi.py)
 EXPORTED = (
@@ -113,7 +114,7 @@ def _declare(lib: ctypes.CDLL) -> None:
         "sd_denoiser_forward": (ctypes.c_int, [vp, vp, vp, i64, i32, vp, i64, vp, sz, vp]),
         "sd_workspace_status": (ctypes.c_int, [vp, vp, sz, ctypes.POINTER(ctypes.c_uint32), vp]),
         "sd_denoiser_trace": (ctypes.c_int, [vp, vp, vp, i64, i32, vp, i64, vp, sz, ctypes.POINTER(vp), i32, vp]),
-        "sd_p_sample_update": (ctypes.c_int, [vp, vp, vp, vp, i64, u64, i64, i32, vp, vp, i64, vp, i64, i64, vp]),
+        "sd_p_sample_update": (ctypes.c_int, [vp, vp, vp, vp, i64, u64, i64, i32, vp, vp, i64, vp, i64, i64, i32, vp]),
         "sd_sample_loop": (ctypes.c_int, [vp, vp, vp, i64, vp, u64, i64, vp, vp, vp, vp, vp, i64, vp, sz, i32, vp]),
         "sd_noise_fill": (ctypes.c_int, [vp, i64, i64, u64, i64, i32, vp]),
         "sd_philox_raw": (ctypes.c_int, [vp, i64, i64, u64, i64, i32, vp]),

@@ -231,10 +231,13 @@ class LatentDiffusion(nn.Module):
 
     @torch.no_grad()
     def p_mean_variance(self, x, t, x_self_cond=None, x_cond=None, clip_denoised=True):
+        """base.py:314-322: x0 from the Denoiser output (HIP engine) per objective, as
+        model_predictions forms it (base.py:219-241: the activation, then predict_start_from_noise /
+        predict_start_from_v for pred_noise / pred_v), clamped unless clip_denoised=False, then the
+        posterior q(x_{t-1} | x_t, x0)."""
         tt = int(t[0]) if torch.is_tensor(t) else int(t)
-        x_start = self.engine.denoiser_forward(x, tt, x_cond)
-        if self.diffusion_activation == "tanh":
-            x_start = torch.tanh(x_start)
+        out = self.engine.denoiser_forward(x, tt, x_cond)
+        x_start = self.engine.start_from_output(x, tt, out)
         if clip_denoised:
             x_start.clamp_(-1.0, 1.0)
         t_b = torch.full((x.shape[0],), tt, device=x.device, dtype=torch.long)
@@ -255,13 +258,11 @@ class LatentDiffusion(nn.Module):
             assert noise2.shape == noise.shape
             img = self.p_interpolate_mean_var_noise(mean, logvar, noise, noise2, **(interpolation_kwargs or {}))
             return img, x_start, noise, mean
-        if not clip_denoised:
-            raise NotImplementedError("the sampling engine always clips x0 (base.py:318-319 default)")
         eps = None
         if t > 0:
             eps = sampling_noise[:, sampling_noise.shape[1] - t] if sampling_noise is not None \
                 else self.get_white_noise(x)
-        return self.engine.p_sample(x, t, x_cond, eps)
+        return self.engine.p_sample(x, t, x_cond, eps, clip=bool(clip_denoised))
 
     @torch.no_grad()
     def p_sample_loop(self, shape, x_cond=None, start_noise=None, sampling_noise=None,
@@ -273,7 +274,10 @@ class LatentDiffusion(nn.Module):
         when start/sampling noise is not supplied (default: drawn from torch's global RNG, so
         torch.manual_seed controls it); `row0` is the global index of the first row, which makes
         device noise independent of how rows are split over launches or GPUs; `out` (rows, J, D)
-        fp32 receives the latents (reusing it keeps a captured hipGraph valid across calls)."""
+        fp32 receives the latents (reusing it keeps a captured hipGraph valid across calls).
+        `clip_denoised` (default True) travels in **kwargs to p_sample, as in the reference
+        (base.py:344,367 -> :325); False leaves x0 unclamped (SD_FLAG_NO_CLIP)."""
+        clip = bool(kwargs.pop("clip_denoised", True))
         if start_noise is not None:
             assert tuple(start_noise.shape) == tuple(shape), f"Shape mismatch: {start_noise.shape} != {shape}"
         if sampling_noise is not None:
@@ -283,7 +287,7 @@ class LatentDiffusion(nn.Module):
         if if_interpolate:
             return self._p_sample_loop_interpolate(shape, x_cond, start_noise, sampling_noise,
                                                    return_sampling_noise, return_timages,
-                                                   noise2interpolate, interpolation_kwargs)
+                                                   noise2interpolate, interpolation_kwargs, clip)
         if self.self_condition:
             raise NotImplementedError("self_condition=True is not supported by the sampling engine")
         if seed is None and (start_noise is None or sampling_noise is None):
@@ -294,7 +298,7 @@ class LatentDiffusion(nn.Module):
         res = self.engine.sample_loop(shape[0], x_cond=x_cond, start_noise=start_noise,
                                       sampling_noise=sampling_noise,
                                       record=(return_sampling_noise, return_timages), seed=seed, row0=row0,
-                                      out=out)
+                                      out=out, clip=clip)
         img, start, noise_t, mean_t, imgs = res
         noise = start
         if return_sampling_noise:
@@ -304,13 +308,13 @@ class LatentDiffusion(nn.Module):
         return img, noise
 
     def _p_sample_loop_interpolate(self, shape, x_cond, start_noise, sampling_noise, return_sampling_noise,
-                                   return_timages, noise2interpolate, interpolation_kwargs):
+                                   return_timages, noise2interpolate, interpolation_kwargs, clip=True):
         img = start_noise if start_noise is not None else self.get_start_noise(shape, device=self.betas.device)
         noise = img.clone()
         noise_t, mean_t, imgs = [], [], []
         for t in reversed(range(self.num_timesteps)):
-            img, _, nt, mean = self.p_sample(img, t, None, sampling_noise=sampling_noise, x_cond=x_cond,
-                                             if_interpolate=True, noise2interpolate=noise2interpolate,
+            img, _, nt, mean = self.p_sample(img, t, None, clip_denoised=clip, sampling_noise=sampling_noise,
+                                             x_cond=x_cond, if_interpolate=True, noise2interpolate=noise2interpolate,
                                              interpolation_kwargs=interpolation_kwargs)
             if t != 0:
                 noise_t.append(nt)

@@ -130,6 +130,7 @@ struct UpdArgs {
     float c1s, c2s, sigs;                  // isotropic scalars
     int obj; float xa, xb;                 // isotropic pred_noise / pred_v (obj 1): x0 = xa x_t - xb act(out)
     int iso; int act; int noise_mode;      // noise_mode: 0 none (t == 0), 1 given, 2 Philox
+    int clip;                              // 1: x0 clamped to [-1, 1] (clip_denoised, base.py:318-319)
     uint64_t seed; int64_t row0; int step; const uint64_t* rng_dev;  // rng_dev: {seed,row0} or null
     int64_t row_shift;                     // added to row0 (either source): a row chunk's first row
     float* out; float* out2; int64_t out2_rs;

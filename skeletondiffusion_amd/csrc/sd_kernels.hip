@@ -826,7 +826,7 @@ __global__ __launch_bounds__(256) void k_update(const UpdArgs p) {
         }
         xtv[j] = ld2x(p.xt, rb + j * D + d, p.xt_bf16);
         if (p.obj) a = start_from_pred(p, xtv[j], a);
-        x0v[j] = floatx2{fminf(fmaxf(a.x, -1.f), 1.f), fminf(fmaxf(a.y, -1.f), 1.f)};
+        x0v[j] = p.clip ? floatx2{fminf(fmaxf(a.x, -1.f), 1.f), fminf(fmaxf(a.y, -1.f), 1.f)} : a;
         if (p.noise_mode == 1)
             ev[j] = ld2(p.eps + row * p.eps_rs + j * D + d);
         else if (p.noise_mode == 2)
@@ -932,7 +932,7 @@ __global__ __launch_bounds__(256) void k_update_row(const UpdArgs p) {
         }
         const floatx2 xt = ld2x(p.xt, rb + o, p.xt_bf16);
         if (p.obj) a = start_from_pred(p, xt, a);
-        st2(sx0 + o, floatx2{fminf(fmaxf(a.x, -1.f), 1.f), fminf(fmaxf(a.y, -1.f), 1.f)});
+        st2(sx0 + o, p.clip ? floatx2{fminf(fmaxf(a.x, -1.f), 1.f), fminf(fmaxf(a.y, -1.f), 1.f)} : a);
         st2(sxt + o, xt);
         floatx2 e;
         if (p.noise_mode == 1) e = ld2(p.eps + row * p.eps_rs + o);
@@ -1160,7 +1160,7 @@ __global__ __launch_bounds__(256) void k_update_mfma(const UpdArgs p) {
         for (int ks = 0; ks < KS; ++ks) {
             float a = bx[q][ks];
             if (p.act == 1) a = tanhf(a);
-            bx[q][ks] = fminf(fmaxf(a, -1.f), 1.f);
+            bx[q][ks] = p.clip ? fminf(fmaxf(a, -1.f), 1.f) : a;
         }
 #ifdef SD_UPD_STAMPS
     {  // the prepass's values in use: the x0 fragments have arrived
@@ -1383,7 +1383,7 @@ __global__ __launch_bounds__(256, 2) void k_update_pipe(const UpdArgs p) {
             for (int ks = 0; ks < KS; ++ks) {
                 float a = bx[k][q][ks];
                 if (p.act == 1) a = tanhf(a);
-                bx[k][q][ks] = fminf(fmaxf(a, -1.f), 1.f);
+                bx[k][q][ks] = p.clip ? fminf(fmaxf(a, -1.f), 1.f) : a;
             }
         floatx4 vres[MT][IB];
 #pragma unroll
@@ -1536,7 +1536,7 @@ __global__ __launch_bounds__(256) void k_update_v2(const UpdArgs p) {
                 a.x = tanhf(a.x);
                 a.y = tanhf(a.y);
             }
-            bx[g][ks] = floatx2{fminf(fmaxf(a.x, -1.f), 1.f), fminf(fmaxf(a.y, -1.f), 1.f)};
+            bx[g][ks] = p.clip ? floatx2{fminf(fmaxf(a.x, -1.f), 1.f), fminf(fmaxf(a.y, -1.f), 1.f)} : a;
         }
     floatx4 vres[NG][2], mres[NG][2];
 #pragma unroll

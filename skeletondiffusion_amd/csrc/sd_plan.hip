@@ -567,8 +567,9 @@ int run_update(const sd_plan* p, const float* x0, const float* xt, const float* 
                const uint64_t* rng_dev, int t, float* out, float* out2, int64_t out2_rs,
                float* mean_out, int64_t mean_rs, float* noise_out, int64_t noise_rs, int64_t rows,
                hipStream_t s, Prof* prof = nullptr, int64_t row_shift = 0, int x0_bf16 = 0, int xt_bf16 = 0,
-               int out_bf16 = 0) {
+               int out_bf16 = 0, int clip = 1) {
     sd::UpdArgs u{};
+    u.clip = clip;
     u.x0_bf16 = x0_bf16;
     u.xt_bf16 = xt_bf16;
     u.out_bf16 = out_bf16;
@@ -988,15 +989,17 @@ int sd_denoiser_trace(const sd_plan* p, const float* x_t, const float* x_cond, i
 int sd_p_sample_update(const sd_plan* p, const float* x0_raw, const float* x_t, const float* eps,
                        int64_t eps_rs, uint64_t seed, int64_t row0, int32_t t, float* x_prev,
                        float* mean_out, int64_t mean_rs, float* noise_out, int64_t noise_rs,
-                       int64_t rows, void* stream) {
+                       int64_t rows, int32_t flags, void* stream) {
     if (!p || !p->finalized) return fail(SD_E_STATE, "plan is not finalized");
+    if (flags & ~SD_FLAG_NO_CLIP) return fail(SD_E_INVALID, "sd_p_sample_update flags: SD_FLAG_NO_CLIP only");
     if (t < 0 || t >= p->T) return fail(SD_E_INVALID, "t out of range");
     if (!x0_raw || !x_t || !x_prev) return fail(SD_E_INVALID, "null tensor");
     if (!eps && p->D % 4) return fail(SD_E_INVALID, "device noise needs latent_dim % 4 == 0");
     const int64_t JD = (int64_t)p->J * p->D;
     return run_update(p, x0_raw, x_t, eps, eps ? eps_rs : JD, eps ? 1 : 2, seed, row0, nullptr, t,
                       x_prev, nullptr, 0, mean_out, mean_out ? mean_rs : JD, noise_out,
-                      noise_out ? noise_rs : JD, rows, (hipStream_t)stream);
+                      noise_out ? noise_rs : JD, rows, (hipStream_t)stream, nullptr, 0, 0, 0, 0,
+                      !(flags & SD_FLAG_NO_CLIP));
 }
 
 static WS shift_ws(const sd_plan* p, const WS& w, int64_t r0, int chain) {
@@ -1124,7 +1127,7 @@ static int record_loop(const sd_plan* p, const float* x_T, const float* x_cond, 
                             (rec && timages) ? timages + r0 * step_rs + k * JD : nullptr, step_rs,
                             (rec && means) ? means + r0 * step_rs + k * JD : nullptr, step_rs,
                             (rec && noise_out) ? noise_out + r0 * step_rs + k * JD : nullptr, step_rs, c.n,
-                            cs[i], nullptr, r0, bf, bf, t > 0 ? bf : 0);
+                            cs[i], nullptr, r0, bf, bf, t > 0 ? bf : 0, !(flags & SD_FLAG_NO_CLIP));
             g_dump = saved;
             if (rc) return rc;
             const int64_t sl = k * kSnapCalls + kSnapCalls - 1;  // diagnostics: the update's output

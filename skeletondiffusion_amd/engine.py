@@ -256,7 +256,7 @@ class SamplingEngine:
                                            len(acts), _stream(self._device)))
         return out, acts
 
-    def p_sample(self, x, t: int, x_cond=None, eps=None):
+    def p_sample(self, x, t: int, x_cond=None, eps=None, clip: bool = True):
         plan = self.plan()
         x = self._f32(x)
         rows = x.shape[0]
@@ -271,23 +271,33 @@ class SamplingEngine:
             seed = int(torch.randint(0, 2 ** 62, (1,)).item())
         else:
             seed = 0
+        flags = 0 if clip else _lib.SD_FLAG_NO_CLIP
         check(L.sd_p_sample_update(plan, ptr(x0_raw), ptr(x), ptr(eps), JD, seed, 0, int(t), ptr(out),
-                                   ptr(mean), JD, ptr(noise_used), JD, rows, _stream(self._device)))
-        x0 = torch.tanh(x0_raw) if self.diff.diffusion_activation == "tanh" else x0_raw
+                                   ptr(mean), JD, ptr(noise_used), JD, rows, flags, _stream(self._device)))
+        x0 = self.start_from_output(x, t, x0_raw)
+        if clip:
+            x0.clamp_(-1.0, 1.0)
+        return out, x0, (noise_used if t > 0 else 0.0), mean
+
+    def start_from_output(self, x, t: int, out):
+        """x0 from the Denoiser output per objective, as model_predictions forms it (base.py:219-241):
+        activation, then predict_start_from_noise / _from_v for the isotropic pred_noise / pred_v
+        (isotropic.py:48-52, 66-70); the update kernels do the same arithmetic before their clamp."""
+        x0 = torch.tanh(out) if self.diff.diffusion_activation == "tanh" else out
         obj = self.diff.objective
-        if obj == "pred_noise":    # isotropic.py:48-52 (the update kernel does the same)
+        if obj == "pred_noise":
             x0 = self.diff.sqrt_recip_alphas_cumprod[t] * x - self.diff.sqrt_recipm1_alphas_cumprod[t] * x0
-        elif obj == "pred_v":      # isotropic.py:66-70
+        elif obj == "pred_v":
             x0 = self.diff.sqrt_alphas_cumprod[t] * x - self.diff.sqrt_one_minus_alphas_cumprod[t] * x0
-        return out, x0.clamp_(-1.0, 1.0), (noise_used if t > 0 else 0.0), mean
+        return x0
 
     def sample_loop(self, rows: int, x_cond=None, start_noise=None, sampling_noise=None,
                     record=(False, False), seed: Optional[int] = None, row0: int = 0,
                     graph: Optional[bool] = None, out: Optional[torch.Tensor] = None,
-                    keep_start: bool = True):
+                    keep_start: bool = True, clip: bool = True):
         """-> (img, start_noise, noise_t, mean_t, imgs).  Unrequested records are None.
         `out` (rows, J, D) fp32 may be passed to reuse an output buffer (keeps a captured
-        hipGraph valid across calls)."""
+        hipGraph valid across calls).  clip=False: x0 is not clamped (clip_denoised=False)."""
         plan = self.plan()
         J, D, T = self.diff.channels, self.diff.seq_length, self.diff.num_timesteps
         dev = self._device
@@ -300,8 +310,11 @@ class SamplingEngine:
             flags |= _lib.SD_FLAG_DEVICE_NOISE
         if graph if graph is not None else self._graph:
             flags |= _lib.SD_FLAG_GRAPH
+        if not clip:
+            flags |= _lib.SD_FLAG_NO_CLIP
         if seed is None:
-            seed = int(torch.randint(0, 2 ** 62, (1,)).item()) if (flags & 6) else 0
+            seed = int(torch.randint(0, 2 ** 62, (1,)).item()) if (flags & (_lib.SD_FLAG_DEVICE_START |
+                                                                             _lib.SD_FLAG_DEVICE_NOISE)) else 0
         xc, rep = self._cond(x_cond, rows)
         rec_noise, rec_img = record
         if out is None:

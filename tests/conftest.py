@@ -134,6 +134,77 @@ def build_readme_diffusion(mode, device="cpu"):
     return d.to(device).eval()
 
 
+def tol_rel(ref, tol):
+    """Absolute tolerance `tol` scaled by the fixture's magnitude (at least 1): the unclamped
+    pred_noise chains reach |x| ~ 1e3, where fp32 rounding alone moves the last digits by 1e-4."""
+    return tol * max(1.0, float(np.abs(np.asarray(ref)).max()))
+
+
+# round 6 fixtures (gen_golden.py gen_iso_paths / gen_options)
+ISO_OBJECTIVES = ["pred_x0", "pred_noise", "pred_v"]
+OPTION_CASES = {  # name -> (T argument, NonisotropicGaussianDiffusion kwargs, oracle schedule / covariance)
+    "anisotropic": (10, dict(diffusion_covariance_type="anisotropic"), ("cosine", "anisotropic", "cosine")),
+    "mono_decrease": (10, dict(gamma_scheduler="mono_decrease"), ("cosine", "skeleton-diffusion", "mono_decrease")),
+    "linear": (100, dict(beta_schedule="linear"), ("linear", "skeleton-diffusion", "cosine")),
+    "exp": (10, dict(beta_schedule="exp"), ("exp", "skeleton-diffusion", "cosine")),
+}
+
+
+def iso_path_inputs():
+    """(start, sampling noise, noise2interpolate) of iso_paths_T10 (README shape, B = 4, T = 10)."""
+    from skeletondiffusion_amd import synthetic
+
+    return (torch.from_numpy(synthetic.normal((4, 16, 96), 11)), torch.from_numpy(synthetic.normal((4, 9, 16, 96), 12)),
+            torch.from_numpy(synthetic.normal((4, 9, 16, 96), 13)))
+
+
+def option_buffers(name, S, L, U):
+    import oracle as O
+
+    T, _, (sched, cov, gamma) = OPTION_CASES[name]
+    return O.nonisotropic_buffers(S, L, U, O.beta_schedule(sched, T), cov_type=cov, gamma_scheduler=gamma)
+
+
+def option_inputs(z, model):
+    """(oracle config, oracle state_dict, x_cond per sequence or None, start, sampling noise) of an
+    option fixture's README (B = 4) or release (2 sequences x 4 futures) chain."""
+    import oracle as O
+    from skeletondiffusion_amd import synthetic
+
+    Tn = int(z["num_timesteps"])
+    if model == "readme":
+        cfg = O.readme_config()
+        return (cfg, O.synthetic_state_dict(cfg, WEIGHT_SEED), None,
+                torch.from_numpy(synthetic.normal((4, 16, 96), 11)), torch.from_numpy(synthetic.normal((4, Tn - 1, 16, 96), 12)))
+    cfg = O.release_config(16, z["node_types"])
+    B = int(z["B_seq"]) * int(z["futures"])
+    return (cfg, O.synthetic_state_dict(cfg, WEIGHT_SEED), torch.from_numpy(synthetic.uniform((int(z["B_seq"]), 16, 96), 21)),
+            torch.from_numpy(synthetic.normal((B, 16, 96), 22)), torch.from_numpy(synthetic.normal((B, Tn - 1, 16, 96), 23)))
+
+
+def build_option_diffusion(name, model, z, device="cpu"):
+    """Product NonisotropicGaussianDiffusion of an option fixture (README or release Denoiser) with
+    the fixture's own Sigma_N / Lambda_N / U."""
+    from skeletondiffusion_amd import synthetic
+    from skeletondiffusion_amd.core.diffusion import NonisotropicGaussianDiffusion
+    from skeletondiffusion_amd.core.network import Denoiser
+
+    T, kw, _ = OPTION_CASES[name]
+    S, L, U = (torch.from_numpy(z[f"{model}_buf_{k}"]) for k in ("Sigma_N", "Lambda_N", "U"))
+    if model == "readme":
+        m = Denoiser(dim=96, cond_dim=0, out_dim=96, channels=16, num_nodes=16)
+        synthetic.fill_module_(m, WEIGHT_SEED)
+        d = NonisotropicGaussianDiffusion(Sigma_N=S, Lambda_N=L, U=U, model=m, diffusion_timesteps=T, **kw)
+    else:
+        m = Denoiser(dim=96, cond_dim=96, out_dim=96, channels=16, num_nodes=16,
+                     node_types=torch.from_numpy(z["node_types"]), use_attention=True, self_condition=False,
+                     norm_type="none", depth=4, attn_dim_head=32, attn_heads=8, learn_influence=True)
+        synthetic.fill_module_(m, WEIGHT_SEED)
+        d = NonisotropicGaussianDiffusion(Sigma_N=S, Lambda_N=L, U=U, model=m, latent_size=96, diffusion_timesteps=T,
+                                          diffusion_objective="pred_x0", diffusion_conditioning=True, **kw)
+    return d.to(device).eval()
+
+
 @pytest.fixture(scope="session")
 def cuda():
     return torch.device("cuda:0")

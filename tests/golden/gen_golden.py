@@ -135,12 +135,13 @@ def build_release(skel_key, T, seed=WEIGHT_SEED, final_scale=1.0, arch=None, **d
             model.final_glin.bias.mul_(final_scale)
     Sigma_N, Lambda_N, U = get_cov_from_corr(correlation_matrix=corr, if_sigma_n_scale=True,
                                              sigma_n_scale="spectral", if_run_as_isotropic=False)
+    kw = dict(beta_schedule="cosine", diffusion_covariance_type="skeleton-diffusion", gamma_scheduler="cosine",
+              loss_reduction_type="l1")
+    kw.update(diff_kw)
     diff = NonisotropicGaussianDiffusion(Sigma_N=Sigma_N, Lambda_N=Lambda_N, U=U, model=model,
                                          latent_size=96, diffusion_timesteps=T,
                                          diffusion_objective="pred_x0",
-                                         diffusion_conditioning=True, beta_schedule="cosine",
-                                         diffusion_covariance_type="skeleton-diffusion",
-                                         gamma_scheduler="cosine", loss_reduction_type="l1", **diff_kw)
+                                         diffusion_conditioning=True, **kw)
     diff.eval()
     return sk, corr, node_types, diff
 
@@ -472,7 +473,136 @@ def gen_best_of_k_metric():
     _save("best_of_k_metric", out_c=out_c, fut_c=fut_c, sim=sim, idx=idx, sel=sel, pose_box_size=1.5)
 
 
+def _interp(n1, n2):
+    a, b = INTERP_W
+    return a * n1 + b * n2
+
+
+def gen_iso_paths():
+    """Round 6: IsotropicGaussianDiffusion (README Denoiser, J=16, B=4, T=10) on the paths that go
+    through p_mean_variance -> model_predictions (base.py:219-241, 314-322): noise interpolation
+    (base.py:335-338, isotropic.py:97-103) for pred_x0 / pred_noise / pred_v x identity / tanh, one
+    direct p_mean_variance call at t=6 with and without the clamp, and sample(clip_denoised=False)
+    (the kwarg reaches p_sample through p_sample_loop's **kwargs, base.py:344,367)."""
+    J, B, T = 16, 4, 10
+    start = torch.from_numpy(synthetic.normal((B, J, 96), seed=11))
+    samp = torch.from_numpy(synthetic.normal((B, T - 1, J, 96), seed=12))
+    noise2 = torch.from_numpy(synthetic.normal((B, T - 1, J, 96), seed=13))
+    keep = [0, 4, 8]  # mean_t steps kept (the inputs are regenerated from the seeds by the consumers)
+    out = {"pmv_t": 6, "mean_t_steps": np.array(keep)}
+    for obj in ("pred_x0", "pred_noise", "pred_v"):
+        for act in ("identity", "tanh"):
+            model = Denoiser(dim=96, cond_dim=0, out_dim=96, channels=J, num_nodes=J)
+            synthetic.fill_module_(model, WEIGHT_SEED)
+            diff = IsotropicGaussianDiffusion(model=model, diffusion_timesteps=T, diffusion_objective=obj,
+                                              diffusion_activation=act).eval()
+            k = f"{obj}_{act}"
+            with torch.no_grad():
+                img, (_, _, mean_t) = diff.sample(batch_size=B, start_noise=start.clone(), sampling_noise=samp.clone(),
+                                                  return_sampling_noise=True, if_interpolate=True,
+                                                  noise2interpolate=noise2.clone(),
+                                                  interpolation_kwargs={"interpolate_funct": _interp})
+                out[f"{k}_interp_img"], out[f"{k}_interp_mean_t"] = img, mean_t[:, keep]
+                tt = torch.full((B,), 6, dtype=torch.long)
+                for clip in (True, False):
+                    mean, var, logvar, x0 = diff.p_mean_variance(start.clone(), tt, clip_denoised=clip)
+                    c = "clip" if clip else "noclip"
+                    out[f"{k}_pmv_{c}_mean"], out[f"{k}_pmv_{c}_x0"] = mean, x0
+                    out[f"{k}_pmv_{c}_var"], out[f"{k}_pmv_{c}_logvar"] = var, logvar
+                img, (_, _, mean_t) = diff.sample(batch_size=B, start_noise=start.clone(), sampling_noise=samp.clone(),
+                                                  return_sampling_noise=True, clip_denoised=False)
+                out[f"{k}_noclip_img"], out[f"{k}_noclip_mean_t"] = img, mean_t[:, keep]
+    _save("iso_paths_T10", **out)
+
+
+def gen_noclip_release():
+    """Round 6: the release H36M J=16 sampler with clip_denoised=False (x0 pushed past +-1 by
+    final_scale 8, so the missing clamp shows), plain and with noise interpolation, and one
+    p_sample step (base.py:324-341 with clip_denoised=False) at t=4."""
+    T, B_seq, futures = 10, 1, 3
+    B = B_seq * futures
+    _, corr, node_types, diff = build_release("h36m16", T, final_scale=8.0)
+    x_cond = torch.from_numpy(synthetic.uniform((B_seq, 16, 96), seed=21)).repeat_interleave(futures, 0)
+    start = torch.from_numpy(synthetic.normal((B, 16, 96), seed=22))
+    samp = torch.from_numpy(synthetic.normal((B, T - 1, 16, 96), seed=23))
+    noise2 = torch.from_numpy(synthetic.normal((B, T - 1, 16, 96), seed=26))
+    out = {"B_seq": B_seq, "futures": futures, "T": T, "final_scale": 8.0, "node_types": node_types, "corr": corr}
+    with torch.no_grad():
+        img, (_, _, mean_t) = diff.sample(batch_size=B, x_cond=x_cond, start_noise=start.clone(),
+                                          sampling_noise=samp.clone(), return_sampling_noise=True, clip_denoised=False)
+        out["img"], out["mean_t"] = img, mean_t
+        img, _ = diff.sample(batch_size=B, x_cond=x_cond, start_noise=start.clone(), sampling_noise=samp.clone(),
+                             if_interpolate=True, noise2interpolate=noise2.clone(),
+                             interpolation_kwargs={"interpolate_funct": _interp}, clip_denoised=False)
+        out["interp_img"] = img
+        x, x0, noise, mean = diff.p_sample(start.clone(), 4, None, clip_denoised=False, sampling_noise=samp.clone(),
+                                           x_cond=x_cond)
+        out.update(step_t=4, step_x=x, step_x0=x0, step_mean=mean)
+    _save("noclip_h36m16_T10", **out)
+
+
+# config-selectable diffusion options (configs/config_train_diffusion/model/skeleton_diffusion.yaml:42-44)
+OPTION_CASES = {
+    "anisotropic": dict(T=10, diff_kw=dict(diffusion_covariance_type="anisotropic")),
+    "mono_decrease": dict(T=10, diff_kw=dict(gamma_scheduler="mono_decrease")),
+    # linear at T=10 reaches beta = 2 (base.py:39-43 is not clipped): NaN buffers; T=100 ends at 0.2
+    "linear": dict(T=100, diff_kw=dict(beta_schedule="linear")),
+    "exp": dict(T=10, diff_kw=dict(beta_schedule="exp")),  # T+1 = 11 steps (base.py:57-61, 116)
+}
+
+
+def gen_options():
+    """Round 6: the reference's config-selectable covariance / schedule options, each on the
+    README Denoiser (J=16, B=4) and the release H36M J=16 Denoiser (2 sequences x 4 futures):
+    every diffusion buffer and the sampled chain with supplied noise (nonisotropic.py:36-68,
+    base.py:39-61,103-116)."""
+    for name, case in OPTION_CASES.items():
+        T, kw = case["T"], case["diff_kw"]
+        out = {"T_arg": T}
+        # README Denoiser, README correlation recipe
+        J, B = 16, 4
+        corr = torch.from_numpy(synthetic.readme_correlation(J, seed=7))
+        model = Denoiser(dim=96, cond_dim=0, out_dim=96, channels=J, num_nodes=J)
+        synthetic.fill_module_(model, WEIGHT_SEED)
+        Sigma_N, Lambda_N, U = get_cov_from_corr(correlation_matrix=corr, if_sigma_n_scale=True,
+                                                 sigma_n_scale="spectral", if_run_as_isotropic=False)
+        diff = NonisotropicGaussianDiffusion(Sigma_N=Sigma_N, Lambda_N=Lambda_N, U=U, model=model,
+                                             diffusion_timesteps=T, **kw).eval()
+        Tn = diff.num_timesteps
+        start = torch.from_numpy(synthetic.normal((B, J, 96), seed=11))
+        samp = torch.from_numpy(synthetic.normal((B, Tn - 1, J, 96), seed=12))
+        with torch.no_grad():
+            img, (_, _, mean_t) = diff.sample(batch_size=B, start_noise=start.clone(), sampling_noise=samp.clone(),
+                                              return_sampling_noise=True)
+        keep = [0, 1, Tn // 2, Tn - 2]
+        out.update(readme_corr=corr, readme_img=img, readme_mean_t=mean_t[:, keep], mean_t_steps=np.array(keep),
+                   num_timesteps=Tn)
+        for k, v in diffusion_buffers(diff).items():
+            out[f"readme_{k}"] = v
+        # release H36M
+        sk, corr, node_types, diff = build_release("h36m16", T, **kw)
+        bs, fu = 2, 4
+        B = bs * fu
+        x_cond = torch.from_numpy(synthetic.uniform((bs, 16, 96), seed=21))
+        start = torch.from_numpy(synthetic.normal((B, 16, 96), seed=22))
+        samp = torch.from_numpy(synthetic.normal((B, Tn - 1, 16, 96), seed=23))
+        with torch.no_grad():
+            img, (_, _, mean_t) = diff.sample(batch_size=B, x_cond=x_cond.repeat_interleave(fu, 0),
+                                              start_noise=start.clone(), sampling_noise=samp.clone(),
+                                              return_sampling_noise=True)
+        out.update(release_img=img, release_mean_t=mean_t[:, keep], node_types=node_types, corr=corr,
+                   B_seq=bs, futures=fu)
+        for k, v in diffusion_buffers(diff).items():
+            out[f"release_{k}"] = v
+        _save(f"option_{name}", **out)
+
+
 def main():
+    if sys.argv[1:] == ["r06"]:
+        gen_iso_paths()
+        gen_noclip_release()
+        gen_options()
+        return
     if sys.argv[1:] == ["best_of_k_metric"]:
         gen_best_of_k_metric()
         return
@@ -511,6 +641,9 @@ def main():
     gen_new_r03()
     gen_best_of_k()
     gen_iso_objectives()
+    gen_iso_paths()
+    gen_noclip_release()
+    gen_options()
 
 
 if __name__ == "__main__":

@@ -24,7 +24,7 @@ def test_library_exports_every_declared_symbol():
     lib = _lib.lib()
     for name in declared_symbols():
         assert hasattr(lib, name), name
-    assert lib.sd_abi_version() == _lib.SD_ABI_VERSION == 2
+    assert lib.sd_abi_version() == _lib.SD_ABI_VERSION == 3
     hdr = open(os.path.join(os.path.dirname(__file__), "..", "include", "skeldiff.h")).read()
     assert re.search(r"#define SD_ABI_VERSION (\d+)", hdr).group(1) == str(_lib.SD_ABI_VERSION)
 
