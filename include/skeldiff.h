@@ -128,13 +128,12 @@ int sd_denoiser_forward(const sd_plan* plan, const float* x_t, const float* x_co
 
 /* Status of the last sd_sample_loop / sd_denoiser_forward / sd_denoiser_trace on `workspace`
  * (synchronises `stream`): flags bit 0 (SD_STATUS_F16_RANGE) = an activation reached |x| >= 65504,
- * outside the f16 range of the split-f16 (v4) products: informational on the split routes (their
- * GEMM phases recomputed those tiles on exact-f32 MFMA), and on the one-kernel route
- * (SD_OPT_SPLIT_ROUTE 1 / 5) the results are not f32-accurate -- run again with
- * SD_OPT_KERNEL_VARIANT = 3.  Bit 1 (SD_STATUS_FUSE_TIMEOUT) = a wait of the fused layer kernel
- * (SD_OPT_SPLIT_ROUTE 6) gave up: the results are invalid (never expected; bounded instead of a
- * hang).  The word is cleared at the start of each of those calls. */
-enum { SD_STATUS_F16_RANGE = 1, SD_STATUS_FUSE_TIMEOUT = 2 };
+ * outside the f16 range of the split-f16 (v4) products; informational: every f16-product kernel
+ * (the split routes' GEMM phases and, since ABI 3, the one-kernel tiles) recomputed the waves'
+ * tiles that left the range on exact-f32 MFMA, so f32 mode stays f32-accurate for any finite
+ * input.  The word is cleared at the start of each of those calls.  (Bit 1, the round-5 fused
+ * layer kernel's timeout, went with that kernel in ABI 3.) */
+enum { SD_STATUS_F16_RANGE = 1 };
 int sd_workspace_status(const sd_plan* plan, const void* workspace, size_t workspace_bytes, uint32_t* flags,
                         void* stream);
 
@@ -275,9 +274,9 @@ int sd_test_qkv_attention(const float* x, int32_t K, const float* W, const int64
  * gl_variant = -1 only queries (returns the current value). */
 int sd_test_set_kernel_variant(int32_t gl_variant, int32_t gl4_tile);
 /* Test hook: the v4 split route of the sd_test_graph_linear* entry points ONLY (as
- * SD_OPT_SPLIT_ROUTE: 0 auto, 1 never, 2 k_gl4y GEMM phase, 3 k_gl4t GEMM phase, 6 k_gl4t + k_gl4f, 5 fused small
- * tile; 2 / 3 / 5 allocate the pre-mix scratch per call).  Returns the previous route, or -1 for an
- * invalid one; route = -1 only queries. */
+ * SD_OPT_SPLIT_ROUTE: 0 auto, 1 never, 2 k_gl4y GEMM phase, 3 k_gl4t GEMM phase, 4 k_gl4t except
+ * to_qkv + attention; 2 / 3 / 4 allocate the pre-mix scratch per call).  Returns the previous route,
+ * or -1 for an invalid one; route = -1 only queries. */
 int sd_test_set_split_route(int32_t route);
 
 /* Per-plan kernel options (read by the launches recorded after the call; part of the graph
@@ -294,18 +293,13 @@ enum {
                                    2 = 0 (a round-2 diagnostic setting, kept for compatibility) */
     SD_OPT_SPLIT_ROUTE = 6,     /* v4 split route (GEMM phase per (tile, node) + mixing phase,
                                    DESIGN.md §4d'; bitwise identical results): 0 auto (k_gl4y at
-                                   <= SKELDIFF_SPLIT_ROWS rows of the call, default 1200; k_gl4t
-                                   for full batches where measured faster), 1 never, 2 always
-                                   (k_gl4y), 3 always with the tiled GEMM phase (k_gl4t: 128 rows
-                                   x up to 192 columns of one node per workgroup), 4 the tiled
-                                   GEMM phase except for to_qkv + attention (one-kernel fused
-                                   tile), 5 the small-batch fused tile (one launch per plain
-                                   graph-linear, J = 16 f32 / half; auto at <= SKELDIFF_SMALL_ROWS
-                                   rows) with the k_gl4y split route for to_qkv + attention, 6 the
-                                   tiled route with every plain J = 16 layer (N = 192) on the fused
-                                   layer kernel k_gl4f: GEMM and mixing phase in one persistent
-                                   launch, Y mixed out of the L2 of the XCD that wrote it
-                                   (auto where SKELDIFF_FUSED=1) */
+                                   <= 1200 rows of the call; k_gl4t for full batches where measured
+                                   faster), 1 never (the one-kernel k_gl4 tiles), 2 always (k_gl4y),
+                                   3 always with the tiled GEMM phase (k_gl4t: 128 rows x up to 192
+                                   columns of one node per workgroup), 4 the tiled GEMM phase except
+                                   for to_qkv + attention (one-kernel fused tile).  ABI 3 removed 5
+                                   (small-batch fused tile) and 6 (fused layer kernel k_gl4f):
+                                   measured slower, DESIGN.md §4i / §4j */
     SD_OPT_LAST_CHAINS = 7,     /* read-only: row chains the plan's last sd_sample_loop ran (the
                                    SD_OPT_ROW_CHAINS value, fewer for batches of fewer than n
                                    32-row units, a ragged last unit counting; auto: 1 at <= 128
@@ -315,23 +309,21 @@ enum {
                                    1 one-kernel k_gl4, 2 fused to_qkv + attention k_gl4, 4 k_gl4y
                                    GEMM phase, 8 k_gl4t GEMM phase, 16 split-route mixing /
                                    attention phase, 32 v5 mixing (J > 21), 64 exact-f32 kernels,
-                                   128 separate k_attention, 256 small-batch fused k_gl4 tile */
+                                   128 separate k_attention, 1024 k_attention_mix (256 / 512: the
+                                   kernels ABI 3 removed) */
     SD_OPT_UPDATE_KERNEL = 9,   /* posterior update: 0 (default) the J x J projections on
                                    v_mfma_f32_16x16x4_f32 where they apply (nonisotropic, J <= 64),
-                                   1 the element-per-thread forms, 2 the persistent pipelined
-                                   matrix-core form for full batches of J <= 16 (A/B: measured no
-                                   faster), 3 that form's arithmetic on 8-B fragment
-                                   loads (A/B); all give the same bits */
+                                   1 the element-per-thread forms; the same bits (ABI 3 removed the
+                                   pipelined forms 2 / 3: measured no faster) */
     SD_OPT_V5_MIX = 10,         /* J > 21 mixing pass (v5): 0 (default) G-hat mixing on
                                    v_mfma_f32_16x16x4_f32 (k_gl5_mixm), 1 the VALU form (k_gl5_mix);
                                    the same j-ordered fmaf chains */
-    SD_OPT_ATTENTION = 11       /* separate attention kernel at 49 <= J <= 52 (MANO), all forms
-                                   the same bits: 0 (default) auto = 2; 1 after the mixing pass, 48
-                                   nodes on the MFMAs + the last J - 48 on an fmaf chain in the
-                                   MFMA's k order (1 % slower on config 3); 2 the to_qkv layer's
-                                   G-hat mixing inside the attention kernel, its pre-mix Y in the
-                                   qkv buffer (k_attention_mix, 5 % faster); 3 after the mixing
-                                   pass, padded to 64 nodes */
+    SD_OPT_ATTENTION = 11       /* separate attention kernel at 49 <= J <= 52 (MANO), both forms
+                                   the same bits: 0 (default) auto = 2; 2 the to_qkv layer's G-hat
+                                   mixing inside the attention kernel, its pre-mix Y in the qkv
+                                   buffer (k_attention_mix, 5 % faster); 3 after the mixing pass,
+                                   padded to 64 nodes.  ABI 3 removed 1 (the 48-node
+                                   tail form, 1 % slower) */
 };
 int sd_plan_set_option(sd_plan* plan, int32_t option, int64_t value);
 int sd_plan_get_option(const sd_plan* plan, int32_t option, int64_t* value);

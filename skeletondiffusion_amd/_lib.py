@@ -50,11 +50,8 @@ EXPORTED = (
 # SD_OPT_LAST_ROUTE bits (sd::RouteBits)
 ROUTE_BITS = {1: "k_gl4 one-kernel", 2: "k_gl4 fused to_qkv+attention", 4: "k_gl4y GEMM phase",
               8: "k_gl4t GEMM phase", 16: "k_gl4 MODE 2/3 mixing phase", 32: "v5 k_gl5 mixing", 64: "exact-f32 kernels",
-              128: "k_attention", 256: "k_gl4 MODE 4 small-batch fused tile",
-              512: "k_gl4f fused layer (GEMM + mixing, one launch)",
-              1024: "k_attention_mix (to_qkv mixing inside the attention kernel)"}
+              128: "k_attention", 1024: "k_attention_mix (to_qkv mixing inside the attention kernel)"}
 SD_STATUS_F16_RANGE = 1
-SD_STATUS_FUSE_TIMEOUT = 2
 
 
 class SDPlanDesc(ctypes.Structure):

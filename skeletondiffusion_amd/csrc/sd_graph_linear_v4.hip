@@ -53,14 +53,6 @@ struct VmCnt4 {
 
 __device__ __forceinline__ floatx4 g4(const float* p) { return *reinterpret_cast<const floatx4*>(p); }
 
-// A 16-B global load the compiler does not track: while an LDS-DMA is in flight hipcc drains it
-// with vmcnt(0) at the first use of any ordinary load's result, which would serialise a
-// pipeline that keeps x two chunks ahead.  Loads issued this way are waited for by hand
-// (s_waitcnt vmcnt(N) + a register fence, k_gl4 XP = 1).
-__device__ __forceinline__ void g4_async(floatx4& d, const float* p) {
-    asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(d) : "v"(p) : "memory");
-}
-
 // tanh(x) = 1 - 2 / (exp(2x) + 1) on v_exp_f32 + v_rcp_f32 (no IEEE division sequence):
 // saturates cleanly at +-1, within ~3e-7 absolute of tanhf
 __device__ __forceinline__ float tanh4(float x) {
@@ -401,83 +393,43 @@ __global__ __launch_bounds__(256) void k_gl4y(const GLArgs p, int ntile_c, int64
 // at CT = 6 vs 2.2 B in the one-kernel k_gl4 32 x 64 tile).  Per accumulator element the MFMA
 // sequence (x_hi W'_hi, x_hi W'_lo, x_lo W'_hi per chunk), RMS sum, scale and bias arithmetic are
 // k_gl4's, so phase 2 (k_gl4 MODE 2 / 3) reproduces the one-kernel route bit for bit.
-// WRES (resident weights, K = 192): the workgroup copies the node's whole weight slice for its CT
-// tiles (NCH chunks, 144 KiB at CT = 6) into LDS once, then every wave runs its K loop with no
-// barrier at all; NWV waves = NWV consecutive 32-row tiles.  Same products in the same order.
-#ifdef SD_GL4T_STAMPS
-// diagnostic build only (tools/gl4t_stamps.py): per workgroup of the N = 192, K = 192 launches,
-// s_memrealtime at entry, after the K loop, after the Y stores, and the CU id; overwritten by
-// every such launch (the last one of a forward is read back)
-__device__ unsigned long long g_gl4t_stamps[8192 * 4];
-__device__ unsigned long long g_gl4t_clock[8192 * 2];  // shader clock (s_memtime) at entry and loop end
-__device__ unsigned long long g_gl4t_chunk[8192 * 16];  // per workgroup: s_memrealtime after each chunk's barrier
-#endif
-// RSTG: the round-3 K loop (weights register-staged into two LDS stages one chunk ahead, x in a
-// PF-deep register ring; 24 KiB of LDS at CT = 6 against the LDS-DMA ring's 60 KiB)
-// ILV: per chunk every weight fragment read from LDS first, then the MFMAs product-major (x_hi W_hi
-// for all CT tiles, then x_hi W_lo, then x_lo W_hi): each accumulator sees the same three products
-// in the same order (bitwise equal), but no tile waits on its own LDS read behind the previous
-// tile's MFMAs and consecutive MFMAs are independent
-// FF (the LDS-DMA ring with x by DMA only): fill(c + PF) issued right after chunk c's barrier,
-// before chunk c's LDS reads and MFMAs (its slot, chunk c - 1's, is free there), so PF chunks of
-// work cover each fill instead of PF - 1
-// LDW (with the ring, x by DMA): one extra loader wave issues every fill (the slice's weight pieces
-// and the NWV x images) PF chunks ahead and waits for them; the NWV compute waves issue no global
-// memory operation in the K loop (LDS reads and MFMAs only), one barrier per chunk for all
-// NU > 1 (the ring with x by DMA, fill first): each workgroup runs NU units -- NU consecutive
-// column groups of one (row group, node), i.e. the same x -- as one continuous ring of NU * NCH
-// chunks; a unit's Y leaves through its own LDS transposes right after its last chunk while the
-// next unit's first chunks are already in flight, so the store tail and the fill prologue of all
-// but the first unit overlap the K loop (to_qkv: 4 column groups per node)
-// LDS bytes of one k_gl4t workgroup (the fused layer kernel k_gl4f carves two of them)
-template <int PREC, int CT, int NCH, int PF, int NWV, bool WRES, bool RSTG, int NU>
+// K loop (round 4, measured forms in DESIGN.md §4i / §4j; the rejected ones -- register-staged
+// weights, resident weights, product-major MFMA order, a loader wave, multi-unit workgroups, three
+// chunks ahead -- live in git history before round 6): an LDS-DMA ring of PF + 1 slots; chunk c's
+// weight slice AND its x image go to slot c % NS by global_load_lds_dwordx4, PF chunks ahead; each
+// chunk's fill c + PF is issued right after its barrier, before its LDS reads and MFMAs ("fill
+// first"), so PF chunks of work cover every fill.  bf16 operands (PREC 2) are their own A fragments
+// and stay in a PF-deep register ring.
+template <int PREC, int CT, int NCH>
 constexpr int gl4t_smem_bytes() {
-    constexpr int TILE_H = PREC ? 512 : 1024, TS = 36, NS = PF + 1;
-    constexpr bool XDMA = !WRES && !RSTG && PREC != 2;
-    constexpr int XSB = XDMA ? NS * NWV * 2048 : 0;
-    constexpr int SBW = (WRES ? NCH : RSTG ? 2 : NS) * CT * TILE_H * 2 + XSB;
-    constexpr int SBT = NU > 1 ? SBW + NWV * 32 * TS * 4 + 2048 : SBW;
-    return SBT > NWV * 32 * TS * 4 ? SBT : NWV * 32 * TS * 4;
+    constexpr int TILE_H = PREC ? 512 : 1024, TS = 36, NWV = 4, NS = 3;
+    constexpr int XSB = PREC != 2 ? NS * NWV * 2048 : 0;
+    constexpr int SBW = NS * CT * TILE_H * 2 + XSB;
+    return SBW > NWV * 32 * TS * 4 ? SBW : NWV * 32 * TS * 4;
 }
 
-// The workgroup's work: unit u = (node j, row group, column group), tid = thread within the
-// workgroup's NWV (+ LDW) waves, smem_raw = its gl4t_smem_bytes of LDS.  k_gl4t derives u from
-// blockIdx; k_gl4f (the fused layer) runs two such bodies side by side in one 8-wave workgroup --
-// every barrier below is reached the same number of times by both halves (same template, same
-// chunk count; dead waves join barriers).
-template <bool RMS, int PREC, int CT, int NCH, bool ROWMAJOR, int PF = 2, int NWV = 4, bool WRES = false, bool RSTG = false,
-          bool ILV = false, bool FF = false, bool LDW = false, int NU = 1>
+// The workgroup's work: unit u = (node j, row group, column group); smem_raw = its
+// gl4t_smem_bytes of LDS.
+template <bool RMS, int PREC, int CT, int NCH, bool ROWMAJOR>
 __device__ __forceinline__ void gl4t_body(const GLArgs& p, int ncg, int64_t ntile_r, const YOut& yo, const int64_t u,
                                           const int tid, char* __restrict__ smem_raw) {
-    constexpr int NT = NWV * 64;  // compute threads (the loader wave, LDW, is wave NWV)
+    constexpr int PF = 2;                       // chunks in flight
+    constexpr int NWV = 4;                      // waves = 32-row tiles per workgroup
+    constexpr int NT = NWV * 64;
     constexpr int TILE_H = PREC ? 512 : 1024;   // halves of one 32-column tile per chunk
     constexpr int PPT = TILE_H / 8;             // 16-B pieces per tile
-    constexpr int NP = (CT * PPT + NT - 1) / NT;  // staged pieces per thread
     constexpr int TS = 36;                      // floats per row of a wave's 32 x 32 output transpose
-    constexpr int NS = PF + 1;                  // LDS-DMA weight ring: chunk c in slot c % NS
+    constexpr int NS = PF + 1;                  // LDS-DMA ring: chunk c in slot c % NS
     // x through the LDS-DMA ring too (f32 operands): per slot and wave the chunk's 32 rows x 16 k
     // image (2 KiB) -- no register-writing global load in the K loop, so the compiler inserts no
     // vmcnt of its own (with a tracked x load beside an LDS-DMA it drained vmcnt(0) every chunk)
-    constexpr bool XDMA = !WRES && !RSTG && PREC != 2;
-    constexpr int XSB = XDMA ? NS * NWV * 2048 : 0;  // bytes of the x slots (after the weight slots)
-    constexpr int SBW = (WRES ? NCH : RSTG ? 2 : NS) * CT * TILE_H * 2 + XSB;
-    // NU > 1: transposes of their own, then two 1-KiB bias slots (unit u's bias in slot u & 1)
-    constexpr int SBT = NU > 1 ? SBW + NWV * 32 * TS * 4 + 2048 : SBW;
-    constexpr int SB = SBT > NWV * 32 * TS * 4 ? SBT : NWV * 32 * TS * 4;
-    static_assert(!WRES || SB <= 160 * 1024, "resident weight slice exceeds the LDS");
-    static_assert(SB == gl4t_smem_bytes<PREC, CT, NCH, PF, NWV, WRES, RSTG, NU>(), "LDS carve");
+    constexpr bool XDMA = PREC != 2;
+    constexpr int SB = gl4t_smem_bytes<PREC, CT, NCH>();
+    static_assert(SB >= NS * CT * TILE_H * 2 + (XDMA ? NS * NWV * 2048 : 0), "LDS carve");
     _Float16(*sW)[CT * TILE_H] = reinterpret_cast<_Float16(*)[CT * TILE_H]>(smem_raw);
     const int lane = tid & 63, l32 = lane & 31, h = lane >> 5;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int J = p.J;
-#ifdef SD_GL4T_STAMPS
-    constexpr bool STAMP = CT == 6 && NCH == 12 && !RMS && PREC == 0 && !ROWMAJOR;
-    unsigned long long st0 = 0, ck0 = 0;
-    if (STAMP && tid == 0) {
-        st0 = wall_clock64();
-        ck0 = clock64();
-    }
-#endif
     // node-major order: column group fastest (the ncg workgroups sharing one x tile), then row
     // groups, then nodes, so an XCD's contiguous share of u holds one or two nodes' weights
     // (N = 768: 5.9 MB of split weights for all 10 types did not fit a 4 MB L2 when every XCD
@@ -487,7 +439,7 @@ __device__ __forceinline__ void gl4t_body(const GLArgs& p, int ncg, int64_t ntil
     const int j = (int)((u / ncg) / nrg);
     const int64_t rgi = (u / ncg) % nrg;
     const int64_t tr = rgi * NWV + wave;
-    const bool live = tr < ntile_r && !(LDW && wave == NWV);  // wave-uniform; a dead wave still joins barriers
+    const bool live = tr < ntile_r;  // wave-uniform; a dead wave still joins barriers
     const int64_t row0 = (live ? tr : 0) * 32;
     constexpr int nchunk = NCH;
     const int64_t arow = row0 + l32;
@@ -497,7 +449,7 @@ __device__ __forceinline__ void gl4t_body(const GLArgs& p, int ncg, int64_t ntil
     const float* x2r = !p.K2 ? nullptr
                              : p.x2_blk ? p.x2 + blk_off(arow, j, 8 * h, J, p.K2) : p.x2 + ac * p.x2_rs + (int64_t)j * p.K2 + 8 * h;
     floatx4 xa[PF], xb[PF];
-    auto issue_x = [&](int c, int sl) {
+    auto issue_x = [&](int c, int sl) {  // PREC 2: the chunk's A operand into register slot sl
         const int k0 = c << 4;
         const float* src;
         int step4;
@@ -508,18 +460,13 @@ __device__ __forceinline__ void gl4t_body(const GLArgs& p, int ncg, int64_t ntil
             src = p.x2_blk ? x2r + ((k0 - p.K1) << 5) : x2r + (k0 - p.K1);
             step4 = p.x2_blk ? 128 : 4;
         }
-        if constexpr (PREC == 2) {
-            // a bf16 operand: its 8 k values (16 B) are the A fragment itself; the same two loads
-            // on both paths (selected addresses, no branch), so the waitcnt pass keeps the ring
-            const bool bsrc = k0 < p.K1 ? p.x1_bf16 : p.x2_bf16;
-            const float* base = k0 < p.K1 ? p.x1 : p.x2;
-            const float* qb = reinterpret_cast<const float*>(reinterpret_cast<const __bf16*>(base) + (src - base));
-            xa[sl] = g4(bsrc ? qb : src);
-            xb[sl] = g4(bsrc ? qb : src + step4);
-        } else {
-            xa[sl] = g4(src);
-            xb[sl] = g4(src + step4);
-        }
+        // a bf16 operand: its 8 k values (16 B) are the A fragment itself; the same two loads on
+        // both paths (selected addresses, no branch), so the waitcnt pass keeps the ring
+        const bool bsrc = k0 < p.K1 ? p.x1_bf16 : p.x2_bf16;
+        const float* base = k0 < p.K1 ? p.x1 : p.x2;
+        const float* qb = reinterpret_cast<const float*>(reinterpret_cast<const __bf16*>(base) + (src - base));
+        xa[sl] = g4(bsrc ? qb : src);
+        xb[sl] = g4(bsrc ? qb : src + step4);
     };
     floatx16 acc[CT];
 #pragma unroll
@@ -529,12 +476,10 @@ __device__ __forceinline__ void gl4t_body(const GLArgs& p, int ncg, int64_t ntil
     float ss = 0.f, amx = 0.f;
     // the epilogue's bias, loaded before the K loop: loaded per tile in the epilogue, each load was
     // the youngest memory op and its vmcnt(0) also waited for the previous tile's stores -- CT
-    // serial memory round trips in the store tail (NU > 1 brings its units' bias by LDS-DMA)
+    // serial memory round trips in the store tail
     float bvp[CT];
-    if constexpr (NU == 1) {
 #pragma unroll
-        for (int ct = 0; ct < CT; ++ct) bvp[ct] = p.bias ? p.bias[p.wrow[j] + (cg * CT + ct) * 32 + l32] : 0.f;
-    }
+    for (int ct = 0; ct < CT; ++ct) bvp[ct] = p.bias ? p.bias[p.wrow[j] + (cg * CT + ct) * 32 + l32] : 0.f;
     auto compute = [&](int c, int sl, const _Float16* wst) {  // wst: the chunk's CT tiles in LDS
         if constexpr (PREC == 2) {  // bf16 mode: one bf16 product per k step (k_gl4 PREC 2's arithmetic)
             const bool bsrc = (c << 4) < p.K1 ? p.x1_bf16 : p.x2_bf16;  // wave-uniform
@@ -570,23 +515,6 @@ __device__ __forceinline__ void gl4t_body(const GLArgs& p, int ncg, int64_t ntil
         halfx8 xl;
         if constexpr (!PREC) xl = __builtin_convertvector(f - __builtin_convertvector(xh, floatx8), halfx8);
         const _Float16* wt = wst + lane * 8;
-        if constexpr (ILV) {
-            halfx8 wh[CT], wl[CT];
-#pragma unroll
-            for (int ct = 0; ct < CT; ++ct) {
-                wh[ct] = *reinterpret_cast<const halfx8*>(wt + ct * TILE_H);
-                if constexpr (!PREC) wl[ct] = *reinterpret_cast<const halfx8*>(wt + ct * TILE_H + 512);
-            }
-#pragma unroll
-            for (int ct = 0; ct < CT; ++ct) acc[ct] = __builtin_amdgcn_mfma_f32_32x32x16_f16(xh, wh[ct], acc[ct], 0, 0, 0);
-            if constexpr (!PREC) {
-#pragma unroll
-                for (int ct = 0; ct < CT; ++ct) acc[ct] = __builtin_amdgcn_mfma_f32_32x32x16_f16(xh, wl[ct], acc[ct], 0, 0, 0);
-#pragma unroll
-                for (int ct = 0; ct < CT; ++ct) acc[ct] = __builtin_amdgcn_mfma_f32_32x32x16_f16(xl, wh[ct], acc[ct], 0, 0, 0);
-            }
-            return;
-        }
 #pragma unroll
         for (int ct = 0; ct < CT; ++ct) {
             const halfx8 wh = *reinterpret_cast<const halfx8*>(wt + ct * TILE_H);
@@ -599,106 +527,6 @@ __device__ __forceinline__ void gl4t_body(const GLArgs& p, int ncg, int64_t ntil
             acc[ct] = t;
         }
     };
-    if constexpr (WRES) {
-        // x of the first PF chunks in flight, then the whole weight slice [chunk][tile][piece] to
-        // LDS in batches of 8 pieces per thread (unconditional clamped loads), one barrier, and a
-        // K loop without barriers
-#pragma unroll
-        for (int i = 0; i < PF; ++i) issue_x(i, i);
-        constexpr int TOT = NCH * CT * PPT, PER = (TOT + NT - 1) / NT, BATCH = 8;
-        const _Float16* wb = p.wsp + ((int64_t)p.ntype[j] * nchunk * p.wsp_nct + cg * CT) * 1024;
-        uint4* dst = reinterpret_cast<uint4*>(smem_raw);
-#pragma unroll
-        for (int b0 = 0; b0 < PER; b0 += BATCH) {
-            uint4 v[BATCH];
-#pragma unroll
-            for (int i = 0; i < BATCH; ++i) {
-                const int q = min(tid + NT * (b0 + i), TOT - 1);
-                const int c = q / (CT * PPT), r = q % (CT * PPT);
-                v[i] = *reinterpret_cast<const uint4*>(wb + ((int64_t)c * p.wsp_nct + r / PPT) * 1024 + (r % PPT) * 8);
-            }
-#pragma unroll
-            for (int i = 0; i < BATCH; ++i)
-                if (tid + NT * (b0 + i) < TOT) dst[tid + NT * (b0 + i)] = v[i];
-        }
-        __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this thread's pieces are in LDS
-        asm volatile("" ::: "memory");
-        __builtin_amdgcn_s_barrier();
-        asm volatile("" ::: "memory");
-        const _Float16* sw = reinterpret_cast<const _Float16*>(smem_raw);
-        if (live) {
-            if constexpr (PF == NCH) {  // every x chunk already in flight
-#pragma unroll
-                for (int c = 0; c < NCH; ++c) compute(c, c, sw + c * (CT * TILE_H));
-            } else {
-#pragma nounroll
-                for (int c0 = 0; c0 < nchunk; c0 += PF) {
-#pragma unroll
-                    for (int i = 0; i < PF; ++i) {
-                        const int c = c0 + i;
-                        compute(c, i, sw + c * (CT * TILE_H));
-                        asm volatile("" ::: "memory");
-                        issue_x(min(c + PF, nchunk - 1), i);
-                    }
-                }
-            }
-        }
-    } else if constexpr (RSTG) {
-    // staged pieces: piece q of a chunk = tile q / PPT, 16-B piece q % PPT of it
-    const _Float16* wsrc[NP];
-#pragma unroll
-    for (int k = 0; k < NP; ++k) {
-        const int q = min(tid + NT * k, CT * PPT - 1);
-        wsrc[k] = p.wsp + ((int64_t)p.ntype[j] * nchunk * p.wsp_nct + cg * CT + q / PPT) * 1024 + (q % PPT) * 8;
-    }
-    const int64_t wcs = (int64_t)p.wsp_nct * 1024;  // halves per chunk
-    // the carried pieces as named registers, loaded unconditionally from clamped sources (an
-    // array under conditional loads was placed in scratch, with a vmcnt(0) before every store)
-    static_assert(NP <= 4, "staged pieces per thread");
-    uint4 w0, w1, w2, w3;
-    auto load_w = [&](int c) {
-        const int64_t o = c * wcs;
-        w0 = *reinterpret_cast<const uint4*>(wsrc[0] + o);
-        if constexpr (NP > 1) w1 = *reinterpret_cast<const uint4*>(wsrc[1] + o);
-        if constexpr (NP > 2) w2 = *reinterpret_cast<const uint4*>(wsrc[2] + o);
-        if constexpr (NP > 3) w3 = *reinterpret_cast<const uint4*>(wsrc[3] + o);
-    };
-    auto store_w = [&](int sl) {
-        uint4* d = reinterpret_cast<uint4*>(&sW[sl][tid * 8]);
-        constexpr bool FULL = CT * PPT % NT == 0;
-        if (FULL || tid < CT * PPT) d[0] = w0;
-        if constexpr (NP > 1) if (FULL || tid + NT < CT * PPT) d[NT] = w1;
-        if constexpr (NP > 2) if (FULL || tid + 2 * NT < CT * PPT) d[2 * NT] = w2;
-        if constexpr (NP > 3) if (FULL || tid + 3 * NT < CT * PPT) d[3 * NT] = w3;
-    };
-    load_w(0);
-#pragma unroll
-    for (int i = 0; i < PF; ++i) issue_x(i, i);
-    // chunk c: weights of c (loaded one chunk earlier, older than every x load in flight) ->
-    // stage c & 1 (free: every wave passed barrier c - 1 after its reads of chunk c - 2) ->
-    // lgkmcnt(0) + s_barrier (not __syncthreads(): its fence would drain the x loads in flight)
-    // -> weights of c + 1 to registers -> MFMAs on c -> x of c + PF into the freed ring slot
-    static_assert(NCH % PF == 0 && PF % 2 == 0, "ring slot and stage parity fixed per unrolled position");
-#pragma nounroll
-    for (int c0 = 0; c0 < nchunk; c0 += PF) {
-#pragma unroll
-        for (int i = 0; i < PF; ++i) {
-            const int c = c0 + i;
-            store_w(i & 1);
-            __builtin_amdgcn_s_waitcnt(0xC07F);
-            asm volatile("" ::: "memory");
-            __builtin_amdgcn_s_barrier();
-            asm volatile("" ::: "memory");
-            // unconditional loads (past the end: a clamped, unused chunk): a branch around them
-            // made the waitcnt pass merge both paths and drain the x ring every chunk
-            load_w(min(c + 1, nchunk - 1));
-            asm volatile("" ::: "memory");  // keep w(c + 1) older than x(c + PF): store_w(c + 1) waits for it alone
-            compute(c, i, sW[i & 1]);
-            asm volatile("" ::: "memory");
-            if constexpr (PF < NCH) issue_x(min(c + PF, nchunk - 1), i);
-        }
-    }
-    } else {
     // LDS-DMA weight ring (round 4; tools/gl4t_probe.hip): chunk c's weight slice goes straight
     // to slot c % NS by global_load_lds_dwordx4 (no VGPRs, no ds_write), issued PF chunks ahead
     // together with that chunk's x loads, so the loads of every chunk are issued in chunk order and
@@ -752,213 +580,24 @@ __device__ __forceinline__ void gl4t_body(const GLArgs& p, int ncg, int64_t ntil
         xa[0] = *reinterpret_cast<const floatx4*>(xs);
         xb[0] = *reinterpret_cast<const floatx4*>(xs + 128);
     };
-    static_assert(PF >= 1 && PF <= 4 && OPA * (PF - 1) < 64, "vmcnt range");
+    static_assert(OPA * (PF - 1) < 64, "vmcnt range");
     auto wait_chunk = [&](int younger) {  // all but the ops of `younger` later chunks done (folds per unrolled step)
     // vmcnt(ops of the younger chunks) AND lgkmcnt(0): every LDS read this wave issued for the
     // previous chunk has returned before it arrives, so a fill issued after the barrier into that
     // chunk's slot cannot overtake a read still in flight (the compiler may schedule the last
     // MFMAs' fragment waits past the barrier otherwise)
-#define SD_WAITN(n)                                                                     \
-    if (wa) __builtin_amdgcn_s_waitcnt(VmCnt4<OPA * (n)>::imm & ~(0xF << 8));           \
-    else __builtin_amdgcn_s_waitcnt(VmCnt4<OPB * (n)>::imm & ~(0xF << 8));
-        if (younger == 0) { SD_WAITN(0) }
-        else if (younger == 1) { SD_WAITN(1) }
-        else if (younger == 2) { SD_WAITN(2 < PF ? 2 : 0) }
-        else { SD_WAITN(3 < PF ? 3 : 0) }
-#undef SD_WAITN
+        if (younger == 0) {
+            if (wa) __builtin_amdgcn_s_waitcnt(VmCnt4<0>::imm & ~(0xF << 8));
+            else __builtin_amdgcn_s_waitcnt(VmCnt4<0>::imm & ~(0xF << 8));
+        } else {
+            if (wa) __builtin_amdgcn_s_waitcnt(VmCnt4<OPA>::imm & ~(0xF << 8));
+            else __builtin_amdgcn_s_waitcnt(VmCnt4<OPB>::imm & ~(0xF << 8));
+        }
         asm volatile("" ::: "memory");
         __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
     };
     static_assert(NCH % PF == 0 && NCH >= 2 * PF, "ring positions fixed per unrolled step");
-    if constexpr (NU > 1) {
-        static_assert(XDMA && !LDW, "multi-unit workgroups: the ring with x by DMA");
-        constexpr int G = NU * NCH;
-        float* const sTd = reinterpret_cast<float*>(smem_raw + SBW) + wave * 32 * TS;
-        // the bias of a unit rides in with its first chunk (one 4-B LDS-DMA per wave: columns
-        // 64 w + lane, clamped): a register load of it in the epilogue would be the youngest
-        // vector-memory op, and waiting for it drained the ring (vmcnt(0) per tile)
-        float* const sBias = reinterpret_cast<float*>(smem_raw + SBW + NWV * 32 * TS * 4);
-        static_assert(CT * 32 <= NWV * 64 && NWV * 64 <= 256, "one bias slot: one 4-B DMA per wave");
-        const _Float16* const wtu = p.wsp + ((int64_t)p.ntype[j] * nchunk * p.wsp_nct + cg * NU * CT) * 1024;
-        auto gfill = [&](int g) {  // global chunk g = unit g / NCH, chunk g % NCH
-            const int uu = g / NCH, c = g - uu * NCH;
-            _Float16* dst = sW[g % NS];
-            const _Float16* w0 = wtu + (int64_t)uu * CT * 1024;
-#pragma unroll
-            for (int k = 0; k < (NPC / 64 + NWV - 1) / NWV; ++k) {
-                const int q0 = wave * 64 + NT * k;
-                if (q0 >= NPC) continue;  // wave-uniform
-                const int q = q0 + lane;
-                const _Float16* src = w0 + ((int64_t)c * p.wsp_nct + q / PPT) * 1024 + (q % PPT) * 8;
-                __builtin_amdgcn_global_load_lds((const void*)src, (lds_void*)(dst + (size_t)q0 * 8), 16, 0, 0);
-            }
-            float* xd = xs0 + (g % NS) * (NWV * 512);
-            __builtin_amdgcn_global_load_lds((const void*)xsrc(c, 0), (lds_void*)xd, 16, 0, 0);
-            __builtin_amdgcn_global_load_lds((const void*)xsrc(c, 1), (lds_void*)(xd + 256), 16, 0, 0);
-            if (c == 0 && p.bias) {  // wave-uniform; one more op on a unit's first chunk keeps every wait conservative
-                const int col = wave * 64 + lane;
-                const float* bs = p.bias + p.wrow[j] + (cg * NU + uu) * CT * 32 + (col < CT * 32 ? col : 0);
-                __builtin_amdgcn_global_load_lds((const void*)bs, (lds_void*)(sBias + (uu & 1) * 256 + wave * 64), 4, 0, 0);
-            }
-        };
-        auto gstep = [&](int g) {  // chunk g's work, then unit g / NCH's Y after its last chunk
-            const int uu = g / NCH, c = g - uu * NCH;
-            const float* xs = xs0 + (g % NS) * (NWV * 512) + h * 256 + l32 * 4;
-            xa[0] = *reinterpret_cast<const floatx4*>(xs);
-            xb[0] = *reinterpret_cast<const floatx4*>(xs + 128);
-            compute(c, 0, sW[g % NS]);
-            if (c != NCH - 1) return;  // wave-uniform
-            if (live) {
-                const bool oor = __builtin_amdgcn_ballot_w64(amx >= 65504.0f) != 0;  // wave-uniform
-                float sc[16];
-#pragma unroll
-                for (int r = 0; r < 16; ++r) sc[r] = p.wsp_unscale;
-                if (RMS) {
-                    const float t = ss + __shfl_xor(ss, 32);
-#pragma unroll
-                    for (int r = 0; r < 16; ++r) {
-                        const float n2 = __shfl(t, (r & 3) + 8 * (r >> 2) + 4 * h);
-                        sc[r] *= 1.0f / fmaxf(sqrtf(n2), 1e-12f);
-                    }
-                }
-                const int cgu = cg * NU + uu;
-                float* y = yo.y + tr * yo.y_ts + j * yo.y_js + (int64_t)cgu * CT * yo.y_cs;
-                auto store_tile = [&](int ct, const floatx16& v) {
-                    const float bv = p.bias ? sBias[(uu & 1) * 256 + ct * 32 + l32] : 0.f;  // LDS: any ct
-#pragma unroll
-                    for (int r = 0; r < 16; ++r) sTd[((r & 3) + 8 * (r >> 2) + 4 * h) * TS + l32] = v[r] * sc[r] + bv;
-                    __builtin_amdgcn_wave_barrier();
-#pragma unroll
-                    for (int q = 0; q < 4; ++q) {
-                        const int row = 8 * q + (lane >> 3), c4 = (lane & 7) * 4;
-                        const floatx4 o = *reinterpret_cast<const floatx4*>(sTd + row * TS + c4);
-                        if (!ROWMAJOR || row0 + row < p.B)
-                            *reinterpret_cast<floatx4*>(y + (int64_t)row * yo.y_rs + ct * yo.y_cs + c4) = o;
-                    }
-                    __builtin_amdgcn_wave_barrier();
-                };
-#pragma unroll
-                for (int ct = 0; ct < CT; ++ct) store_tile(ct, acc[ct]);
-                if (oor) {  // f16 range left: the unit's tiles again on exact-f32 MFMA (as the main epilogue)
-                    if (p.status && lane == 0) atomicOr(p.status, 1u);
-#pragma nounroll
-                    for (int ct = 0; ct < CT; ++ct) store_tile(ct, exact_tile_f32(p, row0, j, (cgu * CT + ct) * 32));
-                }
-            }
-#pragma unroll
-            for (int ct = 0; ct < CT; ++ct)
-#pragma unroll
-                for (int e = 0; e < 16; ++e) acc[ct][e] = 0.f;
-            ss = 0.f;
-            amx = 0.f;
-        };
-        // every wait counts only the younger fills; where a unit's stores were issued since (one
-        // chunk per unit), the wait also covers them -- a conservative, correct count
-#pragma unroll
-        for (int i = 0; i < PF; ++i) gfill(i);
-#pragma nounroll
-        for (int g = 0; g < G - PF; ++g) {
-            wait_chunk(PF - 1);
-            gfill(g + PF);
-            asm volatile("" ::: "memory");
-            gstep(g);
-            asm volatile("" ::: "memory");
-        }
-#pragma unroll
-        for (int i = 0; i < PF; ++i) {
-            wait_chunk(PF - 1 - i);
-            gstep(G - PF + i);
-            asm volatile("" ::: "memory");
-        }
-        return;
-    } else if constexpr (LDW && XDMA) {
-        // loader wave: every fill; compute waves: LDS and MFMA only.  Chunk c: the loader has
-        // waited for fill(c) (vmcnt = the ops of the younger fills in flight), every compute wave
-        // for its LDS reads of chunk c - 1 (lgkmcnt(0)); one barrier; the loader refills chunk
-        // c - 1's slot with chunk c + PF while the compute waves work on chunk c.
-        constexpr int OPL = NPC / 64 + 2 * NWV;  // DMA instructions per fill
-        static_assert(OPL * (PF - 1) < 64, "vmcnt range");
-        if (wave == NWV) {
-            const int64_t rg0 = rgi * NWV;
-            const float* lb1[NWV];
-            const float* lb2[NWV];
-#pragma unroll
-            for (int w = 0; w < NWV; ++w) {  // compute wave w's x bases (feature 4 h of chunk 0)
-                const int64_t ar = (rg0 + w < ntile_r ? rg0 + w : 0) * 32 + l32;
-                const int64_t a2 = ar < p.B ? ar : 0;
-                lb1[w] = p.x1_blk ? p.x1 + blk_off(ar, j, 4 * h, J, p.K1)
-                                  : p.x1 + ((a2 + p.x1_row0) / p.x1_div) * p.x1_rs + (int64_t)j * p.K1 + 4 * h;
-                lb2[w] = !p.K2 ? lb1[w]
-                               : p.x2_blk ? p.x2 + blk_off(ar, j, 4 * h, J, p.K2) : p.x2 + a2 * p.x2_rs + (int64_t)j * p.K2 + 4 * h;
-            }
-            auto lfill = [&](int c) {
-                _Float16* dst = sW[c % NS];
-#pragma unroll
-                for (int k = 0; k < NPC / 64; ++k) {
-                    const int q = 64 * k + lane;
-                    const _Float16* src = wt0 + ((int64_t)c * p.wsp_nct + q / PPT) * 1024 + (q % PPT) * 8;
-                    __builtin_amdgcn_global_load_lds((const void*)src, (lds_void*)(dst + (size_t)(64 * k) * 8), 16, 0, 0);
-                }
-                float* xslot = reinterpret_cast<float*>(smem_raw + NS * CT * TILE_H * 2) + (c % NS) * (NWV * 512);
-#pragma unroll
-                for (int w = 0; w < NWV; ++w) {
-                    // the two bases as values before the select (a select between the two array
-                    // elements' addresses kept the arrays on the stack: scratch loads, counted in vmcnt)
-                    const float* v1 = lb1[w];
-                    const float* v2 = lb2[w];
-                    asm volatile("" : "+v"(v1), "+v"(v2));
-                    const float* b = c < c1 ? v1 + (int64_t)c * cs1 : v2 + (int64_t)(c - c1) * cs2;
-                    const int ks = c < c1 ? ks1 : ks2;
-                    __builtin_amdgcn_global_load_lds((const void*)b, (lds_void*)(xslot + w * 512), 16, 0, 0);
-                    __builtin_amdgcn_global_load_lds((const void*)(b + ks), (lds_void*)(xslot + w * 512 + 256), 16, 0, 0);
-                }
-            };
-            auto lwait = [&](int younger) {
-                if (younger == 0) __builtin_amdgcn_s_waitcnt(VmCnt4<0>::imm);
-                else if (younger == 1) __builtin_amdgcn_s_waitcnt(VmCnt4<OPL>::imm);
-                else if (younger == 2) __builtin_amdgcn_s_waitcnt(VmCnt4<(2 < PF ? 2 : 0) * OPL>::imm);
-                else __builtin_amdgcn_s_waitcnt(VmCnt4<(3 < PF ? 3 : 0) * OPL>::imm);
-                asm volatile("" ::: "memory");
-                __builtin_amdgcn_s_barrier();
-                asm volatile("" ::: "memory");
-            };
-#pragma unroll
-            for (int i = 0; i < PF; ++i) lfill(i);
-#pragma nounroll
-            for (int c0 = 0; c0 < nchunk - PF; c0 += PF) {
-#pragma unroll
-                for (int i = 0; i < PF; ++i) {
-                    lwait(PF - 1);
-                    lfill(c0 + i + PF);
-                }
-            }
-#pragma unroll
-            for (int i = 0; i < PF; ++i) lwait(PF - 1 - i);
-            // the loader's share of the barrier after the K loop, then done: no accumulator is live
-            // on this path (the register allocator kept them, and spilled the loader's pointers)
-            __syncthreads();
-            return;
-        } else {
-            auto cwait = [&]() {
-                __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this wave's reads of the previous chunk returned
-                asm volatile("" ::: "memory");
-                __builtin_amdgcn_s_barrier();
-                asm volatile("" ::: "memory");
-            };
-#pragma nounroll
-            for (int c0 = 0; c0 < nchunk; c0 += PF) {
-#pragma unroll
-                for (int i = 0; i < PF; ++i) {
-                    const int c = c0 + i;
-                    cwait();
-                    x_lds(c);
-                    compute(c, 0, sW[c % NS]);
-                    asm volatile("" ::: "memory");
-                }
-            }
-        }
-    } else {
 #pragma unroll
     for (int i = 0; i < PF; ++i) {
         fill(i);
@@ -970,25 +609,17 @@ __device__ __forceinline__ void gl4t_body(const GLArgs& p, int ncg, int64_t ntil
         for (int i = 0; i < PF; ++i) {
             const int c = c0 + i;
             wait_chunk(PF - 1);
-#ifdef SD_GL4T_STAMPS
-            if (STAMP && tid == 0 && blockIdx.x < 8192 && c < 16) g_gl4t_chunk[blockIdx.x * 16 + c] = wall_clock64();
-#endif
-            if constexpr (XDMA && FF) {
+            if constexpr (XDMA) {  // fill first: the slot of chunk c - 1 is free after the barrier
                 fill(c + PF);
                 asm volatile("" ::: "memory");
                 x_lds(c);
                 compute(c, 0, sW[c % NS]);
-                continue;
-            }
-            if constexpr (XDMA) {
-                x_lds(c);
-                compute(c, 0, sW[c % NS]);
             } else {
                 compute(c, i, sW[c % NS]);
+                asm volatile("" ::: "memory");
+                fill(c + PF);
+                issue_x(c + PF, i);
             }
-            asm volatile("" ::: "memory");
-            fill(c + PF);
-            if constexpr (!XDMA) issue_x(c + PF, i);
         }
     }
     // the last PF chunks: nothing more to issue, the wait shrinks by one chunk each step
@@ -1003,18 +634,7 @@ __device__ __forceinline__ void gl4t_body(const GLArgs& p, int ncg, int64_t ntil
         }
         asm volatile("" ::: "memory");
     }
-    }  // loader-wave / plain ring
-    }  // staged K loop
     __syncthreads();  // every wave past its last chunk: the stages become the output transposes
-#ifdef SD_GL4T_STAMPS
-    if (STAMP && tid == 0 && blockIdx.x < 8192) {
-        g_gl4t_stamps[blockIdx.x * 4 + 0] = st0;
-        g_gl4t_stamps[blockIdx.x * 4 + 1] = wall_clock64();
-        g_gl4t_stamps[blockIdx.x * 4 + 3] = __smid();
-        g_gl4t_clock[blockIdx.x * 2] = ck0;
-        g_gl4t_clock[blockIdx.x * 2 + 1] = clock64();
-    }
-#endif
     if (!live) return;
     const bool oor = PREC != 2 && __builtin_amdgcn_ballot_w64(amx >= 65504.0f) != 0;  // wave-uniform
     float sc[16];
@@ -1058,24 +678,16 @@ __device__ __forceinline__ void gl4t_body(const GLArgs& p, int ncg, int64_t ntil
             store_tile(ct, exact_tile_f32(p, row0, j, col), p.bias ? p.bias[p.wrow[j] + col + l32] : 0.f);
         }
     }
-#ifdef SD_GL4T_STAMPS
-    if (STAMP && lane == 0 && blockIdx.x < 8192) {
-        __builtin_amdgcn_s_waitcnt(0);  // this wave's stores issued and acknowledged
-        atomicMax(&g_gl4t_stamps[blockIdx.x * 4 + 2], wall_clock64());
-    }
-#endif
 }
 
-template <bool RMS, int PREC, int CT, int NCH, bool ROWMAJOR, int PF = 2, int NWV = 4, bool WRES = false, bool RSTG = false,
-          bool ILV = false, bool FF = false, bool LDW = false, int NU = 1>
-__global__ __launch_bounds__((NWV + (LDW ? 1 : 0)) * 64, WRES ? 1 : 2) void k_gl4t(const GLArgs p, int ncg, int64_t ntile_r, const YOut yo) {
-    __shared__ __attribute__((aligned(16))) char smem_raw[gl4t_smem_bytes<PREC, CT, NCH, PF, NWV, WRES, RSTG, NU>()];
+template <bool RMS, int PREC, int CT, int NCH, bool ROWMAJOR>
+__global__ __launch_bounds__(256, 2) void k_gl4t(const GLArgs p, int ncg, int64_t ntile_r, const YOut yo) {
+    __shared__ __attribute__((aligned(16))) char smem_raw[gl4t_smem_bytes<PREC, CT, NCH>()];
     // XCD-aware order (k_gl4's): consecutive u -- the column groups of one (row group, node), which
     // read the same x -- on one XCD (blocks b, b + 8, ... share one), so x reaches that L2 once
     const int nwg = gridDim.x, xcd = blockIdx.x & 7, q8 = nwg >> 3, r8 = nwg & 7;
     const int64_t u = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (blockIdx.x >> 3);
-    gl4t_body<RMS, PREC, CT, NCH, ROWMAJOR, PF, NWV, WRES, RSTG, ILV, FF, LDW, NU>(p, ncg, ntile_r, yo, u, threadIdx.x,
-                                                                                 smem_raw);
+    gl4t_body<RMS, PREC, CT, NCH, ROWMAJOR>(p, ncg, ntile_r, yo, u, threadIdx.x, smem_raw);
 }
 
 // Epilogue of the fused to_qkv + Attention kernel (MODE 1), J <= 32, dh = 32, 8 waves, a
@@ -1261,22 +873,12 @@ __device__ __forceinline__ void attention_epilogue(const GLArgs& p, floatx16 (&a
 //   row-major): a bf16 operand is its own A fragment (one 16-B load per 8 k).
 // STG 0: weight stages filled by LDS-DMA (global_load_lds_dwordx4); STG 1: register-staged
 //   (global_load_dwordx4 a chunk ahead, ds_write_b128 after the chunk's MFMAs).
-// MODE 4: small-batch fused tile (DESIGN.md §4d'): one workgroup = one 32-row tile x one 32-column
-//   tile x all J nodes, wave w = node w; each wave walks its node's whole K extent with x and
-//   weight fragments straight from memory into registers, PF4 chunks ahead (k_gl4y's loop: no
-//   LDS, no barriers), then the MODE 0 mixing / FiLM / tanh / residual epilogue.  One launch and
-//   no scratch round trip per layer instead of the split route's two; every output element sees
-//   the same products in the same order, so it is bitwise equal to MODE 0 and the split routes.
 // The workgroup's work for virtual block index bx of a grid of nwg (k_gl4 passes blockIdx.x /
-// gridDim.x); smem = its dynamic LDS.  YSC1 (MODE 2 inside the fused layer k_gl4f): the pre-mix Y
-// is read with sc1 loads (past this CU's L1, from the XCD's L2 where the same launch wrote it).
-template <int J, int NW, int RT, int CT, bool RMS, int DBG = 0, int MODE = 0, int XP = 0, int PREC = 0, int STG = 0,
-          bool YSC1 = false>
+// gridDim.x); smem = its dynamic LDS.
+template <int J, int NW, int RT, int CT, bool RMS, int MODE = 0, int PREC = 0, int STG = 0>
 __device__ __forceinline__ void gl4_body(const GLArgs& p, const int bx, const int nwg, float* __restrict__ smem) {
-    static_assert(MODE == 0 || MODE == 2 || MODE == 4 || (CT == 3 && RT == 1 && J <= 32 && NW == 8),
-                  "attention mode: 32 x (q|k|v)");
-    static_assert(MODE < 2 || (RT == 1 && XP == 0 && STG == 0 && DBG == 0), "split-route phase 2: one 32-row tile");
-    static_assert(MODE != 4 || (CT == 1 && PREC != 2), "small-batch fused tile: one 32-column tile, f16 products");
+    static_assert(MODE == 0 || MODE == 2 || (CT == 3 && RT == 1 && J <= 32 && NW == 8), "attention mode: 32 x (q|k|v)");
+    static_assert(MODE < 2 || (RT == 1 && STG == 0), "split-route phase 2: one 32-row tile");
     constexpr bool PH2 = MODE == 2 || MODE == 3;  // split-route phase 2: Y from the scratch, no K loop
     constexpr int NPW = (J + NW - 1) / NW;  // nodes per wave
     constexpr int KS = (J + 3) / 4;         // 4-deep k steps of the mixing GEMM (K = J padded)
@@ -1290,7 +892,6 @@ __device__ __forceinline__ void gl4_body(const GLArgs& p, const int bx, const in
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int l32 = lane & 31, h = lane >> 5, lr = lane & 15, lg = lane >> 4;
     constexpr int TILE_H = PREC ? 512 : 1024;   // halves of one 32-column tile per k chunk (hi | hi+lo)
-    static_assert(PREC != 2 || XP == 0, "bf16 mode: one-chunk-ahead x loads");
     const int stage_h = MODE >= 2 ? 0 : p.ntypes * CT * TILE_H;  // halves per weight stage
     const int wfl = stage_h;                   // two stages of halves = stage_h floats
     constexpr bool ATT = MODE == 1 || MODE == 3;
@@ -1391,8 +992,6 @@ __device__ __forceinline__ void gl4_body(const GLArgs& p, const int bx, const in
     };
 
     floatx16 acc[NPW][RT][CT];
-    uint64_t ts[8];  // DBG 6: phase stamps (s_memrealtime, 100 MHz) + shader clock around the K loop
-    uint64_t cs[5];  // DBG 6: shader-clock stamps inside chunk 5
     if constexpr (PH2) {
         // split-route phase 2: the slab's Y (from phase 1's p.zs), G-hat and FiLM all loaded to
         // registers first (one memory round trip), then to LDS, one barrier
@@ -1419,17 +1018,12 @@ __device__ __forceinline__ void gl4_body(const GLArgs& p, const int bx, const in
         floatx4 yv[NYL];
         float gv[NGL];
         float f0 = 1.0f, f1 = 0.0f;
-        [[maybe_unused]] const __amdgpu_buffer_rsrc_t zrsrc = __builtin_amdgcn_make_buffer_rsrc(p.zs, 0, 0x7fffffff, 0x00020000);
 #pragma unroll
         for (int k = 0; k < NYL; ++k) {
             const int q = tid + k * NTH;
             float* d;
             if (q < YQ) {
-                if constexpr (YSC1)  // aux 16 = sc1: past this CU's L1 (k_gl4f; zs < 2 GiB, checked at launch)
-                    yv[k] = __builtin_bit_cast(floatx4, __builtin_amdgcn_raw_buffer_load_b128(
-                                                            zrsrc, (int)((ysrc(q, d) - p.zs) * 4), 0, 16));
-                else
-                    yv[k] = g4(ysrc(q, d));
+                yv[k] = g4(ysrc(q, d));
             }
         }
         if constexpr (MODE == 2 && RES_EARLY)  // the residual in flight with the slab (one memory latency)
@@ -1492,10 +1086,7 @@ __device__ __forceinline__ void gl4_body(const GLArgs& p, const int bx, const in
                     src = p.x2_blk ? x2r[rt] + (int64_t)jn[m] * p.K2 * 32 + (k2 << 5) : x2r[rt] + (int64_t)jn[m] * p.K2 + k2;
                     step4 = p.x2_blk ? 128 : 4;
                 }
-                if constexpr (XP == 1) {
-                    g4_async(xb.a[m][rt], src);
-                    g4_async(xb.b[m][rt], src + step4);
-                } else if (PREC == 2 && (k0 < p.K1 ? p.x1_bf16 : p.x2_bf16)) {
+                if (PREC == 2 && (k0 < p.K1 ? p.x1_bf16 : p.x2_bf16)) {
                     // 8 bf16 k values (16 B): the A fragment itself, kept bit-exact in `a`; the
                     // element offset of src is that of the f32 layout (row-major)
                     const float* base = k0 < p.K1 ? p.x1 : p.x2;
@@ -1615,27 +1206,18 @@ __device__ __forceinline__ void gl4_body(const GLArgs& p, const int bx, const in
     // is a builtin (not inline asm) so the compiler knows x(c) is complete and inserts no
     // further vmcnt waits before the MFMAs.
     auto step = [&](int c, const XBuf& cur, XBuf& nxt) {
-        if (DBG == 6 && c == 5) cs[0] = clock64();
         __builtin_amdgcn_s_waitcnt(VmCnt4<0>::imm);
-        if (DBG == 6 && c == 5) cs[1] = clock64();
         __builtin_amdgcn_s_barrier();
-        if (DBG == 6 && c == 5) cs[2] = clock64();
         if (c + 1 < nchunk) {
             fill_w(c + 1, (c & 1) ? sW0 : sW1);
             load_x(c + 1, nxt);
         }
-        if (DBG == 6 && c == 5) cs[3] = clock64();
         compute(c, cur);
-        if (DBG == 6 && c == 5) {
-            __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): LDS reads of the MFMAs done
-            cs[4] = clock64();
-        }
 #if defined(SD_DEBUG_LDS) && !defined(SD_DEBUG_NO_GL)
         check_stage(c);
 #endif
     };
 
-    if (DBG == 6) ts[0] = wall_clock64();
     // G-hat and FiLM (scale + 1 | shift) for this workgroup's columns -> LDS, bias -> registers:
     // all read by the epilogue only, after the K loop's barriers
     for (int i = tid; i < J * J; i += NTH) sG[i] = p.G[i];
@@ -1652,90 +1234,7 @@ __device__ __forceinline__ void gl4_body(const GLArgs& p, const int bx, const in
             const int ncol = (MODE == 1 ? (ctile + ct * p.attn_heads) * 32 : c0 + 32 * ct) + l32;
             bv[m][ct] = (p.bias && ncol < p.N) ? p.bias[p.wrow[jn[m]] + ncol] : 0.f;
         }
-    if constexpr (MODE == 4) {
-        // k_gl4y's K loop per wave (node jn[m]), PF4 chunks in flight in registers (16 waves per
-        // workgroup leave 128 registers per wave: 4 chunks of 16 operand registers + the tile)
-        constexpr int PF4 = 4;
-        const int64_t arow = row0 + l32;
-        const int64_t ac = arow < p.B ? arow : 0;
-        const float* xr1[NPW];
-        const float* xr2[NPW];
-        const _Float16* wb[NPW];
-#pragma unroll
-        for (int m = 0; m < NPW; ++m) {
-            const int j = jn[m];
-            xr1[m] = p.x1_blk ? p.x1 + blk_off(arow, j, 8 * h, J, p.K1)
-                              : p.x1 + ((ac + p.x1_row0) / p.x1_div) * p.x1_rs + (int64_t)j * p.K1 + 8 * h;
-            xr2[m] = !p.K2 ? nullptr
-                           : p.x2_blk ? p.x2 + blk_off(arow, j, 8 * h, J, p.K2) : p.x2 + ac * p.x2_rs + (int64_t)j * p.K2 + 8 * h;
-            wb[m] = p.wsp + ((int64_t)p.ntype[j] * nchunk * p.wsp_nct + ctile) * 1024 + lane * 8;
-        }
-        const int64_t wcs = (int64_t)p.wsp_nct * 1024;  // halves per chunk
-        floatx4 ya[PF4][NPW], yb[PF4][NPW];
-        halfx8 wh4[PF4][NPW], wl4[PF4][NPW];
-        // every load unconditional (a node check only where J % NW != 0): a conditionally issued
-        // load makes the waitcnt pass merge paths and wait for (nearly) every load in flight at
-        // each chunk, which is what k_gl4y's loop gets (vmcnt(2) per chunk in its ISA)
-        auto live = [&](int m) { return J % NW == 0 || wave + NW * m < J; };
-        auto issue = [&](int c, int sl) {
-            const int k0 = c << 4;
-#pragma unroll
-            for (int m = 0; m < NPW; ++m) {
-                if (!live(m)) continue;  // wave-uniform
-                const float* src;
-                int step4;
-                if (k0 < p.K1) {
-                    src = p.x1_blk ? xr1[m] + (k0 << 5) : xr1[m] + k0;
-                    step4 = p.x1_blk ? 128 : 4;
-                } else {
-                    src = p.x2_blk ? xr2[m] + ((k0 - p.K1) << 5) : xr2[m] + (k0 - p.K1);
-                    step4 = p.x2_blk ? 128 : 4;
-                }
-                ya[sl][m] = g4(src);
-                yb[sl][m] = g4(src + step4);
-                const _Float16* w = wb[m] + c * wcs;
-                wh4[sl][m] = *reinterpret_cast<const halfx8*>(w);
-                if constexpr (!PREC) wl4[sl][m] = *reinterpret_cast<const halfx8*>(w + 512);
-            }
-        };
-        auto comp = [&](int c, int sl) {  // compute()'s arithmetic for one chunk
-            const bool rms_chunk = RMS && (c << 4) < p.K1;
-#pragma unroll
-            for (int m = 0; m < NPW; ++m) {
-                if (!live(m)) continue;
-                const floatx8 f = {ya[sl][m].x, ya[sl][m].y, ya[sl][m].z, ya[sl][m].w,
-                                   yb[sl][m].x, yb[sl][m].y, yb[sl][m].z, yb[sl][m].w};
-                if (rms_chunk) {
-                    const floatx8 q = f * f;
-                    ss[m][0] += ((q[0] + q[1]) + (q[2] + q[3])) + ((q[4] + q[5]) + (q[6] + q[7]));
-                }
-                const floatx8 a = __builtin_elementwise_abs(f);
-                amx = fmaxf(amx, fmaxf(fmaxf(fmaxf(a[0], a[1]), fmaxf(a[2], a[3])), fmaxf(fmaxf(a[4], a[5]), fmaxf(a[6], a[7]))));
-                const halfx8 xh = __builtin_convertvector(f, halfx8);
-                floatx16 t = acc[m][0][0];
-                t = __builtin_amdgcn_mfma_f32_32x32x16_f16(xh, wh4[sl][m], t, 0, 0, 0);
-                if constexpr (!PREC) {
-                    const halfx8 xl = __builtin_convertvector(f - __builtin_convertvector(xh, floatx8), halfx8);
-                    t = __builtin_amdgcn_mfma_f32_32x32x16_f16(xh, wl4[sl][m], t, 0, 0, 0);
-                    t = __builtin_amdgcn_mfma_f32_32x32x16_f16(xl, wh4[sl][m], t, 0, 0, 0);
-                }
-                acc[m][0][0] = t;
-            }
-        };
-        // nchunk % PF4 == 0 (checked at launch): a main loop that always issues, a last round that
-        // never does
-#pragma unroll
-        for (int i = 0; i < PF4; ++i) issue(i, i);
-        for (int c0 = 0; c0 < nchunk - PF4; c0 += PF4) {
-#pragma unroll
-            for (int i = 0; i < PF4; ++i) {
-                comp(c0 + i, i);
-                issue(c0 + i + PF4, i);
-            }
-        }
-#pragma unroll
-        for (int i = 0; i < PF4; ++i) comp(nchunk - PF4 + i, i);
-    } else if constexpr (STG == 1) {
+    if constexpr (STG == 1) {
         // register-staged weights: the pieces of chunk c+1 this thread carries are loaded right
         // after barrier c (with x(c+1)) and written to the other stage after compute(c); its
         // last reads were in phase c-1, before barrier c.  lgkmcnt(0) + barrier c+1 makes the
@@ -1784,69 +1283,38 @@ __device__ __forceinline__ void gl4_body(const GLArgs& p, const int bx, const in
             step_r(c, X0, X1);
             step_r(c + 1, X1, X0);
         }
-    } else if constexpr (XP == 0) {
+    } else {
         fill_w(0, sW0);
         load_x(0, X0);
         for (int c = 0; c < nchunk; c += 2) {
             step(c, X0, X1);
-            if (DBG == 6 && c == 0) {
-                ts[1] = wall_clock64();
-                ts[6] = clock64();
-            }
             step(c + 1, X1, X0);
         }
-    } else {  // XP 1
-        // x two chunks ahead in three register buffers (hand-waited loads), weights one chunk
-        // ahead in two LDS stages.  Issue order in step c: weight DMA (c+1), then x (c+2); at the
-        // top of step c only x(c+1) -- the last 2*RT*NPW loads issued -- stays in flight.
-        constexpr int NX = 2 * RT * NPW;
-        auto fence = [&](XBuf& xb) {
-#pragma unroll
-            for (int m = 0; m < NPW; ++m)
-#pragma unroll
-                for (int rt = 0; rt < RT; ++rt) asm volatile("" : "+v"(xb.a[m][rt]), "+v"(xb.b[m][rt]));
-        };
-        auto step2 = [&](int c, XBuf& cur, XBuf& nxt2) {
-            if (DBG == 6 && c == 5) cs[0] = clock64();
-            if (c + 1 < nchunk) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NX) : "memory");
-            else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            fence(cur);
-            if (DBG == 6 && c == 5) cs[1] = clock64();
-            __builtin_amdgcn_s_barrier();
-            if (DBG == 6 && c == 5) cs[2] = clock64();
-            if (c + 1 < nchunk) fill_w(c + 1, (c & 1) ? sW0 : sW1);
-            if (c + 2 < nchunk) load_x(c + 2, nxt2);
-            if (DBG == 6 && c == 5) cs[3] = clock64();
-            compute(c, cur);
-            if (DBG == 6 && c == 5) {
-                __builtin_amdgcn_s_waitcnt(0xc07f);
-                cs[4] = clock64();
-            }
-        };
-        fill_w(0, sW0);
-        load_x(0, X0);
-        load_x(1, X1);
-        int c = 0;
-        for (; c + 3 <= nchunk; c += 3) {
-            step2(c, X0, X2);
-            if (DBG == 6 && c == 0) {
-                ts[1] = wall_clock64();
-                ts[6] = clock64();
-            }
-            step2(c + 1, X1, X0);
-            step2(c + 2, X2, X1);
-        }
-        if (c < nchunk) step2(c, X0, X2);
-        if (c + 1 < nchunk) step2(c + 1, X1, X0);
     }
-    if (DBG == 6) ts[7] = clock64();
-    if (DBG == 6) ts[2] = wall_clock64();
-    // f16 range guard: an activation the split cannot represent.  The one-kernel tiles (MODE 0 / 1
-    // / 4: J <= 21 on SD_OPT_SPLIT_ROUTE 1 / 5, half precision's J = 16 full-batch default) only
-    // report it in the status word -- their accumulators stay live into the mixing epilogue, and a
-    // recompute here (inline or called) raised their register counts / spills severalfold; the
-    // split-route GEMM phases k_gl4t / k_gl4y recompute such tiles in exact f32 (exact_tile_f32)
-    if (p.status && __builtin_amdgcn_ballot_w64(amx >= 65504.0f) != 0 && lane == 0) atomicOr(p.status, 1u);
+    // f16 range guard: a wave whose f16 operands reached |x| >= 65504 (x_hi would be inf) recomputes
+    // its tiles on exact-f32 MFMA (exact_tile_f32, the split-route GEMM phases' fallback) before the
+    // epilogue, whatever the f16 precision mode (round 6: the one-kernel tiles -- SD_OPT_SPLIT_ROUTE
+    // 1, a gl4_tile option, half precision's J = 16 full-batch default -- only set the status bit
+    // before).  The branch is wave-uniform and never taken in range, so the in-range arithmetic and
+    // every bitwise route equality are unchanged; with the accumulators live the recompute costs
+    // these tiles registers (spills at J = 17 / 21), which only a wave that left the range executes.
+    if constexpr (PREC != 2) {
+        if (__builtin_amdgcn_ballot_w64(amx >= 65504.0f) != 0) {
+            if (p.status && lane == 0) atomicOr(p.status, 1u);
+#pragma unroll
+            for (int m = 0; m < NPW; ++m) {
+                if (wave + NW * m >= J) continue;  // wave-uniform
+#pragma unroll
+                for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+                    for (int ct = 0; ct < CT; ++ct)
+                        acc[m][rt][ct] = exact_tile_f32(p, row0 + 32 * rt, jn[m],
+                                                        MODE == 1 ? (ctile + ct * p.attn_heads) * 32 : c0 + 32 * ct);
+            }
+        }
+    } else {
+        if (p.status && __builtin_amdgcn_ballot_w64(amx >= 65504.0f) != 0 && lane == 0) atomicOr(p.status, 1u);
+    }
 
     // ---- unscale, RMS, bias in the accumulator layout:
     //      D[row = (r&3) + 8(r>>2) + 4h][col = l32] for register r of a 32x32 tile
@@ -1874,7 +1342,6 @@ __device__ __forceinline__ void gl4_body(const GLArgs& p, const int bx, const in
         }
     }
     }  // MODE < 2: K loop
-    if (DBG == 6) ts[3] = wall_clock64();
 #if defined(SD_DEBUG_LDS) && !defined(SD_DEBUG_NO_G)
     {
         unsigned bad = 0;
@@ -1984,27 +1451,12 @@ __device__ __forceinline__ void gl4_body(const GLArgs& p, const int bx, const in
             }
         }
     }
-    if (DBG == 6) {  // stamps of wave 0 lane 0 -> out[blockIdx * 8 ..] (timing experiment only)
-        ts[4] = wall_clock64();
-        __syncthreads();
-        ts[5] = wall_clock64();
-        if (lane == 0) {  // per wave: chunk-5 phase cycles at out[(nwg * 8) + (blockIdx * NW + wave) * 4]
-            unsigned* q = reinterpret_cast<unsigned*>(p.out) + (size_t)nwg * 8 + ((size_t)bx * NW + wave) * 4;
-            for (int i = 0; i < 4; ++i) q[i] = (unsigned)(cs[i + 1] - cs[i]);
-        }
-        if (tid == 0) {
-            unsigned* o = reinterpret_cast<unsigned*>(p.out) + (size_t)bx * 8;
-            for (int i = 0; i < 6; ++i) o[i] = (unsigned)ts[i];
-            o[6] = __smid();
-            o[7] = (unsigned)(ts[7] - ts[6]);  // shader-clock cycles of chunks 2 .. end
-        }
-    }
 }
 
-template <int J, int NW, int RT, int CT, bool RMS, int DBG = 0, int MODE = 0, int XP = 0, int PREC = 0, int STG = 0>
+template <int J, int NW, int RT, int CT, bool RMS, int MODE = 0, int PREC = 0, int STG = 0>
 __global__ __launch_bounds__(NW * 64, 1) void k_gl4(const GLArgs p) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
-    gl4_body<J, NW, RT, CT, RMS, DBG, MODE, XP, PREC, STG>(p, blockIdx.x, gridDim.x, smem);
+    gl4_body<J, NW, RT, CT, RMS, MODE, PREC, STG>(p, blockIdx.x, gridDim.x, smem);
 }
 
 // v4 weight staging (GLArgs::gl4_stage): 0 = LDS-DMA stages, 1 = register-staged stages (2, a
@@ -2017,21 +1469,21 @@ static int g_gl4_stage = [] {
 }();
 int gl4_stage_default() { return g_gl4_stage; }
 
-template <int J, int NW, int RT, int CT, int DBG = 0, int MODE = 0, int XP = 0, int PREC = 0, int STG = 0>
+template <int J, int NW, int RT, int CT, int MODE = 0, int PREC = 0, int STG = 0>
 static hipError_t gl4_launch_t(const GLArgs& a, bool rms, hipStream_t s);
 
-template <int J, int NW, int RT, int CT, int DBG = 0, int MODE = 0, int XP = 0, int PREC = 0>
+template <int J, int NW, int RT, int CT, int MODE = 0, int PREC = 0>
 static hipError_t gl4_launch(const GLArgs& a, bool rms, hipStream_t s) {
     constexpr int TILE_H = PREC ? 512 : 1024;
     // register staging: not for the J > 16 fused attention tile (3 nodes per wave: it would spill)
     if constexpr (MODE == 0 || (MODE == 1 && J <= 16)) {
-        if (a.gl4_stage == 1 && XP == 0 && DBG == 0 && a.ntypes * CT * (TILE_H / 8) <= 8 * NW * 64)
-            return gl4_launch_t<J, NW, RT, CT, DBG, MODE, XP, PREC, 1>(a, rms, s);
+        if (a.gl4_stage == 1 && a.ntypes * CT * (TILE_H / 8) <= 8 * NW * 64)
+            return gl4_launch_t<J, NW, RT, CT, MODE, PREC, 1>(a, rms, s);
     }
-    return gl4_launch_t<J, NW, RT, CT, DBG, MODE, XP, PREC, 0>(a, rms, s);
+    return gl4_launch_t<J, NW, RT, CT, MODE, PREC, 0>(a, rms, s);
 }
 
-template <int J, int NW, int RT, int CT, int DBG, int MODE, int XP, int PREC, int STG>
+template <int J, int NW, int RT, int CT, int MODE, int PREC, int STG>
 static hipError_t gl4_launch_t(const GLArgs& a, bool rms, hipStream_t s) {
     constexpr int COLS = 32 * CT;
     constexpr bool ATT = MODE == 1 || MODE == 3;
@@ -2047,12 +1499,12 @@ static hipError_t gl4_launch_t(const GLArgs& a, bool rms, hipStream_t s) {
     // Every launch takes exactly the LDS it uses and may share its CU with other kernels' workgroups
     // (row chains, concurrent plans): the co-residency hazard of rounds 1-2 was the packed-FP32
     // instructions of the co-resident update kernel, not these tiles (build.py).
-    auto kt = rms ? k_gl4<J, NW, RT, CT, true, DBG, MODE, XP, PREC, STG> : k_gl4<J, NW, RT, CT, false, DBG, MODE, XP, PREC, STG>;
+    auto kt = rms ? k_gl4<J, NW, RT, CT, true, MODE, PREC, STG> : k_gl4<J, NW, RT, CT, false, MODE, PREC, STG>;
     if (lds > 64 * 1024) {
         hipError_t e = hipFuncSetAttribute((const void*)kt, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         if (e != hipSuccess) return e;
     }
-    g_route_bits |= MODE == 4 ? kRouteFusedSmall : MODE >= 2 ? kRouteMixPhase : MODE == 1 ? kRouteFusedAttn : kRouteOneKernel;
+    g_route_bits |= MODE >= 2 ? kRouteMixPhase : MODE == 1 ? kRouteFusedAttn : kRouteOneKernel;
     hipLaunchKernelGGL(kt, grid, dim3(NW * 64), lds, s, a);
     return hipGetLastError();
 }
@@ -2087,15 +1539,14 @@ int64_t split_rows_default() { return g_split_rows; }
 // route with the tiled phase 1 (k_gl4t, full batches).  GLArgs::split: 0 auto, 1 never, 2 always
 // (k_gl4y), 3 always (k_gl4t).
 static int split_route(const GLArgs& a, bool attn) {
-    if (a.split == 5 && !attn) return 0;  // the small-batch fused tile (small_fused) took it
     if (a.split == 1 || !a.zs || (a.N & 31) || a.J > 32) return 0;
     if (a.prec == 2 && a.split < 3 && !(a.split == 0 && a.J == 17)) return 0;  // bf16: tiled only (J = 17 auto)
     const int64_t tiles = (a.B + 31) / 32;
     if (tiles * 32 * a.J * (int64_t)a.N > a.zs_cap) return 0;
     if (a.zs == a.out || a.zs == a.x1 || a.zs == a.x2 || a.zs == a.res) return 0;
     if (attn && (a.attn_heads * 96 != a.N)) return 0;
-    if (a.split == 2 || a.split == 5) return a.prec == 2 ? 0 : 1;
-    if (a.split == 3 || a.split == 6) return 2;
+    if (a.split == 2) return a.prec == 2 ? 0 : 1;
+    if (a.split == 3) return 2;
     if (a.split == 4) return attn ? 0 : 2;  // tiled GEMM phase; to_qkv + attention on the one-kernel tile
     if (a.gl4_cfg != 0) return 0;
     const int64_t rows = a.route_rows > 0 ? a.route_rows : a.B;
@@ -2111,13 +1562,6 @@ static int split_route(const GLArgs& a, bool attn) {
     if (a.J == 16) return a.prec == 0 ? 2 : 0;
     return (a.J == 17 || a.J == 21) ? 2 : 0;
 }
-
-// k_gl4y chunks in flight for grids of at most one workgroup per CU (SKELDIFF_GL4Y_PF at load:
-// 8 or 12): with every chunk of a K = 192 layer in flight the wave pays one memory latency
-static int g_gl4y_pf = [] {
-    const char* e = getenv("SKELDIFF_GL4Y_PF");
-    return (e && atoi(e) == 8) ? 8 : 12;
-}();
 
 template <bool ROWMAJOR, int PF>
 static void launch_gl4y_pf(const GLArgs& a, bool rms, int ntc, int64_t ntile_r, const YOut& yo, dim3 grid, hipStream_t s) {
@@ -2140,8 +1584,8 @@ static hipError_t launch_gl4y(const GLArgs& a, bool rms, int ntc, int64_t ntile_
     g_route_bits |= kRouteGemmWave;
     // chunks in flight: a divisor of nchunk (the K loop's rounds: the loop issues unconditionally,
     // so PF must divide nchunk); every chunk of a K = 192 layer in flight on grids of at most one
-    // workgroup per CU
-    if (g_gl4y_pf == 12 && grid.x <= 256 && a.prec == 0 && nchunk % 12 == 0)
+    // workgroup per CU (the wave pays one memory latency per launch)
+    if (grid.x <= 256 && a.prec == 0 && nchunk % 12 == 0)
         launch_gl4y_pf<ROWMAJOR, 12>(a, rms, ntc, ntile_r, yo, grid, s);
     else if (nchunk % 8 == 0) launch_gl4y_pf<ROWMAJOR, 8>(a, rms, ntc, ntile_r, yo, grid, s);
     else if (nchunk % 6 == 0) launch_gl4y_pf<ROWMAJOR, 6>(a, rms, ntc, ntile_r, yo, grid, s);
@@ -2171,266 +1615,41 @@ hipError_t launch_gemm_split(const GLArgs& a, bool rms, float* z, int64_t z_rs, 
     return launch_gl4y<true>(a, rms, ntc, ntile_r, yo, s);
 }
 
-// k_gl4t's K loop (SKELDIFF_GL4T_CFG, read at load): 0 = the default form (g_gl4t_default);
-// 5 = the round-3 form (weights register-staged into two LDS stages one chunk ahead, x two chunks
-// ahead in registers; 24 KiB of LDS); 6 = the LDS-DMA ring (weights and x by LDS-DMA, 2 chunks
-// ahead; 60 KiB); 7 = 6 with the product-major MFMA order (ILV); 8 = 6 with each fill issued before the chunk's work
-// (FF), 9 = 8 three chunks ahead; 10 = the ring filled by one loader wave (LDW); 11 / 12 = 8 with
-// 2 / 4 units (column groups of one x tile) per workgroup where they divide (NU); K = 192 only: 1 = the ring 4 chunks ahead; 2 / 3 = resident weights, every x
-// chunk in flight, 4 / 8 waves; 4 = resident weights, x 4 chunks ahead, 8 waves
-static int g_gl4t_cfg = [] {
-    const char* e = getenv("SKELDIFF_GL4T_CFG");
-    const int v = e ? atoi(e) : 0;
-    return (v >= 0 && v <= 12) ? v : 0;
-}();
-static constexpr int g_gl4t_default = 8;
-
-template <int CT, int NCH, bool ROWMAJOR, int NWV, bool WRES, int PF = 2, bool RSTG = false, bool ILV = false, bool FF = false,
-          bool LDW = false, int NU = 1>
+template <int CT, int NCH, bool ROWMAJOR>
 static hipError_t launch_gl4t_v(const GLArgs& a, bool rms, int64_t ntile_r, const YOut& yo, hipStream_t s) {
-    if (NU > 1 && (a.prec == 2 || (a.N / (32 * CT)) % NU)) return hipErrorNotSupported;
-    const int ncg = a.N / (32 * CT) / NU;  // column groups of NU units each
-    const dim3 grid((unsigned)(((ntile_r + NWV - 1) / NWV) * a.J * ncg)), block((NWV + (LDW && a.prec != 2 ? 1 : 0)) * 64);
-    auto kt = a.prec == 1 ? (rms ? k_gl4t<true, 1, CT, NCH, ROWMAJOR, PF, NWV, WRES, RSTG, ILV, FF, LDW, NU> : k_gl4t<false, 1, CT, NCH, ROWMAJOR, PF, NWV, WRES, RSTG, ILV, FF, LDW, NU>)
-                          : (rms ? k_gl4t<true, 0, CT, NCH, ROWMAJOR, PF, NWV, WRES, RSTG, ILV, FF, LDW, NU> : k_gl4t<false, 0, CT, NCH, ROWMAJOR, PF, NWV, WRES, RSTG, ILV, FF, LDW, NU>);
+    const int ncg = a.N / (32 * CT);  // column groups
+    const dim3 grid((unsigned)(((ntile_r + 3) / 4) * a.J * ncg)), block(256);
+    auto kt = a.prec == 1 ? (rms ? k_gl4t<true, 1, CT, NCH, ROWMAJOR> : k_gl4t<false, 1, CT, NCH, ROWMAJOR>)
+                          : (rms ? k_gl4t<true, 0, CT, NCH, ROWMAJOR> : k_gl4t<false, 0, CT, NCH, ROWMAJOR>);
     if constexpr (!ROWMAJOR) {  // bf16 mode (precision 2): the split route's scratch output only
-        if (a.prec == 2)
-            kt = rms ? k_gl4t<true, 2, CT, NCH, false, PF, NWV, WRES, RSTG, ILV, FF> : k_gl4t<false, 2, CT, NCH, false, PF, NWV, WRES, RSTG, ILV, FF>;
+        if (a.prec == 2) kt = rms ? k_gl4t<true, 2, CT, NCH, false> : k_gl4t<false, 2, CT, NCH, false>;
     }
     g_route_bits |= kRouteGemmTiled;
     hipLaunchKernelGGL(kt, grid, block, 0, s, a, ncg, ntile_r, yo);
     return hipGetLastError();
 }
 
-template <int CT, int NCH, bool ROWMAJOR>
-static hipError_t launch_gl4t_ct(const GLArgs& a, bool rms, int64_t ntile_r, const YOut& yo, hipStream_t s) {
-    const int cfg = g_gl4t_cfg ? g_gl4t_cfg : g_gl4t_default;
-    if constexpr (NCH == 12) {
-        switch (cfg) {
-            case 1: return launch_gl4t_v<CT, NCH, ROWMAJOR, 4, false, 4>(a, rms, ntile_r, yo, s);
-            case 2: return launch_gl4t_v<CT, NCH, ROWMAJOR, 4, true, 12>(a, rms, ntile_r, yo, s);
-            case 3: return launch_gl4t_v<CT, NCH, ROWMAJOR, 8, true, 12>(a, rms, ntile_r, yo, s);
-            case 4: return launch_gl4t_v<CT, NCH, ROWMAJOR, 8, true, 4>(a, rms, ntile_r, yo, s);
-            default: break;
-        }
-    }
-    if (cfg == 5) return launch_gl4t_v<CT, NCH, ROWMAJOR, 4, false, 2, true>(a, rms, ntile_r, yo, s);
-    if (cfg == 7) return launch_gl4t_v<CT, NCH, ROWMAJOR, 4, false, 2, false, true>(a, rms, ntile_r, yo, s);
-    if (cfg == 8) return launch_gl4t_v<CT, NCH, ROWMAJOR, 4, false, 2, false, false, true>(a, rms, ntile_r, yo, s);
-    if (cfg == 10) return launch_gl4t_v<CT, NCH, ROWMAJOR, 4, false, 2, false, false, false, true>(a, rms, ntile_r, yo, s);
-    if (cfg == 11 || cfg == 12) {  // multi-unit workgroups where the column groups divide (to_qkv), else cfg 8
-        const int ncg0 = a.N / (32 * CT);
-        if (a.prec != 2 && cfg == 11 && ncg0 % 2 == 0)
-            return launch_gl4t_v<CT, NCH, ROWMAJOR, 4, false, 2, false, false, true, false, 2>(a, rms, ntile_r, yo, s);
-        if (a.prec != 2 && cfg == 12 && ncg0 % 4 == 0)
-            return launch_gl4t_v<CT, NCH, ROWMAJOR, 4, false, 2, false, false, true, false, 4>(a, rms, ntile_r, yo, s);
-        return launch_gl4t_v<CT, NCH, ROWMAJOR, 4, false, 2, false, false, true>(a, rms, ntile_r, yo, s);
-    }
-    if constexpr (NCH % 3 == 0)
-        if (cfg == 9) return launch_gl4t_v<CT, NCH, ROWMAJOR, 4, false, 3, false, false, true>(a, rms, ntile_r, yo, s);
-    return launch_gl4t_v<CT, NCH, ROWMAJOR, 4, false>(a, rms, ntile_r, yo, s);
-}
-
-// SKELDIFF_GL4T_CT3=1 (A/B): N = 192, K = 192 layers on 96-column workgroups (two column groups
-// sharing each x tile; fewer accumulators, more waves per SIMD)
-static int g_gl4t_ct3 = [] {
-    const char* e = getenv("SKELDIFF_GL4T_CT3");
-    return e ? atoi(e) : 0;
-}();
-
-// to_qkv (N = 768, K = 192) on 256-column workgroups (3 column groups of 8 tiles instead of 4 of 6:
-// 0.75 of the x re-reads, 24 MFMAs per chunk and wave).  Default on the row-major v5 path (MANO
-// J = 51: 3,757 / 3,766 vs 3,729 / 3,727 futures/s), off on the tiled split route (config 2:
-// 16,104 / 16,353 vs 16,498 / 16,375), profiles/r04_ab/gl4t_ct8.txt.  SKELDIFF_GL4T_CT8 at load:
-// -1 (unset) that default, 0 never, 1 always.
-static int g_gl4t_ct8 = [] {
-    const char* e = getenv("SKELDIFF_GL4T_CT8");
-    return e ? atoi(e) : -1;
-}();
-
 // the release Denoiser's shapes: K = 192 (12 chunks), 256 (to_out, 16) or 384 (24), N a multiple
-// of 96 (192 wide layers, 768 to_qkv, 96 final_glin); hipErrorNotSupported otherwise (k_gl4y)
+// of 96 (192 wide layers, 768 to_qkv, 96 final_glin); hipErrorNotSupported otherwise (k_gl4y).
+// to_qkv (N = 768, K = 192) of the row-major v5 path (J > 21) on 256-column workgroups: 3 column
+// groups of 8 tiles instead of 4 of 6 (0.75 of the x re-reads, 24 MFMAs per chunk and wave; MANO
+// J = 51 3,757 / 3,766 vs 3,729 / 3,727 futures/s); on the tiled split route it measured slower
+// (config 2 16,104 / 16,353 vs 16,498 / 16,375: its 72 KiB workgroups leave less room for the other
+// row chains' kernels), profiles/r04_ab/gl4t_ct8.txt
 template <bool ROWMAJOR>
 static hipError_t launch_gl4t(const GLArgs& a, bool rms, int64_t ntile_r, const YOut& yo, hipStream_t s) {
     const int K = a.K1 + a.K2;
     if (a.K1 % 16 || (a.x1_div != 1 && a.x1_blk)) return hipErrorNotSupported;
-    if ((g_gl4t_ct8 == 1 || (g_gl4t_ct8 < 0 && ROWMAJOR)) && a.N % 256 == 0 && K == 192 && a.prec != 2)
-        return launch_gl4t_v<8, 12, ROWMAJOR, 4, false, 2, false, false, true>(a, rms, ntile_r, yo, s);
-    if (a.N % 192 == 0 && !(g_gl4t_ct3 && a.N == 192 && K == 192)) {
-        if (K == 192) return launch_gl4t_ct<6, 12, ROWMAJOR>(a, rms, ntile_r, yo, s);
-        if (K == 256) return launch_gl4t_ct<6, 16, ROWMAJOR>(a, rms, ntile_r, yo, s);
-        if (K == 384) return launch_gl4t_ct<6, 24, ROWMAJOR>(a, rms, ntile_r, yo, s);
+    if (ROWMAJOR && a.N % 256 == 0 && K == 192 && a.prec != 2) return launch_gl4t_v<8, 12, ROWMAJOR>(a, rms, ntile_r, yo, s);
+    if (a.N % 192 == 0) {
+        if (K == 192) return launch_gl4t_v<6, 12, ROWMAJOR>(a, rms, ntile_r, yo, s);
+        if (K == 256) return launch_gl4t_v<6, 16, ROWMAJOR>(a, rms, ntile_r, yo, s);
+        if (K == 384) return launch_gl4t_v<6, 24, ROWMAJOR>(a, rms, ntile_r, yo, s);
     } else if (a.N % 96 == 0) {
-        if (K == 192) return launch_gl4t_ct<3, 12, ROWMAJOR>(a, rms, ntile_r, yo, s);
-        if (K == 384) return launch_gl4t_ct<3, 24, ROWMAJOR>(a, rms, ntile_r, yo, s);
+        if (K == 192) return launch_gl4t_v<3, 12, ROWMAJOR>(a, rms, ntile_r, yo, s);
+        if (K == 384) return launch_gl4t_v<3, 24, ROWMAJOR>(a, rms, ntile_r, yo, s);
     }
     return hipErrorNotSupported;
-}
-
-// ---- the fused layer kernel k_gl4f (round 5) --------------------------------
-// One launch for a plain J = 16 graph-linear layer of the tiled split route: the GEMM phase
-// (gl4t_body, k_gl4t's K loop and epilogue) and the mixing phase (gl4_body MODE 2, k_gl4's) as
-// work items of one persistent grid, so each 128-row group's pre-mix Y is mixed straight out of
-// the L2 of the XCD that wrote it, and the mixing of one row group overlaps the GEMMs of the next
-// instead of waiting for a kernel boundary.  Same functions, same arithmetic: bitwise equal to
-// the tiled split route.
-//   Work items: per row group rg (128 rows), 8 GEMM items (a node pair: the two 4-wave halves of
-//   the 8-wave workgroup each run one node's 128 x 192 k_gl4t tile, with their own LDS) and 48
-//   mixing items (MODE 2 units: 32-row tile x 16-row slab x 32-column tile).
-//   Queues: one per XCD (the workgroup reads its s_getreg XCC_ID).  XCD x's item stream is slot
-//   after slot: [8 GEMM items of slot s][48 mixing items of slot s - 1]; the workgroup that takes
-//   the first GEMM item of a slot claims the next row group for it (one global counter), so every
-//   item of a row group runs on one XCD, and XCDs that run faster claim more row groups.
-//   Hand-off: the GEMM items store Y plainly (it stays in the XCD's L2), every wave drains its
-//   stores (vmcnt(0)), one agent-scope add per item on the row group's counter; a mixing item
-//   polls that counter (relaxed agent-scope loads) until all 8 are in, then reads Y with sc1 loads
-//   (past its CU's L1).  tools/handoff_probe.hip: plain stores + sc1 loads inside one XCD, 0 stale
-//   words in 2,000 rounds (and every word stale across XCDs -- hence the per-XCD queues).
-//   Progress: a mixing item waits only for GEMM items taken earlier from the same stream, which
-//   never wait (a slot claim waits for the claimant, which took its item earlier) -- no deadlock
-//   whatever the residency; every spin is bounded (SD_STATUS_FUSE_TIMEOUT, then the item is
-//   dropped rather than hang).  The last workgroup out zeroes the queue block for the next launch.
-constexpr int kFusePer = 8 + 48;   // items per slot
-constexpr unsigned kFuseNone = 0xffffffffu;
-typedef __attribute__((address_space(1))) unsigned fgu32;
-
-__device__ __forceinline__ unsigned fq_load(const unsigned* q) {
-    return __hip_atomic_load((fgu32*)q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void fq_store(unsigned* q, unsigned v) {
-    __hip_atomic_store((fgu32*)q, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ unsigned fq_add(unsigned* q, unsigned v) {
-    return __hip_atomic_fetch_add((fgu32*)q, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-// poll until pred(value) (bounded: ~2^24 polls with s_sleep, seconds); returns the value, or
-// kFuseNone with the timeout flag set
-template <typename P>
-__device__ __forceinline__ unsigned fq_wait(const unsigned* q, P pred, unsigned* status) {
-    for (unsigned i = 0; i < (1u << 24); ++i) {
-        const unsigned v = fq_load(q);
-        if (pred(v)) return v;
-        __builtin_amdgcn_s_sleep(2);
-    }
-    if (status) atomicOr(status, 2u);  // SD_STATUS_FUSE_TIMEOUT
-    return kFuseNone;
-}
-
-template <int NCH, int PREC>
-__global__ __launch_bounds__(512, 1) void k_gl4f(const GLArgs p, int64_t ntile_r, const YOut yo) {
-    constexpr int SBH = gl4t_smem_bytes<PREC, 6, NCH, 2, 4, false, false, 1>();  // LDS of one half
-    extern __shared__ __attribute__((aligned(16))) float smem_f[];  // (one extern name, one type: k_gl4's)
-    char* const smem = reinterpret_cast<char*>(smem_f);
-    unsigned* const sq = reinterpret_cast<unsigned*>(smem + 2 * SBH);  // item, row group broadcast
-    const int tid = threadIdx.x, half = tid >> 8;
-    unsigned xcc;
-    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
-    xcc &= 7;
-    const int nrg = (int)((ntile_r + 3) / 4);  // 128-row groups
-    const int S = nrg + 2;                     // slots per XCD stream (all row groups + the end)
-    unsigned* const head = p.fq + 32 * xcc;
-    unsigned* const slot_rg = p.fq + kFqSlot + xcc * S;
-    unsigned* const gdone = p.fq + kFqSlot + 8 * S;
-    for (;;) {
-        if (tid == 0) sq[0] = fq_add(head, 1u);
-        __syncthreads();
-        const unsigned it = sq[0];
-        const int slot = (int)(it / kFusePer), w = (int)(it % kFusePer);
-        if (slot >= S) break;  // past the end of the stream (every slot's row group settled)
-        if (w < 8) {  // GEMM item: node pair w of slot `slot`
-            if (tid == 0) {
-                unsigned v;
-                if (w == 0) {  // claim the next row group for this slot
-                    const unsigned r = fq_add(p.fq + kFqNext, 1u);
-                    v = r < (unsigned)nrg ? r + 1 : kFuseNone;
-                    fq_store(slot_rg + slot, v);
-                } else {
-                    v = fq_wait(slot_rg + slot, [](unsigned x) { return x != 0u; }, p.status);
-                }
-                sq[1] = v;
-            }
-            __syncthreads();
-            const unsigned v = sq[1];
-            if (v != kFuseNone) {
-                const int64_t rg = v - 1;
-                const int64_t u = (int64_t)(2 * w + half) * nrg + rg;  // k_gl4t's (node, row group), ncg = 1
-                gl4t_body<false, PREC, 6, NCH, false, 2, 4, false, false, false, true, false, 1>(
-                    p, 1, ntile_r, yo, u, tid & 255, smem + half * SBH);
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's Y stores are in L2
-                __syncthreads();
-                if (tid == 0) fq_add(gdone + rg, 1u);
-            }
-        } else {  // mixing item w - 8 of slot - 1 (slot 0: no previous slot, nothing to mix)
-            if (tid == 0) {
-                unsigned v = 0u;  // 0: skip this item
-                if (slot > 0) {
-                    v = fq_wait(slot_rg + slot - 1, [](unsigned x) { return x != 0u; }, p.status);
-                    if (v != kFuseNone &&
-                        fq_wait(gdone + (v - 1), [](unsigned x) { return x >= 8u; }, p.status) == kFuseNone)
-                        v = kFuseNone;
-                }
-                sq[1] = v;
-            }
-            __syncthreads();
-            const unsigned v = sq[1];
-            if (v == kFuseNone) break;  // slot - 1 had no row group: the stream is done
-            const int m = w - 8, tl = m / 12, rem = m % 12;
-            const int64_t tile = (int64_t)(v - 1) * 4 + tl;
-            if (v != 0u && tile < ntile_r) {
-                const int bx = (int)(((tile * 6 + (rem >> 1)) << 1) | (rem & 1));  // k_gl4 MODE 2's block index
-                gl4_body<16, 8, 1, 1, false, 0, 2, 0, 0, 0, true>(p, bx, 0, reinterpret_cast<float*>(smem));
-            }
-        }
-        __syncthreads();  // LDS and sq reused by the next item
-    }
-    // the last workgroup out zeroes the block for the next launch (all others are past their last
-    // access: each adds to the exit counter after it)
-    if (tid == 0) {
-        const unsigned n = __hip_atomic_fetch_add((fgu32*)(p.fq + kFqExit), 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
-        sq[2] = n == gridDim.x - 1;
-    }
-    __syncthreads();
-    if (sq[2]) {
-        for (int i = tid; i < 8; i += 512) fq_store(p.fq + 32 * i, 0u);
-        for (int i = tid; i < 8 * S + nrg; i += 512) fq_store(p.fq + kFqSlot + i, 0u);
-        if (tid == 0) {
-            fq_store(p.fq + kFqNext, 0u);
-            fq_store(p.fq + kFqExit, 0u);
-        }
-    }
-}
-
-// k_gl4f eligibility: J = 16 plain (non-RMS, non-attention) layers of N = 192 on split-f16 (f32 or
-// half) products, K = 192 / 256 / 384, the column-tiled scratch; route 6 forces it, the auto
-// route takes it where SKELDIFF_FUSED (process default of new plans' g_fused) says
-static int g_fused = [] {
-    const char* e = getenv("SKELDIFF_FUSED");
-    return e ? atoi(e) : 0;
-}();
-template <int NCH>
-static hipError_t launch_gl4f_n(const GLArgs& a, int64_t ntile_r, const YOut& yo, hipStream_t s) {
-    constexpr int SBH = gl4t_smem_bytes<0, 6, NCH, 2, 4, false, false, 1>();
-    const size_t lds = 2 * SBH + 64;
-    auto kt = a.prec == 1 ? k_gl4f<NCH, 1> : k_gl4f<NCH, 0>;
-    hipError_t e = hipFuncSetAttribute((const void*)kt, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    if (e != hipSuccess) return e;
-    g_route_bits |= kRouteGemmTiled | kRouteMixPhase | kRouteFusedLayer;
-    hipLaunchKernelGGL(kt, dim3(256), dim3(512), lds, s, a, ntile_r, yo);  // one workgroup per CU
-    return hipGetLastError();
-}
-static hipError_t launch_gl4f(const GLArgs& a, int64_t ntile_r, const YOut& yo, hipStream_t s) {
-    const int K = a.K1 + a.K2;
-    if (K == 192) return launch_gl4f_n<12>(a, ntile_r, yo, s);
-    if (K == 256) return launch_gl4f_n<16>(a, ntile_r, yo, s);
-    return launch_gl4f_n<24>(a, ntile_r, yo, s);
-}
-static bool fused_ok(const GLArgs& a, bool rms, bool attn) {
-    if (!a.fq || rms || attn || a.J != 16 || a.prec == 2 || a.N != 192 || a.x2_blk != a.x1_blk) return false;
-    if (!(a.split == 6 || (a.split == 0 && g_fused))) return false;
-    const int K = a.K1 + a.K2;
-    if (!(K == 192 || K == 256 || K == 384) || a.K1 % 16 || (a.x1_div != 1 && a.x1_blk)) return false;
-    if ((int64_t)(a.B + 31) / 32 * 32 * a.J * a.N * 4 >= 0x7fffffffLL) return false;  // sc1 loads: 32-bit offsets
-    return true;
 }
 
 template <int J>
@@ -2438,7 +1657,6 @@ static hipError_t gl4_split(const GLArgs& a, bool rms, bool attn, int route, hip
     const int64_t ntile_r = (a.B + 31) / 32;
     const int ntc = a.N / 32;
     const YOut yo{a.zs, 32, 1024, (int64_t)(a.N / 32) * J * 1024, (int64_t)J * 1024};  // column-tiled (zs_off)
-    if (route == 2 && fused_ok(a, rms, attn)) return launch_gl4f(a, ntile_r, yo, s);
     hipError_t e = route == 2 ? launch_gl4t<false>(a, rms, ntile_r, yo, s) : hipErrorNotSupported;
     if (e == hipErrorNotSupported) {
         if (a.prec == 2) return hipErrorNotSupported;  // k_gl4y has no bf16 form
@@ -2446,28 +1664,11 @@ static hipError_t gl4_split(const GLArgs& a, bool rms, bool attn, int route, hip
     }
     if (e != hipSuccess) return e;
     if (a.prec == 2) {  // bf16 residual / output storage (PREC 2 epilogue)
-        if (attn) return gl4_launch_t<J, 8, 1, 3, 0, 3, 0, 2, 0>(a, false, s);
-        return gl4_launch_t<J, 8, 1, 1, 0, 2, 0, 2, 0>(a, false, s);
+        if (attn) return gl4_launch_t<J, 8, 1, 3, 3, 2, 0>(a, false, s);
+        return gl4_launch_t<J, 8, 1, 1, 2, 2, 0>(a, false, s);
     }
-    if (attn) return gl4_launch_t<J, 8, 1, 3, 0, 3, 0, 0, 0>(a, false, s);
-    return gl4_launch_t<J, 8, 1, 1, 0, 2, 0, 0, 0>(a, false, s);
-}
-
-// Small-batch fused tile (k_gl4 MODE 4) for the plain graph-linears of J = 16 f32 / half plans:
-// GLArgs::split 5 always; auto (0) at <= SKELDIFF_SMALL_ROWS rows of the call (default 0: off --
-// measured slower than the split route, DESIGN.md §4d': config 4 83.5 vs 116.1 futures/s, 12
-// workgroups each pulling 16 nodes' operands through one CU).  to_qkv + attention keeps the split
-// route.
-static int64_t g_small_rows = [] {
-    const char* e = getenv("SKELDIFF_SMALL_ROWS");
-    return e ? (int64_t)atoll(e) : (int64_t)0;
-}();
-static bool small_fused(const GLArgs& a) {
-    if (a.J != 16 || a.prec == 2 || a.split == 1 || a.split == 2 || a.split == 3 || a.split == 4 || a.split == 6) return false;
-    if ((a.K1 + a.K2) % 64) return false;  // MODE 4's K loop: chunks in rounds of 4
-    if (a.split == 5) return true;
-    if (a.gl4_cfg != 0) return false;
-    return (a.route_rows > 0 ? a.route_rows : a.B) <= g_small_rows;
+    if (attn) return gl4_launch_t<J, 8, 1, 3, 3, 0, 0>(a, false, s);
+    return gl4_launch_t<J, 8, 1, 1, 2, 0, 0>(a, false, s);
 }
 
 static hipError_t gl4_split_dispatch(const GLArgs& a, bool rms, bool attn, int route, hipStream_t s) {
@@ -2486,8 +1687,6 @@ hipError_t launch_graph_linear_v4(const GLArgs& a, bool rms, hipStream_t s) {
     if ((a.N & 3) || ((uintptr_t)a.out & 15) || ((uintptr_t)a.res & 15) || (a.res && (a.res_rs & 3)) || (a.out_rs & 3))
         return hipErrorNotSupported;
     if (!a.wsp || (a.K1 + a.K2) % 32 || a.K1 % 16 || (a.x1_blk && a.x1_div != 1)) return hipErrorNotSupported;
-    if (small_fused(a))
-        return a.prec == 1 ? gl4_launch_t<16, 8, 1, 1, 0, 4, 0, 1, 0>(a, rms, s) : gl4_launch_t<16, 8, 1, 1, 0, 4, 0, 0, 0>(a, rms, s);
     if (a.J == 16 || a.J == 17 || a.J == 21)
         if (const int route = split_route(a, false)) {
             const hipError_t e = gl4_split_dispatch(a, rms, false, route, s);
@@ -2497,19 +1696,19 @@ hipError_t launch_graph_linear_v4(const GLArgs& a, bool rms, hipStream_t s) {
     if (a.prec == 2) {  // bf16 mode: row-major operands, the default tiles only
         if (a.x1_blk || a.x2_blk || a.res_blk || a.out_blk) return hipErrorNotSupported;
         switch (a.J) {
-            case 16: return gl4_launch<16, 8, 1, 3, 0, 0, 0, 2>(a, rms, s);
-            case 17: return gl4_launch<17, 8, 1, 2, 0, 0, 0, 2>(a, rms, s);
-            case 21: return gl4_launch<21, 8, 1, 2, 0, 0, 0, 2>(a, rms, s);
+            case 16: return gl4_launch<16, 8, 1, 3, 0, 2>(a, rms, s);
+            case 17: return gl4_launch<17, 8, 1, 2, 0, 2>(a, rms, s);
+            case 21: return gl4_launch<21, 8, 1, 2, 0, 2>(a, rms, s);
             default: return hipErrorNotSupported;
         }
     }
     if (a.prec == 1) {  // half precision mode: the default tiles only
         switch (a.J) {
             case 16:
-                if (cfg == 812) return gl4_launch<16, 8, 1, 2, 0, 0, 0, 1>(a, rms, s);
-                return gl4_launch<16, 8, 1, 3, 0, 0, 0, 1>(a, rms, s);
-            case 17: return gl4_launch<17, 8, 2, 1, 0, 0, 0, 1>(a, rms, s);
-            case 21: return gl4_launch<21, 8, 1, 2, 0, 0, 0, 1>(a, rms, s);
+                if (cfg == 812) return gl4_launch<16, 8, 1, 2, 0, 1>(a, rms, s);
+                return gl4_launch<16, 8, 1, 3, 0, 1>(a, rms, s);
+            case 17: return gl4_launch<17, 8, 2, 1, 0, 1>(a, rms, s);
+            case 21: return gl4_launch<21, 8, 1, 2, 0, 1>(a, rms, s);
             default: return hipErrorNotSupported;
         }
     }
@@ -2522,9 +1721,6 @@ hipError_t launch_graph_linear_v4(const GLArgs& a, bool rms, hipStream_t s) {
             if (cfg == 812) return gl4_launch<16, 8, 1, 2>(a, rms, s);
             if (cfg == 813) return gl4_launch<16, 8, 1, 3>(a, rms, s);
             if (cfg == 811) return gl4_launch<16, 8, 1, 1>(a, rms, s);  // small batches: 3x the workgroups
-            if (cfg == 6) return gl4_launch<16, 8, 1, 3, 6>(a, rms, s);  // phase stamps (tools/stamps.py)
-            if (cfg == 7) return gl4_launch<16, 8, 1, 3, 6, 0, 1>(a, rms, s);  // stamps, x two chunks ahead
-            if (cfg == 1813) return gl4_launch<16, 8, 1, 3, 0, 0, 1>(a, rms, s);
             if (cfg == 822) return gl4_launch<16, 8, 2, 2>(a, rms, s);
             // small grids (a few sequences: config 4, one sequence x 50 futures): 32 x 32 tiles give
             // 3x the workgroups of 32 x 96 and a third of the per-workgroup weight bytes; measured
@@ -2563,38 +1759,17 @@ hipError_t launch_qkv_attention_v4(const GLArgs& a, bool rms, hipStream_t s) {
     // J = 17 / 21: 3 nodes per wave, two 16-node tiles in the softmax
     switch (a.J) {
         case 16:
-            if (a.prec == 2) return gl4_launch<16, 8, 1, 3, 0, 1, 0, 2>(b, rms, s);
-            return a.prec == 1 ? gl4_launch<16, 8, 1, 3, 0, 1, 0, 1>(b, rms, s) : gl4_launch<16, 8, 1, 3, 0, 1>(b, rms, s);
+            if (a.prec == 2) return gl4_launch<16, 8, 1, 3, 1, 2>(b, rms, s);
+            return a.prec == 1 ? gl4_launch<16, 8, 1, 3, 1, 1>(b, rms, s) : gl4_launch<16, 8, 1, 3, 1>(b, rms, s);
         case 17:
-            if (a.prec == 2) return gl4_launch<17, 8, 1, 3, 0, 1, 0, 2>(b, rms, s);
-            return a.prec == 1 ? gl4_launch<17, 8, 1, 3, 0, 1, 0, 1>(b, rms, s) : gl4_launch<17, 8, 1, 3, 0, 1>(b, rms, s);
+            if (a.prec == 2) return gl4_launch<17, 8, 1, 3, 1, 2>(b, rms, s);
+            return a.prec == 1 ? gl4_launch<17, 8, 1, 3, 1, 1>(b, rms, s) : gl4_launch<17, 8, 1, 3, 1>(b, rms, s);
         case 21:  // 13 node types: 2 x 78 KB weight stages + G-hat + FiLM = 158.5 KB of LDS
-            if (a.prec == 2) return gl4_launch<21, 8, 1, 3, 0, 1, 0, 2>(b, rms, s);
-            return a.prec == 1 ? gl4_launch<21, 8, 1, 3, 0, 1, 0, 1>(b, rms, s) : gl4_launch<21, 8, 1, 3, 0, 1>(b, rms, s);
+            if (a.prec == 2) return gl4_launch<21, 8, 1, 3, 1, 2>(b, rms, s);
+            return a.prec == 1 ? gl4_launch<21, 8, 1, 3, 1, 1>(b, rms, s) : gl4_launch<21, 8, 1, 3, 1>(b, rms, s);
         default: return hipErrorNotSupported;
     }
 }
 
 }  // namespace sd
 
-#ifdef SD_GL4T_STAMPS
-extern "C" int sd_debug_gl4t_stamps(unsigned long long* host, int nwg, int reset) {
-    if (reset) {
-        static unsigned long long zeros[8192 * 4] = {};
-        return hipMemcpyToSymbol(HIP_SYMBOL(sd::g_gl4t_stamps), zeros, sizeof(zeros)) == hipSuccess ? 0 : -3;
-    }
-    if (nwg < 0 || nwg > 8192) return -1;
-    return hipMemcpyFromSymbol(host, HIP_SYMBOL(sd::g_gl4t_stamps), (size_t)nwg * 4 * sizeof(unsigned long long)) ==
-                   hipSuccess ? 0 : -3;
-}
-extern "C" int sd_debug_gl4t_clock(unsigned long long* host, int nwg) {
-    if (nwg < 0 || nwg > 8192) return -1;
-    return hipMemcpyFromSymbol(host, HIP_SYMBOL(sd::g_gl4t_clock), (size_t)nwg * 2 * sizeof(unsigned long long)) ==
-                   hipSuccess ? 0 : -3;
-}
-extern "C" int sd_debug_gl4t_chunk_stamps(unsigned long long* host, int nwg) {
-    if (nwg < 0 || nwg > 8192) return -1;
-    return hipMemcpyFromSymbol(host, HIP_SYMBOL(sd::g_gl4t_chunk), (size_t)nwg * 16 * sizeof(unsigned long long)) ==
-                   hipSuccess ? 0 : -3;
-}
-#endif

@@ -507,23 +507,6 @@ __global__ __launch_bounds__(256, 2) void k_gl5_mixd(const GLArgs p, const float
 
 }  // namespace
 
-// 1 (default): the mixing pass on k_gl5_mixm where it applies; 0: k_gl5_mix (SKELDIFF_V5_MIX at
-// load: a diagnostic default under the per-plan SD_OPT_V5_MIX, which selects k_gl5_mix when set)
-static const int g_mix_mfma = [] {
-    const char* e = getenv("SKELDIFF_V5_MIX");
-    // 3 (default): k_gl5_mixd (LDS-DMA ring); 1: k_gl5_mixm; 2: its two-deep register ring (A/B)
-    return e ? std::min(std::max(atoi(e), 0), 3) : 3;
-}();
-static const int g_mixd_cfg = [] {
-    const char* e = getenv("SKELDIFF_V5_MIXD");
-    return e ? atoi(e) : 0;
-}();
-// rows per k_gl5_mixm workgroup (SKELDIFF_V5_ROWS at load: 4, 8 or 16)
-static int g_mix_rows = [] {
-    const char* e = getenv("SKELDIFF_V5_ROWS");
-    return (e && (atoi(e) == 16 || atoi(e) == 4)) ? atoi(e) : 8;
-}();
-
 // The mixing pass alone (the training graph-linear, sd_train.hip): out[r, i, :] = sum_j M[i, j]
 // z[r, j, :] with M = G-hat (transpose 0) or G-hat^T (1), z and out (rows, J, N) row-major; the same
 // j-ordered fmaf chains as sd_train.hip's k_mix.  hipErrorNotSupported unless N % 64 == 0 with
@@ -584,14 +567,14 @@ hipError_t launch_graph_linear_v5(const GLArgs& a, bool rms, hipStream_t s) {
     const int vec = ((uintptr_t)z & 15) == 0 && (a.N & 3) == 0 && (z_rs & 3) == 0;
     g_route_bits |= kRouteV5Mix;
     // the matrix-core mixing pass: 64-column blocks, 16-B z / residual / output pieces
-    const bool mfma = g_mix_mfma && !a.v5_valu && vec && a.N % 64 == 0 && ((uintptr_t)a.out & 15) == 0 && (a.out_rs & 3) == 0 &&
+    const bool mfma = !a.v5_valu && vec && a.N % 64 == 0 && ((uintptr_t)a.out & 15) == 0 && (a.out_rs & 3) == 0 &&
                       (!a.res || (((uintptr_t)a.res & 15) == 0 && (a.res_rs & 3) == 0)) && a.B / 8 < 0x7fffffff;
-    if (mfma && g_mix_mfma == 3 && (int64_t)a.B * a.out_rs * 4 < 0x7fffffff && (!a.res || a.res_rs % 4 == 0)) {
+    if (mfma && (int64_t)a.B * a.out_rs * 4 < 0x7fffffff && (!a.res || a.res_rs % 4 == 0)) {
         // the LDS-DMA form: slabs of 4 ceil(J / 4) rows, 2 slots (row r + 1 in flight while row r is
         // mixed): 53 KiB of LDS at J = 51 with the residual, 3 workgroups per CU -- config 3 4,193 /
-        // 4,195 vs 4,070 / 4,068 futures/s for 3 slots (2 workgroups per CU), profiles/r05k/ab_mixd.txt.
-        // SKELDIFF_V5_MIXD (A/B at load): 1 = 4 rows per workgroup with 3 slots, 3 = 3 slots,
-        // 4 / 5 = 16 / 4 rows per workgroup with 2 slots
+        // 4,195 vs 4,070 / 4,068 futures/s for 3 slots (2 workgroups per CU), profiles/r05k/ab_mixd.txt;
+        // 8 rows per workgroup: 4,095 / 4,097 vs 4,065 / 4,044 (4 rows) and 4,003 / 3,999 (16 rows),
+        // profiles/r05m/ab_mixd_rows.txt (the other forms: git history before round 6)
         const int KS = (a.J + 3) / 4;
         auto launch = [&](auto kt, int R, int PF) -> hipError_t {
             const size_t lds = (size_t)(PF + 1) * (a.res ? 2 : 1) * 4 * KS * 64 * sizeof(float);
@@ -603,24 +586,13 @@ hipError_t launch_graph_linear_v5(const GLArgs& a, bool rms, hipStream_t s) {
                                (const float*)z, z_rs);
             return hipGetLastError();
         };
-        if (g_mixd_cfg == 1) return a.res ? launch(k_gl5_mixd<4, 2, true>, 4, 2) : launch(k_gl5_mixd<4, 2, false>, 4, 2);
-        if (g_mixd_cfg == 3) return a.res ? launch(k_gl5_mixd<8, 2, true>, 8, 2) : launch(k_gl5_mixd<8, 2, false>, 8, 2);
-        if (g_mixd_cfg == 4) return a.res ? launch(k_gl5_mixd<16, 1, true>, 16, 1) : launch(k_gl5_mixd<16, 1, false>, 16, 1);
-        if (g_mixd_cfg == 5) return a.res ? launch(k_gl5_mixd<4, 1, true>, 4, 1) : launch(k_gl5_mixd<4, 1, false>, 4, 1);
         return a.res ? launch(k_gl5_mixd<8, 1, true>, 8, 1) : launch(k_gl5_mixd<8, 1, false>, 8, 1);
     }
     if (mfma) {
         const dim3 blk(256);
         const unsigned ncb = (unsigned)(a.N / 64);
         const size_t lds = (2 * 4 * (size_t)((a.J + 3) / 4) * 80 + 128) * sizeof(float);  // <= 41.5 KB (J <= 64)
-        if (g_mix_mfma == 2)
-            hipLaunchKernelGGL((k_gl5_mixm<8, 2>), dim3((unsigned)((a.B + 7) / 8), ncb), blk, lds, s, a, (const float*)z, z_rs);
-        else if (g_mix_rows == 4)
-            hipLaunchKernelGGL((k_gl5_mixm<4, 1>), dim3((unsigned)((a.B + 3) / 4), ncb), blk, lds, s, a, (const float*)z, z_rs);
-        else if (g_mix_rows == 16)
-            hipLaunchKernelGGL((k_gl5_mixm<16, 1>), dim3((unsigned)((a.B + 15) / 16), ncb), blk, lds, s, a, (const float*)z, z_rs);
-        else
-            hipLaunchKernelGGL((k_gl5_mixm<8, 1>), dim3((unsigned)((a.B + 7) / 8), ncb), blk, lds, s, a, (const float*)z, z_rs);
+        hipLaunchKernelGGL((k_gl5_mixm<8, 1>), dim3((unsigned)((a.B + 7) / 8), ncb), blk, lds, s, a, (const float*)z, z_rs);
         return hipGetLastError();
     }
     const dim3 g2((unsigned)a.B, (unsigned)((a.N + 63) / 64));

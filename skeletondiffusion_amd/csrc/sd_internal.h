@@ -31,8 +31,9 @@ struct GLArgs {
     // the test entry points): generation 0 auto / 1..5 forced, v4 tile <NW><RT><CT> (0 auto),
     // v4 weight staging 0 LDS-DMA (CU held exclusively) / 1 register-staged (CU shareable)
     int variant, gl4_cfg, gl4_stage;
-    // v4 split route for small grids (phase 1 GEMM per (tile, node) into the zs scratch, phase 2
-    // mixing epilogue; bitwise identical to the one-kernel route): 0 auto, 1 never, 2 always
+    // v4 split route (phase 1 GEMM per (tile, node) into the zs scratch, phase 2 mixing epilogue;
+    // bitwise identical to the one-kernel route): 0 auto, 1 never, 2 k_gl4y, 3 k_gl4t, 4 k_gl4t
+    // except for to_qkv + attention
     int split;
     // v5 (J > 21) mixing pass (SD_OPT_V5_MIX): 0 the matrix-core form k_gl5_mixm, 1 the VALU form
     // k_gl5_mix (the same j-ordered fmaf chains)
@@ -70,19 +71,10 @@ struct GLArgs {
     // bf16 storage of operands / result (precision mode 2): the tensor
     // holds bf16 elements at the same element offsets (row-major only)
     int x1_bf16, x2_bf16, res_bf16, out_bf16;
-    // the fused layer kernel k_gl4f (split route 6 / auto): this launch's work-queue block in the
-    // workspace (fq_words(rows) words, zeroed before the first launch of a call; every launch
-    // leaves it zeroed), or null = k_gl4f unavailable
-    unsigned* fq;
     // v5 only (J > 21): run the GEMM phase alone and leave the pre-mix Y in `out` (k_attention_mix
     // mixes the to_qkv layer); hipErrorNotSupported where the route cannot
     int skip_mix = 0;
 };
-// k_gl4f work-queue block: 8 per-XCD item heads (own 128-B lines), the row-group claim counter,
-// the exit counter, per XCD the row group of each slot, per row group its finished GEMM items
-constexpr int kFqNext = 256, kFqExit = 288, kFqSlot = 320, kFqRows = 128;
-inline int64_t fq_rgs(int64_t rows) { return (rows + kFqRows - 1) / kFqRows; }
-inline int64_t fq_words(int64_t rows) { return (kFqSlot + 8 * (fq_rgs(rows) + 2) + fq_rgs(rows) + 63) / 64 * 64; }
 int diag_flags();  // SKELDIFF_DIAG (sd_plan.hip)
 
 // Kernels a sampling call launched (SD_OPT_LAST_ROUTE): every graph-linear / attention launch site
@@ -96,8 +88,7 @@ enum RouteBits : unsigned {
     kRouteV5Mix = 32,      // k_gl5_gemm / k_gl5_mix (J > 21)
     kRouteExact = 64,      // exact-f32 generations v1-v3
     kRouteAttention = 128,  // k_attention: the separate attention kernel (J > 21, unfused routes)
-    kRouteFusedSmall = 256,  // k_gl4 MODE 4: small-batch fused graph-linear tile
-    kRouteFusedLayer = 512,  // k_gl4f: GEMM + mixing phase of a plain layer in one launch
+    // 256 / 512: round 5's small-batch fused tile and fused layer kernel (removed in round 6)
     kRouteAttnMix = 1024     // k_attention_mix: the to_qkv layer's mixing inside the attention kernel
 };
 extern thread_local unsigned g_route_bits;
@@ -116,7 +107,6 @@ hipError_t make_bf16_weights(const float* W, int ntypes, int N, int K, SplitW* o
 // Multi-head attention over joints (attention.py:122-136) from a (B, J, 3*heads*dh) qkv buffer.
 struct AttnArgs {
     const float* qkv; float* out; int64_t B; int J; int heads; int dh; float scale;
-    int tail = 0;  // SD_OPT_ATTENTION 1: k_attention's tail form at 49 <= J <= 52 (default: padded)
     // SD_OPT_ATTENTION 2: qkv holds the to_qkv layer's PRE-mix Y and the kernel mixes it with this
     // (J, J) G-hat first (k_attention_mix, 49 <= J <= 52, dh 32); null: qkv is mixed
     const float* G = nullptr;
@@ -139,8 +129,6 @@ struct UpdArgs {
     unsigned* dbg;  // SD_DEBUG_LDS builds only
     int x0_bf16, xt_bf16, out_bf16;  // bf16 latents (precision mode 2); out2 / records stay f32
     int elementwise;  // SD_OPT_UPDATE_KERNEL: 0 k_update_mfma where it applies, 1 the element-per-thread forms
-    int pipe;         // SD_OPT_UPDATE_KERNEL 2: k_update_pipe for full batches of J <= 16 (A/B)
-    int v2;           // SD_OPT_UPDATE_KERNEL 3: k_update_v2 (8-B fragment loads) for full batches of J <= 16 (A/B)
     // diagnostics only (sd_debug_update_dump): the J values of x0 (activation + clamp applied),
     // x_t and sigma eps each thread computed from, stored after its outputs; null = off
     float* dump_x0; float* dump_xt; float* dump_ev;

@@ -269,17 +269,6 @@ hipError_t launch_graph_linear_v1(const GLArgs& a, bool rms, hipStream_t s) {
 
 // DH: the head width at compile time (32, the release model: both 16-wide chunks' loads are
 // issued together and the V loads with them, so a wave pays one memory latency), 0 = runtime.
-// TAIL (JT = 4, DH = 32, 48 < J <= 52: MANO J = 51 / 52): the last node tile has only J - 48 real
-// rows, so its key rows j = 48 .. J-1 of S^T and its value rows of O^T leave the MFMAs (12 of 16
-// S tiles, 3 of 4 k tiles of O) for an fmaf chain on the VALU in the MFMA's own k order -- the
-// f32 MFMA sums its k = 4 products as an fmaf chain, and the padded rows added exact zeros -- so
-// the result is the padded form's bit for bit (test_attention_tail_bitwise_vs_padded).  Plan option
-// SD_OPT_ATTENTION 1; not the default: config 3 measured 3,641 vs 3,677 futures/s for the padded form
-// (the kernel is not MFMA-bound at 2 waves / SIMD, and the tail adds ~400 VALU / readlane / shuffle
-// instructions per wave to its critical path):
-//   S^T[48 + r][n] (lane n): sum over d in the (u, e, g) order of the QK MFMAs of
-//     K[48 + r][d] (read from the key fragments with v_readlane) * Q[n][d] scale (the lane's row);
-//   O^T[d][n] += V[48 + r][d] P^T[48 + r][n] after the 12 PV k tiles, r = 0 .. J - 49 in order.
 // Where the attention reads q / k / v: the (B, J, 3 hid) qkv rows in HBM (k_attention), or one
 // head's mixed q | k | v in the wave's LDS region (k_attention_mix).  c: a column of the head
 // (0 .. dh - 1), a multiple of 4 for the 16-B forms.
@@ -303,10 +292,9 @@ struct AttnSrcL {
 };
 
 // One wave's attention of (row b, head h) from `src` (k_attention's math; every caller the same bits)
-template <int JT, int DH, bool TAIL, class Src>
+template <int JT, int DH, class Src>
 __device__ __forceinline__ void attention_body(const AttnArgs& p, const Src& src, int64_t b, int h, int lane) {
-    static_assert(!TAIL || (JT == 4 && DH == 32), "the tail form is the MANO J = 49..52 kernel");
-    constexpr int JA = TAIL ? JT - 1 : JT;  // node tiles on the MFMAs as keys / values
+    constexpr int JA = JT;  // node tiles as keys / values (round 5's 48-node tail form: git history)
     const int lr = lane & 15, lg = lane >> 4;
     const int J = p.J, dh = DH ? DH : p.dh, hid = p.heads * dh;
 
@@ -328,19 +316,6 @@ __device__ __forceinline__ void attention_body(const AttnArgs& p, const Src& src
 #pragma unroll
             for (int s4 = 0; s4 < 4; ++s4) v[jt][s4] = src.v(min(jt * 16 + 4 * lg + s4, J - 1), dc + lr);
     };
-    // TAIL: this lane's query row (n = lane, scaled as the B fragments) and the tail value rows
-    // V[48 + r][dc + 4 lg .. + 3] for both 16-wide chunks, issued with the fragment loads
-    constexpr int QW = TAIL ? 8 : 1;
-    floatx4 qrow[QW], vt[TAIL ? 2 : 1][TAIL ? 4 : 1];
-    if constexpr (TAIL) {
-#pragma unroll
-        for (int c = 0; c < 8; ++c) qrow[c] = src.q4(min(lane, J - 1), 4 * c);
-#pragma unroll
-        for (int u = 0; u < 2; ++u)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) vt[u][r] = src.v4(min(48 + r, J - 1), 16 * u + 4 * lg);
-    }
-    float tl[4] = {0.f, 0.f, 0.f, 0.f};  // TAIL: S^T[48 + r][n = lane]
     auto mask_v = [&](floatx4* v) {
 #pragma unroll
         for (int jt = 0; jt < JA; ++jt)
@@ -379,35 +354,8 @@ __device__ __forceinline__ void attention_body(const AttnArgs& p, const Src& src
                 for (int jt = 0; jt < JA; ++jt)
 #pragma unroll
                     for (int nt = 0; nt < JT; ++nt) S[jt][nt] = mfma4(ka[u][jt][e], qv[u][nt][e], S[jt][nt]);
-            if constexpr (TAIL) {  // key rows 48 + r: the MFMA's chain order, k = (e, g), d = 16 u + 4 g + e
-#pragma unroll
-                for (int e = 0; e < 4; ++e)
-#pragma unroll
-                    for (int g = 0; g < 4; ++g) {
-                        const float q = qrow[4 * u + g][e] * p.scale;
-                        // the element through a scalar first: __builtin_bit_cast of a vector-element
-                        // subscript (ka[..][e]) reads element 0 for every e with this compiler
-                        // (found here: tools/readlane_probe.hip)
-                        const float ke = ka[u][JT - 1][e];
-#pragma unroll
-                        for (int r = 0; r < 4; ++r) {
-                            const float k = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(ke), 16 * g + r));
-                            tl[r] = fmaf(k, q, tl[r]);
-                        }
-                    }
-            }
         }
     }
-    if constexpr (TAIL) {  // S^T[48 + 4 lg + i][nt 16 + lr] in the MFMA layout: rows 48 + i at lg = 0, zero rows beyond
-#pragma unroll
-        for (int nt = 0; nt < JT; ++nt)
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                const float t = __shfl(tl[i], nt * 16 + lr);
-                S[JT - 1][nt][i] = (lg == 0 && 48 + i < J) ? t : 0.f;
-            }
-    }
-
     // softmax over j (rows of S^T) for every query column n = nt*16 + lr
 #pragma unroll
     for (int nt = 0; nt < JT; ++nt) {
@@ -451,18 +399,6 @@ __device__ __forceinline__ void attention_body(const AttnArgs& p, const Src& src
             for (int e = 0; e < 4; ++e)
 #pragma unroll
                 for (int nt = 0; nt < JT; ++nt) o[nt] = mfma4(v[jt][e], S[jt][nt][e], o[nt]);
-        if constexpr (TAIL) {  // value rows 48 + r, last in the chain as in the padded k tile
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                if (48 + r >= J) break;  // wave-uniform
-#pragma unroll
-                for (int nt = 0; nt < JT; ++nt) {
-                    const float pr = __shfl(S[JT - 1][nt][r], lr);  // P^T[48 + r][nt 16 + lr] from lane (lr, 0)
-#pragma unroll
-                    for (int i = 0; i < 4; ++i) o[nt][i] = fmaf(vt[dc / 16][r][i], pr, o[nt][i]);
-                }
-            }
-        }
 #pragma unroll
         for (int nt = 0; nt < JT; ++nt) {
             const int n = nt * 16 + lr;
@@ -475,7 +411,7 @@ __device__ __forceinline__ void attention_body(const AttnArgs& p, const Src& src
 }
 
 
-template <int JT, int DH = 0, bool TAIL = false>
+template <int JT, int DH = 0>
 __global__ __launch_bounds__(256) void k_attention(const AttnArgs p) {
     const int lane = threadIdx.x & 63;
     const int64_t pair = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -486,7 +422,7 @@ __global__ __launch_bounds__(256) void k_attention(const AttnArgs p) {
     const int64_t rs = 3 * (int64_t)hid;
     const float* base = p.qkv + b * J * rs;
     const AttnSrcG src{base + h * dh, base + hid + h * dh, base + 2 * hid + h * dh, rs};
-    attention_body<JT, DH, TAIL>(p, src, b, h, lane);
+    attention_body<JT, DH>(p, src, b, h, lane);
 }
 
 // k_attention_mix (SD_OPT_ATTENTION 2; 49 <= J <= 52, dh = 32: MANO): the to_qkv layer's node mixing
@@ -568,7 +504,7 @@ __global__ __launch_bounds__(256, 2) void k_attention_mix(const AttnArgs p) {
                 *reinterpret_cast<floatx4*>(sy + AttnSrcL::at(i, 16 * cb + 4 * l4)) = mo[cb][ib] + 0.f;
         }
     }
-    attention_body<4, DH, false>(p, AttnSrcL{sy}, b, h, lane);
+    attention_body<4, DH>(p, AttnSrcL{sy}, b, h, lane);
 }
 
 hipError_t launch_attention(const AttnArgs& a, hipStream_t s) {
@@ -586,7 +522,6 @@ hipError_t launch_attention(const AttnArgs& a, hipStream_t s) {
         if (a.J <= 16) hipLaunchKernelGGL((k_attention<1, 32>), grid, dim3(256), 0, s, a);
         else if (a.J <= 32) hipLaunchKernelGGL((k_attention<2, 32>), grid, dim3(256), 0, s, a);
         else if (a.J <= 48) hipLaunchKernelGGL((k_attention<3, 32>), grid, dim3(256), 0, s, a);
-        else if (a.J <= 52 && a.tail) hipLaunchKernelGGL((k_attention<4, 32, true>), grid, dim3(256), 0, s, a);
         else hipLaunchKernelGGL((k_attention<4, 32>), grid, dim3(256), 0, s, a);
         return hipGetLastError();
     }
@@ -1264,330 +1199,6 @@ __global__ __launch_bounds__(256) void k_update_mfma(const UpdArgs p) {
 #endif
 }
 
-// k_update_mfma's arithmetic on a persistent, software-pipelined grid (full batches, f32 latents).
-// k_update_mfma gives every 4-row group its own workgroup; at 3,200 rows all 800 are resident at
-// once and walk load -> Philox -> barrier -> MFMA -> store in lockstep -- the hypothesis this form
-// tested (26 us alone, the same with given noise, i.e. not the Philox: profiles/r05d/update_probe.txt);
-// it measured no faster (plan option SD_OPT_UPDATE_KERNEL 2, not the default).  Here a workgroup walks groups g = blockIdx, + gridDim, ... of
-// R rows: group g + gridDim's x0 / x_t fragments are issued before group g's phase A, so the next
-// group's loads stream under this group's Philox, MFMAs and stores; the tables are loaded once per
-// workgroup; sigma . eps is double-buffered in LDS (one barrier per group).  Each row's products,
-// sums and stores are k_update_mfma's: bitwise equal (test_update_mfma_bitwise_vs_elementwise).
-template <int JP, int R, int MT, int NG>
-__global__ __launch_bounds__(256, 2) void k_update_pipe(const UpdArgs p) {
-    constexpr int KS = JP / 4, IB = JP / 16, TSJ = JP + 2;
-    static_assert(JP == 16 && 4 % R == 0, "J <= 16 (NG register sets of B fragments)");
-    const int J = p.J, D = p.D, JD = J * D, QPR = J * (D >> 2);
-    extern __shared__ __attribute__((aligned(16))) float sm[];
-    float* sTab = sm;
-    const int DS = D + 16, EVS = R * J * DS;  // floats per sigma . eps buffer
-    float* sSig = sm + 3 * JP * TSJ;          // sigma_j
-    float* sEv0 = sm + ((3 * JP * TSJ + JP + 3) & ~3);
-    const int tid = threadIdx.x, lane = tid & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int r = wave % R, l16 = lane & 15, l4 = lane >> 4;
-    const int nct = D >> 4, ct0 = wave / R, cstep = 4 / R;
-    const int64_t ngroups = (p.B + R - 1) / R;
-    constexpr int TPT = (3 * JP * JP + 255) / 256;
-    float tv[TPT];
-#pragma unroll
-    for (int k = 0; k < TPT; ++k) {
-        const int q = min(tid + 256 * k, 3 * JP * JP - 1);
-        const int m = q / (JP * JP), ij = q % (JP * JP), i = ij / JP, j = ij % JP;
-        const float* tab = m == 0 ? p.C1 : m == 1 ? p.C2 : p.U;
-        tv[k] = tab[min(i, J - 1) * J + min(j, J - 1)];
-    }
-    float sgv = 1.f;
-    if (tid < J && p.noise_mode != 0) sgv = p.sig[tid];  // before the fragments: its wait leaves them in flight
-    auto load_b = [&](int64_t g, const float* src, float (*dst)[KS]) {
-        const int64_t row = min(g * R + r, p.B - 1);  // clamped: a dead row loads a valid one
-        const float* base = src + row * (int64_t)JD;
-#pragma unroll
-        for (int q = 0; q < MT; ++q)
-#pragma unroll
-            for (int ks = 0; ks < KS; ++ks)
-                dst[q][ks] = base[min(4 * ks + l4, J - 1) * D + 16 * min(ct0 + q * cstep, nct - 1) + l16];
-    };
-    // NG groups per workgroup, g_k = blockIdx + k gridDim; set k holds group k's fragments, issued
-    // one group ahead (straight-line code: no loop-carried register sets for the waitcnt pass)
-    float bx[NG][MT][KS], bt[NG][MT][KS];
-    load_b(blockIdx.x, p.x0, bx[0]);
-    load_b(blockIdx.x, p.xt, bt[0]);
-#pragma unroll
-    for (int k = 0; k < TPT; ++k) {
-        const int q = tid + 256 * k;
-        const int i = (q % (JP * JP)) / JP, j = q % JP;
-        if (q < 3 * JP * JP) sTab[(q / JP) * TSJ + q % JP] = (i < J && j < J) ? tv[k] : 0.f;
-    }
-    if (tid < J) sSig[tid] = sgv;
-    uint64_t seed = p.seed;
-    int64_t row0 = p.row0;
-    if (p.noise_mode == 2 && p.rng_dev) {
-        seed = p.rng_dev[0];
-        row0 = (int64_t)p.rng_dev[1];
-    }
-    row0 += p.row_shift;
-    __syncthreads();  // the tables and sigma
-    float A[3][IB][KS];
-#pragma unroll
-    for (int m = 0; m < 3; ++m)
-#pragma unroll
-        for (int ib = 0; ib < IB; ++ib)
-#pragma unroll
-            for (int ks = 0; ks < KS; ++ks) A[m][ib][ks] = sTab[(m * JP + 16 * ib + l16) * TSJ + 4 * ks + l4];
-    // phase A of group gg into buffer ev (noise mode as a template constant: see k_update_mfma)
-    auto phase_a = [&](auto nm, int64_t gg, float* ev) {
-        constexpr int NM = decltype(nm)::value;
-        // straight-line (J <= 16, D <= 96: at most R * 384 quads): with a runtime trip count the
-        // register allocator split the live in-flight fragments around the loop (vmcnt(0) on entry)
-        constexpr int NQ = (R * JP * 24 + 255) / 256;
-#pragma unroll
-        for (int it = 0; it < NQ; ++it) {
-            const int q = tid + 256 * it;
-            if (q >= R * QPR) continue;
-            const int rr = q / QPR, qq = q - rr * QPR, j = qq / (D >> 2), d = 4 * (qq - j * (D >> 2));
-            const int64_t rw = gg * R + rr;
-            if (rw >= p.B) continue;
-            floatx4 e = {0.f, 0.f, 0.f, 0.f};
-            if constexpr (NM == 1) {
-                e = ld4(p.eps + rw * p.eps_rs + j * D + d);
-            } else if constexpr (NM == 2) {
-                const uint4 x = philox_at(seed, (uint64_t)(row0 + rw), p.step, (uint32_t)qq);
-                const floatx2 z0 = box_muller(x.x, x.y), z1 = box_muller(x.z, x.w);
-                e = floatx4{z0.x, z0.y, z1.x, z1.y};
-            }
-            if (p.noise_out) *reinterpret_cast<floatx4*>(p.noise_out + rw * p.noise_rs + j * D + d) = e;
-            if constexpr (NM != 0) e *= sSig[j];
-            *reinterpret_cast<floatx4*>(ev + (rr * J + j) * DS + d) = e;
-        }
-    };
-#pragma unroll
-    for (int k = 0; k < NG; ++k) {
-        const int64_t gg = blockIdx.x + (int64_t)k * gridDim.x;
-        if (gg >= ngroups) break;  // uniform
-        if (k + 1 < NG && gg + gridDim.x < ngroups) {  // the next group's fragments first
-            load_b(gg + gridDim.x, p.x0, bx[k + 1 < NG ? k + 1 : k]);
-            load_b(gg + gridDim.x, p.xt, bt[k + 1 < NG ? k + 1 : k]);
-        }
-        float* ev = sEv0 + (k & 1) * EVS;  // double-buffered: one barrier per group
-        if (p.noise_mode == 2) phase_a(std::integral_constant<int, 2>{}, gg, ev);
-        else if (p.noise_mode == 1) phase_a(std::integral_constant<int, 1>{}, gg, ev);
-        else phase_a(std::integral_constant<int, 0>{}, gg, ev);
-        __syncthreads();
-        const int64_t row = gg * R + r;
-        if (row >= p.B) continue;  // wave-uniform: the ragged last group (no later group: no later barrier)
-        const int64_t rb = row * (int64_t)JD;
-#pragma unroll
-        for (int q = 0; q < MT; ++q)
-#pragma unroll
-            for (int ks = 0; ks < KS; ++ks) {
-                float a = bx[k][q][ks];
-                if (p.act == 1) a = tanhf(a);
-                bx[k][q][ks] = p.clip ? fminf(fmaxf(a, -1.f), 1.f) : a;
-            }
-        floatx4 vres[MT][IB];
-#pragma unroll
-        for (int q = 0; q < MT; ++q) {
-            const int ct = ct0 + q * cstep;
-            if (ct >= nct) continue;  // wave-uniform
-            const int n = 16 * ct + l16;
-            float bxa[KS], bta[KS], be[KS];
-#pragma unroll
-            for (int ks = 0; ks < KS; ++ks) {
-                const int j = 4 * ks + l4;
-                const bool ok = j < J;
-                bxa[ks] = ok ? bx[k][q][ks] : 0.f;
-                bta[ks] = ok ? bt[k][q][ks] : 0.f;
-                be[ks] = ok ? ev[(r * J + j) * DS + n] : 0.f;
-            }
-#pragma unroll
-            for (int ib = 0; ib < IB; ++ib) {
-                if (16 * ib >= J) continue;
-                floatx4 m1 = {0.f, 0.f, 0.f, 0.f}, m2 = m1, nz = m1;
-#pragma unroll
-                for (int ks = 0; ks < KS; ++ks) {
-                    m1 = __builtin_amdgcn_mfma_f32_16x16x4f32(bxa[ks], A[0][ib][ks], m1, 0, 0, 0);
-                    m2 = __builtin_amdgcn_mfma_f32_16x16x4f32(bta[ks], A[1][ib][ks], m2, 0, 0, 0);
-                    nz = __builtin_amdgcn_mfma_f32_16x16x4f32(be[ks], A[2][ib][ks], nz, 0, 0, 0);
-                }
-                const floatx4 mean = m1 + m2;
-                vres[q][ib] = (p.noise_mode != 0) ? mean + nz : mean;
-                const int i = 16 * ib + l16;
-                if (p.mean_out && i < J)
-                    *reinterpret_cast<floatx4*>(p.mean_out + row * p.mean_rs + i * D + 16 * ct + 4 * l4) = mean;
-            }
-        }
-#pragma unroll
-        for (int q = 0; q < MT; ++q) {
-            const int ct = ct0 + q * cstep;
-            if (ct >= nct) continue;
-            const int n4 = 16 * ct + 4 * l4;
-#pragma unroll
-            for (int ib = 0; ib < IB; ++ib) {
-                const int i = 16 * ib + l16;
-                if (16 * ib >= J || i >= J) continue;
-                *reinterpret_cast<floatx4*>(p.out + rb + i * D + n4) = vres[q][ib];
-                if (p.out2) *reinterpret_cast<floatx4*>(p.out2 + row * p.out2_rs + i * D + n4) = vres[q][ib];
-            }
-        }
-    }
-}
-
-// k_update_mfma (R = 4, J <= 16) with 8-B fragment loads: one wave per row, its 96 columns as three
-// 32-column groups of two "virtual" 16-column tiles.  Lane (l16, l4) loads x[j = 4 ks + l4][32 g +
-// 2 l16 .. + 1] (16 lanes: 128 contiguous bytes, a whole line) and feeds element e of it as the A row
-// l16 of virtual tile (g, e) -- columns 32 g + 2 l16 + e.  The MFMA output row rho = 4 l4 + rr of tile
-// (g, e) is column 32 g + 8 l4 + 2 rr + e, so a lane holds 8 consecutive columns of its node after
-// both tiles: two 16-B stores.  Half the load instructions of k_update_mfma (whose 16 lanes read 64-B
-// half lines) for the same products in the same k order: bitwise equal.  SD_OPT_UPDATE_KERNEL 3.
-template <int JP>
-__global__ __launch_bounds__(256) void k_update_v2(const UpdArgs p) {
-    constexpr int R = 4, KS = JP / 4, TSJ = JP + 2, NG = 3;
-    static_assert(JP == 16, "one 16-node output block");
-    const int J = p.J, D = p.D, JD = J * D, QPR = J * (D >> 2), ng = D >> 5;
-    extern __shared__ __attribute__((aligned(16))) float sm[];
-    float* sTab = sm;
-    const int DS = D + 16;
-    float* sEv = sm + ((3 * JP * TSJ + 3) & ~3);
-    const int tid = threadIdx.x, lane = tid & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int64_t rowg = (int64_t)blockIdx.x * R;
-    const int64_t row = rowg + wave;
-    const bool live = row < p.B;
-    const int64_t rb = (live ? row : 0) * (int64_t)JD;
-    const int l16 = lane & 15, l4 = lane >> 4;
-    constexpr int TPT = (3 * JP * JP + 255) / 256;
-    float tv[TPT];
-#pragma unroll
-    for (int k = 0; k < TPT; ++k) {
-        const int q = min(tid + 256 * k, 3 * JP * JP - 1);
-        const int m = q / (JP * JP), ij = q % (JP * JP), i = ij / JP, j = ij % JP;
-        const float* tab = m == 0 ? p.C1 : m == 1 ? p.C2 : p.U;
-        tv[k] = tab[min(i, J - 1) * J + min(j, J - 1)];
-    }
-    constexpr int SGP = 8;
-    float sgp[SGP];
-    if (p.noise_mode != 0) {
-#pragma unroll
-        for (int it = 0; it < SGP; ++it) sgp[it] = p.sig[min(((tid + 256 * it) % QPR) / (D >> 2), J - 1)];
-    }
-    floatx2 bx[NG][KS], bt[NG][KS];
-#pragma unroll
-    for (int g = 0; g < NG; ++g)
-#pragma unroll
-        for (int ks = 0; ks < KS; ++ks) {
-            const int64_t o = rb + min(4 * ks + l4, J - 1) * D + 32 * min(g, ng - 1) + 2 * l16;
-            bx[g][ks] = ld2(p.x0 + o);
-            bt[g][ks] = ld2(p.xt + o);
-        }
-#pragma unroll
-    for (int k = 0; k < TPT; ++k) {
-        const int q = tid + 256 * k;
-        const int i = (q % (JP * JP)) / JP, j = q % JP;
-        if (q < 3 * JP * JP) sTab[(q / JP) * TSJ + q % JP] = (i < J && j < J) ? tv[k] : 0.f;
-    }
-    uint64_t seed = p.seed;
-    int64_t row0 = p.row0;
-    if (p.noise_mode == 2 && p.rng_dev) {
-        seed = p.rng_dev[0];
-        row0 = (int64_t)p.rng_dev[1];
-    }
-    row0 += p.row_shift;
-    auto phase_a = [&](auto nm, int q, float sg) {
-        constexpr int NM = decltype(nm)::value;
-        const int rr = q / QPR, qq = q % QPR, j = qq / (D >> 2), d = 4 * (qq % (D >> 2));
-        const int64_t rw = rowg + rr;
-        if (rw >= p.B) return;
-        floatx4 e = {0.f, 0.f, 0.f, 0.f};
-        if constexpr (NM == 1) {
-            e = ld4(p.eps + rw * p.eps_rs + j * D + d);
-        } else if constexpr (NM == 2) {
-            const uint4 x = philox_at(seed, (uint64_t)(row0 + rw), p.step, (uint32_t)qq);
-            const floatx2 z0 = box_muller(x.x, x.y), z1 = box_muller(x.z, x.w);
-            e = floatx4{z0.x, z0.y, z1.x, z1.y};
-        }
-        if (p.noise_out) *reinterpret_cast<floatx4*>(p.noise_out + rw * p.noise_rs + j * D + d) = e;
-        if constexpr (NM != 0) e *= sg;
-        *reinterpret_cast<floatx4*>(sEv + (rr * J + j) * DS + d) = e;
-    };
-    auto run_a = [&](auto nm) {
-#pragma unroll
-        for (int it = 0; it < SGP; ++it)
-            if (tid + 256 * it < R * QPR) phase_a(nm, tid + 256 * it, sgp[it]);
-        for (int q = tid + 256 * SGP; q < R * QPR; q += 256)
-            phase_a(nm, q, decltype(nm)::value != 0 ? p.sig[(q % QPR) / (D >> 2)] : 1.f);
-    };
-    if (p.noise_mode == 2) run_a(std::integral_constant<int, 2>{});
-    else if (p.noise_mode == 1) run_a(std::integral_constant<int, 1>{});
-    else run_a(std::integral_constant<int, 0>{});
-    __syncthreads();
-    if (!live) return;
-    float A[3][KS];
-#pragma unroll
-    for (int m = 0; m < 3; ++m)
-#pragma unroll
-        for (int ks = 0; ks < KS; ++ks) A[m][ks] = sTab[(m * JP + l16) * TSJ + 4 * ks + l4];
-#pragma unroll
-    for (int g = 0; g < NG; ++g)
-#pragma unroll
-        for (int ks = 0; ks < KS; ++ks) {
-            floatx2 a = bx[g][ks];
-            if (p.act == 1) {
-                a.x = tanhf(a.x);
-                a.y = tanhf(a.y);
-            }
-            bx[g][ks] = p.clip ? floatx2{fminf(fmaxf(a.x, -1.f), 1.f), fminf(fmaxf(a.y, -1.f), 1.f)} : a;
-        }
-    floatx4 vres[NG][2], mres[NG][2];
-#pragma unroll
-    for (int g = 0; g < NG; ++g) {
-        if (g >= ng) continue;  // wave-uniform
-#pragma unroll
-        for (int e = 0; e < 2; ++e) {
-            const int n = 32 * g + 2 * l16 + e;
-            float bxa[KS], bta[KS], be[KS];
-#pragma unroll
-            for (int ks = 0; ks < KS; ++ks) {
-                const int j = 4 * ks + l4;
-                const bool ok = j < J;
-                bxa[ks] = ok ? bx[g][ks][e] : 0.f;
-                bta[ks] = ok ? bt[g][ks][e] : 0.f;
-                be[ks] = ok ? sEv[(wave * J + j) * DS + n] : 0.f;
-            }
-            floatx4 m1 = {0.f, 0.f, 0.f, 0.f}, m2 = m1, nz = m1;
-#pragma unroll
-            for (int ks = 0; ks < KS; ++ks) {
-                m1 = __builtin_amdgcn_mfma_f32_16x16x4f32(bxa[ks], A[0][ks], m1, 0, 0, 0);
-                m2 = __builtin_amdgcn_mfma_f32_16x16x4f32(bta[ks], A[1][ks], m2, 0, 0, 0);
-                nz = __builtin_amdgcn_mfma_f32_16x16x4f32(be[ks], A[2][ks], nz, 0, 0, 0);
-            }
-            mres[g][e] = m1 + m2;
-            vres[g][e] = (p.noise_mode != 0) ? mres[g][e] + nz : mres[g][e];
-        }
-    }
-    const int i = l16;
-    if (i >= J) return;
-#pragma unroll
-    for (int g = 0; g < NG; ++g) {
-        if (g >= ng) continue;
-        const int n0 = 32 * g + 8 * l4;
-        const floatx4 v0 = {vres[g][0][0], vres[g][1][0], vres[g][0][1], vres[g][1][1]};
-        const floatx4 v1 = {vres[g][0][2], vres[g][1][2], vres[g][0][3], vres[g][1][3]};
-        *reinterpret_cast<floatx4*>(p.out + rb + i * D + n0) = v0;
-        *reinterpret_cast<floatx4*>(p.out + rb + i * D + n0 + 4) = v1;
-        if (p.out2) {
-            *reinterpret_cast<floatx4*>(p.out2 + row * p.out2_rs + i * D + n0) = v0;
-            *reinterpret_cast<floatx4*>(p.out2 + row * p.out2_rs + i * D + n0 + 4) = v1;
-        }
-        if (p.mean_out) {
-            *reinterpret_cast<floatx4*>(p.mean_out + row * p.mean_rs + i * D + n0) =
-                floatx4{mres[g][0][0], mres[g][1][0], mres[g][0][1], mres[g][1][1]};
-            *reinterpret_cast<floatx4*>(p.mean_out + row * p.mean_rs + i * D + n0 + 4) =
-                floatx4{mres[g][0][2], mres[g][1][2], mres[g][0][3], mres[g][1][3]};
-        }
-    }
-}
-
 // rows at or below which launch_update runs k_update_row (process default SKELDIFF_UPDATE_ROWS)
 static int64_t g_update_rows = [] {
     const char* e = getenv("SKELDIFF_UPDATE_ROWS");
@@ -1613,32 +1224,6 @@ hipError_t launch_update(const UpdArgs& a, hipStream_t s) {
         }
         hipLaunchKernelGGL(kern, dim3((unsigned)a.B), dim3(256), lds, s, a);
         return hipGetLastError();
-    }
-    // SD_OPT_UPDATE_KERNEL 3: 8-B fragment loads (A/B), full batches of f32 latents, J <= 16, D 32 .. 96
-    if (a.v2 && !a.iso && a.J <= 16 && a.D % 32 == 0 && a.D <= 96 && a.B > g_update_rows && !a.x0_bf16 && !a.xt_bf16 &&
-        !a.out_bf16 && !a.dump_x0 && !a.dump_ev) {
-        const size_t lds = (((3 * 16 * 18 + 3) & ~(size_t)3) + 4 * (size_t)a.J * (a.D + 16)) * sizeof(float);
-        hipLaunchKernelGGL(k_update_v2<16>, dim3((unsigned)((a.B + 3) / 4)), dim3(256), lds, s, a);
-        return hipGetLastError();
-    }
-    // full batches of f32 latents: the persistent pipelined form (2-row groups, 2 workgroups per CU)
-    // (plan option SD_OPT_UPDATE_KERNEL 2 only: measured no faster -- 27.7 vs 27.1 us with device noise,
-    // 26.5 vs 25.5 with given noise, alone at 3,200 rows; profiles/r05d/update_probe.txt)
-    if (a.pipe && !a.iso && a.J <= 16 && a.D % 16 == 0 && a.D / 16 <= 6 && a.B > g_update_rows &&
-        !a.x0_bf16 && !a.xt_bf16 && !a.out_bf16 && !a.dump_x0 && !a.dump_ev) {
-        constexpr int NG = 3;  // groups per workgroup
-        const int64_t groups = (a.B + 1) / 2;
-        const dim3 grid((unsigned)((groups + NG - 1) / NG));
-        auto go = [&](auto kern, int JP) -> hipError_t {
-            const size_t lds = (((3 * (size_t)JP * (JP + 2) + JP + 3) & ~(size_t)3) + 2 * 2 * (size_t)a.J * (a.D + 16)) * sizeof(float);
-            if (lds > 64 * 1024) {
-                const hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-                if (e != hipSuccess) return e;
-            }
-            hipLaunchKernelGGL(kern, grid, dim3(256), lds, s, a);
-            return hipGetLastError();
-        };
-        return go(k_update_pipe<16, 2, 3, NG>, 16);
     }
     // the instantiations below cover MT column tiles per wave, cstep = 4 / R apart: R = 1 -> MT = 2
     // (tiles w, w + 4: D <= 128), R = 4 -> MT = 6 (tiles 0..5: D <= 96); wider rows take the forms below

@@ -160,9 +160,9 @@ struct sd_plan {
     int prec = 0;          // sd_plan_set_precision: 0 f32-accurate, 1 half (f16 products)
     // kernel options (sd_plan_set_option), initialised from the process defaults at creation
     int variant = 0, gl4_cfg = 0, gl4_stage = 0, split = 0, chains = 0;
-    int upd_elem = 0;  // SD_OPT_UPDATE_KERNEL: 1 = the element-per-thread update forms, 2 = k_update_pipe
+    int upd_elem = 0;  // SD_OPT_UPDATE_KERNEL: 1 = the element-per-thread update forms
     int v5_valu = 0;   // SD_OPT_V5_MIX: 1 = the VALU mixing pass of v5
-    int attn_tail = 0;  // SD_OPT_ATTENTION: 0 auto (= 2 where it applies), 1 tail form, 2 k_attention_mix, 3 padded
+    int attn_tail = 0;  // SD_OPT_ATTENTION: 0 auto (= 2 where it applies), 2 k_attention_mix, 3 separate mixing pass
     bool fuse_attention_now() const { return fuse_ok && (variant == 0 || variant == 4); }
     // SD_OPT_ATTENTION 2 where it applies: the v5 route's to_qkv mixing inside the attention kernel
     bool attn_mix_now() const {
@@ -262,18 +262,22 @@ int dalloc(sd_plan* p, T** out, size_t n) {
 // workspace carve (all offsets 256-B aligned)
 struct WS {
     uint64_t* rng;      // {seed, row0} of the device noise (graph replays); rng + 4: status word
-    unsigned* fq;       // k_gl4f work-queue blocks: one of sd::fq_words(rows) words per row chain
-    int64_t fq_stride;  // words per block
     float *x, *r, *h, *qkv, *o, *res, *x0, *img0, *img1;
 };
 
 size_t align256(size_t v) { return (v + 255) & ~(size_t)255; }
 
+// floats per (row, node) of the qkv buffer: to_qkv's output, and the split route's pre-mix Y scratch
+// of every graph-linear outside the attention block (the widest layer's N: at least H)
+int64_t qkv_width(const sd_plan* p) {
+    return std::max<int64_t>({p->d.use_attention ? 3 * (int64_t)p->hid : 0, (int64_t)p->H, (int64_t)p->O});
+}
+
 size_t carve(const sd_plan* p, int64_t rows, char* base, WS* w) {
     const size_t f = sizeof(float);
     const size_t rp = (size_t)((rows + 31) / 32 * 32);  // activations: padded to the 32-row blocks of the v4 layout
     const size_t nH = rp * p->J * p->H * f;
-    const size_t nQ = rp * p->J * (p->d.use_attention ? 3 * p->hid : p->H) * f;
+    const size_t nQ = rp * p->J * qkv_width(p) * f;
     const size_t nO = rp * p->J * (p->d.use_attention ? p->hid : p->H) * f;  // no attention: GL output
     const size_t nD = (size_t)rows * p->J * p->D * f;
     size_t off = 0;
@@ -285,8 +289,6 @@ size_t carve(const sd_plan* p, int64_t rows, char* base, WS* w) {
     WS tmp;
     WS& W = w ? *w : tmp;
     W.rng = (uint64_t*)take(64);
-    W.fq_stride = sd::fq_words(rows);
-    W.fq = (unsigned*)take((size_t)sd_plan::kMaxChains * W.fq_stride * sizeof(unsigned));
     W.x = (float*)take(nH);
     W.r = (float*)take(nH);
     W.h = (float*)take(nH);
@@ -301,11 +303,9 @@ size_t carve(const sd_plan* p, int64_t rows, char* base, WS* w) {
 
 // the workspace's status word (range-guard flags, sd_workspace_status)
 unsigned* ws_status(const WS& w) { return reinterpret_cast<unsigned*>(w.rng + 4); }
-// entry points zero the status word and every row chain's k_gl4f queue block (each fused launch
-// leaves its block zeroed again, so one memset per call covers all of its launches)
+// entry points zero the status word
 int ws_reset(const WS& w, hipStream_t s) {
     SD_HIP(hipMemsetAsync(ws_status(w), 0, sizeof(unsigned), s));
-    SD_HIP(hipMemsetAsync(w.fq, 0, (size_t)sd_plan::kMaxChains * w.fq_stride * sizeof(unsigned), s));
     return SD_OK;
 }
 
@@ -427,12 +427,11 @@ int run_denoiser(const sd_plan* p, const float* x_t, const float* x_cond, int64_
                                             (int64_t)p->J * H, s));
         return SD_OK;
     };
-    // v5 scratch (pre-mix activations of layers whose residual aliases their output): the qkv
-    // buffer, dead outside the attention block (>= rows * J * H floats)
-    const int64_t zs_cap = (rows + 31) / 32 * 32 * p->J * (int64_t)(p->d.use_attention ? 3 * p->hid : p->H);
+    // split-route / v5 scratch (pre-mix activations; v5: of layers whose residual aliases their
+    // output): the qkv buffer, dead outside the attention block, as wide as the widest layer
+    const int64_t zs_cap = (rows + 31) / 32 * 32 * p->J * qkv_width(p);
     auto lay = [B, tile_hint, &w, zs_cap, &bfl, route_rows](sd::GLArgs& g, int in, int res, int out) {
         g.status = ws_status(w);
-        g.fq = w.fq;
         g.route_rows = route_rows;
         g.zs = w.qkv;
         g.zs_cap = zs_cap;
@@ -515,7 +514,7 @@ int run_denoiser(const sd_plan* p, const float* x_t, const float* x_cond, int64_
                 SD_HIP(ge);
                 if (prof && prof->post(s)) return fail(SD_E_HIP, "hipEventRecord failed");
                 if ((rc = snap(a))) return rc;
-                sd::AttnArgs aa{w.qkv, w.o, rows, p->J, p->d.attn_heads, p->d.attn_dim_head, qscale, p->attn_tail == 1 ? 1 : 0,
+                sd::AttnArgs aa{w.qkv, w.o, rows, p->J, p->d.attn_heads, p->d.attn_dim_head, qscale,
                                 a.skip_mix ? a.G : nullptr};
                 SD_LAUNCH(prof, 1, sd::launch_attention(aa, s));
             }
@@ -596,8 +595,6 @@ int run_update(const sd_plan* p, const float* x0, const float* xt, const float* 
     u.J = p->J;
     u.D = p->D;
     u.elementwise = p->upd_elem == 1;
-    u.pipe = p->upd_elem == 2;
-    u.v2 = p->upd_elem == 3;
 #ifdef SD_DEBUG_LDS
     u.dbg = sd::debug_counters();
 #endif
@@ -691,10 +688,6 @@ int sd_plan_create(sd_plan** out, const sd_plan_desc* desc) {
     p->gl4_cfg = sd::gl4_tile_default();
     p->gl4_stage = sd::gl4_stage_default();
     p->chains = g_chains;
-    {  // SKELDIFF_UPDATE_KERNEL=0 at load: new plans start on the element-per-thread update forms
-        const char* e = getenv("SKELDIFF_UPDATE_KERNEL");
-        p->upd_elem = (e && atoi(e) == 0) ? 1 : 0;
-    }
 #ifdef SD_DEBUG_LDS
     (void)sd::debug_counters();  // allocated here, never during a stream capture
 #endif
@@ -1004,7 +997,6 @@ int sd_p_sample_update(const sd_plan* p, const float* x0_raw, const float* x_t, 
 
 static WS shift_ws(const sd_plan* p, const WS& w, int64_t r0, int chain) {
     WS o = w;
-    o.fq += chain * w.fq_stride;  // a queue block per row chain (chains run concurrently)
     const int64_t J = p->J;
     o.x += r0 * J * p->H;
     o.r += r0 * J * p->H;
@@ -1401,12 +1393,12 @@ static int g_test_variant = -1, g_test_tile = -1;  // -1: the process defaults (
 static int test_variant() { return g_test_variant >= 0 ? g_test_variant : sd::graph_linear_variant(); }
 static int test_tile() { return g_test_tile >= 0 ? g_test_tile : sd::gl4_tile_default(); }
 
-// split route of the test entry points (GLArgs::split: 0 auto, 1 never, 2 k_gl4y, 3 k_gl4t, 5
-// the fused small tile); 2 / 3 / 5 give sd_test_graph_linear* a scratch of its own for the pre-mix Y
+// split route of the test entry points (GLArgs::split: 0 auto, 1 never, 2 k_gl4y, 3 k_gl4t, 4 k_gl4t
+// except to_qkv + attention); 2 / 3 / 4 give sd_test_graph_linear* a scratch of its own for the pre-mix Y
 static int g_test_split = 0;
 int sd_test_set_split_route(int32_t route) {
     if (route == -1) return g_test_split;  // query
-    if (route < 0 || route > 5) return fail(SD_E_INVALID, "split route out of range");
+    if (route < 0 || route > 4) return fail(SD_E_INVALID, "split route out of range");
     const int old = g_test_split;
     g_test_split = route;
     return old;
@@ -1447,16 +1439,14 @@ int sd_plan_set_option(sd_plan* p, int32_t option, int64_t value) {
         case SD_OPT_LAST_CHAINS:
         case SD_OPT_LAST_ROUTE: return fail(SD_E_INVALID, "SD_OPT_LAST_CHAINS / SD_OPT_LAST_ROUTE are read-only");
         case SD_OPT_SPLIT_ROUTE:
-            if (value < 0 || value > 6)
-                return fail(SD_E_INVALID, "split route must be 0 (auto), 1 (never), 2 (always), 3 (always, tiled phase 1), "
-                                          "4 (tiled phase 1 except to_qkv + attention), 5 (small-batch fused tile) or "
-                                          "6 (tiled, plain layers on the fused layer kernel k_gl4f)");
+            if (value < 0 || value > 4)
+                return fail(SD_E_INVALID, "split route must be 0 (auto), 1 (never), 2 (always), 3 (always, tiled phase 1) "
+                                          "or 4 (tiled phase 1 except to_qkv + attention)");
             p->split = (int)value;
             return SD_OK;
         case SD_OPT_UPDATE_KERNEL:
-            if (value < 0 || value > 3)
-                return fail(SD_E_INVALID, "update kernel must be 0 (matrix cores where they apply), 1 (element-per-thread), "
-                                          "2 (the pipelined matrix-core form for full J <= 16 batches) or 3 (its 8-B-load form)");
+            if (value < 0 || value > 1)
+                return fail(SD_E_INVALID, "update kernel must be 0 (matrix cores where they apply) or 1 (element-per-thread)");
             p->upd_elem = (int)value;
             return SD_OK;
         case SD_OPT_V5_MIX:
@@ -1464,10 +1454,9 @@ int sd_plan_set_option(sd_plan* p, int32_t option, int64_t value) {
             p->v5_valu = (int)value;
             return SD_OK;
         case SD_OPT_ATTENTION:
-            if (value < 0 || value > 3)
-                return fail(SD_E_INVALID, "attention must be 0 (auto: 2 where it applies), 1 (tail form at 49 <= J <= 52), "
-                                          "2 (to_qkv mixing inside the attention kernel at 49 <= J <= 52) or 3 (padded form "
-                                          "after the separate mixing pass)");
+            if (value != 0 && value != 2 && value != 3)
+                return fail(SD_E_INVALID, "attention must be 0 (auto: 2 where it applies), 2 (to_qkv mixing inside the "
+                                          "attention kernel at 49 <= J <= 52) or 3 (the separate mixing pass)");
             p->attn_tail = (int)value;
             return SD_OK;
         default: return fail(SD_E_INVALID, "unknown option " + std::to_string(option));

@@ -123,16 +123,18 @@ class SamplingEngine:
     READ_ONLY = ("last_chains", "last_route")
     # The split-f16 graph-linear tiles need |x| < 65504.  A wave whose operands leave that range
     # recomputes its tiles on exact-f32 MFMA inside the kernel (sd_graph_linear_v4.hip:
-    # exact_tile_f32) and sets SD_STATUS_F16_RANGE in the workspace status word for information
-    # (status()); sample() needs no host check, no re-run and no warning: its latents are
+    # exact_tile_f32; every f16-product kernel: the split routes' GEMM phases and the one-kernel
+    # tiles) and sets SD_STATUS_F16_RANGE in the workspace status word for information (status());
+    # sample() needs no host check, no re-run and no warning: in f32 mode its latents are
     # f32-accurate for any finite input.
 
     def set_option(self, name: str, value: int) -> None:
         """Per-plan kernel option (sd_plan_set_option): "kernel_variant" (0 auto, 1..5),
         "gl4_tile" (<waves><row tiles><col tiles>, 0 auto), "row_chains" (1..8), "gl4_staging"
-        (0 LDS-DMA, 1 register-staged), "split_route" (0 auto, 1 never, 2 k_gl4y, 3 k_gl4t),
-        "update_kernel" (0 matrix cores, 1 element-per-thread, 2 pipelined), "attention" (0 auto,
-        1 tail form, 2 to_qkv mixing in the attention kernel, 3 padded), "v5_mix" (0 matrix cores, 1 VALU);
+        (0 LDS-DMA, 1 register-staged), "split_route" (0 auto, 1 never, 2 k_gl4y, 3 k_gl4t, 4 k_gl4t
+        except to_qkv + attention), "update_kernel" (0 matrix cores, 1 element-per-thread),
+        "attention" (0 auto, 2 to_qkv mixing in the attention kernel, 3 separate mixing pass),
+        "v5_mix" (0 matrix cores, 1 VALU);
         get_option("last_chains") reads the row chains the last sample_loop ran.  Kept across plan rebuilds;
         other engines (plans) in the process are unaffected."""
         if name not in self.OPTIONS or name in self.READ_ONLY:
@@ -341,8 +343,9 @@ class SamplingEngine:
     def status(self, rows: int) -> int:
         """Flags of the last sample_loop / denoiser_forward on the `rows`-row workspace
         (sd_workspace_status; synchronises the current stream): SD_STATUS_F16_RANGE = an
-        activation left the f16 range of the split-f16 products and its tiles were recomputed on
-        exact-f32 MFMA in the kernel (informational: the results are f32-accurate either way)."""
+        activation left the f16 range of the f16 products and its tiles were recomputed on
+        exact-f32 MFMA in the kernel (informational: in f32 mode the results are f32-accurate
+        either way; half mode's in-range tiles stay one f16 product)."""
         ws, nb = self.workspace(rows)
         v = ctypes.c_uint32()
         check(_lib.lib().sd_workspace_status(self.plan(), ptr(ws), nb, ctypes.byref(v), _stream(self._device)))

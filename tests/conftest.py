@@ -58,7 +58,8 @@ def pinned_cov(J):
     return tuple(torch.from_numpy(z[k]) for k in ("Sigma_N", "Lambda_N", "U"))
 
 
-def build_release_diffusion(z, device="cpu", T=None, use_attention=True, final_scale=None, **diff_kw):
+def build_release_diffusion(z, device="cpu", T=None, use_attention=True, final_scale=None, attn_heads=8,
+                            attn_dim_head=32, **diff_kw):
     """Product NonisotropicGaussianDiffusion + Denoiser (release architecture) with the fixture's
     synthetic weights (gen_golden.py:build_release)."""
     from skeletondiffusion_amd import synthetic
@@ -69,7 +70,7 @@ def build_release_diffusion(z, device="cpu", T=None, use_attention=True, final_s
     T = int(z["T"]) if T is None else T
     m = Denoiser(dim=96, cond_dim=96, out_dim=96, channels=J, num_nodes=J,
                  node_types=torch.from_numpy(z["node_types"]), use_attention=use_attention, self_condition=False,
-                 norm_type="none", depth=4, attn_dim_head=32, attn_heads=8, learn_influence=True)
+                 norm_type="none", depth=4, attn_dim_head=attn_dim_head, attn_heads=attn_heads, learn_influence=True)
     synthetic.fill_module_(m, WEIGHT_SEED)
     fs = final_scale if final_scale is not None else float(z["final_scale"]) if "final_scale" in z else 1.0
     if fs != 1.0:

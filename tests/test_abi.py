@@ -87,29 +87,31 @@ def test_plan_options_validated_on_host():
     assert lib.sd_plan_create(ctypes.byref(h), ctypes.byref(d)) == 0, lib.sd_last_error()
     try:
         v = ctypes.c_int64()
-        for value in (0, 1, 2, 3, 4, 5, 6):
+        for value in (0, 1, 2, 3, 4):
             assert lib.sd_plan_set_option(h, _lib.SD_OPT_SPLIT_ROUTE, value) == 0
             assert lib.sd_plan_get_option(h, _lib.SD_OPT_SPLIT_ROUTE, ctypes.byref(v)) == 0 and v.value == value
-        assert lib.sd_plan_set_option(h, _lib.SD_OPT_SPLIT_ROUTE, 7) == -1
-        assert b"split route" in lib.sd_last_error()
+        for value in (5, 6, 7):  # 5 / 6: the measured-slower routes ABI 3 removed
+            assert lib.sd_plan_set_option(h, _lib.SD_OPT_SPLIT_ROUTE, value) == -1
+            assert b"split route" in lib.sd_last_error()
         assert lib.sd_plan_set_option(h, _lib.SD_OPT_ROW_CHAINS, -1) == -1
         assert lib.sd_plan_set_option(h, _lib.SD_OPT_ROW_CHAINS, 0) == 0  # auto
         assert lib.sd_plan_set_option(h, _lib.SD_OPT_ROW_CHAINS, 8) == 0
         assert lib.sd_plan_set_option(h, _lib.SD_OPT_GL4_STAGING, 3) == -1
         assert lib.sd_plan_set_option(h, 99, 0) == -1
-        assert lib.sd_plan_set_option(h, _lib.SD_OPT_UPDATE_KERNEL, 2) == 0  # the pipelined form
-        assert lib.sd_plan_set_option(h, _lib.SD_OPT_UPDATE_KERNEL, 3) == 0  # its 8-B-load form
-        assert lib.sd_plan_set_option(h, _lib.SD_OPT_UPDATE_KERNEL, 4) == -1
+        for value in (2, 3, 4):  # 2 / 3: the pipelined forms ABI 3 removed
+            assert lib.sd_plan_set_option(h, _lib.SD_OPT_UPDATE_KERNEL, value) == -1
         assert lib.sd_plan_set_option(h, _lib.SD_OPT_UPDATE_KERNEL, 0) == 0
         assert lib.sd_plan_set_option(h, _lib.SD_OPT_UPDATE_KERNEL, 1) == 0
         assert lib.sd_plan_get_option(h, _lib.SD_OPT_UPDATE_KERNEL, ctypes.byref(v)) == 0 and v.value == 1
         assert lib.sd_plan_set_option(h, _lib.SD_OPT_UPDATE_KERNEL, 0) == 0
-        for opt, top in ((_lib.SD_OPT_V5_MIX, 1), (_lib.SD_OPT_ATTENTION, 3)):  # 0 .. top
+        for opt, ok, bad in ((_lib.SD_OPT_V5_MIX, (1,), (2,)), (_lib.SD_OPT_ATTENTION, (2, 3), (1, 4))):
             assert lib.sd_plan_get_option(h, opt, ctypes.byref(v)) == 0 and v.value == 0
-            for x in range(1, top + 1):
+            for x in ok:
                 assert lib.sd_plan_set_option(h, opt, x) == 0
                 assert lib.sd_plan_get_option(h, opt, ctypes.byref(v)) == 0 and v.value == x
-            assert lib.sd_plan_set_option(h, opt, top + 1) == -1 and lib.sd_plan_set_option(h, opt, 0) == 0
+            for x in bad:  # SD_OPT_ATTENTION 1: the tail form ABI 3 removed
+                assert lib.sd_plan_set_option(h, opt, x) == -1
+            assert lib.sd_plan_set_option(h, opt, 0) == 0
         # SD_OPT_LAST_CHAINS: read-only, 0 before the plan's first sampling call
         assert lib.sd_plan_get_option(h, _lib.SD_OPT_LAST_CHAINS, ctypes.byref(v)) == 0 and v.value == 0
         assert lib.sd_plan_set_option(h, _lib.SD_OPT_LAST_CHAINS, 1) == -1

@@ -231,11 +231,10 @@ def test_strong_scaling_shards_chain_invariant(batch, cuda):
                                           ("amass21", 4, {}), ("freeman17", 2, {}),
                                           ("amass16", 4, {"precision": "half"})])
 def test_split_route_bitwise(cfg, batch, kw, cuda):
-    """SD_OPT_SPLIT_ROUTE (DESIGN.md §4d'): the small-launch routes -- 2: k_gl4y GEMM phase per
-    (tile, node, column tile) + k_gl4 MODE 2 / 3 mixing or attention phase; 5: the fused
-    small-batch tile k_gl4 MODE 4 for the plain graph-linears (J = 16) -- are bitwise equal to the
-    one-kernel route, graph and eager, with the f16 range guard word untouched and the kernels
-    each route launched asserted."""
+    """SD_OPT_SPLIT_ROUTE (DESIGN.md §4d'): the small-launch route 2 -- k_gl4y GEMM phase per
+    (tile, node, column tile) + k_gl4 MODE 2 / 3 mixing or attention phase -- is bitwise equal to
+    the one-kernel route, graph and eager, with the f16 range guard word untouched and the kernels
+    the route launched asserted."""
     from bench import build_config
 
     d, x_cond, rows = build_config(cfg, cuda, T=10, batch=batch)
@@ -246,18 +245,16 @@ def test_split_route_bitwise(cfg, batch, kw, cuda):
     eng.set_option("split_route", 1)
     ref = eng.sample_loop(rows, x_cond=x_cond, seed=5, record=(False, True))
     ref = [ref[0].clone(), ref[4].clone()]
-    J = x_cond.shape[1]
-    for route in (2, 5):
-        eng.set_option("split_route", route)
-        for graph in (False, True):
-            got = eng.sample_loop(rows, x_cond=x_cond, seed=5, graph=graph, record=(False, True))
-            torch.cuda.synchronize()
-            assert torch.equal(got[0], ref[0]) and torch.equal(got[4], ref[1]), (cfg, batch, route, graph)
-        bits = eng.get_option("last_route")
-        if route == 5 and J == 16:
-            assert bits & 256 and bits & 4, bits  # MODE 4 tiles + the k_gl4y attention phase 1
-        else:
-            assert not bits & 256, bits
+    eng.set_option("split_route", 2)
+    for graph in (False, True):
+        got = eng.sample_loop(rows, x_cond=x_cond, seed=5, graph=graph, record=(False, True))
+        torch.cuda.synchronize()
+        assert torch.equal(got[0], ref[0]) and torch.equal(got[4], ref[1]), (cfg, batch, graph)
+    bits = eng.get_option("last_route")
+    assert bits & 4 and bits & 16 and not bits & 3, bits  # k_gl4y + MODE 2 / 3, no one-kernel tile
+    for bad in (5, 6):  # the measured-slower routes ABI 3 removed
+        with pytest.raises(_lib.SkelDiffError):
+            eng.set_option("split_route", bad)
     assert eng.status(rows) == 0
 
 
@@ -285,32 +282,6 @@ def test_tiled_split_route_bitwise(cfg, batch, T, prec, cuda):
             torch.cuda.synchronize()
             assert eng.get_option("last_chains") == min(chains, (rows + 31) // 32)
             assert torch.equal(got[0], ref[0]) and torch.equal(got[4], ref[1]), (cfg, chains, graph)
-    assert eng.status(rows) == 0
-
-
-@pytest.mark.parametrize("batch,T,chains,prec", [(64, 4, 1, "f32"), (64, 4, 3, "f32"), (3, 10, 1, "f32"), (5, 10, 2, "f32"),
-                                                  (32, 4, 3, "half")])
-def test_fused_layer_route_bitwise(batch, T, chains, prec, cuda):
-    """SD_OPT_SPLIT_ROUTE = 6: every plain J = 16 layer on the fused layer kernel
-    k_gl4f (GEMM and mixing phase of a layer as work items of one persistent launch, per-XCD work
-    queues, Y handed over inside the XCD's L2) is bitwise equal to the tiled split route (k_gl4t +
-    k_gl4 MODE 2 launches), graph and eager, on 1-3 row chains and at ragged row groups (150 / 250
-    rows); the fused kernel ran (route bit 512) and no wait timed out (status clear)."""
-    from bench import build_config
-
-    d, x_cond, rows = build_config("amass16", cuda, T=T, batch=batch)
-    eng = d.engine
-    eng.set_precision(prec)
-    eng.set_option("row_chains", chains)
-    eng.set_option("split_route", 3)
-    ref = eng.sample_loop(rows, x_cond=x_cond, seed=31, record=(False, True))
-    ref = [ref[0].clone(), ref[4].clone()]
-    eng.set_option("split_route", 6)
-    for graph in (False, True, True):
-        got = eng.sample_loop(rows, x_cond=x_cond, seed=31, graph=graph, record=(False, True))
-        torch.cuda.synchronize()
-        assert eng.get_option("last_route") & 512, eng.get_option("last_route")
-        assert torch.equal(got[0], ref[0]) and torch.equal(got[4], ref[1]), (batch, chains, graph, _max_err(got[0], ref[0]))
     assert eng.status(rows) == 0
 
 
@@ -503,30 +474,53 @@ def test_graph_linear_rejects_aliased_output(cuda):
     assert rc != 0 and b"invalid" in L.sd_last_error().lower()
 
 
-@pytest.mark.parametrize("route", [0, 2, 3])
-def test_f16_range_exact_in_kernel(route, cuda):
+F16_RANGE_CASES = {  # name -> (plan options, Denoiser attention heads / dim per head, precision)
+    "auto": ({}, (8, 32), "f32"), "split1_one_kernel": ({"split_route": 1}, (8, 32), "f32"),
+    "split2": ({"split_route": 2}, (8, 32), "f32"), "split3": ({"split_route": 3}, (8, 32), "f32"),
+    "tile813_one_kernel": ({"gl4_tile": 813}, (8, 32), "f32"),
+    # attn_dim_head = 64: no fused to_qkv + attention tile, row-major activations, separate k_attention
+    "dh64": ({}, (4, 64), "f32"), "dh64_split1": ({"split_route": 1}, (4, 64), "f32"),
+    # half precision's J = 16 full-batch route is the one-kernel tile; here the auto route at 8 rows
+    "half_split1": ({"split_route": 1}, (8, 32), "half"),
+}
+
+
+@pytest.mark.parametrize("case", list(F16_RANGE_CASES))
+def test_f16_range_exact_in_kernel(case, cuda):
     """Activations the split-f16 products cannot represent (|x| >= 65504; conditioning latents
-    scaled by 1e5 and 3e9) on each default-capable split-f16 route -- auto, k_gl4y + MODE 2 / 3,
-    tiled k_gl4t + MODE 2 / 3 -- with default options: the waves that leave the range recompute
-    their tiles on exact-f32 MFMA in the kernel (exact_tile_f32), with no warning and no host
-    re-run; the status word records that the fallback ran (in range it stays clear).
+    scaled by 1e5 and 3e9) on every split-f16 route -- auto, the one-kernel tiles (split_route 1,
+    a gl4_tile option), k_gl4y + MODE 2 / 3, tiled k_gl4t + MODE 2 / 3, a Denoiser with
+    attn_dim_head = 64 (no fused attention tile) -- with no warning and no host re-run: the waves
+    that leave the range recompute their tiles on exact-f32 MFMA in the kernel (exact_tile_f32, in
+    the one-kernel tiles too since round 6); the status word records that the fallback ran (in
+    range it stays clear).
     Accuracy: at these magnitudes any f32 evaluation order moves the latents by ~1e-3 (an f32 ulp
     of a 1e5 activation is 8e-3, and x0 = clamp(out) passes the rows near +-1 through), so the
     bar is the float64 oracle: sample()'s deviation from it must stay within that of an exact-f32
-    plan (kernel variant 3), i.e. f32-accurate.  In range the 1e-4 latent bar holds (goldens)."""
+    plan (kernel variant 3), i.e. f32-accurate.  In range the 1e-4 latent bar holds (goldens).
+    Half precision: its in-range tiles are one f16 product (not f32-accurate by definition); the
+    out-of-range tiles are recomputed exactly, so the latents stay finite."""
+    import dataclasses
     import warnings
 
+    opts, (heads, dh), prec = F16_RANGE_CASES[case]
     z = golden("release_h36m16_T10")
-    d = build_release_diffusion(z, cuda)
-    if route:
-        d.engine.set_option("split_route", route)
+    d = build_release_diffusion(z, cuda, attn_heads=heads, attn_dim_head=dh)
+    if prec != "f32":
+        d.engine.set_precision(prec)
+    for k, v in opts.items():
+        d.engine.set_option(k, v)
     xcs, fu, start, samp = release_inputs(z)
     kw = dict(batch_size=start.shape[0], start_noise=start.to(cuda), sampling_noise=samp.to(cuda))
     d.sample(x_cond=xcs.to(cuda), **kw)
     assert d.engine.status(start.shape[0]) == 0
-    ref = build_release_diffusion(z, cuda)
+    route = d.engine.get_option("last_route")
+    if "one_kernel" in case:
+        assert route & 3, route  # k_gl4 MODE 0 / 1 ran
+    ref = build_release_diffusion(z, cuda, attn_heads=heads, attn_dim_head=dh)
     ref.engine.set_option("kernel_variant", 3)
     sd, cfg, bufs = _oracle_setup(d)
+    cfg = dataclasses.replace(cfg, heads=heads, dim_head=dh)
     sd64 = {k: v.double() if v.is_floating_point() else v for k, v in sd.items()}
     bufs64 = {k: v.double() if v.is_floating_point() else v for k, v in bufs.items()}
     for scale in (1e5, 3e9):
@@ -536,8 +530,10 @@ def test_f16_range_exact_in_kernel(route, cuda):
             img = d.sample(x_cond=big.to(cuda), **kw)[0]
             torch.cuda.synchronize()
         assert d.engine.status(start.shape[0]) & _lib.SD_STATUS_F16_RANGE
+        assert torch.isfinite(img).all()
+        if prec != "f32":
+            continue
         img_exact = ref.sample(x_cond=big.to(cuda), **kw)[0]
         img64, _ = O.p_sample_loop(sd64, cfg, bufs64, start.double(), samp.double(), x_cond=big.double())
-        assert torch.isfinite(img).all()
         err, err_exact = _max_err(img, img64), _max_err(img_exact, img64)
-        assert err <= max(1.5 * err_exact, TOL), (route, scale, err, err_exact)
+        assert err <= max(1.5 * err_exact, TOL), (case, scale, err, err_exact)

@@ -26,20 +26,19 @@ def test_update_mfma_bitwise_vs_elementwise(cfg, batch, prec, given, cuda):
     g = torch.Generator().manual_seed(11)
     samp = torch.randn((rows, 9, J, 96), generator=g).to(cuda) if given else None
     res = {}
-    # SD_OPT_UPDATE_KERNEL: 1 the element-per-thread forms, 2 the pipelined form, 3 the 8-B-load form
-    # (2 / 3: J <= 16 full batches; elsewhere the default), 0 (default) k_update_mfma
-    for v in (1, 2, 3, 0):
+    # SD_OPT_UPDATE_KERNEL: 1 the element-per-thread forms, 0 (default) k_update_mfma
+    for v in (1, 0):
         eng.set_option("update_kernel", v)
         a = eng.sample_loop(rows, x_cond=x_cond, seed=4, sampling_noise=samp, record=(True, False), graph=False)
         b = eng.sample_loop(rows, x_cond=x_cond, seed=4, sampling_noise=samp, record=(False, True), graph=False)
         torch.cuda.synchronize()
         res[v] = [t.clone() for t in (a[0], a[1], a[2], a[3], b[4])]  # img, start, noise_t, mean_t, imgs
-    for v in (0, 2, 3):
-        for name, x, y in zip(("img", "start", "noise_t", "mean_t", "imgs"), res[v], res[1]):
-            assert torch.equal(x, y), (v, name, float((x - y).abs().max()))
+    for name, x, y in zip(("img", "start", "noise_t", "mean_t", "imgs"), res[0], res[1]):
+        assert torch.equal(x, y), (name, float((x - y).abs().max()))
     assert eng.get_option("update_kernel") == 0
-    with pytest.raises(_lib.SkelDiffError):
-        eng.set_option("update_kernel", 4)
+    for bad in (2, 3, 4):  # 2 / 3: the measured-no-faster forms ABI 3 removed
+        with pytest.raises(_lib.SkelDiffError):
+            eng.set_option("update_kernel", bad)
 
 
 @pytest.mark.parametrize("dim,batch", [(192, 5), (192, 40), (160, 3), (256, 2)])

@@ -37,9 +37,8 @@ OBJDUMP = shutil.which("llvm-objdump") or "/opt/rocm/lib/llvm/bin/llvm-objdump"
 
 pytestmark = pytest.mark.skipif(not os.path.exists(OBJDUMP) or not os.path.exists(LIB), reason="no llvm-objdump / library")
 
-GL4T = "_ZN2sd6k_gl4tILb0ELi0ELi6ELi12ELb0ELi2ELi4ELb0ELb0ELb0ELb1ELb0ELi1EEEvNS_6GLArgsEilNS_4YOutE"
-ATTN = "_ZN2sd11k_attentionILi4ELi32ELb0EEEvNS_8AttnArgsE"
-ATTN_TAIL = "_ZN2sd11k_attentionILi4ELi32ELb1EEEvNS_8AttnArgsE"  # J = 49..52 tail form
+GL4T = "_ZN2sd6k_gl4tILb0ELi0ELi6ELi12ELb0EEEvNS_6GLArgsEilNS_4YOutE"
+ATTN = "_ZN2sd11k_attentionILi4ELi32EEEvNS_8AttnArgsE"
 MIXD = "_ZN2sd12_GLOBAL__N_110k_gl5_mixdILi8ELi1ELb0EEEvNS_6GLArgsEPKfl"
 MIXD_RES = "_ZN2sd12_GLOBAL__N_110k_gl5_mixdILi8ELi1ELb1EEEvNS_6GLArgsEPKfl"
 UPD = "_ZN2sd13k_update_mfmaILi16ELi4ELi6ELb0EEEvNS_7UpdArgsE"
@@ -95,10 +94,10 @@ def test_gl4t_store_tail_has_no_load_waits(tmp_path_factory):
     assert counts.count(0) <= 3 and any(c > 0 for c in counts), counts
 
 
-@pytest.mark.parametrize("sym,nmin", [(ATTN, 40), (ATTN_TAIL, 40)])
+@pytest.mark.parametrize("sym,nmin", [(ATTN, 40)])
 def test_attention_loads_issued_together(sym, nmin, tmp_path_factory):
-    """Every load of a wave (K / Q fragments, V, and in the tail form the lane's query row and the
-    tail value rows) issued before the first vmcnt wait: one memory latency per wave."""
+    """Every load of a wave (K / Q fragments, V) issued before the first vmcnt wait: one memory
+    latency per wave."""
     ins = _disasm(tmp_path_factory, sym)
     first_wait = next(i for i, l in enumerate(ins) if _vmcnt(l) is not None)
     loads = [i for i, l in enumerate(ins) if l.startswith("global_load")]
