@@ -345,7 +345,9 @@ __global__ __launch_bounds__(256) void k_gl4y(const GLArgs p, int ntile_c, int64
     }
 #pragma unroll
     for (int i = 0; i < PF; ++i) compute(nchunk - PF + i, i);
-    const bool oor = __builtin_amdgcn_ballot_w64(amx >= 65504.0f) != 0;  // wave-uniform
+    // the range guard sees the real rows only (the padding rows of a row-blocked buffer hold
+    // whatever the workspace held: never stored, but they must not trigger the fallback)
+    const bool oor = __builtin_amdgcn_ballot_w64(arow < p.B && amx >= 65504.0f) != 0;  // wave-uniform
     float sc[16];
 #pragma unroll
     for (int r = 0; r < 16; ++r) sc[r] = p.wsp_unscale;
@@ -393,39 +395,47 @@ __global__ __launch_bounds__(256) void k_gl4y(const GLArgs p, int ntile_c, int64
 // at CT = 6 vs 2.2 B in the one-kernel k_gl4 32 x 64 tile).  Per accumulator element the MFMA
 // sequence (x_hi W'_hi, x_hi W'_lo, x_lo W'_hi per chunk), RMS sum, scale and bias arithmetic are
 // k_gl4's, so phase 2 (k_gl4 MODE 2 / 3) reproduces the one-kernel route bit for bit.
-// K loop (round 4, measured forms in DESIGN.md §4i / §4j; the rejected ones -- register-staged
-// weights, resident weights, product-major MFMA order, a loader wave, multi-unit workgroups, three
-// chunks ahead -- live in git history before round 6): an LDS-DMA ring of PF + 1 slots; chunk c's
-// weight slice AND its x image go to slot c % NS by global_load_lds_dwordx4, PF chunks ahead; each
-// chunk's fill c + PF is issued right after its barrier, before its LDS reads and MFMAs ("fill
-// first"), so PF chunks of work cover every fill.  bf16 operands (PREC 2) are their own A fragments
-// and stay in a PF-deep register ring.
+// K loop (round 6; the round-4 / round-5 forms and what they measured: DESIGN.md §4i / §4j, git
+// history): the node's weight slice for the workgroup's CT column tiles goes through an LDS-DMA
+// ring of PF + 1 slots (chunk c in slot c % NS by global_load_lds_dwordx4, PF chunks ahead, shared
+// by the NWV waves), each fill issued right after its chunk's barrier ("fill first"); x is each
+// wave's own (RT 32-row tiles), so it goes straight into a register ring of NS slots by
+// global_load_dwordx4 the compiler does not track (inline asm: a tracked load beside in-flight
+// LDS-DMA made the waitcnt pass drain vmcnt(0) at its first use), issued with the chunk's weight
+// fill and covered by the same counted vmcnt wait, then fenced into the compiler's view.  The chunk
+// loop is unrolled whole, so every register slot is static (no loop-carried copies of registers
+// still being written).  RT = 2: every weight fragment read from LDS feeds two row tiles.
+// tools/gl4t_rt_probe.hip (config-2 shape, alone on the GPU, bitwise equal to the round-5 ring):
+// N = 192, 3,200 rows 17.1 vs 20.7 us (RT 2, CT 3), 1,067 rows 10.8 vs 12.5; N = 768 (RT 1, CT 6)
+// 53.6 vs 56.6 and 23.3 vs 25.9 (profiles/r06f/probe.txt).  bf16 operands (PREC 2) are their own A
+// fragments and keep the tracked register ring of the round-5 form (RT = 1).
 template <int PREC, int CT, int NCH>
 constexpr int gl4t_smem_bytes() {
     constexpr int TILE_H = PREC ? 512 : 1024, TS = 36, NWV = 4, NS = 3;
-    constexpr int XSB = PREC != 2 ? NS * NWV * 2048 : 0;
-    constexpr int SBW = NS * CT * TILE_H * 2 + XSB;
+    constexpr int SBW = NS * CT * TILE_H * 2;
     return SBW > NWV * 32 * TS * 4 ? SBW : NWV * 32 * TS * 4;
 }
 
+// A 16-B global load the compiler does not track (k_gl4t's x ring): waited for by hand (counted
+// s_waitcnt vmcnt + a register fence)
+__device__ __forceinline__ void g4_async(floatx4& d, const float* p) {
+    asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(d) : "v"(p) : "memory");
+}
+
 // The workgroup's work: unit u = (node j, row group, column group); smem_raw = its
-// gl4t_smem_bytes of LDS.
-template <bool RMS, int PREC, int CT, int NCH, bool ROWMAJOR>
+// gl4t_smem_bytes of LDS.  A row group is NWV waves x RT 32-row tiles.
+template <bool RMS, int PREC, int CT, int NCH, bool ROWMAJOR, int RT>
 __device__ __forceinline__ void gl4t_body(const GLArgs& p, int ncg, int64_t ntile_r, const YOut& yo, const int64_t u,
                                           const int tid, char* __restrict__ smem_raw) {
+    static_assert(PREC != 2 || RT == 1, "bf16 operands: one row tile per wave");
     constexpr int PF = 2;                       // chunks in flight
-    constexpr int NWV = 4;                      // waves = 32-row tiles per workgroup
+    constexpr int NWV = 4;                      // waves per workgroup
     constexpr int NT = NWV * 64;
     constexpr int TILE_H = PREC ? 512 : 1024;   // halves of one 32-column tile per chunk
     constexpr int PPT = TILE_H / 8;             // 16-B pieces per tile
     constexpr int TS = 36;                      // floats per row of a wave's 32 x 32 output transpose
-    constexpr int NS = PF + 1;                  // LDS-DMA ring: chunk c in slot c % NS
-    // x through the LDS-DMA ring too (f32 operands): per slot and wave the chunk's 32 rows x 16 k
-    // image (2 KiB) -- no register-writing global load in the K loop, so the compiler inserts no
-    // vmcnt of its own (with a tracked x load beside an LDS-DMA it drained vmcnt(0) every chunk)
-    constexpr bool XDMA = PREC != 2;
-    constexpr int SB = gl4t_smem_bytes<PREC, CT, NCH>();
-    static_assert(SB >= NS * CT * TILE_H * 2 + (XDMA ? NS * NWV * 2048 : 0), "LDS carve");
+    constexpr int NS = PF + 1;                  // ring slots: chunk c in slot c % NS
+    constexpr bool XV = PREC != 2;              // x by untracked register loads
     _Float16(*sW)[CT * TILE_H] = reinterpret_cast<_Float16(*)[CT * TILE_H]>(smem_raw);
     const int lane = tid & 63, l32 = lane & 31, h = lane >> 5;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -435,130 +445,61 @@ __device__ __forceinline__ void gl4t_body(const GLArgs& p, int ncg, int64_t ntil
     // (N = 768: 5.9 MB of split weights for all 10 types did not fit a 4 MB L2 when every XCD
     // walked every node: 196 MB fetched per launch for ~45 MB of operands)
     const int cg = (int)(u % ncg);
-    const int64_t nrg = (ntile_r + NWV - 1) / NWV;
+    const int64_t nrg = (ntile_r + NWV * RT - 1) / (NWV * RT);
     const int j = (int)((u / ncg) / nrg);
     const int64_t rgi = (u / ncg) % nrg;
-    const int64_t tr = rgi * NWV + wave;
-    const bool live = tr < ntile_r;  // wave-uniform; a dead wave still joins barriers
-    const int64_t row0 = (live ? tr : 0) * 32;
-    constexpr int nchunk = NCH;
-    const int64_t arow = row0 + l32;
-    const int64_t ac = arow < p.B ? arow : 0;
-    const float* x1r = p.x1_blk ? p.x1 + blk_off(arow, j, 8 * h, J, p.K1)
-                                : p.x1 + ((ac + p.x1_row0) / p.x1_div) * p.x1_rs + (int64_t)j * p.K1 + 8 * h;
-    const float* x2r = !p.K2 ? nullptr
-                             : p.x2_blk ? p.x2 + blk_off(arow, j, 8 * h, J, p.K2) : p.x2 + ac * p.x2_rs + (int64_t)j * p.K2 + 8 * h;
-    floatx4 xa[PF], xb[PF];
-    auto issue_x = [&](int c, int sl) {  // PREC 2: the chunk's A operand into register slot sl
-        const int k0 = c << 4;
-        const float* src;
-        int step4;
-        if (k0 < p.K1) {
-            src = p.x1_blk ? x1r + (k0 << 5) : x1r + k0;
-            step4 = p.x1_blk ? 128 : 4;
-        } else {
-            src = p.x2_blk ? x2r + ((k0 - p.K1) << 5) : x2r + (k0 - p.K1);
-            step4 = p.x2_blk ? 128 : 4;
-        }
-        // a bf16 operand: its 8 k values (16 B) are the A fragment itself; the same two loads on
-        // both paths (selected addresses, no branch), so the waitcnt pass keeps the ring
-        const bool bsrc = k0 < p.K1 ? p.x1_bf16 : p.x2_bf16;
-        const float* base = k0 < p.K1 ? p.x1 : p.x2;
-        const float* qb = reinterpret_cast<const float*>(reinterpret_cast<const __bf16*>(base) + (src - base));
-        xa[sl] = g4(bsrc ? qb : src);
-        xb[sl] = g4(bsrc ? qb : src + step4);
-    };
-    floatx16 acc[CT];
+    const int64_t tr0 = (rgi * NWV + wave) * RT;  // this wave's first 32-row tile
+    // per row tile: its rows (a dead tile -- past the batch -- reads tile 0 and stores nothing)
+    int64_t row0[RT], arow[RT];
+    const float* x1r[RT];
+    const float* x2r[RT];
 #pragma unroll
-    for (int ct = 0; ct < CT; ++ct)
+    for (int rt = 0; rt < RT; ++rt) {
+        row0[rt] = (tr0 + rt < ntile_r ? tr0 + rt : 0) * 32;
+        arow[rt] = row0[rt] + l32;
+        const int64_t ac = arow[rt] < p.B ? arow[rt] : 0;
+        // feature 8 h of chunk 0: the lane's A fragment (rows l32, k 8 h .. 8 h + 7)
+        x1r[rt] = p.x1_blk ? p.x1 + blk_off(arow[rt], j, 8 * h, J, p.K1)
+                           : p.x1 + ((ac + p.x1_row0) / p.x1_div) * p.x1_rs + (int64_t)j * p.K1 + 8 * h;
+        x2r[rt] = !p.K2 ? x1r[rt]
+                        : p.x2_blk ? p.x2 + blk_off(arow[rt], j, 8 * h, J, p.K2) : p.x2 + ac * p.x2_rs + (int64_t)j * p.K2 + 8 * h;
+    }
+    // chunk c's two 16-B pieces of row tile rt: k 16 c + 8 h .. + 3 and + 4 .. + 7 (row-blocked:
+    // 128 floats apart, row-major: 4); x1 for the first K1 / 16 chunks, then x2.  One running
+    // source pointer per row tile, advanced after each chunk's loads (fill runs in chunk order):
+    // with the K loop unrolled whole, per-chunk addresses were hoisted and held live (spills)
+    const int c1 = p.K1 >> 4;
+    const int cs1 = p.x1_blk ? 512 : 16, cs2 = p.x2_blk ? 512 : 16;
+    const int st1 = p.x1_blk ? 128 : 4, st2 = p.x2_blk ? 128 : 4;
+    const float* xp[RT];
 #pragma unroll
-        for (int e = 0; e < 16; ++e) acc[ct][e] = 0.f;
-    float ss = 0.f, amx = 0.f;
+    for (int rt = 0; rt < RT; ++rt) xp[rt] = c1 > 0 ? x1r[rt] : x2r[rt];
+    auto xstep = [&](int c) { return c < c1 ? st1 : st2; };
+    floatx4 xa[NS][RT], xb[NS][RT];
+    floatx16 acc[RT][CT];
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+        for (int ct = 0; ct < CT; ++ct)
+#pragma unroll
+            for (int e = 0; e < 16; ++e) acc[rt][ct][e] = 0.f;
+    float ss[RT], amx[RT];
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt) ss[rt] = amx[rt] = 0.f;
     // the epilogue's bias, loaded before the K loop: loaded per tile in the epilogue, each load was
     // the youngest memory op and its vmcnt(0) also waited for the previous tile's stores -- CT
     // serial memory round trips in the store tail
     float bvp[CT];
 #pragma unroll
     for (int ct = 0; ct < CT; ++ct) bvp[ct] = p.bias ? p.bias[p.wrow[j] + (cg * CT + ct) * 32 + l32] : 0.f;
-    auto compute = [&](int c, int sl, const _Float16* wst) {  // wst: the chunk's CT tiles in LDS
-        if constexpr (PREC == 2) {  // bf16 mode: one bf16 product per k step (k_gl4 PREC 2's arithmetic)
-            const bool bsrc = (c << 4) < p.K1 ? p.x1_bf16 : p.x2_bf16;  // wave-uniform
-            bf16x8 xb16;
-            floatx8 f;
-            if (bsrc) {
-                xb16 = __builtin_bit_cast(bf16x8, xa[sl]);
-                f = __builtin_convertvector(xb16, floatx8);
-            } else {
-                f = floatx8{xa[sl].x, xa[sl].y, xa[sl].z, xa[sl].w, xb[sl].x, xb[sl].y, xb[sl].z, xb[sl].w};
-                xb16 = __builtin_convertvector(f, bf16x8);
-            }
-            if (RMS && (c << 4) < p.K1) {
-                const floatx8 q = f * f;
-                ss += ((q[0] + q[1]) + (q[2] + q[3])) + ((q[4] + q[5]) + (q[6] + q[7]));
-            }
-            const _Float16* wt = wst + lane * 8;
-#pragma unroll
-            for (int ct = 0; ct < CT; ++ct) {
-                const bf16x8 wb = *reinterpret_cast<const bf16x8*>(wt + ct * TILE_H);
-                acc[ct] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(xb16, wb, acc[ct], 0, 0, 0);
-            }
-            return;
-        }
-        const floatx8 f = {xa[sl].x, xa[sl].y, xa[sl].z, xa[sl].w, xb[sl].x, xb[sl].y, xb[sl].z, xb[sl].w};
-        if (RMS && (c << 4) < p.K1) {
-            const floatx8 q = f * f;
-            ss += ((q[0] + q[1]) + (q[2] + q[3])) + ((q[4] + q[5]) + (q[6] + q[7]));
-        }
-        const floatx8 a = __builtin_elementwise_abs(f);
-        amx = fmaxf(amx, fmaxf(fmaxf(fmaxf(a[0], a[1]), fmaxf(a[2], a[3])), fmaxf(fmaxf(a[4], a[5]), fmaxf(a[6], a[7]))));
-        const halfx8 xh = __builtin_convertvector(f, halfx8);
-        halfx8 xl;
-        if constexpr (!PREC) xl = __builtin_convertvector(f - __builtin_convertvector(xh, floatx8), halfx8);
-        const _Float16* wt = wst + lane * 8;
-#pragma unroll
-        for (int ct = 0; ct < CT; ++ct) {
-            const halfx8 wh = *reinterpret_cast<const halfx8*>(wt + ct * TILE_H);
-            floatx16 t = __builtin_amdgcn_mfma_f32_32x32x16_f16(xh, wh, acc[ct], 0, 0, 0);
-            if constexpr (!PREC) {
-                const halfx8 wl = *reinterpret_cast<const halfx8*>(wt + ct * TILE_H + 512);
-                t = __builtin_amdgcn_mfma_f32_32x32x16_f16(xh, wl, t, 0, 0, 0);
-                t = __builtin_amdgcn_mfma_f32_32x32x16_f16(xl, wh, t, 0, 0, 0);
-            }
-            acc[ct] = t;
-        }
-    };
-    // LDS-DMA weight ring (round 4; tools/gl4t_probe.hip): chunk c's weight slice goes straight
-    // to slot c % NS by global_load_lds_dwordx4 (no VGPRs, no ds_write), issued PF chunks ahead
-    // together with that chunk's x loads, so the loads of every chunk are issued in chunk order and
-    // waiting for chunk c (vmcnt = the ops of the PF - 1 younger chunks) never waits for a younger
-    // one.  (The register-staged form loaded w(c + 1) behind x(c + 1 .. c + 3), so every chunk's
-    // weight wait drained the x ring: 24.0 vs 19.0 us per N = 192 launch at 3,200 rows.)  The
-    // barrier after the wait publishes every wave's pieces of chunk c; slot (c + PF) % NS, refilled
-    // after it, was last read in chunk c - 1, which every wave finished before arriving.
+    const _Float16* wt0 = p.wsp + ((int64_t)p.ntype[j] * NCH * p.wsp_nct + cg * CT) * 1024;
     // Pieces of wave w per chunk: q0 = 64 w + NT k < CT * PPT (two counts, wave-uniform).
     constexpr int NPC = CT * PPT;
-    constexpr int XL = 2;  // x loads (XDMA: x DMA instructions) per chunk and lane / wave
+    constexpr int XL = 2 * RT;  // x loads per chunk and lane
     constexpr int OPA = (NPC / 64 + NWV - 1) / NWV + XL, OPB = (NPC / 64) / NWV + XL;
+    static_assert(OPA * (PF - 1) < 64, "vmcnt range");
     const bool wa = wave * 64 + NT * ((NPC / 64 + NWV - 1) / NWV - 1) < NPC;
-    const _Float16* wt0 = p.wsp + ((int64_t)p.ntype[j] * nchunk * p.wsp_nct + cg * CT) * 1024;
-    // XDMA x image of a wave's slot: float k 256 + 4 L (instruction k = 0 / 1, lane L) holds row
-    // row0 + (L & 31), features 16 c + 8 k + 4 (L >> 5) .. + 3, i.e. what lane (l32, h) of the
-    // compute reads as xa (k = h, L = l32) and xb (k = h, L = 32 + l32): the global image of a
-    // row-blocked chunk, gathered per lane from a row-major operand
-    float* const xs0 = reinterpret_cast<float*>(smem_raw + NS * CT * TILE_H * 2) + wave * 512;
-    // this lane's DMA source of chunk c, instruction k: a base per operand (feature 4 h of chunk 0
-    // of x1, of x2) plus c times the chunk stride (512 floats row-blocked, 16 row-major) plus k
-    // times the half-chunk stride (256 / 8) -- loop-invariant address arithmetic, no division
-    const int c1 = p.K1 >> 4;  // first chunk of x2
-    // (x1r / x2r point at feature 8 h: + 256 h row-blocked, + 8 h row-major; feature 4 h is
-    // + 128 h / + 4 h)
-    const float* xb1 = x1r - (p.x1_blk ? 128 * h : 4 * h);
-    const float* xb2 = !p.K2 ? xb1 : x2r - (p.x2_blk ? 128 * h : 4 * h);
-    const int cs1 = p.x1_blk ? 512 : 16, cs2 = p.x2_blk ? 512 : 16;
-    const int ks1 = p.x1_blk ? 256 : 8, ks2 = p.x2_blk ? 256 : 8;
-    auto xsrc = [&](int c, int k) -> const float* {
-        return c < c1 ? xb1 + (int64_t)c * cs1 + k * ks1 : xb2 + (int64_t)(c - c1) * cs2 + k * ks2;
-    };
+    // chunk c: its weight slice to slot c % NS (LDS-DMA), then its x pieces to register slot c % NS
     auto fill = [&](int c) {
         _Float16* dst = sW[c % NS];
 #pragma unroll
@@ -569,125 +510,183 @@ __device__ __forceinline__ void gl4t_body(const GLArgs& p, int ncg, int64_t ntil
             const _Float16* src = wt0 + ((int64_t)c * p.wsp_nct + q / PPT) * 1024 + (q % PPT) * 8;
             __builtin_amdgcn_global_load_lds((const void*)src, (lds_void*)(dst + (size_t)q0 * 8), 16, 0, 0);
         }
-        if constexpr (XDMA) {
-            float* xd = xs0 + (c % NS) * (NWV * 512);
-            __builtin_amdgcn_global_load_lds((const void*)xsrc(c, 0), (lds_void*)xd, 16, 0, 0);
-            __builtin_amdgcn_global_load_lds((const void*)xsrc(c, 1), (lds_void*)(xd + 256), 16, 0, 0);
+        const int s = c % NS;
+#pragma unroll
+        for (int rt = 0; rt < RT; ++rt) {
+            const float* src = xp[rt];
+            xp[rt] = c + 1 == c1 ? x2r[rt] : src + (c < c1 ? cs1 : cs2);
+            if constexpr (XV) {
+                g4_async(xa[s][rt], src);
+                g4_async(xb[s][rt], src + xstep(c));
+            } else {
+                // a bf16 operand: its 8 k values (16 B) are the A fragment itself; the same two loads
+                // on both paths (selected addresses, no branch), so the waitcnt pass keeps the ring
+                const bool bsrc = c < c1 ? p.x1_bf16 : p.x2_bf16;
+                const float* base = c < c1 ? p.x1 : p.x2;
+                const float* qb = reinterpret_cast<const float*>(reinterpret_cast<const __bf16*>(base) + (src - base));
+                xa[s][rt] = g4(bsrc ? qb : src);
+                xb[s][rt] = g4(bsrc ? qb : src + xstep(c));
+            }
         }
     };
-    auto x_lds = [&](int c) {  // XDMA: chunk c's A-operand values into ring slot 0 of xa / xb
-        const float* xs = xs0 + (c % NS) * (NWV * 512) + h * 256 + l32 * 4;
-        xa[0] = *reinterpret_cast<const floatx4*>(xs);
-        xb[0] = *reinterpret_cast<const floatx4*>(xs + 128);
+    auto compute = [&](int c) {
+        const int s = c % NS;
+        const _Float16* wt = sW[s] + lane * 8;
+        const bool rms_chunk = RMS && c < c1;
+        if constexpr (PREC == 2) {  // bf16 mode: one bf16 product per k step (k_gl4 PREC 2's arithmetic)
+            const bool bsrc = c < c1 ? p.x1_bf16 : p.x2_bf16;  // wave-uniform
+            bf16x8 xb16;
+            floatx8 f;
+            if (bsrc) {
+                xb16 = __builtin_bit_cast(bf16x8, xa[s][0]);
+                f = __builtin_convertvector(xb16, floatx8);
+            } else {
+                f = floatx8{xa[s][0].x, xa[s][0].y, xa[s][0].z, xa[s][0].w, xb[s][0].x, xb[s][0].y, xb[s][0].z, xb[s][0].w};
+                xb16 = __builtin_convertvector(f, bf16x8);
+            }
+            if (rms_chunk) {
+                const floatx8 q = f * f;
+                ss[0] += ((q[0] + q[1]) + (q[2] + q[3])) + ((q[4] + q[5]) + (q[6] + q[7]));
+            }
+#pragma unroll
+            for (int ct = 0; ct < CT; ++ct) {
+                const bf16x8 wb = *reinterpret_cast<const bf16x8*>(wt + ct * TILE_H);
+                acc[0][ct] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(xb16, wb, acc[0][ct], 0, 0, 0);
+            }
+            return;
+        }
+        halfx8 xh[RT], xl[RT];
+#pragma unroll
+        for (int rt = 0; rt < RT; ++rt) {
+            const floatx8 f = {xa[s][rt].x, xa[s][rt].y, xa[s][rt].z, xa[s][rt].w,
+                               xb[s][rt].x, xb[s][rt].y, xb[s][rt].z, xb[s][rt].w};
+            if (rms_chunk) {
+                const floatx8 q = f * f;
+                ss[rt] += ((q[0] + q[1]) + (q[2] + q[3])) + ((q[4] + q[5]) + (q[6] + q[7]));
+            }
+            const floatx8 a = __builtin_elementwise_abs(f);
+            amx[rt] = fmaxf(amx[rt], fmaxf(fmaxf(fmaxf(a[0], a[1]), fmaxf(a[2], a[3])), fmaxf(fmaxf(a[4], a[5]), fmaxf(a[6], a[7]))));
+            xh[rt] = __builtin_convertvector(f, halfx8);
+            if constexpr (!PREC) xl[rt] = __builtin_convertvector(f - __builtin_convertvector(xh[rt], floatx8), halfx8);
+            // the guard / norm reductions pinned to this chunk: the whole-unrolled K loop is one
+            // block and, unpinned, the compiler sank the fmax chains into the epilogue (where the
+            // ballot reads them), holding every chunk's x live to there -- 62..270 VGPRs spilled
+            asm volatile("" : "+v"(amx[rt]), "+v"(ss[rt]));
+        }
+        // per accumulator element: x_hi W_hi, x_hi W_lo, x_lo W_hi per chunk, chunks in order --
+        // the round-5 ring's sequence (bitwise equal to it and to the one-kernel route)
+#pragma unroll
+        for (int ct = 0; ct < CT; ++ct) {
+            const halfx8 wh = *reinterpret_cast<const halfx8*>(wt + ct * TILE_H);
+            halfx8 wl;
+            if constexpr (!PREC) wl = *reinterpret_cast<const halfx8*>(wt + ct * TILE_H + 512);
+#pragma unroll
+            for (int rt = 0; rt < RT; ++rt) {
+                floatx16 t = __builtin_amdgcn_mfma_f32_32x32x16_f16(xh[rt], wh, acc[rt][ct], 0, 0, 0);
+                if constexpr (!PREC) {
+                    t = __builtin_amdgcn_mfma_f32_32x32x16_f16(xh[rt], wl, t, 0, 0, 0);
+                    t = __builtin_amdgcn_mfma_f32_32x32x16_f16(xl[rt], wh, t, 0, 0, 0);
+                }
+                acc[rt][ct] = t;
+            }
+        }
     };
-    static_assert(OPA * (PF - 1) < 64, "vmcnt range");
-    auto wait_chunk = [&](int younger) {  // all but the ops of `younger` later chunks done (folds per unrolled step)
-    // vmcnt(ops of the younger chunks) AND lgkmcnt(0): every LDS read this wave issued for the
-    // previous chunk has returned before it arrives, so a fill issued after the barrier into that
-    // chunk's slot cannot overtake a read still in flight (the compiler may schedule the last
-    // MFMAs' fragment waits past the barrier otherwise)
+    // chunk c's weights and x landed: vmcnt(the ops of the younger chunks in flight) AND
+    // lgkmcnt(0) (every LDS read this wave issued for the previous chunk has returned before it
+    // arrives, so a fill issued after the barrier into that chunk's slot cannot overtake a read
+    // still in flight), then the register fence (XV: the compiler sees chunk c's x defined here)
+    // and the barrier (publishes every wave's weight pieces of chunk c)
+    auto wait_chunk = [&](int c, int younger) {
         if (younger == 0) {
-            if (wa) __builtin_amdgcn_s_waitcnt(VmCnt4<0>::imm & ~(0xF << 8));
-            else __builtin_amdgcn_s_waitcnt(VmCnt4<0>::imm & ~(0xF << 8));
+            __builtin_amdgcn_s_waitcnt(VmCnt4<0>::imm & ~(0xF << 8));
         } else {
             if (wa) __builtin_amdgcn_s_waitcnt(VmCnt4<OPA>::imm & ~(0xF << 8));
             else __builtin_amdgcn_s_waitcnt(VmCnt4<OPB>::imm & ~(0xF << 8));
+        }
+        if constexpr (XV) {
+#pragma unroll
+            for (int rt = 0; rt < RT; ++rt) asm volatile("" : "+v"(xa[c % NS][rt]), "+v"(xb[c % NS][rt]) :: "memory");
         }
         asm volatile("" ::: "memory");
         __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
     };
-    static_assert(NCH % PF == 0 && NCH >= 2 * PF, "ring positions fixed per unrolled step");
+    static_assert(NCH >= PF, "ring depth");
 #pragma unroll
-    for (int i = 0; i < PF; ++i) {
-        fill(i);
-        if constexpr (!XDMA) issue_x(i, i);
-    }
-#pragma nounroll
-    for (int c0 = 0; c0 < nchunk - PF; c0 += PF) {
+    for (int i = 0; i < PF; ++i) fill(i);
 #pragma unroll
-        for (int i = 0; i < PF; ++i) {
-            const int c = c0 + i;
-            wait_chunk(PF - 1);
-            if constexpr (XDMA) {  // fill first: the slot of chunk c - 1 is free after the barrier
-                fill(c + PF);
-                asm volatile("" ::: "memory");
-                x_lds(c);
-                compute(c, 0, sW[c % NS]);
-            } else {
-                compute(c, i, sW[c % NS]);
-                asm volatile("" ::: "memory");
-                fill(c + PF);
-                issue_x(c + PF, i);
-            }
-        }
-    }
-    // the last PF chunks: nothing more to issue, the wait shrinks by one chunk each step
-#pragma unroll
-    for (int i = 0; i < PF; ++i) {
-        wait_chunk(PF - 1 - i);
-        if constexpr (XDMA) {
-            x_lds(nchunk - PF + i);
-            compute(nchunk - PF + i, 0, sW[(nchunk - PF + i) % NS]);
-        } else {
-            compute(nchunk - PF + i, i, sW[(nchunk - PF + i) % NS]);
+    for (int c = 0; c < NCH; ++c) {
+        wait_chunk(c, c + 1 < NCH ? PF - 1 : 0);
+        if constexpr (XV) {  // fill first: the slots of chunk c - 1 are free after the barrier
+            if (c + PF < NCH) fill(c + PF);
+            asm volatile("" ::: "memory");
+            compute(c);
+        } else {  // the tracked bf16 register ring: chunk c's registers are read before refilled
+            compute(c);
+            asm volatile("" ::: "memory");
+            if (c + PF < NCH) fill(c + PF);
         }
         asm volatile("" ::: "memory");
     }
     __syncthreads();  // every wave past its last chunk: the stages become the output transposes
-    if (!live) return;
-    const bool oor = PREC != 2 && __builtin_amdgcn_ballot_w64(amx >= 65504.0f) != 0;  // wave-uniform
-    float sc[16];
-#pragma unroll
-    for (int r = 0; r < 16; ++r) sc[r] = p.wsp_unscale;
-    if (RMS) {
-        const float t = ss + __shfl_xor(ss, 32);
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            const float n2 = __shfl(t, (r & 3) + 8 * (r >> 2) + 4 * h);
-            sc[r] *= 1.0f / fmaxf(sqrtf(n2), 1e-12f);
-        }
-    }
     // Y = acc * sc + bias through a per-wave 32 x 32 LDS transpose (the stages are dead: every
     // wave is past its last chunk), stored as 16-B pieces: 4 dwordx4 instead of 16 dword stores
     // per tile.  Launch shapes: N a multiple of 32 CT (launch_gl4t), so every column is real.
     float* sT = reinterpret_cast<float*>(smem_raw) + wave * 32 * TS;
-    float* y = yo.y + tr * yo.y_ts + j * yo.y_js + (int64_t)cg * CT * yo.y_cs;  // YOut as k_gl4y's
-    auto store_tile = [&](int ct, const floatx16& v, float bv) {
 #pragma unroll
-        for (int r = 0; r < 16; ++r) sT[((r & 3) + 8 * (r >> 2) + 4 * h) * TS + l32] = v[r] * sc[r] + bv;
-        __builtin_amdgcn_wave_barrier();  // DS operations of one wave complete in order
+    for (int rt = 0; rt < RT; ++rt) {
+        const int64_t tr = tr0 + rt;
+        if (tr >= ntile_r) break;  // wave-uniform: dead tiles store nothing
+        // (real rows only: the padding rows of a row-blocked buffer are never stored)
+        const bool oor = PREC != 2 && __builtin_amdgcn_ballot_w64(arow[rt] < p.B && amx[rt] >= 65504.0f) != 0;
+        float sc[16];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const int row = 8 * q + (lane >> 3), c4 = (lane & 7) * 4;
-            const floatx4 o = *reinterpret_cast<const floatx4*>(sT + row * TS + c4);
-            if (!ROWMAJOR || row0 + row < p.B)  // row-major z holds rows < B only
-                *reinterpret_cast<floatx4*>(y + (int64_t)row * yo.y_rs + ct * yo.y_cs + c4) = o;
+        for (int r = 0; r < 16; ++r) sc[r] = p.wsp_unscale;
+        if (RMS) {
+            const float t = ss[rt] + __shfl_xor(ss[rt], 32);
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const float n2 = __shfl(t, (r & 3) + 8 * (r >> 2) + 4 * h);
+                sc[r] *= 1.0f / fmaxf(sqrtf(n2), 1e-12f);
+            }
         }
-        __builtin_amdgcn_wave_barrier();
-    };
+        float* y = yo.y + tr * yo.y_ts + j * yo.y_js + (int64_t)cg * CT * yo.y_cs;  // YOut as k_gl4y's
+        auto store_tile = [&](int ct, const floatx16& v, float bv) {
 #pragma unroll
-    for (int ct = 0; ct < CT; ++ct) store_tile(ct, acc[ct], bvp[ct]);
-    // f16 range left: every tile of the wave again on exact-f32 MFMA, stored over the first (same
-    // lanes, same addresses: program order) -- after the stores, with the accumulators dead
-    if (oor) {
-        if (p.status && lane == 0) atomicOr(p.status, 1u);
+            for (int r = 0; r < 16; ++r) sT[((r & 3) + 8 * (r >> 2) + 4 * h) * TS + l32] = v[r] * sc[r] + bv;
+            __builtin_amdgcn_wave_barrier();  // DS operations of one wave complete in order
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int row = 8 * q + (lane >> 3), c4 = (lane & 7) * 4;
+                const floatx4 o = *reinterpret_cast<const floatx4*>(sT + row * TS + c4);
+                if (!ROWMAJOR || row0[rt] + row < p.B)  // row-major z holds rows < B only
+                    *reinterpret_cast<floatx4*>(y + (int64_t)row * yo.y_rs + ct * yo.y_cs + c4) = o;
+            }
+            __builtin_amdgcn_wave_barrier();
+        };
+#pragma unroll
+        for (int ct = 0; ct < CT; ++ct) store_tile(ct, acc[rt][ct], bvp[ct]);
+        // f16 range left: every tile of the row tile again on exact-f32 MFMA, stored over the first
+        // (same lanes, same addresses: program order) -- after the stores
+        if (oor) {
+            if (p.status && lane == 0) atomicOr(p.status, 1u);
 #pragma nounroll
-        for (int ct = 0; ct < CT; ++ct) {
-            const int col = (cg * CT + ct) * 32;
-            store_tile(ct, exact_tile_f32(p, row0, j, col), p.bias ? p.bias[p.wrow[j] + col + l32] : 0.f);
+            for (int ct = 0; ct < CT; ++ct) {
+                const int col = (cg * CT + ct) * 32;
+                store_tile(ct, exact_tile_f32(p, row0[rt], j, col), p.bias ? p.bias[p.wrow[j] + col + l32] : 0.f);
+            }
         }
     }
 }
 
-template <bool RMS, int PREC, int CT, int NCH, bool ROWMAJOR>
+template <bool RMS, int PREC, int CT, int NCH, bool ROWMAJOR, int RT>
 __global__ __launch_bounds__(256, 2) void k_gl4t(const GLArgs p, int ncg, int64_t ntile_r, const YOut yo) {
     __shared__ __attribute__((aligned(16))) char smem_raw[gl4t_smem_bytes<PREC, CT, NCH>()];
     // XCD-aware order (k_gl4's): consecutive u -- the column groups of one (row group, node), which
     // read the same x -- on one XCD (blocks b, b + 8, ... share one), so x reaches that L2 once
     const int nwg = gridDim.x, xcd = blockIdx.x & 7, q8 = nwg >> 3, r8 = nwg & 7;
     const int64_t u = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (blockIdx.x >> 3);
-    gl4t_body<RMS, PREC, CT, NCH, ROWMAJOR>(p, ncg, ntile_r, yo, u, threadIdx.x, smem_raw);
+    gl4t_body<RMS, PREC, CT, NCH, ROWMAJOR, RT>(p, ncg, ntile_r, yo, u, threadIdx.x, smem_raw);
 }
 
 // Epilogue of the fused to_qkv + Attention kernel (MODE 1), J <= 32, dh = 32, 8 waves, a
@@ -1175,7 +1174,7 @@ __device__ __forceinline__ void gl4_body(const GLArgs& p, const int bx, const in
                     const floatx8 q = f * f;
                     ss[m][rt] += ((q[0] + q[1]) + (q[2] + q[3])) + ((q[4] + q[5]) + (q[6] + q[7]));
                 }
-                {
+                if (row0 + 32 * rt + l32 < p.B) {  // real rows only (row-blocked padding rows: any bits)
                     const floatx8 a = __builtin_elementwise_abs(f);
                     amx = fmaxf(amx, fmaxf(fmaxf(fmaxf(a[0], a[1]), fmaxf(a[2], a[3])),
                                            fmaxf(fmaxf(a[4], a[5]), fmaxf(a[6], a[7]))));
@@ -1615,14 +1614,14 @@ hipError_t launch_gemm_split(const GLArgs& a, bool rms, float* z, int64_t z_rs, 
     return launch_gl4y<true>(a, rms, ntc, ntile_r, yo, s);
 }
 
-template <int CT, int NCH, bool ROWMAJOR>
+template <int CT, int NCH, bool ROWMAJOR, int RT>
 static hipError_t launch_gl4t_v(const GLArgs& a, bool rms, int64_t ntile_r, const YOut& yo, hipStream_t s) {
     const int ncg = a.N / (32 * CT);  // column groups
-    const dim3 grid((unsigned)(((ntile_r + 3) / 4) * a.J * ncg)), block(256);
-    auto kt = a.prec == 1 ? (rms ? k_gl4t<true, 1, CT, NCH, ROWMAJOR> : k_gl4t<false, 1, CT, NCH, ROWMAJOR>)
-                          : (rms ? k_gl4t<true, 0, CT, NCH, ROWMAJOR> : k_gl4t<false, 0, CT, NCH, ROWMAJOR>);
-    if constexpr (!ROWMAJOR) {  // bf16 mode (precision 2): the split route's scratch output only
-        if (a.prec == 2) kt = rms ? k_gl4t<true, 2, CT, NCH, false> : k_gl4t<false, 2, CT, NCH, false>;
+    const dim3 grid((unsigned)(((ntile_r + 4 * RT - 1) / (4 * RT)) * a.J * ncg)), block(256);
+    auto kt = a.prec == 1 ? (rms ? k_gl4t<true, 1, CT, NCH, ROWMAJOR, RT> : k_gl4t<false, 1, CT, NCH, ROWMAJOR, RT>)
+                          : (rms ? k_gl4t<true, 0, CT, NCH, ROWMAJOR, RT> : k_gl4t<false, 0, CT, NCH, ROWMAJOR, RT>);
+    if constexpr (!ROWMAJOR && RT == 1) {  // bf16 mode (precision 2): the split route's scratch output only
+        if (a.prec == 2) kt = rms ? k_gl4t<true, 2, CT, NCH, false, 1> : k_gl4t<false, 2, CT, NCH, false, 1>;
     }
     g_route_bits |= kRouteGemmTiled;
     hipLaunchKernelGGL(kt, grid, block, 0, s, a, ncg, ntile_r, yo);
@@ -1631,6 +1630,8 @@ static hipError_t launch_gl4t_v(const GLArgs& a, bool rms, int64_t ntile_r, cons
 
 // the release Denoiser's shapes: K = 192 (12 chunks), 256 (to_out, 16) or 384 (24), N a multiple
 // of 96 (192 wide layers, 768 to_qkv, 96 final_glin); hipErrorNotSupported otherwise (k_gl4y).
+// N = 192 / 96 (f32 / half): 2 row tiles x 3 column tiles per wave (tools/gl4t_rt_probe.hip: 17.1 vs
+// 18.5 us for 1 x 6 at N = 192, 3,200 rows); N = 768 to_qkv: 1 x 6 (53.6 vs 56.4 us for 2 x 3).
 // to_qkv (N = 768, K = 192) of the row-major v5 path (J > 21) on 256-column workgroups: 3 column
 // groups of 8 tiles instead of 4 of 6 (0.75 of the x re-reads, 24 MFMAs per chunk and wave; MANO
 // J = 51 3,757 / 3,766 vs 3,729 / 3,727 futures/s); on the tiled split route it measured slower
@@ -1640,14 +1641,19 @@ template <bool ROWMAJOR>
 static hipError_t launch_gl4t(const GLArgs& a, bool rms, int64_t ntile_r, const YOut& yo, hipStream_t s) {
     const int K = a.K1 + a.K2;
     if (a.K1 % 16 || (a.x1_div != 1 && a.x1_blk)) return hipErrorNotSupported;
-    if (ROWMAJOR && a.N % 256 == 0 && K == 192 && a.prec != 2) return launch_gl4t_v<8, 12, ROWMAJOR>(a, rms, ntile_r, yo, s);
+    if (ROWMAJOR && a.N % 256 == 0 && K == 192 && a.prec != 2) return launch_gl4t_v<8, 12, ROWMAJOR, 1>(a, rms, ntile_r, yo, s);
+    if (a.prec != 2 && a.N <= 192 && a.N % 96 == 0) {  // f16 operands, N = 96 / 192: 2 row tiles x 3 column tiles
+        if (K == 192) return launch_gl4t_v<3, 12, ROWMAJOR, 2>(a, rms, ntile_r, yo, s);
+        if (K == 256) return launch_gl4t_v<3, 16, ROWMAJOR, 2>(a, rms, ntile_r, yo, s);
+        if (K == 384) return launch_gl4t_v<3, 24, ROWMAJOR, 2>(a, rms, ntile_r, yo, s);
+    }
     if (a.N % 192 == 0) {
-        if (K == 192) return launch_gl4t_v<6, 12, ROWMAJOR>(a, rms, ntile_r, yo, s);
-        if (K == 256) return launch_gl4t_v<6, 16, ROWMAJOR>(a, rms, ntile_r, yo, s);
-        if (K == 384) return launch_gl4t_v<6, 24, ROWMAJOR>(a, rms, ntile_r, yo, s);
+        if (K == 192) return launch_gl4t_v<6, 12, ROWMAJOR, 1>(a, rms, ntile_r, yo, s);
+        if (K == 256) return launch_gl4t_v<6, 16, ROWMAJOR, 1>(a, rms, ntile_r, yo, s);
+        if (K == 384) return launch_gl4t_v<6, 24, ROWMAJOR, 1>(a, rms, ntile_r, yo, s);
     } else if (a.N % 96 == 0) {
-        if (K == 192) return launch_gl4t_v<3, 12, ROWMAJOR>(a, rms, ntile_r, yo, s);
-        if (K == 384) return launch_gl4t_v<3, 24, ROWMAJOR>(a, rms, ntile_r, yo, s);
+        if (K == 192) return launch_gl4t_v<3, 12, ROWMAJOR, 1>(a, rms, ntile_r, yo, s);
+        if (K == 384) return launch_gl4t_v<3, 24, ROWMAJOR, 1>(a, rms, ntile_r, yo, s);
     }
     return hipErrorNotSupported;
 }

@@ -2,7 +2,7 @@
 keep the memory-wait shape the audit fixed.  Each case disassembles one kernel symbol of the built
 libskeldiff.so (llvm-objdump --disassemble-symbols) and checks its s_waitcnt / load / store order:
 
-* k_gl4t (tiled GEMM phase, default fill-first ring): the bias is loaded before the K loop, so the
+* k_gl4t (tiled GEMM phase, register-x fill-first ring; the N = 768 and N = 192 forms): the bias is loaded before the K loop, so the
   epilogue has no global load and no vmcnt wait between its stores; the K loop waits with counts
   (vmcnt(5) at two chunks in flight), vmcnt(0) only for the last chunk;
 * k_attention<4, 32> (MANO attention): every K / Q / V load issued before the first vmcnt wait
@@ -37,7 +37,8 @@ OBJDUMP = shutil.which("llvm-objdump") or "/opt/rocm/lib/llvm/bin/llvm-objdump"
 
 pytestmark = pytest.mark.skipif(not os.path.exists(OBJDUMP) or not os.path.exists(LIB), reason="no llvm-objdump / library")
 
-GL4T = "_ZN2sd6k_gl4tILb0ELi0ELi6ELi12ELb0EEEvNS_6GLArgsEilNS_4YOutE"
+GL4T = "_ZN2sd6k_gl4tILb0ELi0ELi6ELi12ELb0ELi1EEEvNS_6GLArgsEilNS_4YOutE"  # N = 768 form (CT 6, one row tile)
+GL4T_RT2 = "_ZN2sd6k_gl4tILb0ELi0ELi3ELi12ELb0ELi2EEEvNS_6GLArgsEilNS_4YOutE"  # N = 192 form (CT 3, two row tiles)
 ATTN = "_ZN2sd11k_attentionILi4ELi32EEEvNS_8AttnArgsE"
 MIXD = "_ZN2sd12_GLOBAL__N_110k_gl5_mixdILi8ELi1ELb0EEEvNS_6GLArgsEPKfl"
 MIXD_RES = "_ZN2sd12_GLOBAL__N_110k_gl5_mixdILi8ELi1ELb1EEEvNS_6GLArgsEPKfl"
@@ -76,15 +77,18 @@ def _vmcnt(line):
     return int(m.group(1)) if m else None
 
 
-def test_gl4t_store_tail_has_no_load_waits(tmp_path_factory):
-    ins = _disasm(tmp_path_factory, GL4T)
+@pytest.mark.parametrize("sym,ntiles", [(GL4T, 6), (GL4T_RT2, 6)])
+def test_gl4t_store_tail_has_no_load_waits(sym, ntiles, tmp_path_factory):
+    ins = _disasm(tmp_path_factory, sym)
     last_barrier = max(i for i, l in enumerate(ins) if l.startswith("s_barrier"))
     tail = ins[last_barrier:]
-    # the normal store tail: 6 tiles x 4 dwordx4 stores; after it only the f16-range fallback
-    # (exact_tile_f32, its own loads and waits, taken by out-of-range waves alone)
+    # the normal store tail: 6 tiles x 4 dwordx4 stores (the first row tile's; per row tile the
+    # f16-range fallback -- exact_tile_f32, its own loads and waits, taken by out-of-range waves
+    # alone -- follows that row tile's stores)
     stores = [i for i, l in enumerate(tail) if l.startswith("global_store")]
-    assert len(stores) >= 24, len(stores)
-    tail = tail[:stores[23] + 1]
+    n = 4 * ntiles if sym == GL4T else 4 * 3
+    assert len(stores) >= n, len(stores)
+    tail = tail[:stores[n - 1] + 1]
     assert not any(l.startswith("global_load") for l in tail), "a global load in the epilogue (bias?)"
     first_store = next(i for i, l in enumerate(tail) if l.startswith("global_store"))
     waits = [l for l in tail[first_store:] if _vmcnt(l) is not None]
@@ -119,14 +123,23 @@ def test_mixd_rows_do_not_drain_fills(tmp_path_factory):
         assert not any(_vmcnt(l) == 0 for l in ins[f:nxt]), ins[f:nxt]
 
 
+@pytest.mark.parametrize("sym", [GL4T, GL4T_RT2])
+def test_gl4t_no_scratch(sym, tmp_path_factory):
+    """The whole-unrolled K loop with its register x ring stays in registers (round 6: unpinned
+    range-guard reductions were sunk into the epilogue and spilled 62..270 VGPRs)."""
+    ins = _disasm(tmp_path_factory, sym)
+    assert not any(l.startswith("scratch_") for l in ins)
+
+
 def test_update_f32_form_has_no_bf16_loads(tmp_path_factory):
     ins = _disasm(tmp_path_factory, UPD)
     assert any(l.startswith("global_load_dword") for l in ins)
     assert not any(l.startswith(("global_load_ushort", "global_load_short")) for l in ins)
 
 
-def test_gl4t_ring_barriers_drain_lds_reads(tmp_path_factory):
-    ins = _disasm(tmp_path_factory, GL4T)
+@pytest.mark.parametrize("sym", [GL4T, GL4T_RT2])
+def test_gl4t_ring_barriers_drain_lds_reads(sym, tmp_path_factory):
+    ins = _disasm(tmp_path_factory, sym)
     bars = [i for i, l in enumerate(ins) if l.startswith("s_barrier")]
     assert len(bars) >= 4, len(bars)  # the unrolled ring steps (PF = 2) + the last chunks + the epilogue
     for i in bars:
