@@ -858,6 +858,52 @@ __device__ __forceinline__ void attention_epilogue(const GLArgs& p, floatx16 (&a
     }
 }
 
+// Block.norm for norm_type 'layer' (attention.py:19-28, 55-58): nn.LayerNorm(J) over the node axis
+// of the graph-linear output, per (row, column), eps 1e-5, biased variance, per-node affine.  In the
+// mixing epilogue's layout lane (lr, lg) holds node i = 16 ib + lr of four consecutive columns, so a
+// (row, column)'s J nodes are the 16 lanes of one lg group (x IB blocks): two xor-butterfly sums
+// over lr, nodes i >= J masked out.
+__device__ __forceinline__ floatx4 sum_lanes16(floatx4 v) {
+#pragma unroll
+    for (int m = 1; m < 16; m <<= 1) {
+        v.x += __shfl_xor(v.x, m);
+        v.y += __shfl_xor(v.y, m);
+        v.z += __shfl_xor(v.z, m);
+        v.w += __shfl_xor(v.w, m);
+    }
+    return v;
+}
+
+template <int IB>
+__device__ __forceinline__ void node_layernorm(floatx4 (&z)[IB], const float* __restrict__ w, const float* __restrict__ b,
+                                               int J, int lr) {
+    const float inv = 1.0f / (float)J;
+    floatx4 s = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ib = 0; ib < IB; ++ib)
+        if (16 * ib + lr < J) s += z[ib];
+    const floatx4 mu = sum_lanes16(s) * inv;
+    floatx4 q = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ib = 0; ib < IB; ++ib)
+        if (16 * ib + lr < J) {
+            const floatx4 d = z[ib] - mu;
+            q += d * d;
+        }
+    q = sum_lanes16(q) * inv;
+    floatx4 rs;
+    rs.x = 1.0f / sqrtf(q.x + 1e-5f);
+    rs.y = 1.0f / sqrtf(q.y + 1e-5f);
+    rs.z = 1.0f / sqrtf(q.z + 1e-5f);
+    rs.w = 1.0f / sqrtf(q.w + 1e-5f);
+#pragma unroll
+    for (int ib = 0; ib < IB; ++ib) {
+        const int i = 16 * ib + lr;
+        const float wi = i < J ? w[i] : 0.f, bi = i < J ? b[i] : 0.f;
+        z[ib] = (z[ib] - mu) * rs * wi + bi;
+    }
+}
+
 // MODE 0: StaticGraphLinear with the FiLM / tanh / residual epilogue.
 // MODE 1: to_qkv + Attention fused (attention.py:105-136): the workgroup's three 32-column tiles
 //   are head h's q, k and v columns (tiles h, heads + h, 2 heads + h), and the epilogue runs
@@ -1428,6 +1474,7 @@ __device__ __forceinline__ void gl4_body(const GLArgs& p, const int bx, const in
                 const bool ok = b < COLS && row < p.B && n < p.N;
                 const floatx4 fa = *reinterpret_cast<const floatx4*>(sF + cc);
                 const floatx4 fb = *reinterpret_cast<const floatx4*>(sF + COLS + cc);
+                if (p.ln_w) node_layernorm<IB>(z[kk], p.ln_w, p.ln_b, J, lr);  // norm_type 'layer'
 #pragma unroll
                 for (int ib = 0; ib < IB; ++ib) {
                     const int i = ib * 16 + lr;
@@ -1642,7 +1689,13 @@ static hipError_t launch_gl4t(const GLArgs& a, bool rms, int64_t ntile_r, const 
     const int K = a.K1 + a.K2;
     if (a.K1 % 16 || (a.x1_div != 1 && a.x1_blk)) return hipErrorNotSupported;
     if (ROWMAJOR && a.N % 256 == 0 && K == 192 && a.prec != 2) return launch_gl4t_v<8, 12, ROWMAJOR, 1>(a, rms, ntile_r, yo, s);
-    if (a.prec != 2 && a.N <= 192 && a.N % 96 == 0) {  // f16 operands, N = 96 / 192: 2 row tiles x 3 column tiles
+    // f16 operands, row-blocked x, N = 96 / 192: 2 row tiles x 3 column tiles per wave (row-major x
+    // -- the J > 21 path -- keeps 1 x 6: its x fragments are 16-B pieces of rows J K floats apart,
+    // and a second row tile doubled them; MANO N = 192 29.1 vs 26.7 us, profiles/r06h)
+#ifndef SD_GL4T_RT2
+#define SD_GL4T_RT2 1
+#endif
+    if (!ROWMAJOR && SD_GL4T_RT2 && a.prec != 2 && a.N <= 192 && a.N % 96 == 0) {
         if (K == 192) return launch_gl4t_v<3, 12, ROWMAJOR, 2>(a, rms, ntile_r, yo, s);
         if (K == 256) return launch_gl4t_v<3, 16, ROWMAJOR, 2>(a, rms, ntile_r, yo, s);
         if (K == 384) return launch_gl4t_v<3, 24, ROWMAJOR, 2>(a, rms, ntile_r, yo, s);

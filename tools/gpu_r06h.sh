@@ -10,7 +10,8 @@ tr() {  # name, lib, bench args
   local name=$1 lib=$2; shift 2
   SKELDIFF_LIB=$lib timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/$name -o run -- \
       python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-exact-line "$@" > $OUT/$name.log 2>&1
-  local rc=$?; echo "$name rc=$rc $(tail -1 $OUT/$name.log | cut -c1-120)"; return $rc
+  local rc=$?; rm -f $OUT/$name/run_kernel_trace.csv  # keep the stats (gpurun_out is capped at 64 MiB)
+  echo "$name rc=$rc $(grep '"metric"' $OUT/$name.log | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); print(round(d["value"],1), round(d["ms_per_step"],2))')"; return $rc
 }
 NEW=$PWD/skeletondiffusion_amd/libskeldiff.so
 tr mano_new $NEW --config mano51 && tr mano_old $PREV --config mano51 && tr amass_old $PREV && \
