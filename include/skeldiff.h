@@ -45,8 +45,9 @@ extern "C" {
  * sd_set_kernel_variant / sd_set_row_chains / sd_set_update_kernel / sd_set_v5_mix removed
  * (per-plan options instead), sd_test_set_split_route and sd_plan_desc::objective added;
  * 3 (round 6) -- SD_FLAG_NO_CLIP (p_sample's clip_denoised = False), sd_p_sample_update takes
- * flags.  Bindings check it at load. */
-#define SD_ABI_VERSION 3
+ * flags, the measured-slower kernel forms and option values removed; 4 (round 6) --
+ * sd_plan_desc::norm_type (Block LayerNorm over the node axis).  Bindings check it at load. */
+#define SD_ABI_VERSION 4
 
 enum {
     SD_OK = 0,
@@ -88,6 +89,9 @@ typedef struct sd_plan_desc {
     float sinusoidal_theta;   /* SinusoidalPosEmb theta (10000) */
     int32_t objective;        /* 0 pred_x0 (release configs); isotropic only: 1 pred_noise, 2 pred_v
                                  (x0 = a[t] x_t - b[t] act(model_out): isotropic.py:48-70) */
+    int32_t norm_type;        /* ResnetBlock Block.norm (attention.py:49-60): 0 'none' (release configs),
+                                 1 'layer' = LayerNorm over the node axis (attention.py:19-28; J = 16, 17
+                                 or 21, v4 kernels; tensors "...blockN.norm.norm.weight/bias") -- ABI 4 */
 } sd_plan_desc;
 
 int32_t sd_abi_version(void);

@@ -237,6 +237,7 @@ class DenoiserConfig:
     learn_influence: bool = False
     node_types: Optional[torch.Tensor] = None
     theta: float = 10000.0
+    norm_type: str = "none"  # Block norm (attention.py:49-60): 'none' (release) or 'layer'
     extra: dict = field(default_factory=dict)
 
 
@@ -279,13 +280,23 @@ class _Net:
     def linear(self, name, x):
         return F.linear(x, self.w(name + ".weight"), self.w(name + ".bias"))
 
+    def block_norm(self, name, h):
+        """Block.norm (attention.py:55-60): identity for norm_type 'none'; 'layer' is LayerNorm over
+        the node axis with a per-node affine (attention.py:19-28: swapaxes, nn.LayerNorm(J), eps 1e-5)."""
+        if not self.has(name + ".norm.norm.weight"):
+            return h
+        w, b = self.w(name + ".norm.norm.weight"), self.w(name + ".norm.norm.bias")
+        mean = h.mean(dim=-2, keepdim=True)
+        var = ((h - mean) ** 2).mean(dim=-2, keepdim=True)
+        return (h - mean) / torch.sqrt(var + 1e-5) * w[:, None] + b[:, None]
+
     def resnet(self, name, x, temb):
-        """attention.py:78-102 (Block :49-75, norm_type 'none', act tanh)."""
+        """attention.py:78-102 (Block :49-75: proj, norm, FiLM, tanh)."""
         ss = self.linear(name + ".mlp.1", torch.tanh(temb)).unsqueeze(1)
         scale, shift = ss.chunk(2, dim=-1)
-        h = self.graph_linear(name + ".block1.proj", x)
+        h = self.block_norm(name + ".block1", self.graph_linear(name + ".block1.proj", x))
         h = torch.tanh(h * (scale + 1) + shift)
-        h = torch.tanh(self.graph_linear(name + ".block2.proj", h))
+        h = torch.tanh(self.block_norm(name + ".block2", self.graph_linear(name + ".block2.proj", h)))
         res = self.graph_linear(name + ".res_linear", x) if self.has(name + ".res_linear.weight") else x
         return h + res
 
@@ -539,7 +550,13 @@ def denoiser_param_shapes(cfg: DenoiserConfig):
     def res(name, fin, fout):
         lin(f"{name}.mlp.1", 4 * H, 2 * fout)
         gl(f"{name}.block1.proj", fin, fout, True)
+        if cfg.norm_type == "layer":  # LayerNorm(num_nodes) (attention.py:57-58)
+            out.append((f"model.{name}.block1.norm.norm.weight", (J,), True))
+            out.append((f"model.{name}.block1.norm.norm.bias", (J,), True))
         gl(f"{name}.block2.proj", fout, fout, True)
+        if cfg.norm_type == "layer":
+            out.append((f"model.{name}.block2.norm.norm.weight", (J,), True))
+            out.append((f"model.{name}.block2.norm.norm.bias", (J,), True))
         if fin != fout:
             gl(f"{name}.res_linear", fin, fout, False)
 

@@ -18,7 +18,7 @@ LIB_PATH = os.environ.get("SKELDIFF_LIB") or os.path.join(HERE, "libskeldiff.so"
 # include/skeldiff.h SD_ABI_VERSION: a library of another ABI is refused at load (round 4 changed
 # signatures under the same number; a client built against the old header would pass shifted
 # arguments instead of failing cleanly)
-SD_ABI_VERSION = 3
+SD_ABI_VERSION = 4
 
 SD_FLAG_GRAPH = 1
 SD_FLAG_DEVICE_START = 2
@@ -73,6 +73,7 @@ class SDPlanDesc(ctypes.Structure):
         ("activation", ctypes.c_int32),
         ("sinusoidal_theta", ctypes.c_float),
         ("objective", ctypes.c_int32),
+        ("norm_type", ctypes.c_int32),  # ABI 4: 0 'none', 1 'layer'
     ]
 
 

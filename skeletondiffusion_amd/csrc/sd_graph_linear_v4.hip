@@ -1474,7 +1474,8 @@ __device__ __forceinline__ void gl4_body(const GLArgs& p, const int bx, const in
                 const bool ok = b < COLS && row < p.B && n < p.N;
                 const floatx4 fa = *reinterpret_cast<const floatx4*>(sF + cc);
                 const floatx4 fb = *reinterpret_cast<const floatx4*>(sF + COLS + cc);
-                if (p.ln_w) node_layernorm<IB>(z[kk], p.ln_w, p.ln_b, J, lr);  // norm_type 'layer'
+                if constexpr (MODE == 2)  // norm_type 'layer' (split route only: no registers taken from MODE 0)
+                    if (p.ln_w) node_layernorm<IB>(z[kk], p.ln_w, p.ln_b, J, lr);
 #pragma unroll
                 for (int ib = 0; ib < IB; ++ib) {
                     const int i = ib * 16 + lr;
@@ -1585,18 +1586,22 @@ int64_t split_rows_default() { return g_split_rows; }
 // route with the tiled phase 1 (k_gl4t, full batches).  GLArgs::split: 0 auto, 1 never, 2 always
 // (k_gl4y), 3 always (k_gl4t).
 static int split_route(const GLArgs& a, bool attn) {
-    if (a.split == 1 || !a.zs || (a.N & 31) || a.J > 32) return 0;
-    if (a.prec == 2 && a.split < 3 && !(a.split == 0 && a.J == 17)) return 0;  // bf16: tiled only (J = 17 auto)
+    // norm_type 'layer': the Block LayerNorm runs in the split route's mixing phase only, so such a
+    // layer takes a split route whatever SD_OPT_SPLIT_ROUTE 1 / a gl4_tile option / half or bf16
+    // precision would choose (launch_graph_linear_v4 never hands it to a one-kernel tile)
+    const bool ln = a.ln_w != nullptr;
+    if ((a.split == 1 && !ln) || !a.zs || (a.N & 31) || a.J > 32) return 0;
     const int64_t tiles = (a.B + 31) / 32;
     if (tiles * 32 * a.J * (int64_t)a.N > a.zs_cap) return 0;
     if (a.zs == a.out || a.zs == a.x1 || a.zs == a.x2 || a.zs == a.res) return 0;
     if (attn && (a.attn_heads * 96 != a.N)) return 0;
+    if (a.prec == 2 && a.split < 3 && !(a.split == 0 && a.J == 17)) return ln ? 2 : 0;  // bf16: tiled only (J = 17 auto)
     if (a.split == 2) return a.prec == 2 ? 0 : 1;
     if (a.split == 3) return 2;
     if (a.split == 4) return attn ? 0 : 2;  // tiled GEMM phase; to_qkv + attention on the one-kernel tile
-    if (a.gl4_cfg != 0) return 0;
+    if (a.gl4_cfg != 0 && !ln) return 0;
     const int64_t rows = a.route_rows > 0 ? a.route_rows : a.B;
-    if (rows <= g_split_rows) return a.prec == 2 ? 0 : 1;
+    if (rows <= g_split_rows) return a.prec == 2 ? (ln ? 2 : 0) : 1;
     // J = 17 / 21 full batches (f32 and half; bf16 at J = 17): the tiled route on one chain measured
     // faster than the one-kernel route on three (FreeMan J = 17 10,954 vs 9,547, AMASS J = 21 8,567
     // vs 8,371 futures/s at 3,200 rows, T = 100; config 5 half 133,002 vs 92,456, bf16 134,084 vs
@@ -1605,7 +1610,7 @@ static int split_route(const GLArgs& a, bool attn) {
     // round 3, same box: 800 rows 8,146 vs 7,516 futures/s for the one-kernel route, 1,600 rows
     // 12,385 vs 12,473, config 2 15,940 vs 14,972 with the fused one-kernel attention tile); in
     // half / bf16 mode the one-kernel tiles stay
-    if (a.J == 16) return a.prec == 0 ? 2 : 0;
+    if (a.J == 16) return a.prec == 0 || ln ? 2 : 0;
     return (a.J == 17 || a.J == 21) ? 2 : 0;
 }
 
@@ -1751,6 +1756,7 @@ hipError_t launch_graph_linear_v4(const GLArgs& a, bool rms, hipStream_t s) {
             const hipError_t e = gl4_split_dispatch(a, rms, false, route, s);
             if (e != hipErrorNotSupported) return e;  // else: nothing launched, the one-kernel route
         }
+    if (a.ln_w) return hipErrorNotSupported;  // the Block LayerNorm lives in the split mixing phase only
     const int cfg = a.gl4_cfg ? a.gl4_cfg : a.tile_hint;
     if (a.prec == 2) {  // bf16 mode: row-major operands, the default tiles only
         if (a.x1_blk || a.x2_blk || a.res_blk || a.out_blk) return hipErrorNotSupported;

@@ -44,6 +44,7 @@ struct GLArgs {
     const float* bias;                                    // (types, N) or null
     const float* G;                                       // (J, J) Ghat, row-major
     const float* film;                                    // (2N): [scale | shift] or null
+    const float* ln_w; const float* ln_b;                 // (J) Block.norm LayerNorm over nodes (norm_type 'layer', v4 only) or null
     const float* res; int64_t res_rs;                     // (B, J, N) or null
     float* out; int64_t out_rs;                           // (B, J, N)
     int64_t B;

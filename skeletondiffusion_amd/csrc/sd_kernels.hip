@@ -224,6 +224,8 @@ hipError_t launch_graph_linear(const GLArgs& a, bool rms, hipStream_t s) {
     // aliases the output would be overwritten by sibling column tiles while still being read
     if (a.B > 0 && (a.x1 == a.out || (a.x2 && a.x2 == a.out))) return hipErrorInvalidValue;
     if (a.skip_mix) return (v == 0 || v == 5) && a.J > 21 && a.prec != 2 ? launch_graph_linear_v5(a, rms, s) : hipErrorNotSupported;
+    // Block.norm 'layer' lives in the v4 mixing epilogue only (J = 16 / 17 / 21; plan-time checked)
+    if (a.ln_w) return v == 0 || v == 4 ? launch_graph_linear_v4(a, rms, s) : hipErrorNotSupported;
     if (v == 1) return launch_graph_linear_v1(a, rms, s);
     if (v == 4 || v == 0) {
         const hipError_t e = launch_graph_linear_v4(a, rms, s);

@@ -74,6 +74,7 @@ struct GL {
     const float* wuse = nullptr; // weights used by the kernel (folded copy for RMS layers)
     bool rms = false;
     int gain = -1;               // RMSNorm gain slot folded into this layer
+    int lnw = -1, lnb = -1;      // Block.norm LayerNorm(J) affine slots (norm_type 'layer')
     sd::SplitW split;            // f16 hi/lo B fragments of wuse for the v4 kernel
     sd::SplitW split_bf;         // bf16 fragments of wuse (precision mode 2)
 };
@@ -225,6 +226,15 @@ struct sd_plan {
         g.N = N;
         return g;
     }
+    // ResnetBlock Block (attention.py:49-75): proj, then with norm_type 'layer' its LayerNorm(J)
+    GL add_block(const std::string& name, int K1, int K2, int N) {
+        GL g = add_gl(name + ".proj", K1, K2, N, true);
+        if (d.norm_type == 1) {
+            g.lnw = add(name + ".norm.norm.weight", J);
+            g.lnb = add(name + ".norm.norm.bias", J);
+        }
+        return g;
+    }
     const float* ptr(int slot) const { return slot < 0 ? nullptr : slots[slot].dev; }
 };
 
@@ -244,6 +254,9 @@ int check_dims(const sd_plan_desc* d) {
     if (d->timesteps < 1) return fail(SD_E_INVALID, "timesteps must be >= 1");
     if (d->activation != 0 && d->activation != 1) return fail(SD_E_INVALID, "activation must be 0 (identity) or 1 (tanh)");
     if (d->objective < 0 || d->objective > 2) return fail(SD_E_INVALID, "objective must be 0 (pred_x0), 1 (pred_noise) or 2 (pred_v)");
+    if (d->norm_type != 0 && d->norm_type != 1) return fail(SD_E_INVALID, "norm_type must be 0 ('none') or 1 ('layer')");
+    if (d->norm_type == 1 && d->num_nodes != 16 && d->num_nodes != 17 && d->num_nodes != 21)
+        return fail(SD_E_INVALID, "norm_type 'layer' runs in the v4 mixing epilogue: num_nodes 16, 17 or 21");
     if (d->objective != 0 && !d->isotropic)
         return fail(SD_E_INVALID, "the nonisotropic sampler supports objective pred_x0 only (the release configs; "
                                   "pred_v is not implemented in the reference, nonisotropic.py:122-124)");
@@ -321,6 +334,8 @@ sd::GLArgs gl_args(const sd_plan* p, const GL& g, const float* x1, int x1_div, c
     a.x2_rs = (int64_t)p->J * g.K2;
     a.W = g.wuse;
     a.bias = p->ptr(g.b);
+    a.ln_w = p->ptr(g.lnw);
+    a.ln_b = p->ptr(g.lnb);
     a.G = g.ghat;
     a.film = film;
     a.res = res;
@@ -685,6 +700,8 @@ int sd_plan_create(sd_plan** out, const sd_plan_desc* desc) {
     if (rc) return rc;
     std::unique_ptr<sd_plan> p(new sd_plan());
     p->variant = sd::graph_linear_variant();
+    if (desc->norm_type == 1 && p->variant != 0 && p->variant != 4)
+        return fail(SD_E_INVALID, "norm_type 'layer' runs on the v4 kernels only (SKELDIFF_GL_VARIANT 0 or 4)");
     p->gl4_cfg = sd::gl4_tile_default();
     p->gl4_stage = sd::gl4_stage_default();
     p->chains = g_chains;
@@ -728,8 +745,8 @@ int sd_plan_create(sd_plan** out, const sd_plan_desc* desc) {
         const std::string r = m + "layers." + std::to_string(l) + ".0.";
         p->mlp_w.push_back(p->add(r + "mlp.1.weight", (int64_t)2 * H * 4 * H));
         p->mlp_b.push_back(p->add(r + "mlp.1.bias", 2 * H));
-        p->r1.push_back(p->add_gl(r + "block1.proj", H, 0, H, true));
-        p->r2.push_back(p->add_gl(r + "block2.proj", H, 0, H, true));
+        p->r1.push_back(p->add_block(r + "block1", H, 0, H));
+        p->r2.push_back(p->add_block(r + "block2", H, 0, H));
         const bool attn = (l != L - 1);  // generator.py:71-76: last layer gets nn.Identity
         p->has_attn[l] = attn;
         if (!attn) continue;
@@ -748,8 +765,8 @@ int sd_plan_create(sd_plan** out, const sd_plan_desc* desc) {
         const std::string r = m + "final_res_block.";
         p->mlp_w.push_back(p->add(r + "mlp.1.weight", (int64_t)2 * H * 4 * H));
         p->mlp_b.push_back(p->add(r + "mlp.1.bias", 2 * H));
-        p->r1.push_back(p->add_gl(r + "block1.proj", H, H, H, true));
-        p->r2.push_back(p->add_gl(r + "block2.proj", H, 0, H, true));
+        p->r1.push_back(p->add_block(r + "block1", H, H, H));
+        p->r2.push_back(p->add_block(r + "block2", H, 0, H));
         p->fres_res = p->add_gl(r + "res_linear", H, H, H, false);
     }
     p->fglin = p->add_gl(m + "final_glin", H, 0, p->O, true);
@@ -1420,6 +1437,8 @@ int sd_plan_set_option(sd_plan* p, int32_t option, int64_t value) {
             if (value < 0 || value > 5) return fail(SD_E_INVALID, "kernel variant must be in [0, 5]");
             if (p->prec == 2 && value != 0 && value != 4)
                 return fail(SD_E_INVALID, "bf16 mode runs on the v4 kernels only (variant 0 or 4)");
+            if (p->d.norm_type == 1 && value != 0 && value != 4)
+                return fail(SD_E_INVALID, "norm_type 'layer' runs on the v4 kernels only (variant 0 or 4)");
             p->variant = (int)value;
             return SD_OK;
         case SD_OPT_GL4_TILE:

@@ -66,8 +66,10 @@ class SamplingEngine:
             unsupported.append("learned_variance")
         if m.self_condition:
             unsupported.append("self_condition")
-        if m.graph_kwargs.get("norm_type", "none") != "none":
-            unsupported.append("norm_type != 'none'")
+        norm_types = {"none": 0, "layer": 1}
+        norm = m.graph_kwargs.get("norm_type", "none")
+        if norm not in norm_types:
+            unsupported.append(f"norm_type {norm!r}")
         objectives = {"pred_x0": 0, "pred_noise": 1, "pred_v": 2}
         iso = not hasattr(self.diff, "posterior_mean_coef1_x0")
         if self.diff.objective not in objectives or (self.diff.objective != "pred_x0" and not iso):
@@ -99,6 +101,7 @@ class SamplingEngine:
         d.activation = 1 if self.diff.diffusion_activation == "tanh" else 0
         d.sinusoidal_theta = float(m.sinusoidal_pos_emb_theta)
         d.objective = objectives.get(self.diff.objective, 0)
+        d.norm_type = norm_types.get(norm, 0)  # 'layer': Block LayerNorm over nodes (J = 16 / 17 / 21)
         return d
 
     PRECISIONS = {"f32": 0, "half": 1, "bf16": 2}

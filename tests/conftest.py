@@ -206,6 +206,58 @@ def build_option_diffusion(name, model, z, device="cpu"):
     return d.to(device).eval()
 
 
+# round 6: norm_type='layer' (gen_golden.py gen_layernorm)
+LAYERNORM_MODELS = ["readme", "h36m16", "amass21"]
+
+
+def layernorm_case(model, z):
+    """(oracle config, oracle state_dict, x_cond per row or None, start, sampling noise, buffers) of
+    one layernorm_T10 chain."""
+    import dataclasses
+
+    import oracle as O
+    from skeletondiffusion_amd import synthetic
+
+    T = int(z["T"])
+    if model == "readme":
+        cfg = dataclasses.replace(O.readme_config(), norm_type="layer")
+        bufs = {k[len("readme_buf_"):]: torch.from_numpy(z[k]) for k in z.files if k.startswith("readme_buf_")}
+        return (cfg, O.synthetic_state_dict(cfg, WEIGHT_SEED), None, torch.from_numpy(synthetic.normal((4, 16, 96), 11)),
+                torch.from_numpy(synthetic.normal((4, T - 1, 16, 96), 12)), bufs)
+    J = int(z[f"{model}_corr"].shape[0])
+    cfg = dataclasses.replace(O.release_config(J, z[f"{model}_node_types"]), norm_type="layer")
+    bs, fu = int(z["B_seq"]), int(z["futures"])
+    S, L, U = pinned_cov(J)
+    return (cfg, O.synthetic_state_dict(cfg, WEIGHT_SEED),
+            torch.from_numpy(synthetic.uniform((bs, J, 96), 21)).repeat_interleave(fu, 0),
+            torch.from_numpy(synthetic.normal((bs * fu, J, 96), 22)), torch.from_numpy(synthetic.normal((bs * fu, T - 1, J, 96), 23)),
+            O.nonisotropic_buffers(S, L, U, O.beta_schedule("cosine", T)))
+
+
+def build_layernorm_diffusion(model, z, device="cpu"):
+    """Product NonisotropicGaussianDiffusion with a norm_type='layer' Denoiser (README or release)."""
+    from skeletondiffusion_amd import synthetic
+    from skeletondiffusion_amd.core.diffusion import NonisotropicGaussianDiffusion
+    from skeletondiffusion_amd.core.network import Denoiser
+
+    T = int(z["T"])
+    if model == "readme":
+        m = Denoiser(dim=96, cond_dim=0, out_dim=96, channels=16, num_nodes=16, norm_type="layer")
+        synthetic.fill_module_(m, WEIGHT_SEED)
+        S, L, U = (torch.from_numpy(z[f"readme_buf_{k}"]) for k in ("Sigma_N", "Lambda_N", "U"))
+        d = NonisotropicGaussianDiffusion(Sigma_N=S, Lambda_N=L, U=U, model=m, diffusion_timesteps=T)
+        return d.to(device).eval()
+    J = int(z[f"{model}_corr"].shape[0])
+    m = Denoiser(dim=96, cond_dim=96, out_dim=96, channels=J, num_nodes=J,
+                 node_types=torch.from_numpy(z[f"{model}_node_types"]), use_attention=True, self_condition=False,
+                 norm_type="layer", depth=4, attn_dim_head=32, attn_heads=8, learn_influence=True)
+    synthetic.fill_module_(m, WEIGHT_SEED)
+    S, L, U = pinned_cov(J)
+    d = NonisotropicGaussianDiffusion(Sigma_N=S, Lambda_N=L, U=U, model=m, latent_size=96, diffusion_timesteps=T,
+                                      diffusion_objective="pred_x0", diffusion_conditioning=True, beta_schedule="cosine")
+    return d.to(device).eval()
+
+
 @pytest.fixture(scope="session")
 def cuda():
     return torch.device("cuda:0")

@@ -597,7 +597,54 @@ def gen_options():
         _save(f"option_{name}", **out)
 
 
+def gen_layernorm():
+    """Round 6: the Denoiser with norm_type='layer' (Block: proj -> LayerNorm over the node axis ->
+    FiLM -> tanh, attention.py:19-28, 49-75): README Denoiser (J=16, B=4, nonisotropic, README
+    correlation) and the release H36M J=16 / AMASS J=21 Denoisers (2 sequences x 4 futures), T=10,
+    supplied noise; one direct Denoiser forward at t=3 per model."""
+    T = 10
+    out = {"T": T, "fwd_t": 3}
+    J, B = 16, 4
+    corr = torch.from_numpy(synthetic.readme_correlation(J, seed=7))
+    model = Denoiser(dim=96, cond_dim=0, out_dim=96, channels=J, num_nodes=J, norm_type="layer")
+    synthetic.fill_module_(model, WEIGHT_SEED)
+    Sigma_N, Lambda_N, U = get_cov_from_corr(correlation_matrix=corr, if_sigma_n_scale=True,
+                                             sigma_n_scale="spectral", if_run_as_isotropic=False)
+    diff = NonisotropicGaussianDiffusion(Sigma_N=Sigma_N, Lambda_N=Lambda_N, U=U, model=model,
+                                         diffusion_timesteps=T).eval()
+    start = torch.from_numpy(synthetic.normal((B, J, 96), seed=11))
+    samp = torch.from_numpy(synthetic.normal((B, T - 1, J, 96), seed=12))
+    with torch.no_grad():
+        img, (_, _, mean_t) = diff.sample(batch_size=B, start_noise=start.clone(), sampling_noise=samp.clone(),
+                                          return_sampling_noise=True)
+        fwd = model(start.clone(), torch.full((B,), 3, dtype=torch.long))
+    out.update(readme_corr=corr, readme_img=img, readme_mean_t=mean_t, readme_fwd=fwd)
+    for k, v in diffusion_buffers(diff).items():
+        out[f"readme_{k}"] = v
+    for key in ("h36m16", "amass21"):
+        sk, corr, node_types, diff = build_release(key, T, arch=dict(norm_type="layer"))
+        J = corr.shape[0]
+        bs, fu = 2, 4
+        B = bs * fu
+        x_cond = torch.from_numpy(synthetic.uniform((bs, J, 96), seed=21))
+        start = torch.from_numpy(synthetic.normal((B, J, 96), seed=22))
+        samp = torch.from_numpy(synthetic.normal((B, T - 1, J, 96), seed=23))
+        with torch.no_grad():
+            img, (_, _, mean_t) = diff.sample(batch_size=B, x_cond=x_cond.repeat_interleave(fu, 0),
+                                              start_noise=start.clone(), sampling_noise=samp.clone(),
+                                              return_sampling_noise=True)
+            fwd = diff.model(start.clone(), torch.full((B,), 3, dtype=torch.long), None,
+                             x_cond.repeat_interleave(fu, 0))
+        out.update({f"{key}_img": img, f"{key}_mean_t": mean_t, f"{key}_fwd": fwd, f"{key}_node_types": node_types,
+                    f"{key}_corr": corr})
+    out.update(B_seq=2, futures=4)
+    _save("layernorm_T10", **out)
+
+
 def main():
+    if sys.argv[1:] == ["layernorm"]:
+        gen_layernorm()
+        return
     if sys.argv[1:] == ["r06"]:
         gen_iso_paths()
         gen_noclip_release()

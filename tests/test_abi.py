@@ -24,7 +24,7 @@ def test_library_exports_every_declared_symbol():
     lib = _lib.lib()
     for name in declared_symbols():
         assert hasattr(lib, name), name
-    assert lib.sd_abi_version() == _lib.SD_ABI_VERSION == 3
+    assert lib.sd_abi_version() == _lib.SD_ABI_VERSION == 4
     hdr = open(os.path.join(os.path.dirname(__file__), "..", "include", "skeldiff.h")).read()
     assert re.search(r"#define SD_ABI_VERSION (\d+)", hdr).group(1) == str(_lib.SD_ABI_VERSION)
 
@@ -120,3 +120,42 @@ def test_plan_options_validated_on_host():
         assert lib.sd_plan_set_option(h, _lib.SD_OPT_LAST_ROUTE, 1) == -1
     finally:
         lib.sd_plan_destroy(h)
+
+
+def test_layernorm_plan_registry_and_limits():
+    """norm_type 'layer' (ABI 4): each Block's LayerNorm(J) affine joins the registry under the
+    reference keys; J outside the v4 mixing epilogue's 16 / 17 / 21 and the exact-f32 variants are
+    refused on the host by name."""
+    import dataclasses
+    import torch
+
+    import oracle as O
+
+    lib = _lib.lib()
+    nt = [0, 1, 2, 0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 7, 8, 9]
+    arr = (ctypes.c_int64 * 16)(*nt)
+    d = _lib.SDPlanDesc(num_nodes=16, latent_dim=96, cond_dim=96, out_dim=96, depth=4, attn_heads=8,
+                        attn_dim_head=32, use_attention=1, self_condition=0, learn_influence=1,
+                        num_node_types=10, timesteps=10, isotropic=0, activation=0, sinusoidal_theta=10000.0,
+                        norm_type=1)
+    d.node_types = ctypes.cast(arr, ctypes.POINTER(ctypes.c_int64))
+    h = ctypes.c_void_p()
+    assert lib.sd_plan_create(ctypes.byref(h), ctypes.byref(d)) == 0, lib.sd_last_error()
+    try:
+        names = {lib.sd_plan_tensor_name(h, i).decode(): lib.sd_plan_tensor_numel(h, i)
+                 for i in range(lib.sd_plan_num_tensors(h))}
+        cfg = dataclasses.replace(O.release_config(16, torch.tensor(nt)), norm_type="layer")
+        expect = {k: int(torch.Size(s).numel()) for k, s, _ in O.denoiser_param_shapes(cfg)}
+        ln = {k for k in expect if ".norm.norm." in k}
+        assert len(ln) == 2 * 2 * 9  # (block1, block2) x (weight, bias) x 9 ResnetBlocks
+        assert ln <= set(names) and all(names[k] == 16 for k in ln)
+        assert lib.sd_plan_set_option(h, _lib.SD_OPT_KERNEL_VARIANT, 3) == -1
+        assert b"norm_type" in lib.sd_last_error()
+        assert lib.sd_plan_set_option(h, _lib.SD_OPT_KERNEL_VARIANT, 4) == 0
+    finally:
+        lib.sd_plan_destroy(h)
+    d.num_nodes, d.num_node_types = 51, 0
+    assert lib.sd_plan_create(ctypes.byref(h), ctypes.byref(d)) == -1
+    assert b"norm_type" in lib.sd_last_error()
+    d.num_nodes, d.norm_type = 16, 2
+    assert lib.sd_plan_create(ctypes.byref(h), ctypes.byref(d)) == -1

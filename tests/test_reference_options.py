@@ -6,7 +6,8 @@
 * p_sample's clip_denoised=False (base.py:318-319 skipped), through sample()'s **kwargs;
 * the config-selectable covariance / schedule options: diffusion_covariance_type='anisotropic',
   gamma_scheduler='mono_decrease', beta_schedule 'linear' / 'exp' (nonisotropic.py:36-68,
-  base.py:39-61; configs/config_train_diffusion/model/skeleton_diffusion.yaml:42-44).
+  base.py:39-61; configs/config_train_diffusion/model/skeleton_diffusion.yaml:42-44);
+* the Denoiser's norm_type='layer' (Block: LayerNorm over the node axis, attention.py:19-28, 49-75).
 
 The GPU side of the same fixtures is tests/test_gpu_options.py."""
 import numpy as np
@@ -14,8 +15,8 @@ import pytest
 import torch
 
 import oracle as O
-from conftest import (ISO_OBJECTIVES, OPTION_CASES, WEIGHT_SEED, golden, interpolate_funct, iso_path_inputs,
-                      option_buffers, option_inputs, tol_rel)
+from conftest import (ISO_OBJECTIVES, LAYERNORM_MODELS, OPTION_CASES, WEIGHT_SEED, golden, interpolate_funct,
+                      iso_path_inputs, layernorm_case, option_buffers, option_inputs, tol_rel)
 
 
 @pytest.mark.parametrize("obj", ISO_OBJECTIVES)
@@ -117,3 +118,37 @@ def test_product_buffers_of_options(name):
                 continue
             ref = z[f"{model}_buf_{k}"]
             np.testing.assert_allclose(v.numpy(), ref, atol=tol_rel(ref, 1e-6), rtol=0, err_msg=f"{model} {k}")
+
+
+@pytest.mark.parametrize("model", LAYERNORM_MODELS)
+def test_oracle_layernorm_denoiser(model):
+    """norm_type='layer': the Denoiser forward at t = 3 and the sampled T = 10 chain (README J = 16,
+    release H36M J = 16, release AMASS J = 21)."""
+    z = golden("layernorm_T10")
+    cfg, sd, xc, start, samp, bufs = layernorm_case(model, z)
+    t = torch.full((start.shape[0],), int(z["fwd_t"]), dtype=torch.long)
+    out = O.denoiser_forward(sd, cfg, start, t, xc)
+    np.testing.assert_allclose(out.numpy(), z[f"{model}_fwd"], atol=2e-6, rtol=0)
+    img, means = O.p_sample_loop(sd, cfg, bufs, start, samp, x_cond=xc, record_means=True)
+    np.testing.assert_allclose(img.numpy(), z[f"{model}_img"], atol=2e-6, rtol=0)
+    np.testing.assert_allclose(means.numpy(), z[f"{model}_mean_t"], atol=2e-6, rtol=0)
+    # the norm is exercised: the same weights without it give another output
+    import dataclasses
+    plain = {k: v for k, v in sd.items() if ".norm.norm." not in k}
+    other = O.denoiser_forward(plain, dataclasses.replace(cfg, norm_type="none"), start, t, xc)
+    assert (other - out).abs().max() > 1e-2
+
+
+def test_product_module_layernorm_forward():
+    """The product Denoiser module (torch path, core/network/layers.py) with norm_type='layer'
+    reproduces the reference's forward."""
+    from conftest import build_layernorm_diffusion
+
+    z = golden("layernorm_T10")
+    for model in LAYERNORM_MODELS:
+        d = build_layernorm_diffusion(model, z)
+        _, _, xc, start, _, _ = layernorm_case(model, z)
+        t = torch.full((start.shape[0],), int(z["fwd_t"]), dtype=torch.long)
+        with torch.no_grad():
+            out = d.model(start, t, None, xc)
+        np.testing.assert_allclose(out.numpy(), z[f"{model}_fwd"], atol=2e-6, rtol=0, err_msg=model)

@@ -17,7 +17,8 @@ OUT=gpurun_out/prof_$TAG
 mkdir -p $OUT
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o run -- \
     python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-exact-line $EXTRA > $OUT/trace.log 2>&1
-rc=$?; echo "trace rc=$rc"; [ $rc -eq 0 ] || exit $rc
+rc=$?; echo "trace rc=$rc"; rm -f $OUT/trace/run_kernel_trace.csv  # stats kept; gpurun_out is capped at 64 MiB
+[ $rc -eq 0 ] || exit $rc
 # one row chain: every dispatch covers the full batch, as the roofline's per-launch timing does
 PMC_ARGS="--T 4 --steps 1 --warmup 1 --no-cpu-baseline --no-exact-line --profile-reps 1 --option row_chains=1 $EXTRA"
 i=0
