@@ -38,8 +38,14 @@ def kind(name):
         return "gemm_wave"
     m = re.match(r"sd::k_gl4<(.*)>", n)
     if m:
-        mode = int(m.group(1).split(",")[6]) if len(m.group(1).split(",")) > 6 else 0
+        args = m.group(1).split(",")
+        # <J, NW, RT, CT, RMS, MODE, PREC, STG> (ABI 3+); rounds 1-5 had two more arguments, MODE 7th
+        mode = int(args[5]) if len(args) == 8 else int(args[6]) if len(args) > 6 else 0
         return {0: "one_kernel", 1: "fused_attention", 2: "mix_phase", 3: "attn_phase", 4: "one_kernel"}.get(mode, "other")
+    if "k_gl5_mix" in n:  # J > 21: the mixing pass of a plain layer
+        return "mix_phase"
+    if "k_attention" in n:  # the attention kernel (k_attention_mix: with to_qkv's mixing)
+        return "attn_phase"
     if "k_update" in n:
         return "update"
     return "other"
