@@ -90,16 +90,16 @@ def test_sample_on_cpu_raises():
 
 
 @pytest.mark.parametrize("kw, reason", [
-    (dict(norm_type="layer"), "norm_type != 'none'"),
     (dict(self_condition=True), "self_condition"),
     (dict(learned_variance=True), "learned_variance"),
     (dict(learned_sinusoidal_cond=True), "learned/random sinusoidal time embedding"),
     (dict(random_fourier_features=True), "learned/random sinusoidal time embedding"),
 ])
 def test_non_release_denoiser_options_refused_with_reason(kw, reason):
-    """Denoiser options no release config uses (attention.py:55-60, generator.py:16-45,80,88) build
-    as torch modules like the reference's, and the sampling engine refuses them by name at plan
-    time instead of sampling something else (engine.py:_desc)."""
+    """Denoiser options no release config uses (generator.py:16-45,80,88) build as torch modules
+    like the reference's, and the sampling engine refuses them by name at plan time instead of
+    sampling something else (engine.py:_desc).  norm_type='layer' (attention.py:55-60) runs on the
+    engine since round 6 (tests/test_gpu_layernorm.py)."""
     from skeletondiffusion_amd.core.diffusion import NonisotropicGaussianDiffusion, get_cov_from_corr
     from skeletondiffusion_amd.core.network import Denoiser
 
