@@ -164,6 +164,7 @@ hipError_t launch_convert_rows(void* dst, int dst_bf16, int64_t dst_rs, const vo
 hipError_t launch_philox_raw(uint32_t* out, int64_t rows, int64_t quads, uint64_t seed,
                              int64_t row0, int step, hipStream_t s);
 hipError_t launch_set_rng(uint64_t* rng_dev, uint64_t seed, int64_t row0, hipStream_t s);
+hipError_t launch_delay(double us, hipStream_t s);  // a stream-ordered wait of `us` microseconds
 hipError_t launch_copy_rows(float* dst, int64_t dst_rs, const float* src, int64_t src_rs,
                             int64_t rows, int64_t n, hipStream_t s);
 // row-blocked v4 activation layout -> row-major (rows, J, F)

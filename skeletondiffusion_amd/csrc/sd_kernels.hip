@@ -665,6 +665,26 @@ __global__ void k_set_rng(uint64_t* rng, uint64_t seed, int64_t row0) {
     }
 }
 
+// One wave that waits `ticks` of the constant-rate wall clock (s_memrealtime), sleeping between
+// reads: a stream-ordered start offset for a row chain (sd_sample_loop's chain stagger).  Every
+// wave leaves once the clock has advanced, whatever the machine does.
+__global__ __launch_bounds__(64) void k_delay(uint64_t ticks) {
+    const uint64_t t0 = wall_clock64();
+    while (wall_clock64() - t0 < ticks) __builtin_amdgcn_s_sleep(16);
+}
+
+hipError_t launch_delay(double us, hipStream_t s) {
+    static const double ticks_per_us = [] {
+        int dev = 0, khz = 0;
+        if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev) != hipSuccess || khz <= 0)
+            khz = 100000;  // the MI355X constant clock: 100 MHz
+        return khz / 1000.0;
+    }();
+    if (us <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_delay, dim3(1), dim3(64), 0, s, (uint64_t)(us * ticks_per_us));
+    return hipGetLastError();
+}
+
 hipError_t launch_set_rng(uint64_t* rng_dev, uint64_t seed, int64_t row0, hipStream_t s) {
     hipLaunchKernelGGL(k_set_rng, dim3(1), dim3(64), 0, s, rng_dev, seed, row0);
     return hipGetLastError();

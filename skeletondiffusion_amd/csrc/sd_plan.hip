@@ -1280,9 +1280,16 @@ int sd_sample_loop(const sd_plan* p, const float* x_T, const float* x_cond, int6
     mp->last_route.store(set->route_bits);
     if ((rc = fork_chains(mp, s, nch, cs))) return rc;
     {
+        // SKELDIFF_CHAIN_STAGGER (µs, A/B): chain i starts i x that much later, so the chains run
+        // different layer types at a time instead of the same one in lockstep
+        static const double stagger = [] {
+            const char* e = getenv("SKELDIFF_CHAIN_STAGGER");
+            return e ? atof(e) : 0.0;
+        }();
         std::lock_guard<std::mutex> g(set->mu);
         for (int i = 0; i < nch; ++i) {
             SD_HIP(hipStreamWaitEvent(cs[i], set->done[i], 0));  // the exec's previous launch (any stream)
+            if (i > 0 && stagger > 0) SD_HIP(sd::launch_delay(stagger * i, cs[i]));
             SD_HIP(hipGraphLaunch(set->execs[i], cs[i]));
             SD_HIP(hipEventRecord(set->done[i], cs[i]));
         }
