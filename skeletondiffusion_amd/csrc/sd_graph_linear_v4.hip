@@ -409,9 +409,9 @@ __global__ __launch_bounds__(256) void k_gl4y(const GLArgs p, int ntile_c, int64
 // N = 192, 3,200 rows 17.1 vs 20.7 us (RT 2, CT 3), 1,067 rows 10.8 vs 12.5; N = 768 (RT 1, CT 6)
 // 53.6 vs 56.6 and 23.3 vs 25.9 (profiles/r06f/probe.txt).  bf16 operands (PREC 2) are their own A
 // fragments and keep the tracked register ring of the round-5 form (RT = 1).
-template <int PREC, int CT, int NCH>
+template <int PREC, int CT, int NCH, int PF>
 constexpr int gl4t_smem_bytes() {
-    constexpr int TILE_H = PREC ? 512 : 1024, TS = 36, NWV = 4, NS = 3;
+    constexpr int TILE_H = PREC ? 512 : 1024, TS = 36, NWV = 4, NS = PF + 1;
     constexpr int SBW = NS * CT * TILE_H * 2;
     return SBW > NWV * 32 * TS * 4 ? SBW : NWV * 32 * TS * 4;
 }
@@ -424,11 +424,11 @@ __device__ __forceinline__ void g4_async(floatx4& d, const float* p) {
 
 // The workgroup's work: unit u = (node j, row group, column group); smem_raw = its
 // gl4t_smem_bytes of LDS.  A row group is NWV waves x RT 32-row tiles.
-template <bool RMS, int PREC, int CT, int NCH, bool ROWMAJOR, int RT>
+template <bool RMS, int PREC, int CT, int NCH, bool ROWMAJOR, int RT, int PF>
 __device__ __forceinline__ void gl4t_body(const GLArgs& p, int ncg, int64_t ntile_r, const YOut& yo, const int64_t u,
                                           const int tid, char* __restrict__ smem_raw) {
     static_assert(PREC != 2 || RT == 1, "bf16 operands: one row tile per wave");
-    constexpr int PF = 2;                       // chunks in flight
+    static_assert(PF >= 2 && PF <= 4, "chunks in flight");
     constexpr int NWV = 4;                      // waves per workgroup
     constexpr int NT = NWV * 64;
     constexpr int TILE_H = PREC ? 512 : 1024;   // halves of one 32-column tile per chunk
@@ -596,12 +596,23 @@ __device__ __forceinline__ void gl4t_body(const GLArgs& p, int ncg, int64_t ntil
     // arrives, so a fill issued after the barrier into that chunk's slot cannot overtake a read
     // still in flight), then the register fence (XV: the compiler sees chunk c's x defined here)
     // and the barrier (publishes every wave's weight pieces of chunk c)
+    // (younger: chunks c + 1 .. issued before this wait, min(PF - 1, NCH - 1 - c); a constant in
+    // the whole-unrolled loop, so the switch folds)
     auto wait_chunk = [&](int c, int younger) {
-        if (younger == 0) {
-            __builtin_amdgcn_s_waitcnt(VmCnt4<0>::imm & ~(0xF << 8));
-        } else {
-            if (wa) __builtin_amdgcn_s_waitcnt(VmCnt4<OPA>::imm & ~(0xF << 8));
-            else __builtin_amdgcn_s_waitcnt(VmCnt4<OPB>::imm & ~(0xF << 8));
+        switch (younger) {
+            case 0: __builtin_amdgcn_s_waitcnt(VmCnt4<0>::imm & ~(0xF << 8)); break;
+            case 1:
+                if (wa) __builtin_amdgcn_s_waitcnt(VmCnt4<OPA>::imm & ~(0xF << 8));
+                else __builtin_amdgcn_s_waitcnt(VmCnt4<OPB>::imm & ~(0xF << 8));
+                break;
+            case 2:
+                if (wa) __builtin_amdgcn_s_waitcnt(VmCnt4<2 * OPA>::imm & ~(0xF << 8));
+                else __builtin_amdgcn_s_waitcnt(VmCnt4<2 * OPB>::imm & ~(0xF << 8));
+                break;
+            default:
+                if (wa) __builtin_amdgcn_s_waitcnt(VmCnt4<3 * OPA>::imm & ~(0xF << 8));
+                else __builtin_amdgcn_s_waitcnt(VmCnt4<3 * OPB>::imm & ~(0xF << 8));
+                break;
         }
         if constexpr (XV) {
 #pragma unroll
@@ -616,7 +627,7 @@ __device__ __forceinline__ void gl4t_body(const GLArgs& p, int ncg, int64_t ntil
     for (int i = 0; i < PF; ++i) fill(i);
 #pragma unroll
     for (int c = 0; c < NCH; ++c) {
-        wait_chunk(c, c + 1 < NCH ? PF - 1 : 0);
+        wait_chunk(c, NCH - 1 - c < PF - 1 ? NCH - 1 - c : PF - 1);
         if constexpr (XV) {  // fill first: the slots of chunk c - 1 are free after the barrier
             if (c + PF < NCH) fill(c + PF);
             asm volatile("" ::: "memory");
@@ -679,14 +690,14 @@ __device__ __forceinline__ void gl4t_body(const GLArgs& p, int ncg, int64_t ntil
     }
 }
 
-template <bool RMS, int PREC, int CT, int NCH, bool ROWMAJOR, int RT>
+template <bool RMS, int PREC, int CT, int NCH, bool ROWMAJOR, int RT, int PF>
 __global__ __launch_bounds__(256, 2) void k_gl4t(const GLArgs p, int ncg, int64_t ntile_r, const YOut yo) {
-    __shared__ __attribute__((aligned(16))) char smem_raw[gl4t_smem_bytes<PREC, CT, NCH>()];
+    __shared__ __attribute__((aligned(16))) char smem_raw[gl4t_smem_bytes<PREC, CT, NCH, PF>()];
     // XCD-aware order (k_gl4's): consecutive u -- the column groups of one (row group, node), which
     // read the same x -- on one XCD (blocks b, b + 8, ... share one), so x reaches that L2 once
     const int nwg = gridDim.x, xcd = blockIdx.x & 7, q8 = nwg >> 3, r8 = nwg & 7;
     const int64_t u = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (blockIdx.x >> 3);
-    gl4t_body<RMS, PREC, CT, NCH, ROWMAJOR, RT>(p, ncg, ntile_r, yo, u, threadIdx.x, smem_raw);
+    gl4t_body<RMS, PREC, CT, NCH, ROWMAJOR, RT, PF>(p, ncg, ntile_r, yo, u, threadIdx.x, smem_raw);
 }
 
 // Epilogue of the fused to_qkv + Attention kernel (MODE 1), J <= 32, dh = 32, 8 waves, a
@@ -1666,14 +1677,14 @@ hipError_t launch_gemm_split(const GLArgs& a, bool rms, float* z, int64_t z_rs, 
     return launch_gl4y<true>(a, rms, ntc, ntile_r, yo, s);
 }
 
-template <int CT, int NCH, bool ROWMAJOR, int RT>
+template <int CT, int NCH, bool ROWMAJOR, int RT, int PF = 2>
 static hipError_t launch_gl4t_v(const GLArgs& a, bool rms, int64_t ntile_r, const YOut& yo, hipStream_t s) {
     const int ncg = a.N / (32 * CT);  // column groups
     const dim3 grid((unsigned)(((ntile_r + 4 * RT - 1) / (4 * RT)) * a.J * ncg)), block(256);
-    auto kt = a.prec == 1 ? (rms ? k_gl4t<true, 1, CT, NCH, ROWMAJOR, RT> : k_gl4t<false, 1, CT, NCH, ROWMAJOR, RT>)
-                          : (rms ? k_gl4t<true, 0, CT, NCH, ROWMAJOR, RT> : k_gl4t<false, 0, CT, NCH, ROWMAJOR, RT>);
+    auto kt = a.prec == 1 ? (rms ? k_gl4t<true, 1, CT, NCH, ROWMAJOR, RT, PF> : k_gl4t<false, 1, CT, NCH, ROWMAJOR, RT, PF>)
+                          : (rms ? k_gl4t<true, 0, CT, NCH, ROWMAJOR, RT, PF> : k_gl4t<false, 0, CT, NCH, ROWMAJOR, RT, PF>);
     if constexpr (!ROWMAJOR && RT == 1) {  // bf16 mode (precision 2): the split route's scratch output only
-        if (a.prec == 2) kt = rms ? k_gl4t<true, 2, CT, NCH, false, 1> : k_gl4t<false, 2, CT, NCH, false, 1>;
+        if (a.prec == 2) kt = rms ? k_gl4t<true, 2, CT, NCH, false, 1, 2> : k_gl4t<false, 2, CT, NCH, false, 1, 2>;
     }
     g_route_bits |= kRouteGemmTiled;
     hipLaunchKernelGGL(kt, grid, block, 0, s, a, ncg, ntile_r, yo);
@@ -1700,15 +1711,22 @@ static hipError_t launch_gl4t(const GLArgs& a, bool rms, int64_t ntile_r, const 
 #ifndef SD_GL4T_RT2
 #define SD_GL4T_RT2 1
 #endif
+#ifndef SD_GL4T_PF
+#define SD_GL4T_PF 2  // chunks in flight of the row-blocked forms (A/B builds: -DSD_GL4T_PF=3 / 4)
+#endif
+#ifndef SD_GL4T_PF6
+#define SD_GL4T_PF6 2
+#endif
+    constexpr int PFB = ROWMAJOR ? 2 : SD_GL4T_PF, PF6 = ROWMAJOR ? 2 : SD_GL4T_PF6;
     if (!ROWMAJOR && SD_GL4T_RT2 && a.prec != 2 && a.N <= 192 && a.N % 96 == 0) {
-        if (K == 192) return launch_gl4t_v<3, 12, ROWMAJOR, 2>(a, rms, ntile_r, yo, s);
-        if (K == 256) return launch_gl4t_v<3, 16, ROWMAJOR, 2>(a, rms, ntile_r, yo, s);
-        if (K == 384) return launch_gl4t_v<3, 24, ROWMAJOR, 2>(a, rms, ntile_r, yo, s);
+        if (K == 192) return launch_gl4t_v<3, 12, ROWMAJOR, 2, PFB>(a, rms, ntile_r, yo, s);
+        if (K == 256) return launch_gl4t_v<3, 16, ROWMAJOR, 2, PFB>(a, rms, ntile_r, yo, s);
+        if (K == 384) return launch_gl4t_v<3, 24, ROWMAJOR, 2, PFB>(a, rms, ntile_r, yo, s);
     }
     if (a.N % 192 == 0) {
-        if (K == 192) return launch_gl4t_v<6, 12, ROWMAJOR, 1>(a, rms, ntile_r, yo, s);
-        if (K == 256) return launch_gl4t_v<6, 16, ROWMAJOR, 1>(a, rms, ntile_r, yo, s);
-        if (K == 384) return launch_gl4t_v<6, 24, ROWMAJOR, 1>(a, rms, ntile_r, yo, s);
+        if (K == 192) return launch_gl4t_v<6, 12, ROWMAJOR, 1, PF6>(a, rms, ntile_r, yo, s);
+        if (K == 256) return launch_gl4t_v<6, 16, ROWMAJOR, 1, PF6>(a, rms, ntile_r, yo, s);
+        if (K == 384) return launch_gl4t_v<6, 24, ROWMAJOR, 1, PF6>(a, rms, ntile_r, yo, s);
     } else if (a.N % 96 == 0) {
         if (K == 192) return launch_gl4t_v<3, 12, ROWMAJOR, 1>(a, rms, ntile_r, yo, s);
         if (K == 384) return launch_gl4t_v<3, 24, ROWMAJOR, 1>(a, rms, ntile_r, yo, s);

@@ -37,8 +37,8 @@ OBJDUMP = shutil.which("llvm-objdump") or "/opt/rocm/lib/llvm/bin/llvm-objdump"
 
 pytestmark = pytest.mark.skipif(not os.path.exists(OBJDUMP) or not os.path.exists(LIB), reason="no llvm-objdump / library")
 
-GL4T = "_ZN2sd6k_gl4tILb0ELi0ELi6ELi12ELb0ELi1EEEvNS_6GLArgsEilNS_4YOutE"  # N = 768 form (CT 6, one row tile)
-GL4T_RT2 = "_ZN2sd6k_gl4tILb0ELi0ELi3ELi12ELb0ELi2EEEvNS_6GLArgsEilNS_4YOutE"  # N = 192 form (CT 3, two row tiles)
+GL4T = "_ZN2sd6k_gl4tILb0ELi0ELi6ELi12ELb0ELi1ELi2EEEvNS_6GLArgsEilNS_4YOutE"  # N = 768 form (CT 6, one row tile)
+GL4T_RT2 = "_ZN2sd6k_gl4tILb0ELi0ELi3ELi12ELb0ELi2ELi2EEEvNS_6GLArgsEilNS_4YOutE"  # N = 192 form (CT 3, two row tiles)
 ATTN = "_ZN2sd11k_attentionILi4ELi32EEEvNS_8AttnArgsE"
 MIXD = "_ZN2sd12_GLOBAL__N_110k_gl5_mixdILi8ELi1ELb0EEEvNS_6GLArgsEPKfl"
 MIXD_RES = "_ZN2sd12_GLOBAL__N_110k_gl5_mixdILi8ELi1ELb1EEEvNS_6GLArgsEPKfl"
