@@ -42,7 +42,7 @@ def test_layernorm_matches_reference(model, cuda):
 def test_layernorm_routes_bitwise(model, cuda):
     """The LayerNorm lives in the split route's mixing phase: SD_OPT_SPLIT_ROUTE 1 (never split) still
     takes the auto split route for the Block layers, and the small-batch (2) and tiled (3) GEMM
-    phases give bitwise equal chains; 3 row chains equal 1; half precision also samples (finite)."""
+    phases give bitwise equal chains; 3 row chains equal 1; half and bf16 precision sample close to it."""
     z = golden("layernorm_T10")
     d = build_layernorm_diffusion(model, z, cuda)
     J = int(z[f"{model}_corr"].shape[0])
@@ -59,8 +59,9 @@ def test_layernorm_routes_bitwise(model, cuda):
         else:
             assert torch.equal(out, ref), (route, chains, float((out - ref).abs().max()))
     d.engine.set_option("split_route", 0)
-    d.engine.set_precision("half")
-    half = d.engine.sample_loop(400, x_cond=xc, seed=4, graph=True)[0]
-    torch.cuda.synchronize()
-    assert torch.isfinite(half).all() and float((half - ref).abs().max()) < 0.05
+    for prec, tol in (("half", 0.05), ("bf16", 0.15)):  # reduced precision: the tiled route, LayerNorm kept
+        d.engine.set_precision(prec)
+        lo = d.engine.sample_loop(400, x_cond=xc, seed=4, graph=True)[0].float()
+        torch.cuda.synchronize()
+        assert torch.isfinite(lo).all() and float((lo - ref).abs().max()) < tol, (prec, float((lo - ref).abs().max()))
     d.engine.set_precision("f32")
